@@ -1,0 +1,126 @@
+"""ctypes binding of libccrdt.so (include/ccrdt.h, include/ccrdt_gen.h).
+
+The engine is native HIP code for gfx950; this module only loads it and
+declares the C signatures.  There is no Python or CPU fallback: importing the
+package without the built library raises, and every engine call on a machine
+without a usable HIP device returns CCRDT_EDEVICE, which is raised as
+CcrdtError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libccrdt.so")
+
+OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS = range(6)
+AVERAGE, TOPK, TOPK_RMV, LEADERBOARD, WORDCOUNT, WORDDOCUMENTCOUNT = range(6)
+TRMV_ADD, TRMV_ADD_R, TRMV_RMV, TRMV_RMV_R = range(4)
+NOOP = 255
+TRMV_MAX_DC = 8
+
+P = C.c_void_p
+I64 = C.c_int64
+U64 = C.c_uint64
+INT = C.c_int
+
+
+class CcrdtError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: {_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_ERRNAMES = {EINVAL: "EINVAL", ERANGE: "ERANGE", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE",
+             ENOSYS: "ENOSYS"}
+
+
+class TrmvOps(C.Structure):
+    _fields_ = [("n_ops", I64), ("n_rmv_rows", I64), ("key_ptr", P), ("kind", P), ("id", P),
+                ("score", P), ("dc", P), ("ts", P), ("rmv_vc", P)]
+
+
+class TrmvExtra(C.Structure):
+    _fields_ = [("kind", P), ("id", P), ("score", P), ("dc", P), ("ts", P), ("vc", P)]
+
+
+class TrmvState(C.Structure):
+    _fields_ = [("vc", P), ("obs_ptr", P), ("obs_id", P), ("obs_score", P), ("obs_ts", P),
+                ("obs_dc", P), ("m_ptr", P), ("m_id", P), ("m_score", P), ("m_ts", P),
+                ("m_dc", P), ("r_ptr", P), ("r_id", P), ("r_vc", P), ("min_valid", P),
+                ("min_id", P), ("min_score", P), ("min_ts", P), ("min_dc", P)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/*.h
+SIGNATURES = {
+    "ccrdt_is_type": (INT, [INT]),
+    "ccrdt_generates_extra_operations": (INT, [INT]),
+    "ccrdt_engine_create": (INT, [INT, I64, I64, INT, INT, C.POINTER(P)]),
+    "ccrdt_engine_destroy": (INT, [P]),
+    "ccrdt_engine_reset": (INT, [P]),
+    "ccrdt_engine_clone": (INT, [P, C.POINTER(P)]),
+    "ccrdt_engine_sync": (INT, [P]),
+    "ccrdt_engine_stream": (P, [P]),
+    "ccrdt_strerror": (C.c_char_p, [INT]),
+    "ccrdt_last_error": (C.c_char_p, []),
+    "ccrdt_device_count": (INT, [C.POINTER(INT)]),
+    "ccrdt_set_device": (INT, [INT]),
+    "ccrdt_device_alloc": (INT, [C.POINTER(P), U64]),
+    "ccrdt_device_free": (INT, [P]),
+    "ccrdt_memcpy_h2d": (INT, [P, P, U64]),
+    "ccrdt_memcpy_d2h": (INT, [P, P, U64]),
+    "ccrdt_device_synchronize": (INT, []),
+    "ccrdt_engine_last_kernel_ms": (INT, [P, C.POINTER(C.c_float)]),
+    "ccrdt_engine_overflow_keys": (INT, [P, INT, C.POINTER(I64)]),
+    "ccrdt_timer_start": (INT, [P]),
+    "ccrdt_timer_stop": (INT, [P, C.POINTER(C.c_float)]),
+    "ccrdt_trmv_apply": (INT, [P, C.POINTER(TrmvOps), C.POINTER(TrmvExtra)]),
+    "ccrdt_trmv_apply_device": (INT, [P, C.POINTER(TrmvOps)]),
+    "ccrdt_trmv_extra_count": (INT, [P, C.POINTER(I64)]),
+    "ccrdt_trmv_fetch_extra": (INT, [P, C.POINTER(TrmvExtra)]),
+    "ccrdt_trmv_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+    "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
+    "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
+    "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),
+    # ccrdt_gen.h
+    "ccrdt_splitmix64": (U64, [U64]),
+    "ccrdt_gen_trmv_count": (I64, [I64, U64, INT]),
+    "ccrdt_gen_trmv": (INT, [I64, I64, INT, I64, I64, INT, INT, INT, INT, U64,
+                             P, P, P, P, P, P, P]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libccrdt.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, where: str) -> None:
+    if rc != OK:
+        msg = lib.ccrdt_last_error().decode(errors="replace")
+        raise CcrdtError(rc, where, msg)
+
+
+def ptr(a) -> int | None:
+    """Data pointer of a numpy array (None for None)."""
+    if a is None:
+        return None
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = INT(0)
+    rc = lib.ccrdt_device_count(C.byref(n))
+    return n.value if rc == OK else 0

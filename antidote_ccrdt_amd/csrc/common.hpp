@@ -1,0 +1,106 @@
+// common.hpp — shared internals of libccrdt (host + device).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/ccrdt.h"
+
+namespace ccrdt {
+
+void set_error(const std::string& msg);
+
+#define CCRDT_HIP(call)                                                        \
+  do {                                                                         \
+    hipError_t _e = (call);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      ::ccrdt::set_error(std::string(#call) + ": " + hipGetErrorString(_e));   \
+      return CCRDT_EDEVICE;                                                    \
+    }                                                                          \
+  } while (0)
+
+#define CCRDT_TRY(call)          \
+  do {                           \
+    int _rc = (call);            \
+    if (_rc != CCRDT_OK) return _rc; \
+  } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+  int ensure(uint64_t need) {
+    if (need <= bytes && p) return CCRDT_OK;
+    if (p) {
+      CCRDT_HIP(hipFree(p));
+      p = nullptr;
+      bytes = 0;
+    }
+    uint64_t b = need < 256 ? 256 : need;
+    CCRDT_HIP(hipMalloc(&p, b));
+    bytes = b;
+    return CCRDT_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ------------------------------------------------------------ wave helpers
+// One wavefront = 64 lanes on CDNA4.  These helpers move wave-uniform values
+// between lanes and SGPRs.
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// Write v into one lane (wave-uniform lane index): v_cmp + v_cndmask.
+__device__ __forceinline__ uint32_t wl32(uint32_t old, int lane, uint32_t v) {
+  return (int)(threadIdx.x & 63) == lane ? v : old;
+}
+__device__ __forceinline__ int64_t wl64(int64_t old, int lane, int64_t v) {
+  return (int)(threadIdx.x & 63) == lane ? v : old;
+}
+// Per-lane gather from another lane (ds_bpermute crossbar).
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+  uint32_t lo = shfl32((uint32_t)v, src);
+  uint32_t hi = shfl32((uint32_t)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// Number of set bits of m below this lane (v_mbcnt).
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    int64_t o = shfl64(v, lane_id() ^ off);
+    v = o < v ? o : v;
+  }
+  return rl64(v, 0);
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    int64_t o = shfl64(v, lane_id() ^ off);
+    v = o > v ? o : v;
+  }
+  return rl64(v, 0);
+}
+
+}  // namespace ccrdt

@@ -1,0 +1,825 @@
+// engine.cpp — libccrdt engine runtime + the topk_rmv C-ABI (include/ccrdt.h).
+//
+// The engine keeps every key's CCRDT state resident in HBM and applies a
+// batch of effect ops (update/2 of the reference behaviour,
+// src/antidote_ccrdt.erl:50) with one pass of hand-written gfx950 kernels.
+// Host code here only sizes buffers, launches, and converts between the
+// canonical state image and the device layout.  There is no CPU compute path:
+// if the HIP runtime or the device is missing, calls fail with CCRDT_EDEVICE.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "common.hpp"
+#include "engine.hpp"
+#include "trmv_kernels.hpp"
+
+namespace ccrdt {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
+int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStream_t st);
+int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
+
+static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
+static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
+static constexpr uint32_t TRMV_MAX_ROWS = 8u * 2u * 16u;  // removal rows per key
+
+}  // namespace ccrdt
+
+using namespace ccrdt;
+
+TrmvSide ccrdt_engine::trmv_side(int s) const {
+  const TrmvBufs& b = trmv[s];
+  TrmvSide t;
+  t.meta = b.meta.as<KeyMeta>();
+  t.pl_id = b.pl_id.as<int64_t>();
+  t.pl_info = b.pl_info.as<uint32_t>();
+  t.m_score = b.m_score.as<int64_t>();
+  t.m_ts = b.m_ts.as<int64_t>();
+  t.m_pd = b.m_pd.as<uint32_t>();
+  t.r_vc = b.r_vc.as<int64_t>();
+  t.vc = b.vc.as<int64_t>();
+  return t;
+}
+
+void ccrdt_engine::release_all() {
+  for (auto& b : trmv) {
+    b.meta.release();
+    b.pl_id.release();
+    b.pl_info.release();
+    b.m_score.release();
+    b.m_ts.release();
+    b.m_pd.release();
+    b.r_vc.release();
+    b.vc.release();
+  }
+  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &ovf_a, &ovf_b, &status, &st_kp,
+                    &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
+    d->release();
+  release_types();
+}
+
+// ===================================================================== C-ABI
+extern "C" {
+
+const char* ccrdt_strerror(int code) {
+  switch (code) {
+    case CCRDT_OK: return "ok";
+    case CCRDT_EINVAL: return "invalid argument or operation";
+    case CCRDT_ERANGE: return "integer outside engine range";
+    case CCRDT_ENOMEM: return "out of device memory or per-key capacity";
+    case CCRDT_EDEVICE: return "HIP device error";
+    case CCRDT_ENOSYS: return "operation not supported for this CCRDT type";
+    default: return "unknown error";
+  }
+}
+const char* ccrdt_last_error(void) { return g_last_error.c_str(); }
+
+int ccrdt_is_type(int type) { return type >= CCRDT_AVERAGE && type <= CCRDT_WORDDOCUMENTCOUNT; }
+int ccrdt_generates_extra_operations(int type) {
+  return type == CCRDT_TOPK_RMV || type == CCRDT_LEADERBOARD;
+}
+
+int ccrdt_device_count(int* n) {
+  CCRDT_HIP(hipGetDeviceCount(n));
+  return CCRDT_OK;
+}
+int ccrdt_set_device(int device) {
+  CCRDT_HIP(hipSetDevice(device));
+  return CCRDT_OK;
+}
+int ccrdt_device_alloc(void** p, uint64_t bytes) {
+  CCRDT_HIP(hipMalloc(p, bytes ? bytes : 1));
+  return CCRDT_OK;
+}
+int ccrdt_device_free(void* p) {
+  CCRDT_HIP(hipFree(p));
+  return CCRDT_OK;
+}
+int ccrdt_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+  CCRDT_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return CCRDT_OK;
+}
+int ccrdt_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+  CCRDT_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return CCRDT_OK;
+}
+int ccrdt_device_synchronize(void) {
+  CCRDT_HIP(hipDeviceSynchronize());
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_create(int type, int64_t k, int64_t n_keys, int n_dc, int device,
+                        ccrdt_engine** out) {
+  if (!out || !ccrdt_is_type(type) || n_keys < 0 || k <= 0) {
+    set_error("engine_create: bad type / k / n_keys");
+    return CCRDT_EINVAL;
+  }
+  if (type == CCRDT_TOPK_RMV && (n_dc < 1 || n_dc > CCRDT_TRMV_MAX_DC)) {
+    set_error("engine_create: topk_rmv needs 1 <= n_dc <= 8");
+    return CCRDT_EINVAL;
+  }
+  if (n_keys > 0xFFFFFFFFll) {
+    set_error("engine_create: n_keys must fit in 32 bits");
+    return CCRDT_EINVAL;
+  }
+  int ndev = 0;
+  CCRDT_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    set_error("engine_create: no such HIP device");
+    return CCRDT_EDEVICE;
+  }
+  CCRDT_HIP(hipSetDevice(device));
+  Engine* e = new Engine();
+  e->type = type;
+  e->k = k;
+  e->n_keys = n_keys;
+  e->n_dc = n_dc;
+  e->device = device;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
+      hipEventCreate(&e->evk0) != hipSuccess || hipEventCreate(&e->evk1) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_status, 64, hipHostMallocDefault) != hipSuccess) {
+    set_error("engine_create: stream/event/pinned allocation failed");
+    delete e;
+    return CCRDT_EDEVICE;
+  }
+  int rc = e->init_type();
+  if (rc != CCRDT_OK) {
+    ccrdt_engine_destroy(e);
+    return rc;
+  }
+  *out = e;
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_destroy(ccrdt_engine* e) {
+  if (!e) return CCRDT_OK;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  e->release_all();
+  if (e->h_status) (void)hipHostFree(e->h_status);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->evk0) (void)hipEventDestroy(e->evk0);
+  if (e->evk1) (void)hipEventDestroy(e->evk1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_reset(ccrdt_engine* e) {
+  if (!e) return CCRDT_EINVAL;
+  e->fresh = true;
+  return e->reset_type();
+}
+
+int ccrdt_engine_sync(ccrdt_engine* e) {
+  if (!e) return CCRDT_EINVAL;
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  return CCRDT_OK;
+}
+void* ccrdt_engine_stream(ccrdt_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int ccrdt_timer_start(ccrdt_engine* e) {
+  if (!e) return CCRDT_EINVAL;
+  CCRDT_HIP(hipSetDevice(e->device));
+  CCRDT_HIP(hipEventRecord(e->ev0, e->stream));
+  return CCRDT_OK;
+}
+int ccrdt_timer_stop(ccrdt_engine* e, float* ms) {
+  if (!e || !ms) return CCRDT_EINVAL;
+  CCRDT_HIP(hipEventRecord(e->ev1, e->stream));
+  CCRDT_HIP(hipEventSynchronize(e->ev1));
+  CCRDT_HIP(hipEventElapsedTime(ms, e->ev0, e->ev1));
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms) {
+  if (!e || !ms) return CCRDT_EINVAL;
+  *ms = e->last_kernel_ms;
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_overflow_keys(ccrdt_engine* e, int slot_class, int64_t* n) {
+  if (!e || !n) return CCRDT_EINVAL;
+  auto it = e->trmv_overflow_keys.find(slot_class);
+  *n = it == e->trmv_overflow_keys.end() ? 0 : it->second;
+  return CCRDT_OK;
+}
+
+// ------------------------------------------------------------------ topk_rmv
+
+static int check_trmv(ccrdt_engine* e) {
+  if (!e) {
+    set_error("null engine");
+    return CCRDT_EINVAL;
+  }
+  if (e->type != CCRDT_TOPK_RMV) {
+    set_error("engine is not topk_rmv");
+    return CCRDT_ENOSYS;
+  }
+  if (hipSetDevice(e->device) != hipSuccess) {
+    set_error("hipSetDevice failed");
+    return CCRDT_EDEVICE;
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
+  CCRDT_TRY(check_trmv(e));
+  if (!ops || !ops->key_ptr || (ops->n_ops > 0 && (!ops->kind || !ops->id || !ops->score ||
+                                                   !ops->dc || !ops->ts))) {
+    set_error("trmv_apply: null op array");
+    return CCRDT_EINVAL;
+  }
+  if (ops->n_ops >= (int64_t)0xFFFFFFFFll) {
+    set_error("trmv_apply: batch too large (n_ops must fit in 32 bits)");
+    return CCRDT_EINVAL;
+  }
+  Engine& E = *e;
+  const int D = E.n_dc;
+  const uint64_t nk = (uint64_t)E.n_keys;
+  const int out = 1 - E.cur;
+  TrmvApplyArgs a{};
+  a.n_keys = E.n_keys;
+  a.n_dc = D;
+  a.k = (uint32_t)std::min<int64_t>(E.k, 0xFFFFFFFFll);
+  a.key_ptr = ops->key_ptr;
+  a.kind = ops->kind;
+  a.id = ops->id;
+  a.score = ops->score;
+  a.dc = ops->dc;
+  a.ts = ops->ts;
+  a.rmv_vc = ops->rmv_vc;
+  a.n_rmv_rows = ops->rmv_vc ? ops->n_rmv_rows : 0;
+  a.fresh = E.fresh ? 1 : 0;
+  a.old_s = E.trmv_side(E.cur);
+  CCRDT_TRY(E.trmv[out].meta.ensure(nk * sizeof(KeyMeta)));
+  a.new_s = E.trmv_side(out);
+  const uint64_t nb = (nk + 1023) / 1024;
+  CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t)));
+  // 1) capacities -> segment offsets of the new state
+  CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
+  uint64_t tot[3] = {0, 0, 0};
+  if (nk) {
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.partials.as<uint64_t>() + nb * 3, 3 * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    memcpy(tot, E.h_status, sizeof(tot));
+  }
+  if (tot[0] >= 0xFFFFFFFFull || tot[1] >= 0xFFFFFFFFull || tot[2] >= 0xFFFFFFFFull) {
+    set_error("trmv_apply: resident state would exceed 2^32 elements");
+    return CCRDT_ENOMEM;
+  }
+  TrmvBufs& ob = E.trmv[out];
+  CCRDT_TRY(ob.pl_id.ensure(tot[0] * 8));
+  CCRDT_TRY(ob.pl_info.ensure(tot[0] * 4));
+  CCRDT_TRY(ob.m_score.ensure(tot[1] * 8));
+  CCRDT_TRY(ob.m_ts.ensure(tot[1] * 8));
+  CCRDT_TRY(ob.m_pd.ensure(tot[1] * 4));
+  CCRDT_TRY(ob.r_vc.ensure(tot[2] * 8 * D));
+  CCRDT_TRY(ob.vc.ensure(nk * 8 * D));
+  a.new_s = E.trmv_side(out);
+  const uint64_t n_ops = (uint64_t)ops->n_ops;
+  CCRDT_TRY(E.ex_cnt.ensure(nk * 4));
+  CCRDT_TRY(E.ex.ensure(n_ops * sizeof(TrmvExtraRec)));
+  CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
+  CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
+  CCRDT_TRY(E.ovf_a.ensure(nk * 4));
+  CCRDT_TRY(E.ovf_b.ensure(nk * 4));
+  CCRDT_TRY(E.status.ensure(64));
+  a.ex_cnt = E.ex_cnt.as<uint32_t>();
+  a.ex = E.ex.as<TrmvExtraRec>();
+  a.ex_vc = E.ex_vc.as<int64_t>();
+  // 2) apply, escalating overflowed keys to larger register classes
+  DevBuf* work = nullptr;
+  uint64_t n_work = nk;
+  float kernel_ms = 0.f;
+  E.trmv_overflow_keys.clear();
+  for (int cls : TRMV_SLOT_CLASSES) {
+    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
+    a.key_list = work ? work->as<uint32_t>() : nullptr;
+    a.n_list = (uint32_t)n_work;
+    a.ovf_list = ovf->as<uint32_t>();
+    a.status = E.status.as<uint32_t>();
+    CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
+    CCRDT_TRY(trmv_launch_apply(a, cls, n_work, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    const uint32_t n_ovf = ((uint32_t*)E.h_status)[0];
+    const uint32_t err = ((uint32_t*)E.h_status)[1];
+    if (err) {
+      std::string m = "trmv_apply: invalid op in batch:";
+      if (err & TRMV_ERR_KIND) m += " kind>3";
+      if (err & TRMV_ERR_DC) m += " dc>=n_dc";
+      if (err & TRMV_ERR_TS) m += " add ts<1";
+      if (err & TRMV_ERR_ROW) m += " rmv row out of range";
+      if (err & TRMV_ERR_VC) m += " negative VcRmv entry";
+      set_error(m);
+      return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
+                 ? CCRDT_ERANGE
+                 : CCRDT_EINVAL;
+    }
+    E.trmv_overflow_keys[cls] = n_ovf;
+    {
+      float ms = 0.f;
+      CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
+      kernel_ms += ms;
+    }
+    if (n_ovf == 0) {
+      work = nullptr;
+      n_work = 0;
+      break;
+    }
+    work = ovf;
+    n_work = n_ovf;
+  }
+  if (n_work) {
+    set_error("trmv_apply: a key exceeds the per-key capacity (1024 Ids or Masked elements, "
+              "256 Removals entries)");
+    return CCRDT_ENOMEM;
+  }
+  CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
+                           E.stream));
+  E.cur = out;
+  E.fresh = false;
+  E.last_n_ops = n_ops;
+  E.last_kernel_ms = kernel_ms;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n) {
+  CCRDT_TRY(check_trmv(e));
+  if (!n) return CCRDT_EINVAL;
+  std::vector<uint32_t> cnt(e->n_keys);
+  if (e->n_keys && e->ex_cnt.p) {
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    CCRDT_HIP(hipMemcpy(cnt.data(), e->ex_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
+  }
+  int64_t s = 0;
+  for (uint32_t c : cnt) s += c;
+  *n = s;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* x) {
+  CCRDT_TRY(check_trmv(e));
+  if (!x) return CCRDT_EINVAL;
+  const uint64_t n_ops = e->last_n_ops, nk = (uint64_t)e->n_keys;
+  const int D = e->n_dc;
+  if (x->kind)
+    for (uint64_t i = 0; i < n_ops; ++i) x->kind[i] = CCRDT_NOOP;
+  if (!n_ops || !nk) return CCRDT_OK;
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  std::vector<uint32_t> cnt(nk);
+  std::vector<uint64_t> kp(nk + 1);
+  std::vector<TrmvExtraRec> rec(n_ops);
+  std::vector<int64_t> vc(n_ops * D);
+  CCRDT_HIP(hipMemcpy(cnt.data(), e->ex_cnt.p, nk * 4, hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(kp.data(), e->ex_key_ptr.p, (nk + 1) * 8, hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(rec.data(), e->ex.p, n_ops * sizeof(TrmvExtraRec), hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(vc.data(), e->ex_vc.p, n_ops * 8 * D, hipMemcpyDeviceToHost));
+  for (uint64_t k = 0; k < nk; ++k) {
+    for (uint32_t j = 0; j < cnt[k]; ++j) {
+      const uint64_t pos = kp[k] + j;
+      const TrmvExtraRec& r = rec[pos];
+      const uint64_t op = r.op;
+      if (op >= n_ops) continue;
+      if (x->kind) x->kind[op] = r.kind;
+      if (x->id) x->id[op] = r.id;
+      if (x->score) x->score[op] = r.score;
+      if (x->dc) x->dc[op] = r.dc;
+      if (x->ts) x->ts[op] = r.ts;
+      if (x->vc && r.kind == CCRDT_TRMV_RMV)
+        for (int d = 0; d < D; ++d) x->vc[op * D + d] = vc[pos * D + d];
+    }
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extra* extra) {
+  CCRDT_TRY(check_trmv(e));
+  if (!ops || !ops->key_ptr) {
+    set_error("trmv_apply: null ops");
+    return CCRDT_EINVAL;
+  }
+  Engine& E = *e;
+  const uint64_t nk = (uint64_t)E.n_keys, n = (uint64_t)ops->n_ops;
+  const int D = E.n_dc;
+  // CSR shape checks (host side; values are validated by the kernel)
+  if (ops->key_ptr[0] != 0 || ops->key_ptr[nk] != n) {
+    set_error("trmv_apply: key_ptr must start at 0 and end at n_ops");
+    return CCRDT_EINVAL;
+  }
+  for (uint64_t k = 0; k < nk; ++k)
+    if (ops->key_ptr[k + 1] < ops->key_ptr[k]) {
+      set_error("trmv_apply: key_ptr not monotone");
+      return CCRDT_EINVAL;
+    }
+  const uint64_t nr = ops->rmv_vc ? (uint64_t)ops->n_rmv_rows : 0;
+  CCRDT_TRY(E.st_kp.ensure((nk + 1) * 8));
+  CCRDT_TRY(E.st_kind.ensure(n));
+  CCRDT_TRY(E.st_id.ensure(n * 8));
+  CCRDT_TRY(E.st_score.ensure(n * 8));
+  CCRDT_TRY(E.st_dc.ensure(n));
+  CCRDT_TRY(E.st_ts.ensure(n * 8));
+  CCRDT_TRY(E.st_rvc.ensure(nr * D * 8));
+  CCRDT_HIP(hipMemcpyAsync(E.st_kp.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyHostToDevice, E.stream));
+  if (n) {
+    CCRDT_HIP(hipMemcpyAsync(E.st_kind.p, ops->kind, n, hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.st_id.p, ops->id, n * 8, hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.st_score.p, ops->score, n * 8, hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.st_dc.p, ops->dc, n, hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.st_ts.p, ops->ts, n * 8, hipMemcpyHostToDevice, E.stream));
+  }
+  if (nr)
+    CCRDT_HIP(hipMemcpyAsync(E.st_rvc.p, ops->rmv_vc, nr * D * 8, hipMemcpyHostToDevice, E.stream));
+  ccrdt_trmv_ops d = *ops;
+  d.key_ptr = E.st_kp.as<uint64_t>();
+  d.kind = E.st_kind.as<uint8_t>();
+  d.id = E.st_id.as<int64_t>();
+  d.score = E.st_score.as<int64_t>();
+  d.dc = E.st_dc.as<uint8_t>();
+  d.ts = E.st_ts.as<int64_t>();
+  d.rmv_vc = nr ? E.st_rvc.as<int64_t>() : nullptr;
+  d.n_rmv_rows = (int64_t)nr;
+  CCRDT_TRY(ccrdt_trmv_apply_device(e, &d));
+  if (extra) CCRDT_TRY(ccrdt_trmv_fetch_extra(e, extra));
+  return CCRDT_OK;
+}
+
+// ---- state image conversion
+
+namespace {
+struct HostTrmv {
+  std::vector<KeyMeta> meta;
+  std::vector<int64_t> pl_id, m_score, m_ts, r_vc, vc;
+  std::vector<uint32_t> pl_info, m_pd;
+};
+
+int download_trmv(Engine& E, HostTrmv& h) {
+  const uint64_t nk = (uint64_t)E.n_keys;
+  const int D = E.n_dc;
+  h.meta.assign(nk, KeyMeta{0, 0, 0, 0, 0, 0, 0, NONE32});
+  h.vc.assign(nk * D, 0);
+  if (E.fresh || !nk) return CCRDT_OK;
+  CCRDT_HIP(hipStreamSynchronize(E.stream));
+  const TrmvBufs& b = E.trmv[E.cur];
+  CCRDT_HIP(hipMemcpy(h.meta.data(), b.meta.p, nk * sizeof(KeyMeta), hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(h.vc.data(), b.vc.p, nk * D * 8, hipMemcpyDeviceToHost));
+  uint64_t np = 0, nm = 0, nr = 0;
+  for (const KeyMeta& m : h.meta) {
+    np = std::max<uint64_t>(np, (uint64_t)m.p_off + m.np);
+    nm = std::max<uint64_t>(nm, (uint64_t)m.m_off + m.nm);
+    nr = std::max<uint64_t>(nr, (uint64_t)m.r_off + m.nr);
+  }
+  h.pl_id.resize(np);
+  h.pl_info.resize(np);
+  h.m_score.resize(nm);
+  h.m_ts.resize(nm);
+  h.m_pd.resize(nm);
+  h.r_vc.resize(nr * D);
+  if (np) {
+    CCRDT_HIP(hipMemcpy(h.pl_id.data(), b.pl_id.p, np * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.pl_info.data(), b.pl_info.p, np * 4, hipMemcpyDeviceToHost));
+  }
+  if (nm) {
+    CCRDT_HIP(hipMemcpy(h.m_score.data(), b.m_score.p, nm * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_ts.data(), b.m_ts.p, nm * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_pd.data(), b.m_pd.p, nm * 4, hipMemcpyDeviceToHost));
+  }
+  if (nr) CCRDT_HIP(hipMemcpy(h.r_vc.data(), b.r_vc.p, nr * D * 8, hipMemcpyDeviceToHost));
+  return CCRDT_OK;
+}
+}  // namespace
+
+int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows) {
+  CCRDT_TRY(check_trmv(e));
+  int64_t o = 0, m = 0, r = 0;
+  if (!e->fresh && e->n_keys) {
+    std::vector<KeyMeta> meta(e->n_keys);
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.p, meta.size() * sizeof(KeyMeta),
+                        hipMemcpyDeviceToHost));
+    for (const KeyMeta& k : meta) {
+      o += k.nobs;
+      m += k.nm;
+      r += k.nr;
+    }
+  }
+  if (n_obs) *n_obs = o;
+  if (n_masked) *n_masked = m;
+  if (n_rows) *n_rows = r;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out) {
+  CCRDT_TRY(check_trmv(e));
+  if (!out) return CCRDT_EINVAL;
+  HostTrmv h;
+  CCRDT_TRY(download_trmv(*e, h));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  const int D = e->n_dc;
+  uint64_t po = 0, pm = 0, pr = 0;
+  if (out->obs_ptr) out->obs_ptr[0] = 0;
+  if (out->m_ptr) out->m_ptr[0] = 0;
+  if (out->r_ptr) out->r_ptr[0] = 0;
+  struct E4 {
+    int64_t id, score;
+    uint8_t dc;
+    int64_t ts;
+  };
+  std::vector<E4> obs, msk;
+  std::vector<std::pair<int64_t, uint32_t>> rows;
+  for (uint64_t k = 0; k < nk; ++k) {
+    const KeyMeta& m = h.meta[k];
+    if (out->vc)
+      for (int d = 0; d < D; ++d) out->vc[k * D + d] = h.vc[k * D + d];
+    obs.clear();
+    msk.clear();
+    rows.clear();
+    for (uint32_t p = 0; p < m.np; ++p) {
+      const uint32_t info = h.pl_info[m.p_off + p];
+      const int64_t id = h.pl_id[m.p_off + p];
+      const uint32_t o = info & 0xFFFFu, r = info >> 16;
+      if (o != NONE16) {
+        const uint64_t g = (uint64_t)m.m_off + o;
+        obs.push_back({id, h.m_score[g], (uint8_t)((h.m_pd[g] >> 16) & 0xFF), h.m_ts[g]});
+      }
+      if (r != NONE16) rows.push_back({id, r});
+    }
+    for (uint32_t i = 0; i < m.nm; ++i) {
+      const uint64_t g = (uint64_t)m.m_off + i;
+      const uint32_t pd = h.m_pd[g];
+      msk.push_back({h.pl_id[m.p_off + (pd & 0xFFFFu)], h.m_score[g], (uint8_t)((pd >> 16) & 0xFF),
+                     h.m_ts[g]});
+    }
+    std::sort(obs.begin(), obs.end(), [](const E4& a, const E4& b) { return a.id < b.id; });
+    std::sort(msk.begin(), msk.end(), [](const E4& a, const E4& b) {
+      return std::tie(a.id, a.score, a.dc, a.ts) < std::tie(b.id, b.score, b.dc, b.ts);
+    });
+    std::sort(rows.begin(), rows.end());
+    for (const E4& x : obs) {
+      if (out->obs_id) out->obs_id[po] = x.id;
+      if (out->obs_score) out->obs_score[po] = x.score;
+      if (out->obs_dc) out->obs_dc[po] = x.dc;
+      if (out->obs_ts) out->obs_ts[po] = x.ts;
+      ++po;
+    }
+    for (const E4& x : msk) {
+      if (out->m_id) out->m_id[pm] = x.id;
+      if (out->m_score) out->m_score[pm] = x.score;
+      if (out->m_dc) out->m_dc[pm] = x.dc;
+      if (out->m_ts) out->m_ts[pm] = x.ts;
+      ++pm;
+    }
+    for (const auto& [id, r] : rows) {
+      if (out->r_id) out->r_id[pr] = id;
+      if (out->r_vc)
+        for (int d = 0; d < D; ++d) out->r_vc[pr * D + d] = h.r_vc[((uint64_t)m.r_off + r) * D + d];
+      ++pr;
+    }
+    if (out->obs_ptr) out->obs_ptr[k + 1] = po;
+    if (out->m_ptr) out->m_ptr[k + 1] = pm;
+    if (out->r_ptr) out->r_ptr[k + 1] = pr;
+    const bool mv = m.minq != NONE32;
+    if (out->min_valid) out->min_valid[k] = mv ? 1 : 0;
+    int64_t mid = 0, msc = 0, mts = 0;
+    uint8_t mdc = 0;
+    if (mv) {
+      const uint32_t o = h.pl_info[m.p_off + m.minq] & 0xFFFFu;
+      const uint64_t g = (uint64_t)m.m_off + o;
+      mid = h.pl_id[m.p_off + m.minq];
+      msc = h.m_score[g];
+      mts = h.m_ts[g];
+      mdc = (uint8_t)((h.m_pd[g] >> 16) & 0xFF);
+    }
+    if (out->min_id) out->min_id[k] = mid;
+    if (out->min_score) out->min_score[k] = msc;
+    if (out->min_ts) out->min_ts[k] = mts;
+    if (out->min_dc) out->min_dc[k] = mdc;
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
+  CCRDT_TRY(check_trmv(e));
+  if (!in || !in->vc || !in->obs_ptr || !in->m_ptr || !in->r_ptr || !in->min_valid) {
+    set_error("trmv_import: missing arrays");
+    return CCRDT_EINVAL;
+  }
+  Engine& E = *e;
+  const uint64_t nk = (uint64_t)E.n_keys;
+  const int D = E.n_dc;
+  HostTrmv h;
+  h.meta.resize(nk);
+  h.vc.assign(in->vc, in->vc + nk * D);
+  for (int64_t v : h.vc)
+    if (v < 0) {
+      set_error("trmv_import: negative Vc entry");
+      return CCRDT_ERANGE;
+    }
+  std::vector<int64_t> ids;
+  for (uint64_t k = 0; k < nk; ++k) {
+    KeyMeta m{};
+    m.p_off = (uint32_t)h.pl_id.size();
+    m.m_off = (uint32_t)h.m_score.size();
+    m.r_off = (uint32_t)(h.r_vc.size() / D);
+    ids.clear();
+    for (uint64_t i = in->m_ptr[k]; i < in->m_ptr[k + 1]; ++i) ids.push_back(in->m_id[i]);
+    for (uint64_t i = in->r_ptr[k]; i < in->r_ptr[k + 1]; ++i) ids.push_back(in->r_id[i]);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const uint64_t nmk = in->m_ptr[k + 1] - in->m_ptr[k], nrk = in->r_ptr[k + 1] - in->r_ptr[k];
+    if (ids.size() > TRMV_MAX_CAP || nmk > TRMV_MAX_CAP || nrk > TRMV_MAX_ROWS) {
+      set_error("trmv_import: key exceeds per-key capacity");
+      return CCRDT_ENOMEM;
+    }
+    auto pidx = [&](int64_t id) {
+      return (uint32_t)(std::lower_bound(ids.begin(), ids.end(), id) - ids.begin());
+    };
+    const uint32_t p0 = m.p_off, m0 = m.m_off;
+    for (int64_t id : ids) {
+      h.pl_id.push_back(id);
+      h.pl_info.push_back(NONE32);
+    }
+    for (uint64_t i = in->m_ptr[k]; i < in->m_ptr[k + 1]; ++i) {
+      if (in->m_dc[i] >= D || in->m_ts[i] < 1) {
+        set_error("trmv_import: Masked element with bad dc or ts < 1");
+        return CCRDT_ERANGE;
+      }
+      h.m_score.push_back(in->m_score[i]);
+      h.m_ts.push_back(in->m_ts[i]);
+      h.m_pd.push_back(pidx(in->m_id[i]) | ((uint32_t)in->m_dc[i] << 16));
+    }
+    for (uint64_t i = in->r_ptr[k]; i < in->r_ptr[k + 1]; ++i) {
+      const uint32_t q = pidx(in->r_id[i]);
+      const uint32_t r = (uint32_t)(i - in->r_ptr[k]);
+      h.pl_info[p0 + q] = (h.pl_info[p0 + q] & 0xFFFFu) | (r << 16);
+      for (int d = 0; d < D; ++d) {
+        const int64_t v = in->r_vc[i * D + d];
+        if (v < 0) {
+          set_error("trmv_import: negative Removals entry");
+          return CCRDT_ERANGE;
+        }
+        h.r_vc.push_back(v);
+      }
+    }
+    uint32_t nobs = 0;
+    for (uint64_t i = in->obs_ptr[k]; i < in->obs_ptr[k + 1]; ++i) {
+      // Observed ⊆ Masked: find the element in the pool
+      uint32_t found = NONE32;
+      for (uint32_t j = 0; j < nmk; ++j) {
+        const uint64_t g = m0 + j;
+        if (h.pl_id[p0 + (h.m_pd[g] & 0xFFFFu)] == in->obs_id[i] && h.m_score[g] == in->obs_score[i] &&
+            h.m_ts[g] == in->obs_ts[i] && ((h.m_pd[g] >> 16) & 0xFF) == in->obs_dc[i]) {
+          found = j;
+          break;
+        }
+      }
+      if (found == NONE32) {
+        set_error("trmv_import: Observed element not in Masked");
+        return CCRDT_EINVAL;
+      }
+      const uint32_t q = pidx(in->obs_id[i]);
+      if ((h.pl_info[p0 + q] & 0xFFFFu) != NONE16) {
+        set_error("trmv_import: duplicate Observed Id");
+        return CCRDT_EINVAL;
+      }
+      h.pl_info[p0 + q] = (h.pl_info[p0 + q] & 0xFFFF0000u) | found;
+      ++nobs;
+    }
+    if ((int64_t)nobs > E.k) {
+      set_error("trmv_import: |Observed| > Size");
+      return CCRDT_EINVAL;
+    }
+    for (uint32_t j = 0; j < nmk; ++j) {
+      const uint32_t q = h.m_pd[m0 + j] & 0xFFFFu;
+      if ((h.pl_info[p0 + q] & 0xFFFFu) != NONE16) h.m_pd[m0 + j] |= PD_INOBS;
+    }
+    m.minq = NONE32;
+    if (in->min_valid[k]) {
+      const uint32_t q = pidx(in->min_id[k]);
+      const uint32_t o = q < ids.size() && ids[q] == in->min_id[k] ? (h.pl_info[p0 + q] & 0xFFFFu) : NONE16;
+      if (o == NONE16 || h.m_score[m0 + o] != in->min_score[k] || h.m_ts[m0 + o] != in->min_ts[k]) {
+        set_error("trmv_import: Min is not an Observed element");
+        return CCRDT_EINVAL;
+      }
+      m.minq = q;
+    } else if (nobs) {
+      set_error("trmv_import: Min is nil but Observed is not empty");
+      return CCRDT_EINVAL;
+    }
+    m.np = (uint32_t)ids.size();
+    m.nm = (uint32_t)nmk;
+    m.nr = (uint32_t)nrk;
+    m.nobs = nobs;
+    h.meta[k] = m;
+  }
+  TrmvBufs& b = E.trmv[E.cur];
+  CCRDT_TRY(b.meta.ensure(nk * sizeof(KeyMeta)));
+  CCRDT_TRY(b.vc.ensure(nk * D * 8));
+  CCRDT_TRY(b.pl_id.ensure(h.pl_id.size() * 8));
+  CCRDT_TRY(b.pl_info.ensure(h.pl_info.size() * 4));
+  CCRDT_TRY(b.m_score.ensure(h.m_score.size() * 8));
+  CCRDT_TRY(b.m_ts.ensure(h.m_ts.size() * 8));
+  CCRDT_TRY(b.m_pd.ensure(h.m_pd.size() * 4));
+  CCRDT_TRY(b.r_vc.ensure(h.r_vc.size() * 8));
+  CCRDT_HIP(hipStreamSynchronize(E.stream));
+  if (nk) {
+    CCRDT_HIP(hipMemcpy(b.meta.p, h.meta.data(), nk * sizeof(KeyMeta), hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.vc.p, h.vc.data(), nk * D * 8, hipMemcpyHostToDevice));
+  }
+  if (!h.pl_id.empty()) {
+    CCRDT_HIP(hipMemcpy(b.pl_id.p, h.pl_id.data(), h.pl_id.size() * 8, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.pl_info.p, h.pl_info.data(), h.pl_info.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (!h.m_score.empty()) {
+    CCRDT_HIP(hipMemcpy(b.m_score.p, h.m_score.data(), h.m_score.size() * 8, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.m_ts.p, h.m_ts.data(), h.m_ts.size() * 8, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.m_pd.p, h.m_pd.data(), h.m_pd.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (!h.r_vc.empty())
+    CCRDT_HIP(hipMemcpy(b.r_vc.p, h.r_vc.data(), h.r_vc.size() * 8, hipMemcpyHostToDevice));
+  E.fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,
+                          const int64_t* id, const int64_t* score, const uint8_t* dc,
+                          const int64_t* ts, uint8_t* out_kind, int64_t* out_vc) {
+  CCRDT_TRY(check_trmv(e));
+  if (n < 0 || (n > 0 && (!key || !op || !id || !score || !dc || !ts || !out_kind))) {
+    set_error("trmv_downstream: null arrays");
+    return CCRDT_EINVAL;
+  }
+  Engine& E = *e;
+  const int D = E.n_dc;
+  for (int64_t i = 0; i < n; ++i) {
+    if (key[i] >= (uint64_t)E.n_keys || op[i] > 1 || (op[i] == 0 && (dc[i] >= D || ts[i] < 1))) {
+      set_error("trmv_downstream: bad request (key, op, dc or ts)");
+      return CCRDT_EINVAL;
+    }
+  }
+  if (n == 0) return CCRDT_OK;
+  const uint64_t un = (uint64_t)n;
+  CCRDT_TRY(E.st_kp.ensure(un * 8));
+  CCRDT_TRY(E.st_kind.ensure(un));
+  CCRDT_TRY(E.st_id.ensure(un * 8));
+  CCRDT_TRY(E.st_score.ensure(un * 8));
+  CCRDT_TRY(E.st_dc.ensure(un));
+  CCRDT_TRY(E.st_ts.ensure(un * 8));
+  CCRDT_TRY(E.st_out_kind.ensure(un));
+  CCRDT_TRY(E.st_out_vc.ensure(un * D * 8));
+  CCRDT_HIP(hipMemcpyAsync(E.st_kp.p, key, un * 8, hipMemcpyHostToDevice, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.st_kind.p, op, un, hipMemcpyHostToDevice, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.st_id.p, id, un * 8, hipMemcpyHostToDevice, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.st_score.p, score, un * 8, hipMemcpyHostToDevice, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.st_dc.p, dc, un, hipMemcpyHostToDevice, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.st_ts.p, ts, un * 8, hipMemcpyHostToDevice, E.stream));
+  TrmvDownArgs a{};
+  a.n = n;
+  a.n_dc = D;
+  a.k = (uint32_t)std::min<int64_t>(E.k, 0xFFFFFFFFll);
+  a.key = E.st_kp.as<uint64_t>();
+  a.op = E.st_kind.as<uint8_t>();
+  a.id = E.st_id.as<int64_t>();
+  a.score = E.st_score.as<int64_t>();
+  a.dc = E.st_dc.as<uint8_t>();
+  a.ts = E.st_ts.as<int64_t>();
+  a.out_kind = E.st_out_kind.as<uint8_t>();
+  a.out_vc = E.st_out_vc.as<int64_t>();
+  a.s = E.trmv_side(E.cur);
+  a.fresh = E.fresh ? 1 : 0;
+  CCRDT_TRY(trmv_launch_downstream(a, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(out_kind, E.st_out_kind.p, un, hipMemcpyDeviceToHost, E.stream));
+  if (out_vc)
+    CCRDT_HIP(hipMemcpyAsync(out_vc, E.st_out_vc.p, un * D * 8, hipMemcpyDeviceToHost, E.stream));
+  CCRDT_HIP(hipStreamSynchronize(E.stream));
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_clone(const ccrdt_engine* src, ccrdt_engine** out) {
+  if (!src || !out) return CCRDT_EINVAL;
+  ccrdt_engine* e = nullptr;
+  CCRDT_TRY(ccrdt_engine_create(src->type, src->k, src->n_keys, src->n_dc, src->device, &e));
+  int rc = e->clone_from(*src);
+  if (rc != CCRDT_OK) {
+    ccrdt_engine_destroy(e);
+    return rc;
+  }
+  *out = e;
+  return CCRDT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+// trmv_kernels.hpp — device layout of GPU-resident topk_rmv state and the
+// kernel argument blocks shared by trmv_kernels.hip and engine.cpp.
+//
+// Per key, the reference state {Observed, Masked, Removals, Vc, Min, Size}
+// (src/antidote_ccrdt_topk_rmv.erl:67-74) is held in HBM as variable-length
+// segments addressed through one 32-byte KeyMeta:
+//   players  pl_id[i64], pl_info[u32]   one per distinct Id ever seen by the key
+//            pl_info = obs pool index (low 16, 0xFFFF = not in Observed)
+//                    | removal row (high 16, 0xFFFF = no Removals entry)
+//   pool     m_score[i64], m_ts[i64], m_pd[u32]   the Masked elements
+//            m_pd = owner player (low 16) | dc rank (bits 16..23)
+//                 | INOBS (bit 31: owner currently in Observed)
+//   rows     r_vc[n_dc x i64]           Removals[Id] (0 = DC absent)
+//   vc       vc[n_dc x i64]             replica Vc (0 = DC absent)
+//   meta     offsets + counts + Observed size + Min (a player index)
+// Observed is implicit: Obs[Id] is the pool element pl_info.obs of Id's
+// player (Observed ⊆ Masked), and Min is always Obs[minq].
+#pragma once
+#include <cstdint>
+
+namespace ccrdt {
+
+constexpr uint32_t NONE16 = 0xFFFFu;
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr uint32_t PD_INOBS = 1u << 31;
+constexpr uint32_t PD_ALIVE = 1u << 30;  // in-register only
+constexpr int TRMV_DPAD = 8;             // lanes per removal row (n_dc <= 8)
+
+struct alignas(32) KeyMeta {
+  uint32_t p_off, m_off, r_off;  // segment starts (elements / rows)
+  uint32_t np, nm, nr;           // players, pool elements, removal rows
+  uint32_t nobs;                 // |Observed|
+  uint32_t minq;                 // player index of Min, NONE32 = nil
+};
+static_assert(sizeof(KeyMeta) == 32, "KeyMeta is one 32-byte record");
+
+// One ping-pong side of the resident state.
+struct TrmvSide {
+  KeyMeta* meta;
+  int64_t* pl_id;
+  uint32_t* pl_info;
+  int64_t* m_score;
+  int64_t* m_ts;
+  uint32_t* m_pd;
+  int64_t* r_vc;
+  int64_t* vc;
+};
+
+// Extra effect record, compacted per key inside the key's op range.
+struct alignas(16) TrmvExtraRec {
+  uint32_t op;    // global op index
+  uint8_t kind;   // CCRDT_TRMV_ADD or CCRDT_TRMV_RMV
+  uint8_t dc;
+  uint16_t pad;
+  int64_t id;
+  int64_t score;
+  int64_t ts;
+};
+
+struct TrmvApplyArgs {
+  int64_t n_keys;
+  int32_t n_dc;
+  uint32_t k;  // Size (clamped)
+  // ops (device)
+  const uint64_t* key_ptr;
+  const uint8_t* kind;
+  const int64_t* id;
+  const int64_t* score;
+  const uint8_t* dc;
+  const int64_t* ts;
+  const int64_t* rmv_vc;
+  int64_t n_rmv_rows;
+  // state
+  TrmvSide old_s;  // ignored when fresh
+  TrmvSide new_s;  // new_s.meta offsets precomputed by the scan
+  int32_t fresh;
+  // extra effects
+  uint32_t* ex_cnt;       // [n_keys]
+  TrmvExtraRec* ex;       // [n_ops]
+  int64_t* ex_vc;         // [n_ops * n_dc]
+  // work list (nullptr = all keys) and overflow list
+  const uint32_t* key_list;
+  uint32_t n_list;
+  uint32_t* ovf_list;
+  uint32_t* status;  // [0] overflow count, [1] error flags
+};
+
+enum : uint32_t {
+  TRMV_ERR_KIND = 1u,
+  TRMV_ERR_DC = 2u,
+  TRMV_ERR_TS = 4u,
+  TRMV_ERR_ROW = 8u,
+  TRMV_ERR_VC = 16u,
+};
+
+struct TrmvDownArgs {
+  int64_t n;
+  int32_t n_dc;
+  uint32_t k;
+  const uint64_t* key;
+  const uint8_t* op;
+  const int64_t* id;
+  const int64_t* score;
+  const uint8_t* dc;
+  const int64_t* ts;
+  uint8_t* out_kind;
+  int64_t* out_vc;
+  TrmvSide s;
+  int32_t fresh;
+};
+
+}  // namespace ccrdt

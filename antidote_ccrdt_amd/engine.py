@@ -1,0 +1,321 @@
+"""Batch engines over libccrdt (one per CCRDT type), numpy in / numpy out.
+
+An engine holds ``n_keys`` CCRDT objects resident in HBM and applies whole
+batches of effect ops -- the reference's ``Mod:update(Effect, State)``
+(src/antidote_ccrdt.erl:50) for every op of the batch -- with one pass of the
+gfx950 kernels.  Ops are grouped CSR-by-key in stream order
+(``key_ptr[k]:key_ptr[k+1]`` are key ``k``'s ops).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, fields
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ------------------------------------------------------------------ topk_rmv
+@dataclass
+class TrmvBatch:
+    """A topk_rmv effect batch (layout of ccrdt_trmv_ops)."""
+    key_ptr: np.ndarray  # uint64 [n_keys+1]
+    kind: np.ndarray     # uint8  [n_ops]  0 add 1 add_r 2 rmv 3 rmv_r
+    id: np.ndarray       # int64
+    score: np.ndarray    # int64
+    dc: np.ndarray       # uint8
+    ts: np.ndarray       # int64 (rmv: row of rmv_vc)
+    rmv_vc: np.ndarray   # int64 [n_rmv, n_dc]
+
+    @property
+    def n_ops(self) -> int:
+        return int(self.kind.shape[0])
+
+    @property
+    def n_keys(self) -> int:
+        return int(self.key_ptr.shape[0]) - 1
+
+    def normalized(self) -> "TrmvBatch":
+        return TrmvBatch(_c(self.key_ptr, np.uint64), _c(self.kind, np.uint8), _c(self.id, np.int64),
+                         _c(self.score, np.int64), _c(self.dc, np.uint8), _c(self.ts, np.int64),
+                         _c(self.rmv_vc, np.int64))
+
+    def nbytes(self) -> int:
+        return sum(getattr(self, f.name).nbytes for f in fields(self))
+
+
+@dataclass
+class TrmvExtra:
+    """Extra effects of a batch, indexed by op (kind 255 = none)."""
+    kind: np.ndarray
+    id: np.ndarray
+    score: np.ndarray
+    dc: np.ndarray
+    ts: np.ndarray
+    vc: np.ndarray  # [n_ops, n_dc]
+
+
+@dataclass
+class TrmvState:
+    """Canonical state image (layout of ccrdt_trmv_state)."""
+    vc: np.ndarray
+    obs_ptr: np.ndarray
+    obs_id: np.ndarray
+    obs_score: np.ndarray
+    obs_dc: np.ndarray
+    obs_ts: np.ndarray
+    m_ptr: np.ndarray
+    m_id: np.ndarray
+    m_score: np.ndarray
+    m_dc: np.ndarray
+    m_ts: np.ndarray
+    r_ptr: np.ndarray
+    r_id: np.ndarray
+    r_vc: np.ndarray
+    min_valid: np.ndarray
+    min_id: np.ndarray
+    min_score: np.ndarray
+    min_dc: np.ndarray
+    min_ts: np.ndarray
+
+    @staticmethod
+    def empty(n_keys: int, n_dc: int, n_obs: int, n_masked: int, n_rows: int) -> "TrmvState":
+        z = np.zeros
+        return TrmvState(
+            vc=z((n_keys, n_dc), np.int64), obs_ptr=z(n_keys + 1, np.uint64),
+            obs_id=z(n_obs, np.int64), obs_score=z(n_obs, np.int64), obs_dc=z(n_obs, np.uint8),
+            obs_ts=z(n_obs, np.int64), m_ptr=z(n_keys + 1, np.uint64), m_id=z(n_masked, np.int64),
+            m_score=z(n_masked, np.int64), m_dc=z(n_masked, np.uint8), m_ts=z(n_masked, np.int64),
+            r_ptr=z(n_keys + 1, np.uint64), r_id=z(n_rows, np.int64),
+            r_vc=z((n_rows, n_dc), np.int64), min_valid=z(n_keys, np.uint8),
+            min_id=z(n_keys, np.int64), min_score=z(n_keys, np.int64), min_dc=z(n_keys, np.uint8),
+            min_ts=z(n_keys, np.int64))
+
+    def as_c(self) -> _lib.TrmvState:
+        s = _lib.TrmvState()
+        for f in fields(self):
+            setattr(s, f.name, ptr(getattr(self, f.name)))
+        return s
+
+    def diff(self, other: "TrmvState") -> list[str]:
+        """Names of fields that differ (bit-exact comparison)."""
+        return [f.name for f in fields(self)
+                if not np.array_equal(getattr(self, f.name), getattr(other, f.name))]
+
+    def key_state(self, k: int) -> dict:
+        """One key as plain Python (for debugging and the behaviour mirror)."""
+        o0, o1 = int(self.obs_ptr[k]), int(self.obs_ptr[k + 1])
+        m0, m1 = int(self.m_ptr[k]), int(self.m_ptr[k + 1])
+        r0, r1 = int(self.r_ptr[k]), int(self.r_ptr[k + 1])
+        return {
+            "obs": [(int(self.obs_id[i]), int(self.obs_score[i]), int(self.obs_dc[i]),
+                     int(self.obs_ts[i])) for i in range(o0, o1)],
+            "masked": [(int(self.m_id[i]), int(self.m_score[i]), int(self.m_dc[i]),
+                        int(self.m_ts[i])) for i in range(m0, m1)],
+            "removals": [(int(self.r_id[i]), [int(x) for x in self.r_vc[i]]) for i in range(r0, r1)],
+            "vc": [int(x) for x in self.vc[k]],
+            "min": ((int(self.min_id[k]), int(self.min_score[k]), int(self.min_dc[k]),
+                     int(self.min_ts[k])) if self.min_valid[k] else None),
+        }
+
+
+class DeviceArray:
+    """A device buffer owned by Python (freed on close / GC)."""
+
+    def __init__(self, host: np.ndarray):
+        self.nbytes = int(host.nbytes)
+        p = C.c_void_p()
+        check(lib.ccrdt_device_alloc(C.byref(p), max(self.nbytes, 1)), "device_alloc")
+        self.p = p.value
+        if self.nbytes:
+            check(lib.ccrdt_memcpy_h2d(self.p, ptr(np.ascontiguousarray(host)), self.nbytes), "h2d")
+
+    def close(self):
+        if self.p:
+            lib.ccrdt_device_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceTrmvBatch:
+    """A TrmvBatch resident in HBM (for ccrdt_trmv_apply_device)."""
+
+    def __init__(self, b: TrmvBatch):
+        b = b.normalized()
+        self.n_ops = b.n_ops
+        self.n_rmv = int(b.rmv_vc.shape[0])
+        self.bufs = {f.name: DeviceArray(getattr(b, f.name)) for f in fields(b)}
+        self.c = _lib.TrmvOps(self.n_ops, self.n_rmv, *[self.bufs[n].p for n in
+                                                        ("key_ptr", "kind", "id", "score", "dc",
+                                                         "ts", "rmv_vc")])
+
+    def close(self):
+        for d in self.bufs.values():
+            d.close()
+
+
+class _Engine:
+    TYPE = -1
+
+    def __init__(self, n_keys: int, k: int = 100, n_dc: int = 1, device: int = 0):
+        self.n_keys, self.k, self.n_dc, self.device = int(n_keys), int(k), int(n_dc), int(device)
+        h = C.c_void_p()
+        check(lib.ccrdt_engine_create(self.TYPE, self.k, self.n_keys, self.n_dc, self.device,
+                                      C.byref(h)), "engine_create")
+        self.h = h.value
+
+    @classmethod
+    def _wrap(cls, h, n_keys, k, n_dc, device):
+        e = cls.__new__(cls)
+        e.n_keys, e.k, e.n_dc, e.device, e.h = n_keys, k, n_dc, device, h
+        return e
+
+    def clone(self):
+        h = C.c_void_p()
+        check(lib.ccrdt_engine_clone(self.h, C.byref(h)), "engine_clone")
+        return type(self)._wrap(h.value, self.n_keys, self.k, self.n_dc, self.device)
+
+    def reset(self):
+        check(lib.ccrdt_engine_reset(self.h), "engine_reset")
+
+    def sync(self):
+        check(lib.ccrdt_engine_sync(self.h), "engine_sync")
+
+    def timer_start(self):
+        check(lib.ccrdt_timer_start(self.h), "timer_start")
+
+    def timer_stop(self) -> float:
+        ms = C.c_float()
+        check(lib.ccrdt_timer_stop(self.h, C.byref(ms)), "timer_stop")
+        return float(ms.value)
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        check(lib.ccrdt_engine_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
+        return float(ms.value)
+
+    def overflow_keys(self, slot_class: int) -> int:
+        n = C.c_int64()
+        check(lib.ccrdt_engine_overflow_keys(self.h, slot_class, C.byref(n)), "overflow_keys")
+        return int(n.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.ccrdt_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TopkRmvEngine(_Engine):
+    """antidote_ccrdt_topk_rmv over n_keys keys (src/antidote_ccrdt_topk_rmv.erl)."""
+    TYPE = _lib.TOPK_RMV
+
+    def __init__(self, n_keys: int, k: int = 100, n_dc: int = 8, device: int = 0):
+        super().__init__(n_keys, k, n_dc, device)
+
+    def _ops(self, b: TrmvBatch) -> _lib.TrmvOps:
+        return _lib.TrmvOps(b.n_ops, int(b.rmv_vc.shape[0]), ptr(b.key_ptr), ptr(b.kind),
+                            ptr(b.id), ptr(b.score), ptr(b.dc), ptr(b.ts), ptr(b.rmv_vc))
+
+    def apply(self, batch: TrmvBatch, want_extra: bool = True) -> TrmvExtra | None:
+        """update/2 for every op of the batch (topk_rmv.erl:140-148)."""
+        b = batch.normalized()
+        if b.n_keys != self.n_keys:
+            raise ValueError("batch key_ptr must have n_keys+1 entries")
+        if b.rmv_vc.ndim != 2 or (b.rmv_vc.shape[0] and b.rmv_vc.shape[1] != self.n_dc):
+            raise ValueError("rmv_vc must be [n_rmv, n_dc]")
+        ops = self._ops(b)
+        if not want_extra:
+            check(lib.ccrdt_trmv_apply(self.h, C.byref(ops), None), "trmv_apply")
+            return None
+        n = b.n_ops
+        x = TrmvExtra(np.empty(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64),
+                      np.zeros(n, np.uint8), np.zeros(n, np.int64), np.zeros((n, self.n_dc), np.int64))
+        cx = _lib.TrmvExtra(ptr(x.kind), ptr(x.id), ptr(x.score), ptr(x.dc), ptr(x.ts), ptr(x.vc))
+        check(lib.ccrdt_trmv_apply(self.h, C.byref(ops), C.byref(cx)), "trmv_apply")
+        return x
+
+    def apply_device(self, db: DeviceTrmvBatch) -> None:
+        check(lib.ccrdt_trmv_apply_device(self.h, C.byref(db.c)), "trmv_apply_device")
+
+    def extra_count(self) -> int:
+        n = C.c_int64()
+        check(lib.ccrdt_trmv_extra_count(self.h, C.byref(n)), "trmv_extra_count")
+        return int(n.value)
+
+    def sizes(self) -> tuple[int, int, int]:
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        check(lib.ccrdt_trmv_state_sizes(self.h, C.byref(a), C.byref(b), C.byref(c)), "sizes")
+        return int(a.value), int(b.value), int(c.value)
+
+    def export(self) -> TrmvState:
+        """Canonical image of every key (to_binary/1 analogue, topk_rmv.erl:156-158)."""
+        n_obs, n_m, n_r = self.sizes()
+        st = TrmvState.empty(self.n_keys, self.n_dc, n_obs, n_m, n_r)
+        cs = st.as_c()
+        check(lib.ccrdt_trmv_export(self.h, C.byref(cs)), "trmv_export")
+        return st
+
+    def import_state(self, st: TrmvState) -> None:
+        """from_binary/1 analogue (topk_rmv.erl:161-163)."""
+        cs = st.as_c()
+        check(lib.ccrdt_trmv_import(self.h, C.byref(cs)), "trmv_import")
+
+    def downstream(self, key, op, id, score, dc, ts):
+        """downstream/2 probes (topk_rmv.erl:102-124).  op 0 add, 1 rmv.
+
+        Returns (kind[n] uint8, vc[n, n_dc]) -- vc is the replica Vc shipped
+        with rmv effects."""
+        key = _c(key, np.uint64)
+        n = key.shape[0]
+        op, id, score = _c(op, np.uint8), _c(id, np.int64), _c(score, np.int64)
+        dc, ts = _c(dc, np.uint8), _c(ts, np.int64)
+        out = np.empty(n, np.uint8)
+        vc = np.zeros((n, self.n_dc), np.int64)
+        check(lib.ccrdt_trmv_downstream(self.h, n, ptr(key), ptr(op), ptr(id), ptr(score), ptr(dc),
+                                        ptr(ts), ptr(out), ptr(vc)), "trmv_downstream")
+        return out, vc
+
+
+def gen_trmv(n_ops: int, n_keys: int, n_dc: int = 8, n_players: int = 256,
+             score_max: int = 10**6, rmv_pm: int = 100, lag_max: int = 64, dup_pm: int = 0,
+             swap_pm: int = 0, seed: int = 0xCC0DE + 2) -> TrmvBatch:
+    """Seeded synthetic topk_rmv stream, CSR by key (include/ccrdt_gen.h)."""
+    n_rmv = int(lib.ccrdt_gen_trmv_count(n_ops, seed, rmv_pm))
+    b = TrmvBatch(np.empty(n_keys + 1, np.uint64), np.empty(n_ops, np.uint8),
+                  np.empty(n_ops, np.int64), np.empty(n_ops, np.int64), np.empty(n_ops, np.uint8),
+                  np.empty(n_ops, np.int64), np.empty((n_rmv, n_dc), np.int64))
+    check(lib.ccrdt_gen_trmv(n_ops, n_keys, n_dc, n_players, score_max, rmv_pm, lag_max, dup_pm,
+                             swap_pm, seed, ptr(b.key_ptr), ptr(b.kind), ptr(b.id), ptr(b.score),
+                             ptr(b.dc), ptr(b.ts), ptr(b.rmv_vc)), "gen_trmv")
+    return b
+
+
+def trmv_algorithmic_bytes(batch: TrmvBatch, st_sizes: tuple[int, int, int], n_keys: int,
+                           n_extra: int, n_dc: int = 8) -> int:
+    """Algorithmic HBM bytes of one apply: op bytes (add 26 B,
+    rmv 9 + 8*n_dc B) + final state (masked elems x 25 B, |Obs| x 2 B index,
+    removal rows x (8 + 8*n_dc) B, Vc 8*n_dc B + 16 B meta per key) + extra
+    effects (32 B each)."""
+    n_rmv = int(np.count_nonzero(batch.kind >= 2))
+    n_add = batch.n_ops - n_rmv
+    n_obs, n_m, n_r = st_sizes
+    ops = n_add * 26 + n_rmv * (9 + 8 * n_dc)
+    state = n_m * 25 + n_obs * 2 + n_r * (8 + 8 * n_dc) + n_keys * (8 * n_dc + 16)
+    return ops + state + n_extra * 32

@@ -1,0 +1,203 @@
+/* ccrdt.h — C-ABI of libccrdt, the MI355X batch engine for antidote_ccrdt.
+ *
+ * The reference is a pure-Erlang behaviour (src/antidote_ccrdt.erl:47-59):
+ * every CCRDT module exports new/0, value/1, downstream/2, update/2, equal/2,
+ * to_binary/1, from_binary/1, is_operation/1, is_replicate_tagged/1,
+ * can_compact/2, compact_ops/2 and require_state_downstream/1.  Antidote
+ * calls Mod:update(Effect, State) once per effect per replica.  This ABI is
+ * what a NIF shim over that behaviour would bind: the host
+ * batches effects per key (CSR by key, stream order inside a key) and one
+ * call applies the whole batch on the GPU, with every key's state resident in
+ * HBM.  Each entry point below names the reference function(s) it replaces.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  `host` pointers are read/written
+ *    synchronously by the call; `_device` variants take device pointers and
+ *    enqueue on the engine stream without synchronising.
+ *  - Integers are int64 (Erlang integers are unbounded): values
+ *    outside the engine's range are rejected with CCRDT_ERANGE so the caller
+ *    can keep that key on its BEAM path.
+ *  - DC ids are ranks 0..n_dc-1 that preserve Erlang term order between the
+ *    DcIds.  Vector clocks are dense [n_dc] int64 rows where 0
+ *    means "no entry" (vc_get_timestamp/2 default, topk_rmv.erl:350-355), so
+ *    every stored timestamp must be >= 1.
+ *  - Return codes are CCRDT_* below; ccrdt_last_error() gives a message for
+ *    the calling thread.  Invalid ops (the reference crashes with
+ *    function_clause, e.g. topk_rmv.erl:141-148) give CCRDT_EINVAL and leave
+ *    the engine state unchanged.
+ *  - Threading: one engine per GPU; calls on one engine must be serialised by
+ *    the caller (a NIF would run them on a dirty scheduler).
+ */
+#ifndef CCRDT_H
+#define CCRDT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCRDT_OK 0
+#define CCRDT_EINVAL 1  /* malformed op / argument: reference would crash */
+#define CCRDT_ERANGE 2  /* integer outside engine range (Q17) */
+#define CCRDT_ENOMEM 3  /* device or per-key capacity exhausted */
+#define CCRDT_EDEVICE 4 /* HIP / RCCL failure */
+#define CCRDT_ENOSYS 5  /* operation not supported for this type */
+
+/* Registry: antidote_ccrdt:?CCRDTS (src/antidote_ccrdt.erl:28-35). */
+#define CCRDT_AVERAGE 0
+#define CCRDT_TOPK 1
+#define CCRDT_TOPK_RMV 2
+#define CCRDT_LEADERBOARD 3
+#define CCRDT_WORDCOUNT 4
+#define CCRDT_WORDDOCUMENTCOUNT 5
+
+/* Effect kinds of topk_rmv (topk_rmv.erl:77-78) — also extra-effect kinds. */
+#define CCRDT_TRMV_ADD 0
+#define CCRDT_TRMV_ADD_R 1
+#define CCRDT_TRMV_RMV 2
+#define CCRDT_TRMV_RMV_R 3
+#define CCRDT_NOOP 255 /* downstream result `noop` / "no extra effect" */
+
+/* Per-key capacity of the register-resident topk_rmv apply kernel. */
+#define CCRDT_TRMV_MAX_DC 8
+
+typedef struct ccrdt_engine ccrdt_engine;
+
+/* ---------------------------------------------------------------- engine */
+
+/* antidote_ccrdt:is_type/1 (src/antidote_ccrdt.erl:61-62) */
+int ccrdt_is_type(int type);
+/* antidote_ccrdt:generates_extra_operations/1 (src/antidote_ccrdt.erl:64-65) */
+int ccrdt_generates_extra_operations(int type);
+
+/* Create an engine holding `n_keys` CCRDT objects of `type`, each equal to
+ * Mod:new(k) (topk_rmv.erl:86-88, leaderboard.erl:79-81, topk.erl:70-71;
+ * average.erl:56-57 and wordcount.erl:44-45 ignore k), on HIP device
+ * `device`.  n_dc is the number of DCs (topk_rmv only, <= CCRDT_TRMV_MAX_DC). */
+int ccrdt_engine_create(int type, int64_t k, int64_t n_keys, int n_dc, int device,
+                        ccrdt_engine** out);
+int ccrdt_engine_destroy(ccrdt_engine* e);
+/* Every key back to Mod:new(k).  O(1): marks the resident state empty. */
+int ccrdt_engine_reset(ccrdt_engine* e);
+/* Deep copy (used for the functional update/2 of the behaviour mirror). */
+int ccrdt_engine_clone(const ccrdt_engine* src, ccrdt_engine** out);
+int ccrdt_engine_sync(ccrdt_engine* e);
+/* hipStream_t the engine enqueues on (for event timing by callers). */
+void* ccrdt_engine_stream(ccrdt_engine* e);
+const char* ccrdt_strerror(int code);
+const char* ccrdt_last_error(void);
+
+/* Device memory helpers so callers need no HIP headers. */
+int ccrdt_device_count(int* n);
+int ccrdt_set_device(int device);
+int ccrdt_device_alloc(void** p, uint64_t bytes);
+int ccrdt_device_free(void* p);
+int ccrdt_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
+int ccrdt_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+int ccrdt_device_synchronize(void);
+
+/* Duration (HIP events on the engine stream) of the apply kernel launches of
+ * the last batch (all register classes) — the dominant kernel whose roofline
+ * bench.py reports. */
+int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms);
+/* Keys that overflowed register class `slot_class` (2,4,8,16) in the last
+ * topk_rmv batch and were re-run in the next class. */
+int ccrdt_engine_overflow_keys(ccrdt_engine* e, int slot_class, int64_t* n);
+
+/* Event timing on the engine stream (for bench.py; HIP events). */
+int ccrdt_timer_start(ccrdt_engine* e);
+/* Milliseconds since ccrdt_timer_start, synchronising the stream. */
+int ccrdt_timer_stop(ccrdt_engine* e, float* ms);
+
+/* --------------------------------------------------------------- topk_rmv */
+
+/* A batch of topk_rmv effects, CSR by key, stream order inside each key.
+ * op i belongs to key k iff key_ptr[k] <= i < key_ptr[k+1].
+ *   kind[i]  CCRDT_TRMV_ADD / _ADD_R  -> add/4   (topk_rmv.erl:141-144,231-249)
+ *            CCRDT_TRMV_RMV / _RMV_R  -> rmv/3   (topk_rmv.erl:145-148,252-298)
+ *   add:  id, score, dc (rank), ts (>= 1)        = {Id, Score, {DcId, Ts}}
+ *   rmv:  id, and ts[i] = row r of rmv_vc: VcRmv = rmv_vc[r*n_dc .. +n_dc)
+ *         (0 = DC absent from the Erlang map); score/dc ignored. */
+typedef struct {
+  int64_t n_ops;
+  int64_t n_rmv_rows;
+  const uint64_t* key_ptr; /* [n_keys+1] */
+  const uint8_t* kind;     /* [n_ops] */
+  const int64_t* id;       /* [n_ops] */
+  const int64_t* score;    /* [n_ops] */
+  const uint8_t* dc;       /* [n_ops] */
+  const int64_t* ts;       /* [n_ops] */
+  const int64_t* rmv_vc;   /* [n_rmv_rows * n_dc] */
+} ccrdt_trmv_ops;
+
+/* Extra effects ({ok, State, [Effect]}, at most one per op — SURVEY Q3),
+ * indexed by op.  kind[i] = CCRDT_NOOP when op i returned {ok, State}.
+ *   CCRDT_TRMV_ADD -> {add, {Id, Score, {Dc, Ts}}}   promotion (topk_rmv.erl:295)
+ *   CCRDT_TRMV_RMV -> {rmv, {Id, Vc}}, Vc in vc[i*n_dc..] (topk_rmv.erl:237)
+ * Any pointer may be NULL (not wanted). */
+typedef struct {
+  uint8_t* kind;   /* [n_ops] */
+  int64_t* id;     /* [n_ops] */
+  int64_t* score;  /* [n_ops] */
+  uint8_t* dc;     /* [n_ops] */
+  int64_t* ts;     /* [n_ops] */
+  int64_t* vc;     /* [n_ops * n_dc] */
+} ccrdt_trmv_extra;
+
+/* update/2 over a whole batch, host buffers (uploaded by the call). */
+int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extra* extra);
+
+/* update/2 over a batch already resident in HBM (device pointers, n_ops and
+ * key_ptr in HBM too).  Enqueued on the engine stream; extra effects stay on
+ * the device (ccrdt_trmv_extra_count / ccrdt_trmv_fetch_extra). */
+int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* dev_ops);
+/* Number of extra effects produced by the last apply. */
+int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n);
+/* Copy the last apply's extra effects into op-indexed host arrays. */
+int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* extra);
+
+/* Canonical state image (host arrays), used by export/import:
+ *   vc[n_keys*n_dc]                                   replica Vc
+ *   obs_ptr[n_keys+1], obs_{id,score,dc,ts}           Observed, sorted by id
+ *   m_ptr[n_keys+1],  m_{id,score,dc,ts}              Masked elems, sorted by
+ *                                                     (id, score, dc, ts)
+ *   r_ptr[n_keys+1],  r_id, r_vc[*n_dc]               Removals, sorted by id
+ *   min_valid[n_keys], min_{id,score,dc,ts}           Min ({nil,nil,nil} = 0)
+ * (topkrmv() = {Observed, Masked, Removals, Vc, Min, Size}, topk_rmv.erl:67-74) */
+typedef struct {
+  int64_t* vc;
+  uint64_t* obs_ptr;
+  int64_t *obs_id, *obs_score, *obs_ts;
+  uint8_t* obs_dc;
+  uint64_t* m_ptr;
+  int64_t *m_id, *m_score, *m_ts;
+  uint8_t* m_dc;
+  uint64_t* r_ptr;
+  int64_t *r_id, *r_vc;
+  uint8_t* min_valid;
+  int64_t *min_id, *min_score, *min_ts;
+  uint8_t* min_dc;
+} ccrdt_trmv_state;
+
+/* Totals for sizing a ccrdt_trmv_state. */
+int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows);
+/* to_binary/1 analogue (topk_rmv.erl:156-158): canonical image of every key. */
+int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out);
+/* from_binary/1 analogue (topk_rmv.erl:161-163).  Arrays as in export
+ * (sorting not required); invariants of the reference are checked. */
+int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in);
+
+/* downstream/2 (topk_rmv.erl:102-124) for n requests against the current
+ * state (read-only).  op[i] 0 = {add, {Id, Score}}, 1 = {rmv, Id}.  For add,
+ * dc[i]/ts[i] are the origin's DC rank and clock (?DC_META_DATA, ?TIME).
+ * out_kind[i] = CCRDT_TRMV_ADD / _ADD_R / _RMV / _RMV_R / CCRDT_NOOP.  For rmv
+ * the effect's Vc is the key's replica Vc, written to out_vc[i*n_dc..] if
+ * out_vc is not NULL. */
+int ccrdt_trmv_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,
+                          const int64_t* id, const int64_t* score, const uint8_t* dc,
+                          const int64_t* ts, uint8_t* out_kind, int64_t* out_vc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCRDT_H */

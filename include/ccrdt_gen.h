@@ -1,0 +1,27 @@
+/* ccrdt_gen.h — seeded synthetic effect streams for benchmarks and tests
+ * (SURVEY §8d).  Not part of the drop-in boundary: a workload utility that
+ * produces arrays in exactly the layout ccrdt_*_apply expects. */
+#ifndef CCRDT_GEN_H
+#define CCRDT_GEN_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+uint64_t ccrdt_splitmix64(uint64_t x);
+
+/* Number of rmv ops (= rmv_vc rows) ccrdt_gen_trmv will produce. */
+int64_t ccrdt_gen_trmv_count(int64_t n_ops, uint64_t seed, int rmv_pm);
+
+/* topk_rmv effect stream, CSR by key (see gen.cpp for the distribution).
+ * Outputs: key_ptr[n_keys+1], kind/id/score/dc/ts[n_ops],
+ * rmv_vc[ccrdt_gen_trmv_count(...) * n_dc]. */
+int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, int64_t score_max,
+                   int rmv_pm, int lag_max, int dup_pm, int swap_pm, uint64_t seed,
+                   uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score, uint8_t* dc,
+                   int64_t* ts, int64_t* rmv_vc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

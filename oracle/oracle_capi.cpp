@@ -1,0 +1,168 @@
+// oracle_capi.cpp — ctypes-callable C API over ccrdt_oracle.hpp.
+//
+// TEST INFRASTRUCTURE ONLY (parity checker and bench.py cpu_baseline leg).
+// Batch layouts mirror include/ccrdt.h so the same arrays feed both sides.
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ccrdt_oracle.hpp"
+
+using namespace ccrdt_oracle;
+
+namespace {
+struct TrmvSet {
+  std::vector<TopkRmv> keys;
+  int D;
+};
+struct LbSet {
+  std::vector<Leaderboard> keys;
+};
+struct TkSet {
+  std::vector<Topk> keys;
+};
+struct AvgSet {
+  std::vector<Average> keys;
+};
+
+template <class F>
+void parallel_keys(int64_t n_keys, int n_threads, F f) {
+  if (n_threads <= 1 || n_keys < 2) {
+    f(0, n_keys);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t chunk = (n_keys + n_threads - 1) / n_threads;
+  for (int t = 0; t < n_threads; ++t) {
+    const int64_t b = t * chunk, e = std::min<int64_t>(n_keys, b + chunk);
+    if (b >= e) break;
+    th.emplace_back([=] { f(b, e); });
+  }
+  for (auto& x : th) x.join();
+}
+
+Vc dense_to_vc(const int64_t* row, int D) {
+  Vc v;
+  for (int d = 0; d < D; ++d)
+    if (row[d] != 0) v[d] = row[d];
+  return v;
+}
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------- topk_rmv
+void* orc_trmv_create(int64_t n_keys, int64_t k, int n_dc) {
+  auto* s = new TrmvSet();
+  s->keys.assign(n_keys, TopkRmv(k));
+  s->D = n_dc;
+  return s;
+}
+void orc_trmv_destroy(void* h) { delete (TrmvSet*)h; }
+
+// Same op layout as ccrdt_trmv_ops.  Extra effects are op-indexed
+// (ex_kind = 255 for none); any ex_* pointer may be null.
+int orc_trmv_apply(void* h, const uint64_t* key_ptr, const uint8_t* kind, const int64_t* id,
+                   const int64_t* score, const uint8_t* dc, const int64_t* ts,
+                   const int64_t* rmv_vc, int n_threads, uint8_t* ex_kind, int64_t* ex_id,
+                   int64_t* ex_score, uint8_t* ex_dc, int64_t* ex_ts, int64_t* ex_vc) {
+  auto* s = (TrmvSet*)h;
+  const int D = s->D;
+  parallel_keys((int64_t)s->keys.size(), n_threads, [&](int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      TopkRmv& st = s->keys[k];
+      for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i) {
+        RExtra x;
+        if (kind[i] <= 1) x = st.update_add(id[i], score[i], dc[i], ts[i]);
+        else x = st.update_rmv(id[i], dense_to_vc(rmv_vc + ts[i] * D, D));
+        if (ex_kind) ex_kind[i] = x.kind == R_NOOP ? 255 : (uint8_t)x.kind;
+        if (x.kind == R_ADD) {
+          if (ex_id) ex_id[i] = x.elem.id;
+          if (ex_score) ex_score[i] = x.elem.score;
+          if (ex_dc) ex_dc[i] = (uint8_t)x.elem.dc;
+          if (ex_ts) ex_ts[i] = x.elem.ts;
+        } else if (x.kind == R_RMV) {
+          if (ex_id) ex_id[i] = x.id;
+          if (ex_vc)
+            for (int d = 0; d < D; ++d) ex_vc[i * D + d] = vc_get(x.vc, d);
+        }
+      }
+    }
+  });
+  return 0;
+}
+
+void orc_trmv_sizes(void* h, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows) {
+  auto* s = (TrmvSet*)h;
+  int64_t o = 0, m = 0, r = 0;
+  for (auto& st : s->keys) {
+    o += st.obs.size();
+    for (auto& [i, set] : st.masked) m += set.size();
+    r += st.removals.size();
+  }
+  *n_obs = o;
+  *n_masked = m;
+  *n_rows = r;
+}
+
+// Canonical image, same layout as ccrdt_trmv_state.
+void orc_trmv_export(void* h, int64_t* vc, uint64_t* obs_ptr, int64_t* obs_id, int64_t* obs_score,
+                     uint8_t* obs_dc, int64_t* obs_ts, uint64_t* m_ptr, int64_t* m_id,
+                     int64_t* m_score, uint8_t* m_dc, int64_t* m_ts, uint64_t* r_ptr, int64_t* r_id,
+                     int64_t* r_vc, uint8_t* min_valid, int64_t* min_id, int64_t* min_score,
+                     uint8_t* min_dc, int64_t* min_ts) {
+  auto* s = (TrmvSet*)h;
+  const int D = s->D;
+  uint64_t po = 0, pm = 0, pr = 0;
+  obs_ptr[0] = m_ptr[0] = r_ptr[0] = 0;
+  for (size_t k = 0; k < s->keys.size(); ++k) {
+    const TopkRmv& st = s->keys[k];
+    for (int d = 0; d < D; ++d) vc[k * D + d] = vc_get(st.vc, d);
+    for (auto& [i, e] : st.obs) {  // std::map: sorted by id
+      obs_id[po] = e.id;
+      obs_score[po] = e.score;
+      obs_dc[po] = (uint8_t)e.dc;
+      obs_ts[po] = e.ts;
+      ++po;
+    }
+    for (auto& [i, set] : st.masked) {  // by id, then term order inside
+      for (auto& e : set) {
+        m_id[pm] = e.id;
+        m_score[pm] = e.score;
+        m_dc[pm] = (uint8_t)e.dc;
+        m_ts[pm] = e.ts;
+        ++pm;
+      }
+    }
+    for (auto& [i, v] : st.removals) {
+      r_id[pr] = i;
+      for (int d = 0; d < D; ++d) r_vc[pr * D + d] = vc_get(v, d);
+      ++pr;
+    }
+    obs_ptr[k + 1] = po;
+    m_ptr[k + 1] = pm;
+    r_ptr[k + 1] = pr;
+    min_valid[k] = st.min ? 1 : 0;
+    min_id[k] = st.min ? st.min->id : 0;
+    min_score[k] = st.min ? st.min->score : 0;
+    min_dc[k] = st.min ? (uint8_t)st.min->dc : 0;
+    min_ts[k] = st.min ? st.min->ts : 0;
+  }
+}
+
+// downstream/2: op 0 add (dc, ts supplied), 1 rmv.  out_kind: 0 add 1 add_r
+// 2 rmv 3 rmv_r 255 noop.
+void orc_trmv_downstream(void* h, int64_t n, const uint64_t* key, const uint8_t* op,
+                         const int64_t* id, const int64_t* score, const uint8_t* dc,
+                         const int64_t* ts, uint8_t* out_kind) {
+  auto* s = (TrmvSet*)h;
+  for (int64_t i = 0; i < n; ++i) {
+    const TopkRmv& st = s->keys[key[i]];
+    int r = op[i] == 0 ? st.downstream_add(id[i], score[i], dc[i], ts[i]) : st.downstream_rmv(id[i]);
+    out_kind[i] = r == R_NOOP ? 255 : (uint8_t)r;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,158 @@
+"""topk_rmv on the GPU vs the oracle: bit-exact state, extra effects and
+downstream results (all through the C-ABI)."""
+import numpy as np
+import pytest
+
+import oracle as orc
+from antidote_ccrdt_amd import _lib
+from antidote_ccrdt_amd.engine import TopkRmvEngine, TrmvState, gen_trmv
+from trmv_helpers import effects_to_batch, extra_term, load, run_fixture, state_key
+
+pytestmark = pytest.mark.gpu
+
+
+class EngineBackend:
+    def apply(self, size, n_dc, effects):
+        e = TopkRmvEngine(1, size, n_dc)
+        x = e.apply(effects_to_batch(effects, n_dc))
+        return state_key(e.export(), 0, n_dc), extra_term(x, len(effects) - 1, n_dc)
+
+    def downstream(self, size, n_dc, effects, op, id, score, dc, ts):
+        e = TopkRmvEngine(1, size, n_dc)
+        if effects:
+            e.apply(effects_to_batch(effects, n_dc), want_extra=False)
+        kind, vc = e.downstream([0], [op], [id], [score], [dc], [ts])
+        return int(kind[0]), vc[0]
+
+
+FIXTURES = load("topk_rmv")
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_golden(gpu, fx):
+    run_fixture(fx, EngineBackend())
+
+
+def _compare(eng, orac, batch, n_dc, x_eng=None, x_orc=None):
+    se = eng.export()
+    so = TrmvState(**orac.export())
+    bad = se.diff(so)
+    assert not bad, f"state fields differ: {bad}"
+    if x_eng is not None:
+        for f in ("kind", "id", "score", "dc", "ts", "vc"):
+            a, b = getattr(x_eng, f), x_orc[f]
+            if f != "kind":
+                m = x_orc["kind"] != 255
+                if f in ("score", "dc", "ts"):
+                    m = x_orc["kind"] == 0
+                if f == "vc":
+                    m = x_orc["kind"] == 2
+                a, b = a[m], b[m]
+            assert np.array_equal(a, b), f"extra field {f} differs"
+
+
+CONFIGS = [
+    # n_ops, n_keys, n_dc, n_players, score_max, rmv_pm, lag, dup_pm, swap_pm, K
+    (20000, 300, 8, 256, 10**6, 100, 64, 0, 0, 100),     # headline shape, small
+    (20000, 200, 8, 12, 20, 150, 8, 50, 30, 4),          # ties, evictions, promotions
+    (20000, 100, 3, 40, 5, 250, 4, 100, 50, 7),          # heavy churn, many dups/swaps
+    (5000, 50, 1, 5, 3, 300, 2, 80, 80, 1),              # K=1
+    (30000, 30, 8, 600, 10**6, 30, 64, 0, 0, 100),       # big keys -> slot-class escalation
+    (3000, 4000, 8, 256, 10**6, 100, 64, 0, 0, 100),     # many empty keys
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[f"cfg{i}" for i in range(len(CONFIGS))])
+def test_random_streams(gpu, cfg):
+    n_ops, nk, D, npl, smax, rmv, lag, dup, swp, K = cfg
+    b = gen_trmv(n_ops, nk, D, npl, smax, rmv, lag, dup, swp, seed=1234 + n_ops + nk)
+    eng = TopkRmvEngine(nk, K, D)
+    orac = orc.TrmvOracle(nk, K, D)
+    xe = eng.apply(b)
+    xo = orac.apply(b)
+    _compare(eng, orac, b, D, xe, xo)
+
+
+def test_multi_batch_and_import(gpu):
+    """State carried across batches; export -> import -> continue."""
+    nk, D, K = 150, 4, 5
+    eng = TopkRmvEngine(nk, K, D)
+    orac = orc.TrmvOracle(nk, K, D)
+    for i in range(4):
+        b = gen_trmv(4000, nk, D, 20, 50, 120, 8, 30, 20, seed=77 + i)
+        # clocks restart per generated batch: shift ts so they keep growing
+        add = b.kind < 2
+        b.ts[add] += i * 10**6
+        b.rmv_vc[b.rmv_vc > 0] += i * 10**6
+        xe, xo = eng.apply(b), orac.apply(b)
+        _compare(eng, orac, b, D, xe, xo)
+    st = eng.export()
+    e2 = TopkRmvEngine(nk, K, D)
+    e2.import_state(st)
+    assert not e2.export().diff(st)
+    b = gen_trmv(4000, nk, D, 20, 50, 120, 8, 30, 20, seed=99)
+    b.ts[b.kind < 2] += 10**7
+    b.rmv_vc[b.rmv_vc > 0] += 10**7
+    xe, xo = e2.apply(b), orac.apply(b)
+    _compare(e2, orac, b, D, xe, xo)
+    c = e2.clone()
+    assert not c.export().diff(e2.export())
+
+
+def test_downstream_batch(gpu):
+    nk, D, K = 200, 8, 6
+    b = gen_trmv(20000, nk, D, 30, 100, 100, 16, 0, 0, seed=5)
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    eng.apply(b, want_extra=False)
+    orac.apply(b, want_extra=False)
+    rng = np.random.default_rng(0)
+    n = 5000
+    key = rng.integers(0, nk, n).astype(np.uint64)
+    op = rng.integers(0, 2, n).astype(np.uint8)
+    pid = rng.integers(0, 35, n)
+    sc = rng.integers(1, 101, n)
+    dc = rng.integers(0, D, n).astype(np.uint8)
+    ts = rng.integers(1, 10**7, n)
+    ke, vce = eng.downstream(key, op, pid, sc, dc, ts)
+    ko = orac.downstream(key, op, pid, sc, dc, ts)
+    assert np.array_equal(ke, ko)
+    vc = orac.export()["vc"]
+    rm = op == 1
+    assert np.array_equal(vce[rm], vc[key[rm].astype(np.int64)])
+
+
+def test_invalid_ops_leave_state(gpu):
+    nk, D = 10, 2
+    eng = TopkRmvEngine(nk, 3, D)
+    b = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=3)
+    eng.apply(b)
+    before = eng.export()
+    bad = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=4)
+    bad.kind[7] = 9
+    with pytest.raises(_lib.CcrdtError) as ei:
+        eng.apply(bad)
+    assert ei.value.code == _lib.EINVAL
+    assert not eng.export().diff(before)
+    bad = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=4)
+    i = int(np.nonzero(bad.kind < 2)[0][0])
+    bad.ts[i] = 0
+    with pytest.raises(_lib.CcrdtError) as ei:
+        eng.apply(bad)
+    assert ei.value.code == _lib.ERANGE
+    assert not eng.export().diff(before)
+
+
+def test_empty_batch_and_reset(gpu):
+    nk, D = 64, 8
+    eng = TopkRmvEngine(nk, 100, D)
+    b = gen_trmv(0, nk, D, seed=1)
+    eng.apply(b)
+    assert eng.sizes() == (0, 0, 0)
+    b = gen_trmv(3000, nk, D, seed=2)
+    eng.apply(b)
+    assert eng.sizes()[1] > 0
+    eng.reset()
+    assert eng.sizes() == (0, 0, 0)
+    orac = orc.TrmvOracle(nk, 100, D)
+    xe, xo = eng.apply(b), orac.apply(b)
+    _compare(eng, orac, b, D, xe, xo)
