@@ -235,7 +235,7 @@ class TopkRmvEngine(_Engine):
 
     def apply(self, batch: TrmvBatch, want_extra: bool = True) -> TrmvExtra | None:
         """update/2 for every op of the batch (topk_rmv.erl:140-148)."""
-        b = batch.normalized()
+        b = TrmvBatch(*(getattr(batch, f.name) for f in fields(TrmvBatch))).normalized()
         if b.n_keys != self.n_keys:
             raise ValueError("batch key_ptr must have n_keys+1 entries")
         if b.rmv_vc.ndim != 2 or (b.rmv_vc.shape[0] and b.rmv_vc.shape[1] != self.n_dc):
