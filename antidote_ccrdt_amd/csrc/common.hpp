@@ -86,6 +86,18 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
+// Exclusive prefix sum over the 64 lanes; `total` = wave sum.
+__device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, uint32_t& total) {
+  const int lane = lane_id();
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = shfl32(inc, lane >= off ? lane - off : lane);
+    if (lane >= off) inc += o;
+  }
+  total = rl32(inc, 63);
+  return inc - v;
+}
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {

@@ -26,6 +26,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
 int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
+int trmv_launch_fast(const TrmvApplyArgs& a, hipStream_t st);
 
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
@@ -43,7 +44,8 @@ TrmvSide ccrdt_engine::trmv_side(int s) const {
   t.pl_info = b.pl_info.as<uint32_t>();
   t.m_score = b.m_score.as<int64_t>();
   t.m_ts = b.m_ts.as<int64_t>();
-  t.m_pd = b.m_pd.as<uint32_t>();
+  t.m_dc = b.m_dc.as<uint8_t>();
+  t.pl_slab = b.pl_slab.as<uint32_t>();
   t.r_vc = b.r_vc.as<int64_t>();
   t.vc = b.vc.as<int64_t>();
   return t;
@@ -56,7 +58,8 @@ void ccrdt_engine::release_all() {
     b.pl_info.release();
     b.m_score.release();
     b.m_ts.release();
-    b.m_pd.release();
+    b.m_dc.release();
+    b.pl_slab.release();
     b.r_vc.release();
     b.vc.release();
   }
@@ -266,14 +269,22 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.new_s = E.trmv_side(out);
   const uint64_t nb = (nk + 1023) / 1024;
   CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t)));
+  CCRDT_TRY(E.status.ensure(64));
+  a.status = E.status.as<uint32_t>();
+  CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
   // 1) capacities -> segment offsets of the new state
   CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
   uint64_t tot[3] = {0, 0, 0};
   if (nk) {
     CCRDT_HIP(hipMemcpyAsync(E.h_status, E.partials.as<uint64_t>() + nb * 3, 3 * sizeof(uint64_t),
                              hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipMemcpyAsync((char*)E.h_status + 32, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
     memcpy(tot, E.h_status, sizeof(tot));
+    if (((uint32_t*)((char*)E.h_status + 32))[1] & TRMV_ERR_SEG) {
+      set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
+      return CCRDT_ENOMEM;
+    }
   }
   if (tot[0] >= 0xFFFFFFFFull || tot[1] >= 0xFFFFFFFFull || tot[2] >= 0xFFFFFFFFull) {
     set_error("trmv_apply: resident state would exceed 2^32 elements");
@@ -282,9 +293,10 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   TrmvBufs& ob = E.trmv[out];
   CCRDT_TRY(ob.pl_id.ensure(tot[0] * 8));
   CCRDT_TRY(ob.pl_info.ensure(tot[0] * 4));
+  CCRDT_TRY(ob.pl_slab.ensure(tot[0] * 4));
   CCRDT_TRY(ob.m_score.ensure(tot[1] * 8));
   CCRDT_TRY(ob.m_ts.ensure(tot[1] * 8));
-  CCRDT_TRY(ob.m_pd.ensure(tot[1] * 4));
+  CCRDT_TRY(ob.m_dc.ensure(tot[1]));
   CCRDT_TRY(ob.r_vc.ensure(tot[2] * 8 * D));
   CCRDT_TRY(ob.vc.ensure(nk * 8 * D));
   a.new_s = E.trmv_side(out);
@@ -295,52 +307,68 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
   CCRDT_TRY(E.ovf_a.ensure(nk * 4));
   CCRDT_TRY(E.ovf_b.ensure(nk * 4));
-  CCRDT_TRY(E.status.ensure(64));
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
-  // 2) apply, escalating overflowed keys to larger register classes
+  // 2) per-player-parallel pass over every key, then the sequential kernel
+  //    (escalating register classes) for the keys it hands back
   DevBuf* work = nullptr;
   uint64_t n_work = nk;
   float kernel_ms = 0.f;
   E.trmv_overflow_keys.clear();
+  auto read_status = [&](uint32_t& n_ovf, uint32_t& err) -> int {
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    n_ovf = ((uint32_t*)E.h_status)[0];
+    err = ((uint32_t*)E.h_status)[1];
+    return CCRDT_OK;
+  };
+  auto fail_err = [&](uint32_t err) -> int {
+    std::string m = "trmv_apply: invalid op in batch:";
+    if (err & TRMV_ERR_KIND) m += " kind>3";
+    if (err & TRMV_ERR_DC) m += " dc>=n_dc";
+    if (err & TRMV_ERR_TS) m += " add ts<1";
+    if (err & TRMV_ERR_ROW) m += " rmv row out of range";
+    if (err & TRMV_ERR_VC) m += " negative VcRmv entry";
+    set_error(m);
+    return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
+               ? CCRDT_ERANGE
+               : CCRDT_EINVAL;
+  };
+  if (nk) {
+    a.key_list = nullptr;
+    a.n_list = (uint32_t)nk;
+    a.ovf_list = E.ovf_a.as<uint32_t>();
+    CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
+    CCRDT_TRY(trmv_launch_fast(a, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
+    uint32_t n_ovf = 0, err = 0;
+    CCRDT_TRY(read_status(n_ovf, err));
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
+    kernel_ms += ms;
+    E.trmv_overflow_keys[0] = n_ovf;
+    if (err) return fail_err(err);
+    work = &E.ovf_a;
+    n_work = n_ovf;
+  }
   for (int cls : TRMV_SLOT_CLASSES) {
+    if (n_work == 0) break;
     DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
-    a.key_list = work ? work->as<uint32_t>() : nullptr;
+    a.key_list = work->as<uint32_t>();
     a.n_list = (uint32_t)n_work;
     a.ovf_list = ovf->as<uint32_t>();
-    a.status = E.status.as<uint32_t>();
     CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
     CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
     CCRDT_TRY(trmv_launch_apply(a, cls, n_work, E.stream));
     CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
-    CCRDT_HIP(hipStreamSynchronize(E.stream));
-    const uint32_t n_ovf = ((uint32_t*)E.h_status)[0];
-    const uint32_t err = ((uint32_t*)E.h_status)[1];
-    if (err) {
-      std::string m = "trmv_apply: invalid op in batch:";
-      if (err & TRMV_ERR_KIND) m += " kind>3";
-      if (err & TRMV_ERR_DC) m += " dc>=n_dc";
-      if (err & TRMV_ERR_TS) m += " add ts<1";
-      if (err & TRMV_ERR_ROW) m += " rmv row out of range";
-      if (err & TRMV_ERR_VC) m += " negative VcRmv entry";
-      set_error(m);
-      return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
-                 ? CCRDT_ERANGE
-                 : CCRDT_EINVAL;
-    }
+    uint32_t n_ovf = 0, err = 0;
+    CCRDT_TRY(read_status(n_ovf, err));
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
+    kernel_ms += ms;
+    if (err) return fail_err(err);
     E.trmv_overflow_keys[cls] = n_ovf;
-    {
-      float ms = 0.f;
-      CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
-      kernel_ms += ms;
-    }
-    if (n_ovf == 0) {
-      work = nullptr;
-      n_work = 0;
-      break;
-    }
     work = ovf;
     n_work = n_ovf;
   }
@@ -464,7 +492,8 @@ namespace {
 struct HostTrmv {
   std::vector<KeyMeta> meta;
   std::vector<int64_t> pl_id, m_score, m_ts, r_vc, vc;
-  std::vector<uint32_t> pl_info, m_pd;
+  std::vector<uint32_t> pl_info, pl_slab;
+  std::vector<uint8_t> m_dc;
 };
 
 int download_trmv(Engine& E, HostTrmv& h) {
@@ -477,26 +506,25 @@ int download_trmv(Engine& E, HostTrmv& h) {
   const TrmvBufs& b = E.trmv[E.cur];
   CCRDT_HIP(hipMemcpy(h.meta.data(), b.meta.p, nk * sizeof(KeyMeta), hipMemcpyDeviceToHost));
   CCRDT_HIP(hipMemcpy(h.vc.data(), b.vc.p, nk * D * 8, hipMemcpyDeviceToHost));
-  uint64_t np = 0, nm = 0, nr = 0;
-  for (const KeyMeta& m : h.meta) {
-    np = std::max<uint64_t>(np, (uint64_t)m.p_off + m.np);
-    nm = std::max<uint64_t>(nm, (uint64_t)m.m_off + m.nm);
-    nr = std::max<uint64_t>(nr, (uint64_t)m.r_off + m.nr);
-  }
+  const uint64_t np = std::min({b.pl_id.bytes / 8, b.pl_info.bytes / 4, b.pl_slab.bytes / 4});
+  const uint64_t nm = std::min({b.m_dc.bytes, b.m_score.bytes / 8, b.m_ts.bytes / 8});
+  const uint64_t nr = b.r_vc.bytes / (8 * D);
   h.pl_id.resize(np);
   h.pl_info.resize(np);
+  h.pl_slab.resize(np);
   h.m_score.resize(nm);
   h.m_ts.resize(nm);
-  h.m_pd.resize(nm);
+  h.m_dc.resize(nm);
   h.r_vc.resize(nr * D);
   if (np) {
     CCRDT_HIP(hipMemcpy(h.pl_id.data(), b.pl_id.p, np * 8, hipMemcpyDeviceToHost));
     CCRDT_HIP(hipMemcpy(h.pl_info.data(), b.pl_info.p, np * 4, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.pl_slab.data(), b.pl_slab.p, np * 4, hipMemcpyDeviceToHost));
   }
   if (nm) {
     CCRDT_HIP(hipMemcpy(h.m_score.data(), b.m_score.p, nm * 8, hipMemcpyDeviceToHost));
     CCRDT_HIP(hipMemcpy(h.m_ts.data(), b.m_ts.p, nm * 8, hipMemcpyDeviceToHost));
-    CCRDT_HIP(hipMemcpy(h.m_pd.data(), b.m_pd.p, nm * 4, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_dc.data(), b.m_dc.p, nm, hipMemcpyDeviceToHost));
   }
   if (nr) CCRDT_HIP(hipMemcpy(h.r_vc.data(), b.r_vc.p, nr * D * 8, hipMemcpyDeviceToHost));
   return CCRDT_OK;
@@ -548,21 +576,26 @@ int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out) {
     obs.clear();
     msk.clear();
     rows.clear();
+    int64_t mid = 0, msc = 0, mts = 0;
+    uint8_t mdc = 0;
     for (uint32_t p = 0; p < m.np; ++p) {
-      const uint32_t info = h.pl_info[m.p_off + p];
-      const int64_t id = h.pl_id[m.p_off + p];
+      const uint64_t pp = (uint64_t)m.p_off + p;
+      const uint32_t info = h.pl_info[pp], slab = h.pl_slab[pp];
+      const int64_t id = h.pl_id[pp];
+      const uint64_t g0 = (uint64_t)m.m_off + (slab & 0xFFFFu);
+      for (uint32_t j = 0; j < (slab >> 16); ++j)
+        msk.push_back({id, h.m_score[g0 + j], h.m_dc[g0 + j], h.m_ts[g0 + j]});
       const uint32_t o = info & 0xFFFFu, r = info >> 16;
       if (o != NONE16) {
-        const uint64_t g = (uint64_t)m.m_off + o;
-        obs.push_back({id, h.m_score[g], (uint8_t)((h.m_pd[g] >> 16) & 0xFF), h.m_ts[g]});
+        obs.push_back({id, h.m_score[g0 + o], h.m_dc[g0 + o], h.m_ts[g0 + o]});
+        if (p == m.minq) {
+          mid = id;
+          msc = h.m_score[g0 + o];
+          mts = h.m_ts[g0 + o];
+          mdc = h.m_dc[g0 + o];
+        }
       }
       if (r != NONE16) rows.push_back({id, r});
-    }
-    for (uint32_t i = 0; i < m.nm; ++i) {
-      const uint64_t g = (uint64_t)m.m_off + i;
-      const uint32_t pd = h.m_pd[g];
-      msk.push_back({h.pl_id[m.p_off + (pd & 0xFFFFu)], h.m_score[g], (uint8_t)((pd >> 16) & 0xFF),
-                     h.m_ts[g]});
     }
     std::sort(obs.begin(), obs.end(), [](const E4& a, const E4& b) { return a.id < b.id; });
     std::sort(msk.begin(), msk.end(), [](const E4& a, const E4& b) {
@@ -594,16 +627,6 @@ int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out) {
     if (out->r_ptr) out->r_ptr[k + 1] = pr;
     const bool mv = m.minq != NONE32;
     if (out->min_valid) out->min_valid[k] = mv ? 1 : 0;
-    int64_t mid = 0, msc = 0, mts = 0;
-    uint8_t mdc = 0;
-    if (mv) {
-      const uint32_t o = h.pl_info[m.p_off + m.minq] & 0xFFFFu;
-      const uint64_t g = (uint64_t)m.m_off + o;
-      mid = h.pl_id[m.p_off + m.minq];
-      msc = h.m_score[g];
-      mts = h.m_ts[g];
-      mdc = (uint8_t)((h.m_pd[g] >> 16) & 0xFF);
-    }
     if (out->min_id) out->min_id[k] = mid;
     if (out->min_score) out->min_score[k] = msc;
     if (out->min_ts) out->min_ts[k] = mts;
@@ -629,7 +652,13 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
       set_error("trmv_import: negative Vc entry");
       return CCRDT_ERANGE;
     }
+  struct E3 {
+    int64_t score;
+    uint8_t dc;
+    int64_t ts;
+  };
   std::vector<int64_t> ids;
+  std::vector<std::vector<E3>> per;
   for (uint64_t k = 0; k < nk; ++k) {
     KeyMeta m{};
     m.p_off = (uint32_t)h.pl_id.size();
@@ -645,27 +674,36 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
       set_error("trmv_import: key exceeds per-key capacity");
       return CCRDT_ENOMEM;
     }
-    auto pidx = [&](int64_t id) {
-      return (uint32_t)(std::lower_bound(ids.begin(), ids.end(), id) - ids.begin());
+    auto pidx = [&](int64_t id) -> uint32_t {
+      auto it = std::lower_bound(ids.begin(), ids.end(), id);
+      return (it != ids.end() && *it == id) ? (uint32_t)(it - ids.begin()) : NONE32;
     };
-    const uint32_t p0 = m.p_off, m0 = m.m_off;
-    for (int64_t id : ids) {
-      h.pl_id.push_back(id);
-      h.pl_info.push_back(NONE32);
-    }
+    per.assign(ids.size(), {});
     for (uint64_t i = in->m_ptr[k]; i < in->m_ptr[k + 1]; ++i) {
       if (in->m_dc[i] >= D || in->m_ts[i] < 1) {
         set_error("trmv_import: Masked element with bad dc or ts < 1");
         return CCRDT_ERANGE;
       }
-      h.m_score.push_back(in->m_score[i]);
-      h.m_ts.push_back(in->m_ts[i]);
-      h.m_pd.push_back(pidx(in->m_id[i]) | ((uint32_t)in->m_dc[i] << 16));
+      per[pidx(in->m_id[i])].push_back({in->m_score[i], in->m_dc[i], in->m_ts[i]});
+    }
+    std::vector<uint32_t> info(ids.size(), NONE32), slab(ids.size(), 0);
+    uint32_t off = 0;
+    for (size_t q = 0; q < ids.size(); ++q) {
+      slab[q] = off | ((uint32_t)per[q].size() << 16);
+      for (const E3& x : per[q]) {
+        h.m_score.push_back(x.score);
+        h.m_dc.push_back(x.dc);
+        h.m_ts.push_back(x.ts);
+      }
+      off += (uint32_t)per[q].size();
     }
     for (uint64_t i = in->r_ptr[k]; i < in->r_ptr[k + 1]; ++i) {
       const uint32_t q = pidx(in->r_id[i]);
-      const uint32_t r = (uint32_t)(i - in->r_ptr[k]);
-      h.pl_info[p0 + q] = (h.pl_info[p0 + q] & 0xFFFFu) | (r << 16);
+      if ((info[q] >> 16) != NONE16) {
+        set_error("trmv_import: duplicate Removals Id");
+        return CCRDT_EINVAL;
+      }
+      info[q] = (info[q] & 0xFFFFu) | ((uint32_t)(i - in->r_ptr[k]) << 16);
       for (int d = 0; d < D; ++d) {
         const int64_t v = in->r_vc[i * D + d];
         if (v < 0) {
@@ -677,41 +715,35 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     }
     uint32_t nobs = 0;
     for (uint64_t i = in->obs_ptr[k]; i < in->obs_ptr[k + 1]; ++i) {
-      // Observed ⊆ Masked: find the element in the pool
+      // Observed ⊆ Masked: find the element in the player's slab
+      const uint32_t q = pidx(in->obs_id[i]);
       uint32_t found = NONE32;
-      for (uint32_t j = 0; j < nmk; ++j) {
-        const uint64_t g = m0 + j;
-        if (h.pl_id[p0 + (h.m_pd[g] & 0xFFFFu)] == in->obs_id[i] && h.m_score[g] == in->obs_score[i] &&
-            h.m_ts[g] == in->obs_ts[i] && ((h.m_pd[g] >> 16) & 0xFF) == in->obs_dc[i]) {
-          found = j;
+      for (size_t j = 0; q != NONE32 && j < per[q].size(); ++j)
+        if (per[q][j].score == in->obs_score[i] && per[q][j].ts == in->obs_ts[i] &&
+            per[q][j].dc == in->obs_dc[i]) {
+          found = (uint32_t)j;
           break;
         }
-      }
       if (found == NONE32) {
         set_error("trmv_import: Observed element not in Masked");
         return CCRDT_EINVAL;
       }
-      const uint32_t q = pidx(in->obs_id[i]);
-      if ((h.pl_info[p0 + q] & 0xFFFFu) != NONE16) {
+      if ((info[q] & 0xFFFFu) != NONE16) {
         set_error("trmv_import: duplicate Observed Id");
         return CCRDT_EINVAL;
       }
-      h.pl_info[p0 + q] = (h.pl_info[p0 + q] & 0xFFFF0000u) | found;
+      info[q] = (info[q] & 0xFFFF0000u) | found;
       ++nobs;
     }
     if ((int64_t)nobs > E.k) {
       set_error("trmv_import: |Observed| > Size");
       return CCRDT_EINVAL;
     }
-    for (uint32_t j = 0; j < nmk; ++j) {
-      const uint32_t q = h.m_pd[m0 + j] & 0xFFFFu;
-      if ((h.pl_info[p0 + q] & 0xFFFFu) != NONE16) h.m_pd[m0 + j] |= PD_INOBS;
-    }
     m.minq = NONE32;
     if (in->min_valid[k]) {
       const uint32_t q = pidx(in->min_id[k]);
-      const uint32_t o = q < ids.size() && ids[q] == in->min_id[k] ? (h.pl_info[p0 + q] & 0xFFFFu) : NONE16;
-      if (o == NONE16 || h.m_score[m0 + o] != in->min_score[k] || h.m_ts[m0 + o] != in->min_ts[k]) {
+      const uint32_t o = q != NONE32 ? (info[q] & 0xFFFFu) : NONE16;
+      if (o == NONE16 || per[q][o].score != in->min_score[k] || per[q][o].ts != in->min_ts[k]) {
         set_error("trmv_import: Min is not an Observed element");
         return CCRDT_EINVAL;
       }
@@ -719,6 +751,11 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     } else if (nobs) {
       set_error("trmv_import: Min is nil but Observed is not empty");
       return CCRDT_EINVAL;
+    }
+    for (size_t q = 0; q < ids.size(); ++q) {
+      h.pl_id.push_back(ids[q]);
+      h.pl_info.push_back(info[q]);
+      h.pl_slab.push_back(slab[q]);
     }
     m.np = (uint32_t)ids.size();
     m.nm = (uint32_t)nmk;
@@ -731,9 +768,10 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   CCRDT_TRY(b.vc.ensure(nk * D * 8));
   CCRDT_TRY(b.pl_id.ensure(h.pl_id.size() * 8));
   CCRDT_TRY(b.pl_info.ensure(h.pl_info.size() * 4));
+  CCRDT_TRY(b.pl_slab.ensure(h.pl_slab.size() * 4));
   CCRDT_TRY(b.m_score.ensure(h.m_score.size() * 8));
   CCRDT_TRY(b.m_ts.ensure(h.m_ts.size() * 8));
-  CCRDT_TRY(b.m_pd.ensure(h.m_pd.size() * 4));
+  CCRDT_TRY(b.m_dc.ensure(h.m_dc.size()));
   CCRDT_TRY(b.r_vc.ensure(h.r_vc.size() * 8));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   if (nk) {
@@ -743,11 +781,12 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   if (!h.pl_id.empty()) {
     CCRDT_HIP(hipMemcpy(b.pl_id.p, h.pl_id.data(), h.pl_id.size() * 8, hipMemcpyHostToDevice));
     CCRDT_HIP(hipMemcpy(b.pl_info.p, h.pl_info.data(), h.pl_info.size() * 4, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.pl_slab.p, h.pl_slab.data(), h.pl_slab.size() * 4, hipMemcpyHostToDevice));
   }
   if (!h.m_score.empty()) {
     CCRDT_HIP(hipMemcpy(b.m_score.p, h.m_score.data(), h.m_score.size() * 8, hipMemcpyHostToDevice));
     CCRDT_HIP(hipMemcpy(b.m_ts.p, h.m_ts.data(), h.m_ts.size() * 8, hipMemcpyHostToDevice));
-    CCRDT_HIP(hipMemcpy(b.m_pd.p, h.m_pd.data(), h.m_pd.size() * 4, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.m_dc.p, h.m_dc.data(), h.m_dc.size(), hipMemcpyHostToDevice));
   }
   if (!h.r_vc.empty())
     CCRDT_HIP(hipMemcpy(b.r_vc.p, h.r_vc.data(), h.r_vc.size() * 8, hipMemcpyHostToDevice));

@@ -10,7 +10,7 @@ namespace ccrdt {
 
 // One ping-pong side of GPU-resident topk_rmv state (trmv_kernels.hpp).
 struct TrmvBufs {
-  DevBuf meta, pl_id, pl_info, m_score, m_ts, m_pd, r_vc, vc;
+  DevBuf meta, pl_id, pl_info, pl_slab, m_score, m_ts, m_dc, r_vc, vc;
 };
 
 // Per-type resident state of the simpler CCRDTs (types.hip).

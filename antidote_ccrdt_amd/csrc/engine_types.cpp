@@ -39,7 +39,8 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
     CCRDT_TRY(copy_buf(d.pl_info, s.pl_info, stream));
     CCRDT_TRY(copy_buf(d.m_score, s.m_score, stream));
     CCRDT_TRY(copy_buf(d.m_ts, s.m_ts, stream));
-    CCRDT_TRY(copy_buf(d.m_pd, s.m_pd, stream));
+    CCRDT_TRY(copy_buf(d.m_dc, s.m_dc, stream));
+    CCRDT_TRY(copy_buf(d.pl_slab, s.pl_slab, stream));
     CCRDT_TRY(copy_buf(d.r_vc, s.r_vc, stream));
     CCRDT_TRY(copy_buf(d.vc, s.vc, stream));
   } else {

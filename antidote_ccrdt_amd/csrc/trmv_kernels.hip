@@ -425,7 +425,15 @@ __device__ __forceinline__ void op_rmv(const TrmvApplyArgs& a, KeyState<S>& st, 
 }
 
 template <int S>
-__device__ __forceinline__ void trmv_process_key(const TrmvApplyArgs& a, uint32_t key, int64_t* stage) {
+struct SeqLds {
+  int64_t stage[64 * TRMV_DPAD];  // removal clocks of the current 64-op chunk
+  uint16_t own[64 * S];           // load: owner player of flat pool entry e
+  uint16_t src[64 * S];           // load: slab-relative index of entry e
+};
+
+template <int S>
+__device__ __forceinline__ void trmv_process_key(const TrmvApplyArgs& a, uint32_t key,
+                                                 SeqLds<S>& L) {
   const int lane = lane_id();
   const int D = a.n_dc;
   KeyState<S> st;
@@ -464,18 +472,48 @@ __device__ __forceinline__ void trmv_process_key(const TrmvApplyArgs& a, uint32_
   st.vcv = 0;
   st.min_sc = st.min_id = st.min_ts = 0;
   if (!a.fresh) {  // wave-uniform: fresh keys read nothing
+    // players, and the flat position of every player's Masked slab
+    V32<S> fs;
+    uint32_t base = 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const uint32_t p = s * 64 + lane;
+      uint32_t slab = 0;
       if (p < st.np) {
         st.qid[s] = a.old_s.pl_id[om.p_off + p];
         st.qinfo[s] = a.old_s.pl_info[om.p_off + p];
+        slab = a.old_s.pl_slab[om.p_off + p];
       }
-      if (p < st.npool) {
-        st.ps[s] = a.old_s.m_score[om.m_off + p];
-        st.pt[s] = a.old_s.m_ts[om.m_off + p];
-        st.pm[s] = a.old_s.m_pd[om.m_off + p] | PD_ALIVE;
+      uint32_t tot;
+      fs[s] = base + wave_excl_scan_u32(slab >> 16, tot);
+      base += tot;
+      // scatter owner / slab index of each of this player's elements
+      for (uint32_t j = 0; j < (slab >> 16); ++j) {
+        L.own[fs[s] + j] = (uint16_t)p;
+        L.src[fs[s] + j] = (uint16_t)((slab & 0xFFFFu) + j);
       }
+      // Observed index: slab-relative -> flat
+      const uint32_t o = st.qinfo[s] & 0xFFFFu;
+      if (p < st.np && o != NONE16) st.qinfo[s] = (st.qinfo[s] & 0xFFFF0000u) | (fs[s] + o);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t e = s * 64 + lane;
+      if (e < st.npool) {
+        const uint32_t q = L.own[e];
+        const uint64_t g = (uint64_t)om.m_off + L.src[e];
+        st.ps[s] = a.old_s.m_score[g];
+        st.pt[s] = a.old_s.m_ts[g];
+        st.pm[s] = q | ((uint32_t)a.old_s.m_dc[g] << 16) | PD_ALIVE;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {  // INOBS: owner is in Observed
+      const uint32_t q = st.pm[s] & 0xFFFFu;
+      const uint32_t qi = slot_gather<S>(st.qinfo, q == 0xFFFFu ? 0u : q);
+      if (q != 0xFFFFu && (qi & 0xFFFFu) != NONE16) st.pm[s] |= PD_INOBS;
     }
 #pragma unroll
     for (int s = 0; s < (int)KeyState<S>::RSLOTS; ++s) {
@@ -524,7 +562,7 @@ __device__ __forceinline__ void trmv_process_key(const TrmvApplyArgs& a, uint32_
       for (int d = 0; d < D; ++d) {
         const int64_t x = a.rmv_vc[(uint64_t)ots * D + d];
         if (x < 0) err |= TRMV_ERR_VC;
-        stage[lane * TRMV_DPAD + d] = x;
+        L.stage[lane * TRMV_DPAD + d] = x;
       }
     }
     const uint64_t em = ballot(err != 0);
@@ -540,38 +578,58 @@ __device__ __forceinline__ void trmv_process_key(const TrmvApplyArgs& a, uint32_
       if ((k & 0xFFu) < 2) {
         op_add<S>(a, st, op0, base + j, id, rl64(osc, j), k >> 8, rl64(ots, j));
       } else {
-        op_rmv<S>(a, st, op0, base + j, id, stage + j * TRMV_DPAD);
+        op_rmv<S>(a, st, op0, base + j, id, L.stage + j * TRMV_DPAD);
       }
     }
     __syncthreads();
   }
   if (st.ovf) goto overflow;
 
-  // ---- write the new state (pool compacted: removed elements dropped)
+  // ---- write the new state: Masked elements grouped into one slab per
+  // player (flat order inside a slab), removed elements dropped
   {
-    V32<S> rank;
-    uint32_t nm = 0;
+    V32<S> npos;
+    V32<S> qslab;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      npos[s] = 0;
+      qslab[s] = 0;
+    }
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < st.np; ++q) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const bool mine = (uint32_t)(s * 64 + lane) < st.npool && (st.pm[s] & PD_ALIVE) &&
+                          (st.pm[s] & 0xFFFFu) == q;
+        const uint64_t m = ballot(mine);
+        if (mine) npos[s] = base + c + mbcnt(m);
+        c += __builtin_popcountll(m);
+      }
+      slot_set<S>(qslab, q, base | (c << 16));
+      base += c;
+    }
+    const uint32_t nm = base;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const bool al = (uint32_t)(s * 64 + lane) < st.npool && (st.pm[s] & PD_ALIVE);
-      const uint64_t m = ballot(al);
-      rank[s] = nm + mbcnt(m);
-      nm += __builtin_popcountll(m);
       if (al) {
-        const uint64_t dst = (uint64_t)nmeta.m_off + rank[s];
+        const uint64_t dst = (uint64_t)nmeta.m_off + npos[s];
         a.new_s.m_score[dst] = st.ps[s];
         a.new_s.m_ts[dst] = st.pt[s];
-        a.new_s.m_pd[dst] = st.pm[s] & ~PD_ALIVE;
+        a.new_s.m_dc[dst] = (uint8_t)((st.pm[s] >> 16) & 0xFFu);
       }
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const uint32_t p = s * 64 + lane;
       const uint32_t o = st.qinfo[s] & 0xFFFFu;
-      const uint32_t no = slot_gather<S>(rank, o == NONE16 ? 0u : o);
+      const uint32_t no = slot_gather<S>(npos, o == NONE16 ? 0u : o);
       if (p < st.np) {
         a.new_s.pl_id[nmeta.p_off + p] = st.qid[s];
-        a.new_s.pl_info[nmeta.p_off + p] = (st.qinfo[s] & 0xFFFF0000u) | (o == NONE16 ? NONE16 : no);
+        const uint32_t rel = o == NONE16 ? NONE16 : no - (qslab[s] & 0xFFFFu);
+        a.new_s.pl_info[nmeta.p_off + p] = (st.qinfo[s] & 0xFFFF0000u) | rel;
+        a.new_s.pl_slab[nmeta.p_off + p] = qslab[s];
       }
     }
 #pragma unroll
@@ -603,10 +661,10 @@ overflow:
 
 template <int S>
 __global__ __launch_bounds__(64) void trmv_apply_kernel(TrmvApplyArgs a) {
-  __shared__ int64_t stage[64 * TRMV_DPAD];
+  __shared__ SeqLds<S> lds;
   const uint64_t w = blockIdx.x;
   const uint32_t key = a.key_list ? a.key_list[w] : (uint32_t)w;
-  trmv_process_key<S>(a, key, stage);
+  trmv_process_key<S>(a, key, lds);
 }
 
 // ------------------------------------------------------------- capacity scan
@@ -626,6 +684,7 @@ __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint
     c[1] = m.nm + nops;
     c[2] = m.nr + nops;
   }
+  if (c[1] > TRMV_SEG_MAX) atomicOr(&a.status[1], TRMV_ERR_SEG);  // u16 slab offsets
 }
 
 __device__ __forceinline__ void block_scan3(uint64_t v[3], uint64_t total[3]) {
@@ -747,29 +806,26 @@ __global__ __launch_bounds__(64) void trmv_downstream_kernel(TrmvDownArgs a) {
     if (hit) q = b + __builtin_ctzll(hit);
   }
   const uint32_t info = q == NONE32 ? NONE32 : a.s.pl_info[m.p_off + q];
+  const uint32_t slab = q == NONE32 ? 0u : a.s.pl_slab[m.p_off + q];
   const uint32_t o = info & 0xFFFFu;
   uint8_t kind;
   if (a.op[r] == 0) {
     const int64_t sc = a.score[r], ts = a.ts[r];
     bool changes;
     if (o != NONE16) {
-      changes = trmv_cmp(sc, id, ts, a.s.m_score[m.m_off + o], id, a.s.m_ts[m.m_off + o]);
+      const uint64_t g = (uint64_t)m.m_off + (slab & 0xFFFFu) + o;
+      changes = trmv_cmp(sc, id, ts, a.s.m_score[g], id, a.s.m_ts[g]);
     } else if (m.minq == NONE32) {
       changes = true;  // cmp(_, nil) = true
     } else {
-      const uint32_t mo = a.s.pl_info[m.p_off + m.minq] & 0xFFFFu;
-      changes = trmv_cmp(sc, id, ts, a.s.m_score[m.m_off + mo], a.s.pl_id[m.p_off + m.minq],
-                         a.s.m_ts[m.m_off + mo]);
+      const uint32_t mi = a.s.pl_info[m.p_off + m.minq] & 0xFFFFu;
+      const uint32_t ms = a.s.pl_slab[m.p_off + m.minq];
+      const uint64_t g = (uint64_t)m.m_off + (ms & 0xFFFFu) + mi;
+      changes = trmv_cmp(sc, id, ts, a.s.m_score[g], a.s.pl_id[m.p_off + m.minq], a.s.m_ts[g]);
     }
     kind = changes ? CCRDT_TRMV_ADD : CCRDT_TRMV_ADD_R;
   } else {
-    bool in_masked = false;
-    if (q != NONE32) {
-      for (uint32_t b = 0; b < m.nm && !in_masked; b += 64) {
-        const uint32_t e = b + lane;
-        in_masked = ballot(e < m.nm && (a.s.m_pd[m.m_off + e] & 0xFFFFu) == q) != 0;
-      }
-    }
+    const bool in_masked = (slab >> 16) != 0;  // Id in Masked
     kind = !in_masked ? (uint8_t)CCRDT_NOOP : (o != NONE16 ? CCRDT_TRMV_RMV : CCRDT_TRMV_RMV_R);
     if (a.out_vc && lane < D)
       a.out_vc[r * D + lane] = a.fresh ? 0 : a.s.vc[key * D + lane];

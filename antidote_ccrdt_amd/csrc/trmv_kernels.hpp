@@ -1,20 +1,23 @@
 // trmv_kernels.hpp — device layout of GPU-resident topk_rmv state and the
-// kernel argument blocks shared by trmv_kernels.hip and engine.cpp.
+// kernel argument blocks shared by the trmv kernels and engine.cpp.
 //
 // Per key, the reference state {Observed, Masked, Removals, Vc, Min, Size}
 // (src/antidote_ccrdt_topk_rmv.erl:67-74) is held in HBM as variable-length
 // segments addressed through one 32-byte KeyMeta:
-//   players  pl_id[i64], pl_info[u32]   one per distinct Id ever seen by the key
-//            pl_info = obs pool index (low 16, 0xFFFF = not in Observed)
-//                    | removal row (high 16, 0xFFFF = no Removals entry)
-//   pool     m_score[i64], m_ts[i64], m_pd[u32]   the Masked elements
-//            m_pd = owner player (low 16) | dc rank (bits 16..23)
-//                 | INOBS (bit 31: owner currently in Observed)
-//   rows     r_vc[n_dc x i64]           Removals[Id] (0 = DC absent)
-//   vc       vc[n_dc x i64]             replica Vc (0 = DC absent)
-//   meta     offsets + counts + Observed size + Min (a player index)
-// Observed is implicit: Obs[Id] is the pool element pl_info.obs of Id's
-// player (Observed ⊆ Masked), and Min is always Obs[minq].
+//   players  pl_id[i64]   one per distinct Id the key has seen (Masked or
+//                         Removals entry; players are never dropped)
+//            pl_info[u32] obs (low 16): index of Obs[Id] inside the player's
+//                         Masked slab, 0xFFFF = Id not in Observed;
+//                         row (high 16): Removals row, 0xFFFF = none
+//            pl_slab[u32] Masked slab of the player inside the key's pool
+//                         segment: offset (low 16) | element count (high 16)
+//   pool     m_score[i64], m_ts[i64], m_dc[u8]   the Masked elements, one
+//                         slab per player (slabs may leave holes)
+//   rows     r_vc[n_dc x i64]   Removals[Id] (0 = DC absent)
+//   vc       vc[n_dc x i64]     replica Vc (0 = DC absent)
+//   meta     segment offsets, counts, |Observed| and Min (a player index)
+// Observed is implicit (Observed ⊆ Masked) and Min is always
+// Obs[minq] (Min == min_observed(Observed) is an invariant of the reference).
 #pragma once
 #include <cstdint>
 
@@ -22,13 +25,16 @@ namespace ccrdt {
 
 constexpr uint32_t NONE16 = 0xFFFFu;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
-constexpr uint32_t PD_INOBS = 1u << 31;
-constexpr uint32_t PD_ALIVE = 1u << 30;  // in-register only
+constexpr uint32_t PD_INOBS = 1u << 31;  // in-register flags (sequential kernel)
+constexpr uint32_t PD_ALIVE = 1u << 30;
 constexpr int TRMV_DPAD = 8;             // lanes per removal row (n_dc <= 8)
+constexpr uint32_t TRMV_SEG_MAX = 0xFFFFu;  // pool elements addressable per key
 
 struct alignas(32) KeyMeta {
-  uint32_t p_off, m_off, r_off;  // segment starts (elements / rows)
-  uint32_t np, nm, nr;           // players, pool elements, removal rows
+  uint32_t p_off, m_off, r_off;  // segment starts (players / pool elements / rows)
+  uint32_t np;                   // players
+  uint32_t nm;                   // Masked elements (sum of slab counts)
+  uint32_t nr;                   // Removals rows
   uint32_t nobs;                 // |Observed|
   uint32_t minq;                 // player index of Min, NONE32 = nil
 };
@@ -39,14 +45,16 @@ struct TrmvSide {
   KeyMeta* meta;
   int64_t* pl_id;
   uint32_t* pl_info;
+  uint32_t* pl_slab;
   int64_t* m_score;
   int64_t* m_ts;
-  uint32_t* m_pd;
+  uint8_t* m_dc;
   int64_t* r_vc;
   int64_t* vc;
 };
 
-// Extra effect record, compacted per key inside the key's op range.
+// Extra effect record; a key's records sit inside the key's op range, in any
+// order (the host orders them by `op`).
 struct alignas(16) TrmvExtraRec {
   uint32_t op;    // global op index
   uint8_t kind;   // CCRDT_TRMV_ADD or CCRDT_TRMV_RMV
@@ -91,6 +99,7 @@ enum : uint32_t {
   TRMV_ERR_TS = 4u,
   TRMV_ERR_ROW = 8u,
   TRMV_ERR_VC = 16u,
+  TRMV_ERR_SEG = 32u,  // a key's pool segment would exceed TRMV_SEG_MAX
 };
 
 struct TrmvDownArgs {

@@ -120,7 +120,7 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    overflow = {c: eng.overflow_keys(c) for c in (2, 4, 8)}
+    overflow = {c: eng.overflow_keys(c) for c in (0, 2, 4, 8)}
 
     cpu = None
     if rank == 0 and args.cpu_sample_keys > 0:

@@ -73,13 +73,15 @@ def test_random_streams(gpu, cfg):
     _compare(eng, orac, b, D, xe, xo)
 
 
-def test_multi_batch_and_import(gpu):
-    """State carried across batches; export -> import -> continue."""
-    nk, D, K = 150, 4, 5
+@pytest.mark.parametrize("K,npl", [(5, 20), (100, 40), (30, 28)])
+def test_multi_batch_and_import(gpu, K, npl):
+    """State carried across batches (fast per-player path and sequential
+    path); export -> import -> continue."""
+    nk, D = 150, 4
     eng = TopkRmvEngine(nk, K, D)
     orac = orc.TrmvOracle(nk, K, D)
     for i in range(4):
-        b = gen_trmv(4000, nk, D, 20, 50, 120, 8, 30, 20, seed=77 + i)
+        b = gen_trmv(4000, nk, D, npl, 50, 120, 8, 30, 20, seed=77 + i)
         # clocks restart per generated batch: shift ts so they keep growing
         add = b.kind < 2
         b.ts[add] += i * 10**6
@@ -90,7 +92,7 @@ def test_multi_batch_and_import(gpu):
     e2 = TopkRmvEngine(nk, K, D)
     e2.import_state(st)
     assert not e2.export().diff(st)
-    b = gen_trmv(4000, nk, D, 20, 50, 120, 8, 30, 20, seed=99)
+    b = gen_trmv(4000, nk, D, npl, 50, 120, 8, 30, 20, seed=99)
     b.ts[b.kind < 2] += 10**7
     b.rmv_vc[b.rmv_vc > 0] += 10**7
     xe, xo = e2.apply(b), orac.apply(b)
