@@ -73,6 +73,7 @@ SIGNATURES = {
     "ccrdt_device_synchronize": (INT, []),
     "ccrdt_engine_last_kernel_ms": (INT, [P, C.POINTER(C.c_float)]),
     "ccrdt_engine_overflow_keys": (INT, [P, INT, C.POINTER(I64)]),
+    "ccrdt_engine_tier_ms": (INT, [P, INT, C.POINTER(C.c_float)]),
     "ccrdt_timer_start": (INT, [P]),
     "ccrdt_timer_stop": (INT, [P, C.POINTER(C.c_float)]),
     "ccrdt_trmv_apply": (INT, [P, C.POINTER(TrmvOps), C.POINTER(TrmvExtra)]),

@@ -26,7 +26,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
 int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
-int trmv_launch_fast(const TrmvApplyArgs& a, hipStream_t st);
+int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st);
 
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
@@ -211,6 +211,13 @@ int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms) {
   return CCRDT_OK;
 }
 
+int ccrdt_engine_tier_ms(ccrdt_engine* e, int tier, float* ms) {
+  if (!e || !ms) return CCRDT_EINVAL;
+  auto it = e->trmv_tier_ms.find(tier);
+  *ms = it == e->trmv_tier_ms.end() ? 0.f : it->second;
+  return CCRDT_OK;
+}
+
 int ccrdt_engine_overflow_keys(ccrdt_engine* e, int slot_class, int64_t* n) {
   if (!e || !n) return CCRDT_EINVAL;
   auto it = e->trmv_overflow_keys.find(slot_class);
@@ -316,6 +323,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   uint64_t n_work = nk;
   float kernel_ms = 0.f;
   E.trmv_overflow_keys.clear();
+  E.trmv_tier_ms.clear();
   auto read_status = [&](uint32_t& n_ovf, uint32_t& err) -> int {
     CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
@@ -335,21 +343,30 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
                ? CCRDT_ERANGE
                : CCRDT_EINVAL;
   };
-  if (nk) {
-    a.key_list = nullptr;
-    a.n_list = (uint32_t)nk;
-    a.ovf_list = E.ovf_a.as<uint32_t>();
+  // CCRDT_TRMV_FIRST_TIER (tuning knob, default 0): 1 skips the all-LDS tier,
+  // 2 sends every key to the sequential kernel.
+  static const int first_tier = [] {
+    const char* v = getenv("CCRDT_TRMV_FIRST_TIER");
+    return v ? atoi(v) : 0;
+  }();
+  for (int tier = first_tier; tier < 2 && n_work; ++tier) {
+    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
+    a.key_list = work ? work->as<uint32_t>() : nullptr;
+    a.n_list = (uint32_t)n_work;
+    a.ovf_list = ovf->as<uint32_t>();
+    CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
     CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
-    CCRDT_TRY(trmv_launch_fast(a, E.stream));
+    CCRDT_TRY(trmv_launch_fast(a, tier, n_work, E.stream));
     CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
     uint32_t n_ovf = 0, err = 0;
     CCRDT_TRY(read_status(n_ovf, err));
     float ms = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
     kernel_ms += ms;
-    E.trmv_overflow_keys[0] = n_ovf;
+    E.trmv_tier_ms[tier] = ms;
+    E.trmv_overflow_keys[tier] = n_ovf;
     if (err) return fail_err(err);
-    work = &E.ovf_a;
+    work = ovf;
     n_work = n_ovf;
   }
   for (int cls : TRMV_SLOT_CLASSES) {
@@ -369,6 +386,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     kernel_ms += ms;
     if (err) return fail_err(err);
     E.trmv_overflow_keys[cls] = n_ovf;
+    E.trmv_tier_ms[cls] = ms;
     work = ovf;
     n_work = n_ovf;
   }

@@ -52,7 +52,8 @@ struct ccrdt_engine {
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, ovf_a, ovf_b, status;
   uint64_t last_n_ops = 0;
-  std::map<int, uint32_t> trmv_overflow_keys;  // per slot class, last apply
+  std::map<int, uint32_t> trmv_overflow_keys;  // per tier / slot class, last apply
+  std::map<int, float> trmv_tier_ms;
   // host-API staging
   ccrdt::DevBuf st_kp, st_kind, st_id, st_score, st_dc, st_ts, st_rvc, st_out_kind, st_out_vc;
 

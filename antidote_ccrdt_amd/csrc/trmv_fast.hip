@@ -14,39 +14,60 @@
 // So the key's state decomposes into independent per-player histories: each
 // lane of the wave owns one player and replays that player's effects in
 // stream order; only the replica Vc (elementwise max, order-free) and the
-// final Min are shared.  Keys with P > K (or beyond this kernel's LDS caps)
-// go to the sequential kernel (trmv_kernels.hip) through the overflow list.
+// final Min are shared.  Keys with P > K go to the sequential kernel
+// (trmv_kernels.hip) through the overflow list.
 //
 // Per key (one wavefront):
 //   1. hash the key's old players into LDS (id -> player index);
-//   2. op lanes look up / claim their Id (parallel open addressing, new
-//      players numbered in claim order) and count ops per player;
+//   2. op lanes load their op (coalesced), look up / claim their Id (parallel
+//      open addressing, new players numbered in claim order), count ops per
+//      player;
 //   3. counting sort of the key's ops by player (each player's list is then
 //      re-sorted by op index, so replay order = stream order);
-//   4. player lanes replay their ops against their own Masked slab (in HBM,
-//      updated in place), Removals row (registers) and Obs element;
+//   4. player lanes replay their ops against their own Masked slab, Removals
+//      row (registers) and Obs element;
 //   5. Vc (LDS atomic max), Min (wave reduction), metadata.
+// Two tiers: SMALL keeps the op fields, the removal clocks and the Masked
+// slabs in LDS (every replay access is an LDS access; the slabs go to HBM in
+// one coalesced pass); LARGE has 2x the caps and works on the slabs in HBM.
 #include "common.hpp"
 #include "trmv_kernels.hpp"
 
 namespace ccrdt {
 
-constexpr int F_HCAP = 512;  // hash slots (power of two)
-constexpr int F_PCAP = 256;  // players per key
-constexpr int F_OCAP = 512;  // ops per key per batch
 constexpr uint32_t F_CLAIM = 1u << 31;
 
+template <bool SMALL>
+struct FastCfg;
+template <>
+struct FastCfg<true> {
+  static constexpr int HCAP = 256, PCAP = 128, OCAP = 192, MCAP = 192, RCAP = 16;
+};
+template <>
+struct FastCfg<false> {
+  static constexpr int HCAP = 512, PCAP = 256, OCAP = 512, MCAP = 1, RCAP = 1;
+};
+
+template <bool SMALL>
 struct FastLds {
-  uint32_t hslot[F_HCAP];   // 0 empty | player+1 | F_CLAIM|lane (claim in flight)
-  int64_t pid[F_PCAP];      // player ids
-  int64_t claim_id[64];     // id being claimed by each lane
+  using C = FastCfg<SMALL>;
+  uint32_t hslot[C::HCAP];  // 0 empty | player+1 | F_CLAIM|lane (claim in flight)
+  int64_t pid[C::PCAP];     // player ids
   unsigned long long vc[TRMV_DPAD];  // replica Vc (values >= 0)
-  uint16_t opl[F_OCAP];     // player of each op
-  uint16_t sorted[F_OCAP];  // ops grouped by player
-  uint32_t pcnt[F_PCAP];    // ops per player in this batch
-  uint32_t pfill[F_PCAP];
-  uint32_t pstart[F_PCAP];
+  uint32_t kd[C::OCAP];     // player << 16 | dc << 8 | kind
+  uint16_t sorted[C::OCAP]; // ops grouped by player
+  uint32_t pcnt[C::PCAP];   // ops per player in this batch
+  uint32_t pfill[C::PCAP];
+  uint32_t pstart[C::PCAP];
   uint32_t nex;             // extra effects emitted by this key
+  uint32_t nrmv;            // staged removal clocks
+  // SMALL only: op fields, removal clocks, working Masked slabs
+  int64_t osc[SMALL ? C::OCAP : 1];  // score (rmv: staged clock slot or -1)
+  int64_t ots[SMALL ? C::OCAP : 1];  // ts (rmv: row of rmv_vc)
+  int64_t rvc[SMALL ? C::RCAP * TRMV_DPAD : 1];
+  int64_t msc[SMALL ? C::MCAP : 64];  // (LARGE: claim ids)
+  int64_t mts[SMALL ? C::MCAP : 1];
+  uint8_t mdc[SMALL ? C::MCAP : 1];
 };
 
 __device__ __forceinline__ uint32_t hash_id(int64_t id) {
@@ -64,7 +85,8 @@ __device__ __forceinline__ int64_t pick8(const Row8& v, uint32_t d) {
   return r;
 }
 
-__device__ __forceinline__ void emit_extra(const TrmvApplyArgs& a, FastLds& L, uint64_t op0,
+template <bool SMALL>
+__device__ __forceinline__ void emit_extra(const TrmvApplyArgs& a, FastLds<SMALL>& L, uint64_t op0,
                                            uint64_t op, uint8_t kind, int64_t id, int64_t sc,
                                            uint32_t dc, int64_t ts, const Row8& row) {
   const uint32_t pos = atomicAdd(&L.nex, 1u);
@@ -83,9 +105,34 @@ __device__ __forceinline__ void emit_extra(const TrmvApplyArgs& a, FastLds& L, u
       if (d < a.n_dc) a.ex_vc[(op0 + pos) * a.n_dc + d] = row[d];
 }
 
-// Returns false (having written nothing) if the key must take the
-// sequential path.
-__device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) {
+// Masked slab of one player: LDS (SMALL) or the new pool in HBM (LARGE).
+template <bool SMALL>
+struct Slab {
+  FastLds<SMALL>& L;
+  const TrmvSide& s;
+  uint64_t g;  // SMALL: LDS index; LARGE: pool index
+  __device__ __forceinline__ int64_t sc(uint32_t j) const { return SMALL ? L.msc[g + j] : s.m_score[g + j]; }
+  __device__ __forceinline__ int64_t ts(uint32_t j) const { return SMALL ? L.mts[g + j] : s.m_ts[g + j]; }
+  __device__ __forceinline__ uint32_t dc(uint32_t j) const { return SMALL ? L.mdc[g + j] : s.m_dc[g + j]; }
+  __device__ __forceinline__ void set(uint32_t j, int64_t v, int64_t t, uint32_t d) const {
+    if (SMALL) {
+      L.msc[g + j] = v;
+      L.mts[g + j] = t;
+      L.mdc[g + j] = (uint8_t)d;
+    } else {
+      s.m_score[g + j] = v;
+      s.m_ts[g + j] = t;
+      s.m_dc[g + j] = (uint8_t)d;
+    }
+  }
+};
+
+// Returns false (having written nothing to HBM) if the key must take the
+// next tier.
+template <bool SMALL>
+__device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key,
+                                              FastLds<SMALL>& L) {
+  using C = FastCfg<SMALL>;
   const int lane = lane_id();
   const int D = a.n_dc;
   const KeyMeta nmeta = a.new_s.meta[key];
@@ -100,18 +147,22 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
   const uint64_t op0 = a.key_ptr[key];
   const uint64_t op1 = a.key_ptr[key + 1];
   const uint32_t nops = (uint32_t)(op1 - op0);
-  const uint32_t pmax = a.k < (uint32_t)F_PCAP ? a.k : (uint32_t)F_PCAP;
-  if (nops > (uint32_t)F_OCAP || om.np > pmax) return false;
+  const uint32_t pmax = a.k < (uint32_t)C::PCAP ? a.k : (uint32_t)C::PCAP;
+  if (nops > (uint32_t)C::OCAP || om.np > pmax) return false;
+  if (SMALL && om.nm + nops > (uint32_t)C::MCAP) return false;
 
   // ---- 1. clear LDS, hash the old players
-  for (int i = lane; i < F_HCAP; i += 64) L.hslot[i] = 0;
-  for (int i = lane; i < F_PCAP; i += 64) {
+  for (int i = lane; i < C::HCAP; i += 64) L.hslot[i] = 0;
+  for (int i = lane; i < C::PCAP; i += 64) {
     L.pcnt[i] = 0;
     L.pfill[i] = 0;
   }
   if (lane < TRMV_DPAD)
     L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
-  if (lane == 0) L.nex = 0;
+  if (lane == 0) {
+    L.nex = 0;
+    L.nrmv = 0;
+  }
   __syncthreads();
   bool bad = false;
   for (uint32_t b = 0; b < om.np; b += 64) {
@@ -119,8 +170,8 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
     if (p < om.np) {
       const int64_t id = a.old_s.pl_id[om.p_off + p];
       L.pid[p] = id;
-      uint32_t h = hash_id(id) & (F_HCAP - 1);
-      while (atomicCAS(&L.hslot[h], 0u, p + 1) != 0u) h = (h + 1) & (F_HCAP - 1);
+      uint32_t h = hash_id(id) & (C::HCAP - 1);
+      while (atomicCAS(&L.hslot[h], 0u, p + 1) != 0u) h = (h + 1) & (C::HCAP - 1);
       // every player with Masked elements must be in Observed (true for any
       // state with P <= K that the reference's transitions can reach)
       const bool has_m = (a.old_s.pl_slab[om.p_off + p] >> 16) != 0;
@@ -131,15 +182,46 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
   if (ballot(bad)) return false;
   __syncthreads();
 
-  // ---- 2. player of every op (new Ids claimed in lane order)
+  // ---- 2. load ops, player of every op (new Ids claimed in lane order)
+  int64_t* claim_id = SMALL ? L.msc : L.msc;  // LDS scratch, 64 entries
   uint32_t np = om.np;
+  uint32_t err = 0;
   for (uint32_t b = 0; b < nops; b += 64) {
     const uint32_t l = b + lane;
     const bool valid = l < nops;
-    const int64_t id = valid ? a.id[op0 + l] : 0;
-    L.claim_id[lane] = id;
+    const uint64_t i = op0 + l;
+    const int64_t id = valid ? a.id[i] : 0;
+    uint32_t kd = 0;
+    if (SMALL && valid) {
+      const uint32_t kind = a.kind[i], dc = a.dc[i];
+      const int64_t sc = a.score[i], t = a.ts[i];
+      kd = kind | (dc << 8);
+      int64_t slot = -1;
+      if (kind > 3) {
+        err |= TRMV_ERR_KIND;
+      } else if (kind < 2) {
+        if ((int)dc >= D) err |= TRMV_ERR_DC;
+        if (t < 1) err |= TRMV_ERR_TS;
+      } else if (t < 0 || t >= a.n_rmv_rows) {
+        err |= TRMV_ERR_ROW;
+      } else {
+        const uint32_t r = atomicAdd(&L.nrmv, 1u);
+        if (r < (uint32_t)C::RCAP) {
+          slot = r;
+#pragma unroll
+          for (int d = 0; d < TRMV_DPAD; ++d) {
+            const int64_t x = d < D ? a.rmv_vc[(uint64_t)t * D + d] : 0;
+            if (x < 0) err |= TRMV_ERR_VC;
+            L.rvc[r * TRMV_DPAD + d] = x;
+          }
+        }
+      }
+      L.osc[l] = kind < 2 ? sc : slot;
+      L.ots[l] = t;
+    }
+    claim_id[lane] = id;
     __syncthreads();
-    uint32_t h = hash_id(id) & (F_HCAP - 1);
+    uint32_t h = hash_id(id) & (C::HCAP - 1);
     bool resolved = !valid, claimed = false;
     int follow = -1;
     uint32_t p = 0;
@@ -153,35 +235,39 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
           }  // lost the race: re-read the slot next round
         } else if (s & F_CLAIM) {
           const int c = (int)(s & 63u);
-          if (L.claim_id[c] == id) {
+          if (claim_id[c] == id) {
             follow = c;
             resolved = true;
           } else {
-            h = (h + 1) & (F_HCAP - 1);
+            h = (h + 1) & (C::HCAP - 1);
           }
         } else if (L.pid[s - 1] == id) {
           p = s - 1;
           resolved = true;
         } else {
-          h = (h + 1) & (F_HCAP - 1);
+          h = (h + 1) & (C::HCAP - 1);
         }
       }
     }
     const uint64_t cm = ballot(claimed);
     if (claimed) {
       p = np + mbcnt(cm);
-      if (p < (uint32_t)F_PCAP) L.pid[p] = id;
+      if (p < (uint32_t)C::PCAP) L.pid[p] = id;
       L.hslot[h] = p + 1;
     }
     np += (uint32_t)__builtin_popcountll(cm);
     const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
     if (follow >= 0) p = fp;
-    if (np > pmax) return false;  // Observed could fill: sequential path
+    if (np > pmax) return false;  // Observed could fill: next tier
     if (valid) {
-      L.opl[l] = (uint16_t)p;
+      L.kd[l] = kd | (p << 16);
       atomicAdd(&L.pcnt[p], 1u);
     }
     __syncthreads();
+  }
+  if (SMALL && ballot(err != 0)) {
+    if (err) atomicOr(&a.status[1], err);
+    return true;  // the host rejects the batch
   }
 
   // ---- 3. counting sort of ops by player
@@ -198,7 +284,7 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
   }
   __syncthreads();
   for (uint32_t l = lane; l < nops; l += 64) {
-    const uint32_t p = L.opl[l];
+    const uint32_t p = L.kd[l] >> 16;
     const uint32_t pos = atomicAdd(&L.pfill[p], 1u);
     L.sorted[L.pstart[p] + pos] = (uint16_t)l;
   }
@@ -208,7 +294,6 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
   uint32_t slab_base = 0, row_base = 0, nm = 0, nobs = 0;
   int64_t best_sc = 0, best_id = 0;
   uint32_t best_q = NONE32;
-  uint32_t err = 0;
   for (uint32_t b = 0; b < np; b += 64) {
     const uint32_t p = b + lane;
     const bool act = p < np;
@@ -233,22 +318,22 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
     uint32_t tot;
     const uint32_t moff = slab_base + wave_excl_scan_u32(act ? cnt_old + cnt_ops : 0u, tot);
     slab_base += tot;
-    const uint64_t g = (uint64_t)nmeta.m_off + moff;  // my slab in the new pool
-    // copy the old slab
-    for (uint32_t j = 0; j < cnt_old; ++j) {
+    const Slab<SMALL> sl{L, a.new_s, SMALL ? (uint64_t)moff : (uint64_t)nmeta.m_off + moff};
+    // maxts bounds the ts of every element ever in the slab: an add with a
+    // larger ts cannot duplicate one (skips the set-membership scan)
+    int64_t maxts = 0;
+    for (uint32_t j = 0; j < cnt_old; ++j) {  // copy the old slab
       const uint64_t go = (uint64_t)om.m_off + (slab_old & 0xFFFFu) + j;
-      a.new_s.m_score[g + j] = a.old_s.m_score[go];
-      a.new_s.m_ts[g + j] = a.old_s.m_ts[go];
-      a.new_s.m_dc[g + j] = a.old_s.m_dc[go];
+      const int64_t t = a.old_s.m_ts[go];
+      maxts = t > maxts ? t : maxts;
+      sl.set(j, a.old_s.m_score[go], t, a.old_s.m_dc[go]);
     }
     uint32_t cnt = cnt_old;
     uint32_t o = info & 0xFFFFu;  // Obs[Id] as slab index
     int64_t osc = 0, ots = 0;
-    uint32_t odc = 0;
     if (act && o != NONE16) {
-      osc = a.new_s.m_score[g + o];
-      ots = a.new_s.m_ts[g + o];
-      odc = a.new_s.m_dc[g + o];
+      osc = sl.sc(o);
+      ots = sl.ts(o);
     }
     bool has_row = false;
     Row8 row = (Row8)(0);
@@ -261,66 +346,75 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
     }
     const int64_t id = act ? L.pid[p] : 0;
     for (uint32_t x = 0; x < cnt_ops; ++x) {
-      const uint64_t i = op0 + L.sorted[st0 + x];
-      const uint32_t kind = a.kind[i];
-      const int64_t tsf = a.ts[i];
-      if (kind > 3) {
-        err |= TRMV_ERR_KIND;
-        break;
-      }
-      if (kind < 2) {  // add/4 (:231-249)
-        const uint32_t dc = a.dc[i];
-        const int64_t sc = a.score[i];
-        if ((int)dc >= D || tsf < 1) {
+      const uint32_t l = L.sorted[st0 + x];
+      const uint64_t i = op0 + l;
+      uint32_t kind, dc;
+      int64_t sc, tsf;
+      if (SMALL) {
+        kind = L.kd[l] & 0xFFu;
+        dc = (L.kd[l] >> 8) & 0xFFu;
+        sc = L.osc[l];
+        tsf = L.ots[l];
+      } else {
+        kind = a.kind[i];
+        dc = a.dc[i];
+        sc = a.score[i];
+        tsf = a.ts[i];
+        if (kind > 3) {
+          err |= TRMV_ERR_KIND;
+          break;
+        }
+        if (kind < 2 && ((int)dc >= D || tsf < 1)) {
           err |= ((int)dc >= D ? TRMV_ERR_DC : 0u) | (tsf < 1 ? TRMV_ERR_TS : 0u);
           break;
         }
+        if (kind >= 2 && (tsf < 0 || tsf >= a.n_rmv_rows)) {
+          err |= TRMV_ERR_ROW;
+          break;
+        }
+      }
+      if (kind < 2) {  // add/4 (:231-249)
         atomicMax(&L.vc[dc], (unsigned long long)tsf);  // vc_update (:233)
         if (has_row && pick8(row, dc) >= tsf) {          // dominated (:234-237)
-          emit_extra(a, L, op0, i, CCRDT_TRMV_RMV, id, 0, 0, 0, row);
+          emit_extra<SMALL>(a, L, op0, i, CCRDT_TRMV_RMV, id, 0, 0, 0, row);
           continue;
         }
         uint32_t e = NONE32;  // gb_sets:add_element (set semantics)
-        for (uint32_t j = 0; j < cnt && e == NONE32; ++j)
-          if (a.new_s.m_ts[g + j] == tsf && a.new_s.m_dc[g + j] == dc && a.new_s.m_score[g + j] == sc)
-            e = j;
+        if (tsf <= maxts)
+          for (uint32_t j = 0; j < cnt && e == NONE32; ++j)
+            if (sl.ts(j) == tsf && sl.dc(j) == dc && sl.sc(j) == sc) e = j;
+        maxts = tsf > maxts ? tsf : maxts;
         if (e == NONE32) {
           e = cnt++;
-          a.new_s.m_score[g + e] = sc;
-          a.new_s.m_ts[g + e] = tsf;
-          a.new_s.m_dc[g + e] = (uint8_t)dc;
+          sl.set(e, sc, tsf, dc);
         }
         // recompute_observed (:301-324; never full here)
         if (o == NONE16 || sc > osc || (sc == osc && tsf > ots)) {
           o = e;
           osc = sc;
           ots = tsf;
-          odc = dc;
         }
       } else {  // rmv/3 (:252-298)
-        if (tsf < 0 || tsf >= a.n_rmv_rows) {
-          err |= TRMV_ERR_ROW;
-          break;
-        }
         Row8 vr = (Row8)(0);
+        const bool staged = SMALL && sc >= 0;
 #pragma unroll
         for (int d = 0; d < TRMV_DPAD; ++d) {
-          vr[d] = d < D ? a.rmv_vc[(uint64_t)tsf * D + d] : 0;
-          if (vr[d] < 0) err |= TRMV_ERR_VC;
+          if (staged) {
+            vr[d] = L.rvc[sc * TRMV_DPAD + d];
+          } else {
+            vr[d] = d < D ? a.rmv_vc[(uint64_t)tsf * D + d] : 0;
+            if (vr[d] < 0) err |= TRMV_ERR_VC;
+          }
           row[d] = has_row ? (vr[d] > row[d] ? vr[d] : row[d]) : vr[d];  // merge_vc
         }
         has_row = true;
         // filter Masked[Id]: keep Ts > VcRmv[DcId] (:255-266)
         uint32_t w = 0, no = NONE16;
         for (uint32_t j = 0; j < cnt; ++j) {
-          const int64_t t = a.new_s.m_ts[g + j];
-          const uint32_t edc = a.new_s.m_dc[g + j];
+          const int64_t t = sl.ts(j);
+          const uint32_t edc = sl.dc(j);
           if (t > pick8(vr, edc)) {
-            if (w != j) {
-              a.new_s.m_score[g + w] = a.new_s.m_score[g + j];
-              a.new_s.m_ts[g + w] = t;
-              a.new_s.m_dc[g + w] = (uint8_t)edc;
-            }
+            if (w != j) sl.set(w, sl.sc(j), t, edc);
             if (j == o) no = w;
             ++w;
           }
@@ -331,11 +425,11 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
             o = NONE16;
           } else {  // promote gb_sets:largest of the survivors (:291-295)
             uint32_t bj = 0;
-            int64_t bsc = a.new_s.m_score[g], bts = a.new_s.m_ts[g];
-            uint32_t bdc = a.new_s.m_dc[g];
+            int64_t bsc = sl.sc(0), bts = sl.ts(0);
+            uint32_t bdc = sl.dc(0);
             for (uint32_t j = 1; j < cnt; ++j) {
-              const int64_t s2 = a.new_s.m_score[g + j], t2 = a.new_s.m_ts[g + j];
-              const uint32_t d2 = a.new_s.m_dc[g + j];
+              const int64_t s2 = sl.sc(j), t2 = sl.ts(j);
+              const uint32_t d2 = sl.dc(j);
               if (s2 > bsc || (s2 == bsc && (d2 > bdc || (d2 == bdc && t2 > bts)))) {
                 bj = j;
                 bsc = s2;
@@ -346,14 +440,15 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
             o = bj;
             osc = bsc;
             ots = bts;
-            odc = bdc;
-            emit_extra(a, L, op0, i, CCRDT_TRMV_ADD, id, bsc, bdc, bts, row);
+            emit_extra<SMALL>(a, L, op0, i, CCRDT_TRMV_ADD, id, bsc, bdc, bts, row);
           }
         } else {
           o = no;
         }
       }
     }
+    if (SMALL)  // mark the unused tail of the slab as a hole
+      for (uint32_t j = cnt; j < cnt_old + cnt_ops; ++j) L.mdc[moff + j] = 0xFF;
     // removal row index (player order) and the player record
     const uint64_t rm = ballot(act && has_row);
     const uint32_t rix = row_base + mbcnt(rm);
@@ -369,30 +464,49 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
           if (d < D) a.new_s.r_vc[r0 + d] = row[d];
       }
     }
-    (void)odc;
-    // counts and Min = min_observed(Observed) by (Score, Id)
+    // lane-local counts and Min candidate (reduced once per key below)
     const bool inobs = act && o != NONE16;
     nobs += (uint32_t)__builtin_popcountll(ballot(inobs));
-    uint32_t ctot;
-    (void)wave_excl_scan_u32(act ? cnt : 0u, ctot);
-    nm += ctot;
-    if (ballot(inobs)) {
-      const int64_t ms = wave_min_i64(inobs ? osc : INT64_MAX);
-      const int64_t mi = wave_min_i64(inobs && osc == ms ? id : INT64_MAX);
-      const uint64_t hit = ballot(inobs && osc == ms && id == mi);
-      if (best_q == NONE32 || ms < best_sc || (ms == best_sc && mi < best_id)) {
-        best_q = b + (uint32_t)__builtin_ctzll(hit);
-        best_sc = ms;
-        best_id = mi;
-      }
+    nm += act ? cnt : 0u;
+    if (inobs && (best_q == NONE32 || osc < best_sc || (osc == best_sc && id < best_id))) {
+      best_q = p;
+      best_sc = osc;
+      best_id = id;
     }
+  }
+  // Min = min_observed(Observed) by (Score, Id) — Ids are distinct
+  {
+    const bool has = best_q != NONE32;
+    if (ballot(has)) {
+      const int64_t ms = wave_min_i64(has ? best_sc : INT64_MAX);
+      const int64_t mi = wave_min_i64(has && best_sc == ms ? best_id : INT64_MAX);
+      const uint64_t hit = ballot(has && best_sc == ms && best_id == mi);
+      best_q = shfl32(best_q, (int)__builtin_ctzll(hit));
+      best_q = rl32(best_q, 0);
+    } else {
+      best_q = NONE32;
+    }
+    uint32_t tot;
+    (void)wave_excl_scan_u32(nm, tot);
+    nm = tot;
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
-    return true;  // batch rejected by the host; nothing else to do
+    return true;  // the host rejects the batch
   }
   __syncthreads();
-  // ---- 5. Vc, metadata
+  // ---- 5. Masked slabs to HBM (SMALL), Vc, metadata
+  if (SMALL) {
+    for (uint32_t j = lane; j < slab_base; j += 64) {
+      const uint32_t d = L.mdc[j];
+      if (d != 0xFFu) {
+        const uint64_t gj = (uint64_t)nmeta.m_off + j;
+        a.new_s.m_score[gj] = L.msc[j];
+        a.new_s.m_ts[gj] = L.mts[j];
+        a.new_s.m_dc[gj] = (uint8_t)d;
+      }
+    }
+  }
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   if (lane == 0) {
     KeyMeta out = nmeta;
@@ -407,10 +521,12 @@ __device__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t key, FastLds& L) 
   return true;
 }
 
+template <bool SMALL>
 __global__ __launch_bounds__(64) void trmv_fast_kernel(TrmvApplyArgs a) {
-  __shared__ FastLds lds;
-  const uint32_t key = (uint32_t)blockIdx.x;
-  if (!trmv_fast_key(a, key, lds)) {
+  __shared__ FastLds<SMALL> lds;
+  const uint64_t w = blockIdx.x;
+  const uint32_t key = a.key_list ? a.key_list[w] : (uint32_t)w;
+  if (!trmv_fast_key<SMALL>(a, key, lds)) {
     if (lane_id() == 0) {
       const uint32_t pos = atomicAdd(&a.status[0], 1u);
       a.ovf_list[pos] = key;
@@ -418,9 +534,13 @@ __global__ __launch_bounds__(64) void trmv_fast_kernel(TrmvApplyArgs a) {
   }
 }
 
-int trmv_launch_fast(const TrmvApplyArgs& a, hipStream_t st) {
-  if (a.n_keys == 0) return CCRDT_OK;
-  hipLaunchKernelGGL(trmv_fast_kernel, dim3((unsigned)a.n_keys), dim3(64), 0, st, a);
+// tier 0 = SMALL (all-LDS), tier 1 = LARGE (slabs in HBM)
+int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st) {
+  if (n_work == 0) return CCRDT_OK;
+  if (tier == 0)
+    hipLaunchKernelGGL(trmv_fast_kernel<true>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(trmv_fast_kernel<false>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -205,6 +205,11 @@ class _Engine:
         check(lib.ccrdt_engine_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
         return float(ms.value)
 
+    def tier_ms(self, tier: int) -> float:
+        ms = C.c_float()
+        check(lib.ccrdt_engine_tier_ms(self.h, tier, C.byref(ms)), "tier_ms")
+        return float(ms.value)
+
     def overflow_keys(self, slot_class: int) -> int:
         n = C.c_int64()
         check(lib.ccrdt_engine_overflow_keys(self.h, slot_class, C.byref(n)), "overflow_keys")

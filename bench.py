@@ -120,7 +120,8 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    overflow = {c: eng.overflow_keys(c) for c in (0, 2, 4, 8)}
+    overflow = {c: eng.overflow_keys(c) for c in (0, 1, 2, 4, 8)}
+    tier_ms = {c: round(eng.tier_ms(c), 4) for c in (0, 1, 2, 4, 8)}
 
     cpu = None
     if rank == 0 and args.cpu_sample_keys > 0:
@@ -182,7 +183,8 @@ def main():
             "detail": {
                 "final_state": {"observed": sizes[0], "masked": sizes[1], "removal_rows": sizes[2]},
                 "extra_effects": n_extra,
-                "overflow_keys_by_class": overflow,
+                "keys_handed_on_by_tier": overflow,
+                "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),
             },
         }

@@ -100,9 +100,12 @@ int ccrdt_device_synchronize(void);
  * the last batch (all register classes) — the dominant kernel whose roofline
  * bench.py reports. */
 int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms);
-/* Keys that overflowed register class `slot_class` (2,4,8,16) in the last
- * topk_rmv batch and were re-run in the next class. */
-int ccrdt_engine_overflow_keys(ccrdt_engine* e, int slot_class, int64_t* n);
+/* Keys handed on by tier `t` of the last topk_rmv batch: t = 0 / 1 are the
+ * per-player-parallel kernels (LDS / HBM slabs), t = 2,4,8,16 the register
+ * classes of the sequential kernel. */
+int ccrdt_engine_overflow_keys(ccrdt_engine* e, int t, int64_t* n);
+/* Kernel time (HIP events) of tier `t` in the last topk_rmv batch. */
+int ccrdt_engine_tier_ms(ccrdt_engine* e, int t, float* ms);
 
 /* Event timing on the engine stream (for bench.py; HIP events). */
 int ccrdt_timer_start(ccrdt_engine* e);
