@@ -52,6 +52,32 @@ class TrmvState(C.Structure):
                 ("min_id", P), ("min_score", P), ("min_ts", P), ("min_dc", P)]
 
 
+class AvgOps(C.Structure):
+    _fields_ = [("n_ops", I64), ("key_ptr", P), ("value", P), ("n", P)]
+
+
+class TopkOps(C.Structure):
+    _fields_ = [("n_ops", I64), ("key_ptr", P), ("id", P), ("score", P)]
+
+
+class LbOps(C.Structure):
+    _fields_ = [("n_ops", I64), ("key_ptr", P), ("kind", P), ("id", P), ("score", P)]
+
+
+class LbExtra(C.Structure):
+    _fields_ = [("kind", P), ("id", P), ("score", P)]
+
+
+class LbState(C.Structure):
+    _fields_ = [("obs_ptr", P), ("obs_id", P), ("obs_score", P), ("m_ptr", P), ("m_id", P),
+                ("m_score", P), ("b_ptr", P), ("b_id", P), ("min_valid", P), ("min_id", P),
+                ("min_score", P)]
+
+
+class WcDocs(C.Structure):
+    _fields_ = [("n_docs", I64), ("key_ptr", P), ("doc_off", P), ("bytes", P), ("n_bytes", U64)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/*.h
 SIGNATURES = {
     "ccrdt_is_type": (INT, [INT]),
@@ -84,6 +110,33 @@ SIGNATURES = {
     "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),
+    # average
+    "ccrdt_avg_apply": (INT, [P, C.POINTER(AvgOps)]),
+    "ccrdt_avg_apply_device": (INT, [P, C.POINTER(AvgOps)]),
+    "ccrdt_avg_export": (INT, [P, P, P]),
+    "ccrdt_avg_import": (INT, [P, P, P]),
+    "ccrdt_avg_value": (INT, [P, P, P]),
+    # topk
+    "ccrdt_topk_apply": (INT, [P, C.POINTER(TopkOps)]),
+    "ccrdt_topk_apply_device": (INT, [P, C.POINTER(TopkOps)]),
+    "ccrdt_topk_size": (INT, [P, C.POINTER(I64)]),
+    "ccrdt_topk_export": (INT, [P, P, P, P]),
+    "ccrdt_topk_import": (INT, [P, P, P, P]),
+    "ccrdt_topk_value": (INT, [P, P, P, P]),
+    "ccrdt_topk_downstream": (INT, [P, I64, P, P]),
+    # leaderboard
+    "ccrdt_lb_apply": (INT, [P, C.POINTER(LbOps), C.POINTER(LbExtra)]),
+    "ccrdt_lb_apply_device": (INT, [P, C.POINTER(LbOps)]),
+    "ccrdt_lb_fetch_extra": (INT, [P, C.POINTER(LbExtra)]),
+    "ccrdt_lb_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+    "ccrdt_lb_export": (INT, [P, C.POINTER(LbState)]),
+    "ccrdt_lb_import": (INT, [P, C.POINTER(LbState)]),
+    "ccrdt_lb_downstream": (INT, [P, I64, P, P, P, P, P]),
+    # wordcount / worddocumentcount
+    "ccrdt_wc_apply": (INT, [P, C.POINTER(WcDocs)]),
+    "ccrdt_wc_apply_device": (INT, [P, C.POINTER(WcDocs)]),
+    "ccrdt_wc_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64)]),
+    "ccrdt_wc_export": (INT, [P, P, P, P, P]),
     # ccrdt_gen.h
     "ccrdt_splitmix64": (U64, [U64]),
     "ccrdt_gen_trmv_count": (I64, [I64, U64, INT]),

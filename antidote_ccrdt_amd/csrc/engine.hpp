@@ -13,23 +13,26 @@ struct TrmvBufs {
   DevBuf meta, pl_id, pl_info, pl_slab, m_score, m_ts, m_dc, r_vc, vc;
 };
 
-// Per-type resident state of the simpler CCRDTs (types.hip).
+// Per-type resident state of the other CCRDTs (types_kernels.hip); [2] =
+// ping-pong sides, tcur = side holding the current state.
 struct TypeBufs {
+  int tcur = 0;
   // average: sum[n_keys], num[n_keys]
-  DevBuf avg_sum, avg_num;
-  // topk: per-key open-addressing table (id, score, used flag), capacity per
-  // key in tk_cap (power of two), plus the sorted value/1 output.
-  DevBuf tk_id, tk_score, tk_cnt, tk_off, tk_scratch;
-  uint64_t tk_slots = 0;
-  // leaderboard: per-key register-resident board image (lb_* in types.hip)
-  DevBuf lb_meta, lb_id, lb_score, lb_flag;
-  DevBuf lb_meta2, lb_id2, lb_score2, lb_flag2;
-  uint64_t lb_cap_total = 0;
-  // wordcount / worddocumentcount: global hash table of words
-  DevBuf wc_hash, wc_off, wc_len, wc_cnt, wc_bytes, wc_used, wc_status;
-  uint64_t wc_slots = 0, wc_byte_cap = 0;
-  // scratch
-  DevBuf scratch0, scratch1, scratch2, scratch3;
+  DevBuf avg_sum[2], avg_num[2];
+  // topk: per key a segment (off[k], cnt[k]) of (id, score) entries
+  DevBuf tk_off[2], tk_cnt[2], tk_id[2], tk_score[2];
+  // leaderboard: per board LbMeta + a segment of (id, score, status)
+  DevBuf lb_meta[2], lb_id[2], lb_score[2], lb_st[2];
+  // wordcount / worddocumentcount: word table (open addressing on the
+  // 64-bit word hash) + byte arena of the words
+  DevBuf t_hash[2], t_key[2], t_len[2], t_pos[2], t_arena[2], t_cnt[2];
+  uint64_t t_slots[2] = {0, 0};
+  DevBuf arena, arena_top, d_hash;
+  uint64_t arena_cap = 0;
+  // scratch shared by the types
+  DevBuf caps, part, ovf_a, ovf_b, status, ex_cnt, ex, kp, stage[6];
+  // HBM class of topk / leaderboard (keys beyond the LDS classes)
+  DevBuf hb_off, hb_cap, hb_a, hb_b, hb_c, hb_d;
 };
 
 }  // namespace ccrdt

@@ -1,6 +1,38 @@
-// engine_types.cpp — per-type engine lifecycle (init / reset / clone).
+// engine_types.cpp — per-type engine lifecycle and the C-ABI of average,
+// topk, leaderboard and wordcount/worddocumentcount (include/ccrdt.h).
+// Host code only sizes buffers, launches kernels (types_kernels.hip) and
+// converts canonical images; every update/2 runs on the GPU.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <tuple>
+#include <vector>
+
 #include "common.hpp"
 #include "engine.hpp"
+#include "types_kernels.hpp"
+
+namespace ccrdt {
+int avg_launch_apply(const AvgArgs& a, hipStream_t st);
+int avg_launch_value(const int64_t* sum, const int64_t* num, int64_t n_keys, int fresh, double* out,
+                     uint8_t* defined, hipStream_t st);
+int topk_launch_apply(const TopkArgs& a, int cls, uint64_t n_work, hipStream_t st);
+int topk_launch_value(const TopkValueArgs& a, int cls, uint64_t n_work, hipStream_t st);
+int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st);
+int lb_launch_downstream(const LbDownArgs& a, hipStream_t st);
+int launch_ovf_need(const uint32_t* list, uint64_t n, const uint64_t* key_ptr, const uint32_t* cnt,
+                    uint32_t stride, uint64_t* need, hipStream_t st);
+int launch_caps_scan(const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stride, uint64_t n,
+                     uint64_t* caps, uint64_t* off, uint64_t* part, hipStream_t st);
+int wc_launch_count(const uint64_t* doc_off, const uint8_t* bytes, uint64_t n_docs, uint64_t* ntok,
+                    hipStream_t st);
+int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key, hipStream_t st);
+int wc_launch_insert(const WcArgs& a, hipStream_t st);
+int wc_launch_verify(const WcArgs& a, hipStream_t st);
+int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st);
+int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
+                     const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st);
+}  // namespace ccrdt
 
 using namespace ccrdt;
 
@@ -8,6 +40,22 @@ static int copy_buf(DevBuf& dst, const DevBuf& src, hipStream_t st) {
   if (!src.p) return CCRDT_OK;
   CCRDT_TRY(dst.ensure(src.bytes));
   CCRDT_HIP(hipMemcpyAsync(dst.p, src.p, src.bytes, hipMemcpyDeviceToDevice, st));
+  return CCRDT_OK;
+}
+
+static int h2d(DevBuf& d, const void* src, uint64_t bytes, hipStream_t st) {
+  CCRDT_TRY(d.ensure(bytes));
+  if (bytes) CCRDT_HIP(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
+  return CCRDT_OK;
+}
+
+template <class T>
+static int d2h(std::vector<T>& v, const DevBuf& d, uint64_t n, hipStream_t st) {
+  v.resize(n);
+  if (n) {
+    CCRDT_HIP(hipMemcpyAsync(v.data(), d.p, n * sizeof(T), hipMemcpyDeviceToHost, st));
+    CCRDT_HIP(hipStreamSynchronize(st));
+  }
   return CCRDT_OK;
 }
 
@@ -19,12 +67,19 @@ int ccrdt_engine::init_type() {
 int ccrdt_engine::reset_type() { return CCRDT_OK; }
 
 void ccrdt_engine::release_types() {
-  for (DevBuf* d : {&tb.avg_sum, &tb.avg_num, &tb.tk_id, &tb.tk_score, &tb.tk_cnt, &tb.tk_off,
-                    &tb.tk_scratch, &tb.lb_meta, &tb.lb_id, &tb.lb_score, &tb.lb_flag, &tb.lb_meta2,
-                    &tb.lb_id2, &tb.lb_score2, &tb.lb_flag2, &tb.wc_hash, &tb.wc_off, &tb.wc_len,
-                    &tb.wc_cnt, &tb.wc_bytes, &tb.wc_used, &tb.wc_status, &tb.scratch0, &tb.scratch1,
-                    &tb.scratch2, &tb.scratch3})
+  for (int s = 0; s < 2; ++s) {
+    for (DevBuf* d : {&tb.avg_sum[s], &tb.avg_num[s], &tb.tk_off[s], &tb.tk_cnt[s], &tb.tk_id[s],
+                      &tb.tk_score[s], &tb.lb_meta[s], &tb.lb_id[s], &tb.lb_score[s], &tb.lb_st[s],
+                      &tb.t_hash[s], &tb.t_key[s], &tb.t_len[s], &tb.t_pos[s], &tb.t_arena[s],
+                      &tb.t_cnt[s]})
+      d->release();
+  }
+  for (DevBuf* d : {&tb.hb_off, &tb.hb_cap, &tb.hb_a, &tb.hb_b, &tb.hb_c, &tb.hb_d})
     d->release();
+  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
+                    &tb.status, &tb.ex_cnt, &tb.ex, &tb.kp})
+    d->release();
+  for (auto& d : tb.stage) d.release();
 }
 
 int ccrdt_engine::clone_from(const ccrdt_engine& src) {
@@ -37,35 +92,976 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
     CCRDT_TRY(copy_buf(d.meta, s.meta, stream));
     CCRDT_TRY(copy_buf(d.pl_id, s.pl_id, stream));
     CCRDT_TRY(copy_buf(d.pl_info, s.pl_info, stream));
+    CCRDT_TRY(copy_buf(d.pl_slab, s.pl_slab, stream));
     CCRDT_TRY(copy_buf(d.m_score, s.m_score, stream));
     CCRDT_TRY(copy_buf(d.m_ts, s.m_ts, stream));
     CCRDT_TRY(copy_buf(d.m_dc, s.m_dc, stream));
-    CCRDT_TRY(copy_buf(d.pl_slab, s.pl_slab, stream));
     CCRDT_TRY(copy_buf(d.r_vc, s.r_vc, stream));
     CCRDT_TRY(copy_buf(d.vc, s.vc, stream));
   } else {
+    const int c = src.tb.tcur;
+    tb.tcur = c;
     const TypeBufs& s = src.tb;
-    CCRDT_TRY(copy_buf(tb.avg_sum, s.avg_sum, stream));
-    CCRDT_TRY(copy_buf(tb.avg_num, s.avg_num, stream));
-    CCRDT_TRY(copy_buf(tb.tk_id, s.tk_id, stream));
-    CCRDT_TRY(copy_buf(tb.tk_score, s.tk_score, stream));
-    CCRDT_TRY(copy_buf(tb.tk_cnt, s.tk_cnt, stream));
-    CCRDT_TRY(copy_buf(tb.tk_off, s.tk_off, stream));
-    tb.tk_slots = s.tk_slots;
-    CCRDT_TRY(copy_buf(tb.lb_meta, s.lb_meta, stream));
-    CCRDT_TRY(copy_buf(tb.lb_id, s.lb_id, stream));
-    CCRDT_TRY(copy_buf(tb.lb_score, s.lb_score, stream));
-    CCRDT_TRY(copy_buf(tb.lb_flag, s.lb_flag, stream));
-    tb.lb_cap_total = s.lb_cap_total;
-    CCRDT_TRY(copy_buf(tb.wc_hash, s.wc_hash, stream));
-    CCRDT_TRY(copy_buf(tb.wc_off, s.wc_off, stream));
-    CCRDT_TRY(copy_buf(tb.wc_len, s.wc_len, stream));
-    CCRDT_TRY(copy_buf(tb.wc_cnt, s.wc_cnt, stream));
-    CCRDT_TRY(copy_buf(tb.wc_bytes, s.wc_bytes, stream));
-    CCRDT_TRY(copy_buf(tb.wc_used, s.wc_used, stream));
-    tb.wc_slots = s.wc_slots;
-    tb.wc_byte_cap = s.wc_byte_cap;
+    for (auto [dd, ss] : {std::pair<DevBuf*, const DevBuf*>{&tb.avg_sum[c], &s.avg_sum[c]},
+                          {&tb.avg_num[c], &s.avg_num[c]}, {&tb.tk_off[c], &s.tk_off[c]},
+                          {&tb.tk_cnt[c], &s.tk_cnt[c]}, {&tb.tk_id[c], &s.tk_id[c]},
+                          {&tb.tk_score[c], &s.tk_score[c]}, {&tb.lb_meta[c], &s.lb_meta[c]},
+                          {&tb.lb_id[c], &s.lb_id[c]}, {&tb.lb_score[c], &s.lb_score[c]},
+                          {&tb.lb_st[c], &s.lb_st[c]}, {&tb.t_hash[c], &s.t_hash[c]},
+                          {&tb.t_key[c], &s.t_key[c]}, {&tb.t_len[c], &s.t_len[c]},
+                          {&tb.t_pos[c], &s.t_pos[c]}, {&tb.t_arena[c], &s.t_arena[c]},
+                          {&tb.t_cnt[c], &s.t_cnt[c]}, {&tb.arena, &s.arena},
+                          {&tb.arena_top, &s.arena_top}})
+      CCRDT_TRY(copy_buf(*dd, *ss, stream));
+    tb.t_slots[c] = s.t_slots[c];
+    tb.arena_cap = s.arena_cap;
   }
   CCRDT_HIP(hipStreamSynchronize(stream));
   return CCRDT_OK;
 }
+
+static int check_type(ccrdt_engine* e, int type) {
+  if (!e) {
+    set_error("null engine");
+    return CCRDT_EINVAL;
+  }
+  if (e->type != type &&
+      !(type == CCRDT_WORDCOUNT && e->type == CCRDT_WORDDOCUMENTCOUNT)) {
+    set_error("operation does not match the engine's CCRDT type");
+    return CCRDT_ENOSYS;
+  }
+  if (hipSetDevice(e->device) != hipSuccess) {
+    set_error("hipSetDevice failed");
+    return CCRDT_EDEVICE;
+  }
+  return CCRDT_OK;
+}
+
+static int check_csr(const uint64_t* key_ptr, uint64_t nk, uint64_t n) {
+  if (key_ptr[0] != 0 || key_ptr[nk] != n) {
+    set_error("key_ptr must start at 0 and end at the op count");
+    return CCRDT_EINVAL;
+  }
+  for (uint64_t k = 0; k < nk; ++k)
+    if (key_ptr[k + 1] < key_ptr[k]) {
+      set_error("key_ptr not monotone");
+      return CCRDT_EINVAL;
+    }
+  return CCRDT_OK;
+}
+
+static int read_status(ccrdt_engine* e, uint32_t* out2) {
+  CCRDT_HIP(hipMemcpyAsync(e->h_status, e->tb.status.p, 8, hipMemcpyDeviceToHost, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  memcpy(out2, e->h_status, 8);
+  return CCRDT_OK;
+}
+
+// segment offsets off[0..nk] of the new side: caps = cnt (stride) + ops
+static int scan_caps(ccrdt_engine* e, const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stride,
+                     DevBuf& off, uint64_t* total) {
+  const uint64_t nk = (uint64_t)e->n_keys;
+  CCRDT_TRY(e->tb.caps.ensure((nk + 1) * 8));
+  CCRDT_TRY(e->tb.part.ensure(((nk + 255) / 256 + 2) * 8));
+  CCRDT_TRY(off.ensure((nk + 1) * 8));
+  CCRDT_TRY(launch_caps_scan(key_ptr, cnt, stride, nk, e->tb.caps.as<uint64_t>(), off.as<uint64_t>(),
+                             e->tb.part.as<uint64_t>(), e->stream));
+  CCRDT_HIP(hipMemcpyAsync(e->h_status, off.as<uint64_t>() + nk, 8, hipMemcpyDeviceToHost, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  memcpy(total, e->h_status, 8);
+  return CCRDT_OK;
+}
+
+// HBM class for the n keys left in `list`: per key a scratch region of
+// cap = the power of two >= max(64, mult * need) slots, need = ops of the key
+// + cnt[k * stride]; offsets (exclusive scan of the caps) and caps go to
+// tb.hb_off / tb.hb_cap.  *total = sum of the caps.
+static int hbm_regions(ccrdt_engine* e, const uint32_t* list, uint64_t n, const uint64_t* key_ptr,
+                       const uint32_t* cnt, uint32_t stride, uint64_t mult, uint64_t* total) {
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.caps.ensure(n * 8));
+  CCRDT_TRY(launch_ovf_need(list, n, key_ptr, cnt, stride, T.caps.as<uint64_t>(), e->stream));
+  std::vector<uint64_t> need;
+  CCRDT_TRY(d2h(need, T.caps, n, e->stream));
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> cap(n);
+  uint64_t t = 0;
+  for (uint64_t w = 0; w < n; ++w) {
+    uint64_t c = 64;
+    while (c < mult * need[w]) c <<= 1;
+    if (c > (1ull << 31)) {
+      set_error("a key needs more than 2^31 slots in one batch");
+      return CCRDT_ENOMEM;
+    }
+    off[w] = t;
+    cap[w] = (uint32_t)c;
+    t += c;
+  }
+  CCRDT_TRY(h2d(T.hb_off, off.data(), n * 8, e->stream));
+  CCRDT_TRY(h2d(T.hb_cap, cap.data(), n * 4, e->stream));
+  *total = t;
+  return CCRDT_OK;
+}
+
+extern "C" {
+
+// ======================================================================= average
+int ccrdt_avg_apply_device(ccrdt_engine* e, const ccrdt_avg_ops* ops) {
+  CCRDT_TRY(check_type(e, CCRDT_AVERAGE));
+  if (!ops || !ops->key_ptr || (ops->n_ops && (!ops->value || !ops->n))) {
+    set_error("avg_apply: null arrays");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  const int in = T.tcur, out = 1 - T.tcur;
+  const uint64_t nk = (uint64_t)e->n_keys;
+  CCRDT_TRY(T.avg_sum[out].ensure(nk * 8));
+  CCRDT_TRY(T.avg_num[out].ensure(nk * 8));
+  CCRDT_TRY(T.status.ensure(64));
+  CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+  AvgArgs a{};
+  a.n_keys = e->n_keys;
+  a.key_ptr = ops->key_ptr;
+  a.v = ops->value;
+  a.n = ops->n;
+  a.sum_in = T.avg_sum[in].as<int64_t>();
+  a.num_in = T.avg_num[in].as<int64_t>();
+  a.sum_out = T.avg_sum[out].as<int64_t>();
+  a.num_out = T.avg_num[out].as<int64_t>();
+  a.fresh = e->fresh ? 1 : 0;
+  a.status = T.status.as<uint32_t>();
+  CCRDT_HIP(hipEventRecord(e->evk0, e->stream));
+  CCRDT_TRY(avg_launch_apply(a, e->stream));
+  CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
+  uint32_t st[2];
+  CCRDT_TRY(read_status(e, st));
+  CCRDT_HIP(hipEventElapsedTime(&e->last_kernel_ms, e->evk0, e->evk1));
+  if (st[0] & AVG_ERR_NEG) {
+    set_error("avg_apply: {add, {V, N}} with N < 0 (no function clause)");
+    return CCRDT_EINVAL;
+  }
+  if (st[0] & AVG_ERR_RANGE) {
+    set_error("avg_apply: Sum or Num leaves int64");
+    return CCRDT_ERANGE;
+  }
+  T.tcur = out;
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_avg_apply(ccrdt_engine* e, const ccrdt_avg_ops* ops) {
+  CCRDT_TRY(check_type(e, CCRDT_AVERAGE));
+  if (!ops || !ops->key_ptr) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
+  CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(h2d(T.kp, ops->key_ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[0], ops->value, n * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[1], ops->n, n * 8, e->stream));
+  ccrdt_avg_ops d{ops->n_ops, T.kp.as<uint64_t>(), T.stage[0].as<int64_t>(), T.stage[1].as<int64_t>()};
+  return ccrdt_avg_apply_device(e, &d);
+}
+
+int ccrdt_avg_export(ccrdt_engine* e, int64_t* sum, int64_t* num) {
+  CCRDT_TRY(check_type(e, CCRDT_AVERAGE));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  if (e->fresh) {
+    if (sum) memset(sum, 0, nk * 8);
+    if (num) memset(num, 0, nk * 8);
+    return CCRDT_OK;
+  }
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  if (sum && nk) CCRDT_HIP(hipMemcpy(sum, e->tb.avg_sum[e->tb.tcur].p, nk * 8, hipMemcpyDeviceToHost));
+  if (num && nk) CCRDT_HIP(hipMemcpy(num, e->tb.avg_num[e->tb.tcur].p, nk * 8, hipMemcpyDeviceToHost));
+  return CCRDT_OK;
+}
+
+int ccrdt_avg_import(ccrdt_engine* e, const int64_t* sum, const int64_t* num) {
+  CCRDT_TRY(check_type(e, CCRDT_AVERAGE));
+  if (!sum || !num) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys;
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(h2d(T.avg_sum[T.tcur], sum, nk * 8, e->stream));
+  CCRDT_TRY(h2d(T.avg_num[T.tcur], num, nk * 8, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_avg_value(ccrdt_engine* e, double* value, uint8_t* defined) {
+  CCRDT_TRY(check_type(e, CCRDT_AVERAGE));
+  if (!value || !defined) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys;
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.stage[2].ensure(nk * 8));
+  CCRDT_TRY(T.stage[3].ensure(nk));
+  CCRDT_TRY(T.avg_sum[T.tcur].ensure(8));
+  CCRDT_TRY(T.avg_num[T.tcur].ensure(8));
+  CCRDT_TRY(avg_launch_value(T.avg_sum[T.tcur].as<int64_t>(), T.avg_num[T.tcur].as<int64_t>(), e->n_keys,
+                             e->fresh ? 1 : 0, T.stage[2].as<double>(), T.stage[3].as<uint8_t>(),
+                             e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  if (nk) {
+    CCRDT_HIP(hipMemcpy(value, T.stage[2].p, nk * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(defined, T.stage[3].p, nk, hipMemcpyDeviceToHost));
+  }
+  return CCRDT_OK;
+}
+
+// ========================================================================== topk
+int ccrdt_topk_apply_device(ccrdt_engine* e, const ccrdt_topk_ops* ops) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  if (!ops || !ops->key_ptr || (ops->n_ops && (!ops->id || !ops->score))) {
+    set_error("topk_apply: null arrays");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  const int in = T.tcur, out = 1 - T.tcur;
+  const uint64_t nk = (uint64_t)e->n_keys;
+  uint64_t total = 0;
+  CCRDT_TRY(scan_caps(e, ops->key_ptr, e->fresh ? nullptr : T.tk_cnt[in].as<uint32_t>(), 1,
+                      T.tk_off[out], &total));
+  CCRDT_TRY(T.tk_cnt[out].ensure(nk * 4));
+  CCRDT_TRY(T.tk_id[out].ensure(total * 8));
+  CCRDT_TRY(T.tk_score[out].ensure(total * 8));
+  CCRDT_TRY(T.ovf_a.ensure(nk * 4));
+  CCRDT_TRY(T.ovf_b.ensure(nk * 4));
+  CCRDT_TRY(T.status.ensure(64));
+  TopkArgs a{};
+  a.n_keys = e->n_keys;
+  a.key_ptr = ops->key_ptr;
+  a.op_id = ops->id;
+  a.op_score = ops->score;
+  a.off_in = T.tk_off[in].as<uint64_t>();
+  a.cnt_in = T.tk_cnt[in].as<uint32_t>();
+  a.id_in = T.tk_id[in].as<int64_t>();
+  a.score_in = T.tk_score[in].as<int64_t>();
+  a.off_out = T.tk_off[out].as<uint64_t>();
+  a.cnt_out = T.tk_cnt[out].as<uint32_t>();
+  a.id_out = T.tk_id[out].as<int64_t>();
+  a.score_out = T.tk_score[out].as<int64_t>();
+  a.fresh = e->fresh ? 1 : 0;
+  a.status = T.status.as<uint32_t>();
+  uint64_t n_work = nk;
+  const uint32_t* list = nullptr;
+  float total_ms = 0.f;
+  for (int cls = 0; cls < 3 && n_work; ++cls) {
+    DevBuf* ovf = (list == T.ovf_a.as<uint32_t>()) ? &T.ovf_b : &T.ovf_a;
+    a.key_list = list;
+    a.ovf_list = ovf->as<uint32_t>();
+    if (cls == 2) {  // HBM hash: cap + 1 slots per key
+      uint64_t slots = 0;
+      CCRDT_TRY(hbm_regions(e, list, n_work, ops->key_ptr, e->fresh ? nullptr : a.cnt_in, 1, 2, &slots));
+      slots += n_work;
+      CCRDT_TRY(T.hb_a.ensure(slots * 8));
+      CCRDT_TRY(T.hb_b.ensure(slots * 4));
+      a.tab_off = T.hb_off.as<uint64_t>();
+      a.tab_cap = T.hb_cap.as<uint32_t>();
+      a.g_id = T.hb_a.as<int64_t>();
+      a.g_seq = T.hb_b.as<int32_t>();
+    }
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+    CCRDT_HIP(hipEventRecord(e->evk0, e->stream));
+    CCRDT_TRY(topk_launch_apply(a, cls, n_work, e->stream));
+    CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
+    uint32_t st[2];
+    CCRDT_TRY(read_status(e, st));
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, e->evk0, e->evk1));
+    total_ms += ms;
+    n_work = st[0];
+    list = ovf->as<uint32_t>();
+  }
+  e->last_kernel_ms = total_ms;
+  T.tcur = out;
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_apply(ccrdt_engine* e, const ccrdt_topk_ops* ops) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  if (!ops || !ops->key_ptr) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
+  CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(h2d(T.kp, ops->key_ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[0], ops->id, n * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[1], ops->score, n * 8, e->stream));
+  ccrdt_topk_ops d{ops->n_ops, T.kp.as<uint64_t>(), T.stage[0].as<int64_t>(), T.stage[1].as<int64_t>()};
+  return ccrdt_topk_apply_device(e, &d);
+}
+
+namespace {
+struct TopkHost {
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> cnt;
+  std::vector<int64_t> id, score;
+};
+int topk_download(ccrdt_engine* e, TopkHost& h) {
+  const uint64_t nk = (uint64_t)e->n_keys;
+  h.cnt.assign(nk, 0);
+  h.off.assign(nk + 1, 0);
+  if (e->fresh || !nk) return CCRDT_OK;
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  CCRDT_TRY(d2h(h.off, T.tk_off[c], nk + 1, e->stream));
+  CCRDT_TRY(d2h(h.cnt, T.tk_cnt[c], nk, e->stream));
+  const uint64_t n = std::min(T.tk_id[c].bytes, T.tk_score[c].bytes) / 8;
+  CCRDT_TRY(d2h(h.id, T.tk_id[c], n, e->stream));
+  CCRDT_TRY(d2h(h.score, T.tk_score[c], n, e->stream));
+  return CCRDT_OK;
+}
+}  // namespace
+
+int ccrdt_topk_size(ccrdt_engine* e, int64_t* n_entries) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  int64_t s = 0;
+  if (!e->fresh && nk) {
+    std::vector<uint32_t> cnt;
+    CCRDT_TRY(d2h(cnt, e->tb.tk_cnt[e->tb.tcur], nk, e->stream));
+    for (uint32_t c : cnt) s += c;
+  }
+  *n_entries = s;
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_export(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  TopkHost h;
+  CCRDT_TRY(topk_download(e, h));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  std::vector<std::pair<int64_t, int64_t>> v;
+  uint64_t p = 0;
+  ptr[0] = 0;
+  for (uint64_t k = 0; k < nk; ++k) {
+    v.clear();
+    for (uint32_t j = 0; j < h.cnt[k]; ++j) v.push_back({h.id[h.off[k] + j], h.score[h.off[k] + j]});
+    std::sort(v.begin(), v.end());
+    for (auto& [i, s] : v) {
+      id[p] = i;
+      score[p++] = s;
+    }
+    ptr[k + 1] = p;
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_import(ccrdt_engine* e, const uint64_t* ptr, const int64_t* id, const int64_t* score) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  TypeBufs& T = e->tb;
+  std::vector<uint32_t> cnt(nk);
+  for (uint64_t k = 0; k < nk; ++k) {
+    cnt[k] = (uint32_t)(ptr[k + 1] - ptr[k]);
+    std::vector<int64_t> ids(id + ptr[k], id + ptr[k + 1]);
+    std::sort(ids.begin(), ids.end());
+    if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) {
+      set_error("topk_import: duplicate Id in a key");
+      return CCRDT_EINVAL;
+    }
+  }
+  const int c = T.tcur;
+  CCRDT_TRY(h2d(T.tk_off[c], ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.tk_cnt[c], cnt.data(), nk * 4, e->stream));
+  CCRDT_TRY(h2d(T.tk_id[c], id, ptr[nk] * 8, e->stream));
+  CCRDT_TRY(h2d(T.tk_score[c], score, ptr[nk] * 8, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_value(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  if (e->fresh || !nk) {
+    for (uint64_t k = 0; k <= nk; ++k) ptr[k] = 0;
+    return CCRDT_OK;
+  }
+  uint64_t total = 0;
+  CCRDT_TRY(scan_caps(e, nullptr, T.tk_cnt[c].as<uint32_t>(), 1, T.stage[4], &total));
+  CCRDT_TRY(T.stage[2].ensure(total * 8 + 8));
+  CCRDT_TRY(T.stage[3].ensure(total * 8 + 8));
+  CCRDT_TRY(T.ovf_a.ensure(nk * 4));
+  CCRDT_TRY(T.ovf_b.ensure(nk * 4));
+  CCRDT_TRY(T.status.ensure(64));
+  TopkValueArgs a{};
+  a.off = T.tk_off[c].as<uint64_t>();
+  a.cnt = T.tk_cnt[c].as<uint32_t>();
+  a.id = T.tk_id[c].as<int64_t>();
+  a.score = T.tk_score[c].as<int64_t>();
+  a.out_ptr = T.stage[4].as<uint64_t>();
+  a.out_id = T.stage[2].as<int64_t>();
+  a.out_score = T.stage[3].as<int64_t>();
+  a.status = T.status.as<uint32_t>();
+  uint64_t n_work = nk;
+  const uint32_t* list = nullptr;
+  for (int cls = 0; cls < 3 && n_work; ++cls) {
+    DevBuf* ovf = (list == T.ovf_a.as<uint32_t>()) ? &T.ovf_b : &T.ovf_a;
+    a.key_list = list;
+    a.ovf_list = ovf->as<uint32_t>();
+    if (cls == 2) {  // HBM bitonic sort regions
+      uint64_t slots = 0;
+      CCRDT_TRY(hbm_regions(e, list, n_work, nullptr, a.cnt, 1, 1, &slots));
+      CCRDT_TRY(T.hb_a.ensure(slots * 8));
+      CCRDT_TRY(T.hb_b.ensure(slots * 8));
+      a.tab_off = T.hb_off.as<uint64_t>();
+      a.tab_cap = T.hb_cap.as<uint32_t>();
+      a.g_id = T.hb_a.as<int64_t>();
+      a.g_score = T.hb_b.as<int64_t>();
+    }
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+    CCRDT_TRY(topk_launch_value(a, cls, n_work, e->stream));
+    uint32_t st[2];
+    CCRDT_TRY(read_status(e, st));
+    n_work = st[0];
+    list = ovf->as<uint32_t>();
+  }
+  CCRDT_HIP(hipMemcpy(ptr, T.stage[4].p, (nk + 1) * 8, hipMemcpyDeviceToHost));
+  if (total) {
+    CCRDT_HIP(hipMemcpy(id, T.stage[2].p, total * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(score, T.stage[3].p, total * 8, hipMemcpyDeviceToHost));
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_downstream(ccrdt_engine* e, int64_t n, const int64_t* score, uint8_t* out_kind) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  // changes_state/2 (topk.erl:164-166) compares the op's Score with Size
+  // only; no state is read.
+  for (int64_t i = 0; i < n; ++i) out_kind[i] = score[i] > e->k ? 0 : CCRDT_NOOP;
+  return CCRDT_OK;
+}
+
+// =================================================================== leaderboard
+int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* ops) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  if (!ops || !ops->key_ptr || (ops->n_ops && (!ops->kind || !ops->id || !ops->score))) {
+    set_error("lb_apply: null arrays");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  const int in = T.tcur, out = 1 - T.tcur;
+  const uint64_t nk = (uint64_t)e->n_keys, n_ops = (uint64_t)ops->n_ops;
+  uint64_t total = 0;
+  CCRDT_TRY(T.stage[5].ensure((nk + 1) * 8));
+  CCRDT_TRY(scan_caps(e, ops->key_ptr,
+                      e->fresh ? nullptr : (const uint32_t*)T.lb_meta[in].as<LbMeta>() + 1, 4,
+                      T.stage[5], &total));
+  if (total >= 0xFFFFFFFFull) {
+    set_error("lb_apply: resident entries would exceed 2^32");
+    return CCRDT_ENOMEM;
+  }
+  CCRDT_TRY(T.lb_meta[out].ensure(nk * sizeof(LbMeta)));
+  CCRDT_TRY(T.lb_id[out].ensure(total * 8));
+  CCRDT_TRY(T.lb_score[out].ensure(total * 8));
+  CCRDT_TRY(T.lb_st[out].ensure(total));
+  CCRDT_TRY(T.ex_cnt.ensure(nk * 4));
+  CCRDT_TRY(T.ex.ensure(n_ops * sizeof(LbExtraRec)));
+  CCRDT_TRY(T.ovf_a.ensure(nk * 4));
+  CCRDT_TRY(T.ovf_b.ensure(nk * 4));
+  CCRDT_TRY(T.status.ensure(64));
+  CCRDT_TRY(T.kp.ensure((nk + 1) * 8));
+  LbArgs a{};
+  a.n_keys = e->n_keys;
+  a.k = (uint32_t)std::min<int64_t>(e->k, 0xFFFFFFFFll);
+  a.key_ptr = ops->key_ptr;
+  a.kind = ops->kind;
+  a.id = ops->id;
+  a.score = ops->score;
+  a.meta_in = T.lb_meta[in].as<LbMeta>();
+  a.id_in = T.lb_id[in].as<int64_t>();
+  a.score_in = T.lb_score[in].as<int64_t>();
+  a.st_in = T.lb_st[in].as<uint8_t>();
+  a.meta_out = T.lb_meta[out].as<LbMeta>();
+  a.off_out = T.stage[5].as<uint64_t>();
+  a.id_out = T.lb_id[out].as<int64_t>();
+  a.score_out = T.lb_score[out].as<int64_t>();
+  a.st_out = T.lb_st[out].as<uint8_t>();
+  a.fresh = e->fresh ? 1 : 0;
+  a.ex_cnt = T.ex_cnt.as<uint32_t>();
+  a.ex = T.ex.as<LbExtraRec>();
+  a.status = T.status.as<uint32_t>();
+  uint64_t n_work = nk;
+  const uint32_t* list = nullptr;
+  float total_ms = 0.f;
+  for (int cls = 0; cls < 3 && n_work; ++cls) {
+    DevBuf* ovf = (list == T.ovf_a.as<uint32_t>()) ? &T.ovf_b : &T.ovf_a;
+    a.key_list = list;
+    a.ovf_list = ovf->as<uint32_t>();
+    if (cls == 2) {  // HBM boards: entries + a 2x hash per board
+      uint64_t slots = 0;
+      CCRDT_TRY(hbm_regions(e, list, n_work, ops->key_ptr,
+                            e->fresh ? nullptr : (const uint32_t*)a.meta_in + 1, 4, 1, &slots));
+      CCRDT_TRY(T.hb_a.ensure(slots * 8));
+      CCRDT_TRY(T.hb_b.ensure(slots * 8));
+      CCRDT_TRY(T.hb_c.ensure(slots));
+      CCRDT_TRY(T.hb_d.ensure(slots * 8));
+      a.tab_off = T.hb_off.as<uint64_t>();
+      a.tab_cap = T.hb_cap.as<uint32_t>();
+      a.g_eid = T.hb_a.as<int64_t>();
+      a.g_esc = T.hb_b.as<int64_t>();
+      a.g_est = T.hb_c.as<uint8_t>();
+      a.g_hslot = T.hb_d.as<uint32_t>();
+    }
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+    CCRDT_HIP(hipEventRecord(e->evk0, e->stream));
+    CCRDT_TRY(lb_launch_apply(a, cls, n_work, e->stream));
+    CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
+    uint32_t st[2];
+    CCRDT_TRY(read_status(e, st));
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, e->evk0, e->evk1));
+    total_ms += ms;
+    if (st[1]) {
+      set_error("lb_apply: effect kind > 2 (no function clause)");
+      return CCRDT_EINVAL;
+    }
+    n_work = st[0];
+    list = ovf->as<uint32_t>();
+  }
+  CCRDT_HIP(hipMemcpyAsync(T.kp.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice, e->stream));
+  e->last_kernel_ms = total_ms;
+  e->last_n_ops = n_ops;
+  T.tcur = out;
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_fetch_extra(ccrdt_engine* e, ccrdt_lb_extra* x) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  const uint64_t nk = (uint64_t)e->n_keys, n = e->last_n_ops;
+  if (x->kind)
+    for (uint64_t i = 0; i < n; ++i) x->kind[i] = CCRDT_NOOP;
+  if (!n || !nk) return CCRDT_OK;
+  std::vector<uint32_t> cnt;
+  std::vector<uint64_t> kp;
+  std::vector<LbExtraRec> rec;
+  CCRDT_TRY(d2h(cnt, e->tb.ex_cnt, nk, e->stream));
+  CCRDT_TRY(d2h(kp, e->tb.kp, nk + 1, e->stream));
+  CCRDT_TRY(d2h(rec, e->tb.ex, n, e->stream));
+  for (uint64_t k = 0; k < nk; ++k)
+    for (uint32_t j = 0; j < cnt[k]; ++j) {
+      const LbExtraRec& r = rec[kp[k] + j];
+      if (r.op >= n) continue;
+      if (x->kind) x->kind[r.op] = CCRDT_LB_ADD;
+      if (x->id) x->id[r.op] = r.id;
+      if (x->score) x->score[r.op] = r.score;
+    }
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_apply(ccrdt_engine* e, const ccrdt_lb_ops* ops, ccrdt_lb_extra* extra) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  if (!ops || !ops->key_ptr) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
+  CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(h2d(T.stage[0], ops->key_ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[1], ops->kind, n, e->stream));
+  CCRDT_TRY(h2d(T.stage[2], ops->id, n * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[3], ops->score, n * 8, e->stream));
+  ccrdt_lb_ops d{ops->n_ops, T.stage[0].as<uint64_t>(), T.stage[1].as<uint8_t>(), T.stage[2].as<int64_t>(),
+                 T.stage[3].as<int64_t>()};
+  CCRDT_TRY(ccrdt_lb_apply_device(e, &d));
+  if (extra) CCRDT_TRY(ccrdt_lb_fetch_extra(e, extra));
+  return CCRDT_OK;
+}
+
+namespace {
+struct LbHost {
+  std::vector<LbMeta> meta;
+  std::vector<int64_t> id, score;
+  std::vector<uint8_t> st;
+};
+int lb_download(ccrdt_engine* e, LbHost& h) {
+  const uint64_t nk = (uint64_t)e->n_keys;
+  h.meta.assign(nk, LbMeta{0, 0, 0, 0xFFFFFFFFu});
+  if (e->fresh || !nk) return CCRDT_OK;
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  CCRDT_TRY(d2h(h.meta, T.lb_meta[c], nk, e->stream));
+  const uint64_t n = std::min({T.lb_id[c].bytes / 8, T.lb_score[c].bytes / 8, T.lb_st[c].bytes});
+  CCRDT_TRY(d2h(h.id, T.lb_id[c], n, e->stream));
+  CCRDT_TRY(d2h(h.score, T.lb_score[c], n, e->stream));
+  CCRDT_TRY(d2h(h.st, T.lb_st[c], n, e->stream));
+  return CCRDT_OK;
+}
+}  // namespace
+
+int ccrdt_lb_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  LbHost h;
+  CCRDT_TRY(lb_download(e, h));
+  int64_t o = 0, m = 0, b = 0;
+  for (const LbMeta& mt : h.meta)
+    for (uint32_t j = 0; j < mt.n; ++j) {
+      const uint8_t s = h.st[mt.off + j];
+      o += s == LB_OBS;
+      m += s == LB_MASKED;
+      b += s == LB_BANNED;
+    }
+  *n_obs = o;
+  *n_masked = m;
+  *n_bans = b;
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_export(ccrdt_engine* e, ccrdt_lb_state* out) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  LbHost h;
+  CCRDT_TRY(lb_download(e, h));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  uint64_t po = 0, pm = 0, pb = 0;
+  out->obs_ptr[0] = out->m_ptr[0] = out->b_ptr[0] = 0;
+  std::vector<std::pair<int64_t, int64_t>> o, m;
+  std::vector<int64_t> b;
+  for (uint64_t k = 0; k < nk; ++k) {
+    const LbMeta& mt = h.meta[k];
+    o.clear();
+    m.clear();
+    b.clear();
+    for (uint32_t j = 0; j < mt.n; ++j) {
+      const uint64_t g = (uint64_t)mt.off + j;
+      if (h.st[g] == LB_OBS) o.push_back({h.id[g], h.score[g]});
+      else if (h.st[g] == LB_MASKED) m.push_back({h.id[g], h.score[g]});
+      else b.push_back(h.id[g]);
+    }
+    std::sort(o.begin(), o.end());
+    std::sort(m.begin(), m.end());
+    std::sort(b.begin(), b.end());
+    for (auto& [i, s] : o) {
+      out->obs_id[po] = i;
+      out->obs_score[po++] = s;
+    }
+    for (auto& [i, s] : m) {
+      out->m_id[pm] = i;
+      out->m_score[pm++] = s;
+    }
+    for (int64_t i : b) out->b_id[pb++] = i;
+    out->obs_ptr[k + 1] = po;
+    out->m_ptr[k + 1] = pm;
+    out->b_ptr[k + 1] = pb;
+    const bool mv = mt.minq != 0xFFFFFFFFu;
+    out->min_valid[k] = mv;
+    out->min_id[k] = mv ? h.id[mt.off + mt.minq] : 0;
+    out->min_score[k] = mv ? h.score[mt.off + mt.minq] : 0;
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_import(ccrdt_engine* e, const ccrdt_lb_state* in) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  std::vector<LbMeta> meta(nk);
+  std::vector<int64_t> id, score;
+  std::vector<uint8_t> st;
+  for (uint64_t k = 0; k < nk; ++k) {
+    LbMeta m{(uint32_t)id.size(), 0, 0, 0xFFFFFFFFu};
+    std::vector<int64_t> all;
+    auto put = [&](int64_t i, int64_t s, uint8_t t) {
+      id.push_back(i);
+      score.push_back(s);
+      st.push_back(t);
+      all.push_back(i);
+    };
+    for (uint64_t j = in->obs_ptr[k]; j < in->obs_ptr[k + 1]; ++j) put(in->obs_id[j], in->obs_score[j], LB_OBS);
+    for (uint64_t j = in->m_ptr[k]; j < in->m_ptr[k + 1]; ++j) put(in->m_id[j], in->m_score[j], LB_MASKED);
+    for (uint64_t j = in->b_ptr[k]; j < in->b_ptr[k + 1]; ++j) put(in->b_id[j], 0, LB_BANNED);
+    std::sort(all.begin(), all.end());
+    if (std::adjacent_find(all.begin(), all.end()) != all.end()) {
+      set_error("lb_import: Observed, Masked and Bans must be disjoint by Id");
+      return CCRDT_EINVAL;
+    }
+    const uint64_t nobs = in->obs_ptr[k + 1] - in->obs_ptr[k];
+    const uint64_t nmask = in->m_ptr[k + 1] - in->m_ptr[k];
+    if ((int64_t)nobs > e->k || (nmask && (int64_t)nobs != e->k)) {
+      set_error("lb_import: |Observed| > Size, or Masked non-empty with Observed not full");
+      return CCRDT_EINVAL;
+    }
+    m.n = (uint32_t)(id.size() - m.off);
+    m.nobs = (uint32_t)nobs;
+    if (in->min_valid[k]) {
+      for (uint32_t j = 0; j < nobs; ++j)
+        if (id[m.off + j] == in->min_id[k] && score[m.off + j] == in->min_score[k]) m.minq = j;
+      if (m.minq == 0xFFFFFFFFu) {
+        set_error("lb_import: Min is not an Observed pair");
+        return CCRDT_EINVAL;
+      }
+    } else if (nobs) {
+      set_error("lb_import: Min is nil but Observed is not empty");
+      return CCRDT_EINVAL;
+    }
+    meta[k] = m;
+  }
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  CCRDT_TRY(h2d(T.lb_meta[c], meta.data(), nk * sizeof(LbMeta), e->stream));
+  CCRDT_TRY(h2d(T.lb_id[c], id.data(), id.size() * 8, e->stream));
+  CCRDT_TRY(h2d(T.lb_score[c], score.data(), score.size() * 8, e->stream));
+  CCRDT_TRY(h2d(T.lb_st[c], st.data(), st.size(), e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,
+                        const int64_t* id, const int64_t* score, uint8_t* out_kind) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  if (n <= 0) return CCRDT_OK;
+  for (int64_t i = 0; i < n; ++i)
+    if (key[i] >= (uint64_t)e->n_keys || op[i] > 1) {
+      set_error("lb_downstream: bad key or op");
+      return CCRDT_EINVAL;
+    }
+  TypeBufs& T = e->tb;
+  const uint64_t un = (uint64_t)n;
+  CCRDT_TRY(h2d(T.stage[0], key, un * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[1], op, un, e->stream));
+  CCRDT_TRY(h2d(T.stage[2], id, un * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[3], score, un * 8, e->stream));
+  CCRDT_TRY(T.stage[4].ensure(un));
+  const int c = T.tcur;
+  for (DevBuf* d : {&T.lb_meta[c], &T.lb_id[c], &T.lb_score[c], &T.lb_st[c]}) CCRDT_TRY(d->ensure(8));
+  LbDownArgs a{};
+  a.n = n;
+  a.k = (uint32_t)std::min<int64_t>(e->k, 0xFFFFFFFFll);
+  a.key = T.stage[0].as<uint64_t>();
+  a.op = T.stage[1].as<uint8_t>();
+  a.id = T.stage[2].as<int64_t>();
+  a.score = T.stage[3].as<int64_t>();
+  a.out = T.stage[4].as<uint8_t>();
+  a.meta = T.lb_meta[c].as<LbMeta>();
+  a.eid = T.lb_id[c].as<int64_t>();
+  a.escore = T.lb_score[c].as<int64_t>();
+  a.est = T.lb_st[c].as<uint8_t>();
+  a.fresh = e->fresh ? 1 : 0;
+  CCRDT_TRY(lb_launch_downstream(a, e->stream));
+  CCRDT_HIP(hipMemcpyAsync(out_kind, T.stage[4].p, un, hipMemcpyDeviceToHost, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  return CCRDT_OK;
+}
+
+// ============================================== wordcount / worddocumentcount
+static uint64_t pow2_at_least(uint64_t x) {
+  uint64_t p = 1024;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+static WcArgs wc_table_args(ccrdt_engine* e, int side) {
+  TypeBufs& T = e->tb;
+  WcArgs a{};
+  a.n_keys = e->n_keys;
+  a.wdc = e->type == CCRDT_WORDDOCUMENTCOUNT;
+  a.t_hash = T.t_hash[side].as<uint64_t>();
+  a.t_key = T.t_key[side].as<uint32_t>();
+  a.t_len = T.t_len[side].as<uint32_t>();
+  a.t_pos = T.t_pos[side].as<uint64_t>();
+  a.t_arena = T.t_arena[side].as<uint64_t>();
+  a.t_cnt = T.t_cnt[side].as<unsigned long long>();
+  a.t_mask = T.t_slots[side] ? T.t_slots[side] - 1 : 0;
+  a.arena = T.arena.as<uint8_t>();
+  a.status = T.status.as<uint32_t>();
+  return a;
+}
+
+static int wc_alloc_table(ccrdt_engine* e, int side, uint64_t slots) {
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.t_hash[side].ensure(slots * 8));
+  CCRDT_TRY(T.t_key[side].ensure(slots * 4));
+  CCRDT_TRY(T.t_len[side].ensure(slots * 4));
+  CCRDT_TRY(T.t_pos[side].ensure(slots * 8));
+  CCRDT_TRY(T.t_arena[side].ensure(slots * 8));
+  CCRDT_TRY(T.t_cnt[side].ensure(slots * 8));
+  CCRDT_HIP(hipMemsetAsync(T.t_hash[side].p, 0, slots * 8, e->stream));
+  CCRDT_HIP(hipMemsetAsync(T.t_cnt[side].p, 0, slots * 8, e->stream));
+  T.t_slots[side] = slots;
+  return CCRDT_OK;
+}
+
+int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (!docs || !docs->key_ptr || !docs->doc_off || (docs->n_bytes && !docs->bytes)) {
+    set_error("wc_apply: null arrays");
+    return CCRDT_EINVAL;
+  }
+  if (e->n_keys > 0xFFFFFFFFll) return CCRDT_EINVAL;
+  TypeBufs& T = e->tb;
+  const uint64_t nd = (uint64_t)docs->n_docs, nk = (uint64_t)e->n_keys;
+  CCRDT_TRY(T.status.ensure(64));
+  CCRDT_TRY(T.arena_top.ensure(16));
+  if (e->fresh) {
+    CCRDT_HIP(hipMemsetAsync(T.arena_top.p, 0, 16, e->stream));
+    T.t_slots[T.tcur] = 0;
+  }
+  // document keys and token counts
+  CCRDT_TRY(T.stage[0].ensure(nd * 8 + 8));
+  CCRDT_TRY(T.stage[1].ensure(nd * 8 + 8));
+  CCRDT_TRY(wc_launch_doc_key(docs->key_ptr, nk, T.stage[0].as<uint64_t>(), e->stream));
+  CCRDT_TRY(wc_launch_count(docs->doc_off, docs->bytes, nd, T.stage[1].as<uint64_t>(), e->stream));
+  std::vector<uint64_t> ntok;
+  CCRDT_TRY(d2h(ntok, T.stage[1], nd, e->stream));
+  uint64_t tokens = 0;
+  for (uint64_t t : ntok) tokens += t;
+  std::vector<uint64_t> top;
+  CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
+  const uint64_t words_old = e->fresh ? 0 : top[1], arena_used = e->fresh ? 0 : top[0];
+  // arena: room for every byte of the batch (upper bound of new word bytes)
+  if (arena_used + docs->n_bytes > T.arena_cap) {
+    DevBuf grown;
+    const uint64_t cap = std::max<uint64_t>(2 * (arena_used + docs->n_bytes), 4096);
+    CCRDT_TRY(grown.ensure(cap));
+    if (arena_used)
+      CCRDT_HIP(hipMemcpyAsync(grown.p, T.arena.p, arena_used, hipMemcpyDeviceToDevice, e->stream));
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    T.arena.release();
+    T.arena = grown;
+    grown.p = nullptr;
+    T.arena_cap = cap;
+  }
+  const int in = T.tcur, out = 1 - T.tcur;
+  uint64_t slots = pow2_at_least(2 * (words_old + std::min<uint64_t>(tokens, 1ull << 22)));
+  for (int attempt = 0;; ++attempt) {
+    // new table (rehash of the current words), then the batch
+    CCRDT_TRY(wc_alloc_table(e, out, slots));
+    WcArgs a = wc_table_args(e, out);
+    if (!e->fresh && T.t_slots[in])
+      CCRDT_TRY(wc_launch_rehash(T.t_hash[in].as<uint64_t>(), T.t_key[in].as<uint32_t>(),
+                                 T.t_len[in].as<uint32_t>(), T.t_arena[in].as<uint64_t>(),
+                                 T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+    a.doc_off = docs->doc_off;
+    a.bytes = docs->bytes;
+    a.n_bytes = docs->n_bytes;
+    CCRDT_HIP(hipEventRecord(e->evk0, e->stream));
+    // worddocumentcount: the per-document dedupe table is sized by the
+    // chunk's tokens; documents are processed in chunks of <= 2^27 tokens
+    uint64_t d0 = 0;
+    while (d0 < nd) {
+      uint64_t d1 = d0, tk = 0;
+      while (d1 < nd && (d1 == d0 || tk + ntok[d1] <= (1ull << 27))) tk += ntok[d1++];
+      a.n_docs = (int64_t)(d1 - d0);
+      a.doc_key = T.stage[0].as<uint64_t>() + d0;
+      a.doc_off = docs->doc_off + d0;
+      if (a.wdc) {
+        const uint64_t ds = pow2_at_least(2 * tk);
+        CCRDT_TRY(T.d_hash.ensure(ds * 8));
+        CCRDT_HIP(hipMemsetAsync(T.d_hash.p, 0, ds * 8, e->stream));
+        a.d_hash = T.d_hash.as<uint64_t>();
+        a.d_mask = ds - 1;
+      }
+      CCRDT_TRY(wc_launch_insert(a, e->stream));
+      d0 = d1;
+    }
+    CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
+    uint32_t st[2];
+    CCRDT_TRY(read_status(e, st));
+    CCRDT_HIP(hipEventElapsedTime(&e->last_kernel_ms, e->evk0, e->evk1));
+    if (st[0] && attempt < 4) {  // table (or dedupe table) too small
+      slots *= 4;
+      continue;
+    }
+    if (st[0]) {
+      set_error("wc_apply: word table overflow");
+      return CCRDT_ENOMEM;
+    }
+    // exactness: every token equals its word's representative
+    a.doc_key = T.stage[0].as<uint64_t>();
+    a.doc_off = docs->doc_off;
+    a.n_docs = (int64_t)nd;
+    CCRDT_TRY(wc_launch_verify(a, e->stream));
+    CCRDT_TRY(read_status(e, st));
+    if (st[1]) {
+      set_error(st[1] & 1 ? "wc_apply: 64-bit word hash collision between distinct words"
+                          : "wc_apply: token lost (table overflow)");
+      return CCRDT_ERANGE;
+    }
+    CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
+    CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    break;
+  }
+  T.tcur = out;
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (!docs || !docs->key_ptr || !docs->doc_off) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys, nd = (uint64_t)docs->n_docs;
+  CCRDT_TRY(check_csr(docs->key_ptr, nk, nd));
+  if (docs->doc_off[0] != 0 || docs->doc_off[nd] != docs->n_bytes) {
+    set_error("wc_apply: doc_off must start at 0 and end at n_bytes");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(h2d(T.kp, docs->key_ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[2], docs->doc_off, (nd + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[3], docs->bytes, docs->n_bytes, e->stream));
+  CCRDT_TRY(T.stage[3].ensure(8));
+  ccrdt_wc_docs d{docs->n_docs, T.kp.as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[3].as<uint8_t>(),
+                  docs->n_bytes};
+  return ccrdt_wc_apply_device(e, &d);
+}
+
+int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (e->fresh) {
+    *n_words = *n_bytes = 0;
+    return CCRDT_OK;
+  }
+  std::vector<uint64_t> top;
+  CCRDT_TRY(d2h(top, e->tb.arena_top, 2, e->stream));
+  *n_words = (int64_t)top[1];
+  *n_bytes = (int64_t)top[0];
+  return CCRDT_OK;
+}
+
+int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint8_t* word_bytes,
+                    int64_t* count) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  key_ptr[0] = 0;
+  word_off[0] = 0;
+  if (e->fresh) {
+    for (uint64_t k = 0; k < nk; ++k) key_ptr[k + 1] = 0;
+    return CCRDT_OK;
+  }
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  const uint64_t n = T.t_slots[c];
+  std::vector<uint64_t> h, ar, top;
+  std::vector<uint32_t> key, len;
+  std::vector<unsigned long long> cnt;
+  std::vector<uint8_t> arena;
+  CCRDT_TRY(d2h(h, T.t_hash[c], n, e->stream));
+  CCRDT_TRY(d2h(key, T.t_key[c], n, e->stream));
+  CCRDT_TRY(d2h(len, T.t_len[c], n, e->stream));
+  CCRDT_TRY(d2h(ar, T.t_arena[c], n, e->stream));
+  CCRDT_TRY(d2h(cnt, T.t_cnt[c], n, e->stream));
+  CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
+  CCRDT_TRY(d2h(arena, T.arena, top[0], e->stream));
+  std::vector<std::tuple<uint32_t, std::string, uint64_t>> words;
+  for (uint64_t i = 0; i < n; ++i)
+    if (h[i]) words.emplace_back(key[i], std::string((const char*)arena.data() + ar[i], len[i]), cnt[i]);
+  std::sort(words.begin(), words.end());
+  uint64_t w = 0, b = 0, p = 0;
+  for (uint64_t k = 0; k < nk; ++k) {
+    while (p < words.size() && std::get<0>(words[p]) == k) {
+      const std::string& s = std::get<1>(words[p]);
+      memcpy(word_bytes + b, s.data(), s.size());
+      b += s.size();
+      count[w] = (int64_t)std::get<2>(words[p]);
+      word_off[++w] = b;
+      ++p;
+    }
+    key_ptr[k + 1] = w;
+  }
+  return CCRDT_OK;
+}
+
+}  // extern "C"

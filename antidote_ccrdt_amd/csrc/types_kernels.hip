@@ -1,0 +1,1016 @@
+// types_kernels.hip — gfx950 kernels for antidote_ccrdt_average and
+// antidote_ccrdt_topk (update/2 over CSR batches, and topk value/1).
+#include "common.hpp"
+#include "types_kernels.hpp"
+
+namespace ccrdt {
+
+// ===================================================================== average
+// update/2 (src/antidote_ccrdt_average.erl:88-94, add/3 :137-139) for every
+// op of a key: {add,{_,0}} is a no-op (Q14), N < 0 has no clause (EINVAL),
+// otherwise Sum += V, Num += N.  One wave per key, 128-bit partial sums so an
+// int64 overflow of the true (bignum) result is reported (ERANGE), never
+// wrapped.  Integer adds commute, so the result is order-independent.
+struct I128 {
+  uint64_t lo;
+  int64_t hi;
+};
+__device__ __forceinline__ I128 add128(I128 a, I128 b) {
+  I128 r;
+  r.lo = a.lo + b.lo;
+  r.hi = a.hi + b.hi + (r.lo < a.lo ? 1 : 0);
+  return r;
+}
+__device__ __forceinline__ I128 from64(int64_t v) { return I128{(uint64_t)v, v < 0 ? -1 : 0}; }
+__device__ __forceinline__ bool fits64(I128 a) {
+  return (a.hi == 0 && (int64_t)a.lo >= 0) || (a.hi == -1 && (int64_t)a.lo < 0);
+}
+__device__ __forceinline__ I128 wave_sum128(I128 v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    I128 o;
+    o.lo = (uint64_t)shfl64((int64_t)v.lo, lane_id() ^ off);
+    o.hi = shfl64(v.hi, lane_id() ^ off);
+    v = add128(v, o);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64) void avg_apply_kernel(AvgArgs a) {
+  const uint64_t k = blockIdx.x;
+  const uint64_t i0 = a.key_ptr[k], i1 = a.key_ptr[k + 1];
+  I128 s{0, 0}, n{0, 0};
+  uint32_t err = 0;
+  for (uint64_t i = i0 + lane_id(); i < i1; i += 64) {
+    const int64_t nn = a.n[i];
+    if (nn < 0) err |= AVG_ERR_NEG;
+    else if (nn > 0) {
+      s = add128(s, from64(a.v[i]));
+      n = add128(n, from64(nn));
+    }
+  }
+  s = wave_sum128(s);
+  n = wave_sum128(n);
+  if (ballot(err != 0)) {
+    if (err) atomicOr(a.status, err);
+    return;
+  }
+  if (lane_id() == 0) {
+    const I128 s2 = add128(s, from64(a.fresh ? 0 : a.sum_in[k]));
+    const I128 n2 = add128(n, from64(a.fresh ? 0 : a.num_in[k]));
+    if (!fits64(s2) || !fits64(n2)) {
+      atomicOr(a.status, AVG_ERR_RANGE);
+      return;
+    }
+    a.sum_out[k] = (int64_t)s2.lo;
+    a.num_out[k] = (int64_t)n2.lo;
+  }
+}
+
+// value/1 (:68-70): Sum / Num as IEEE doubles; Num = 0 is badarith.
+__global__ void avg_value_kernel(const int64_t* sum, const int64_t* num, int64_t n_keys, int fresh,
+                                 double* out, uint8_t* defined) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_keys) return;
+  const int64_t s = fresh ? 0 : sum[k], m = fresh ? 0 : num[k];
+  defined[k] = m != 0;
+  out[k] = m != 0 ? (double)s / (double)m : 0.0;
+}
+
+// ======================================================================= topk
+// update/2 (src/antidote_ccrdt_topk.erl:100-104): {add,{Id,Score}} is
+// maps:put — last writer wins, no bound (Q10); {add_map, M} is maps:merge, i.e.
+// the same puts in sequence (flattened by the host).  One wave per key: the
+// key's old entries and the batch's ops go into an LDS hash by Id; each slot
+// keeps the largest op index (atomicMax), so the surviving score is the last
+// writer's.  Surviving entries are written compacted to the new segment.
+template <int HCAP>
+struct TopkLds {
+  int64_t sid[HCAP];   // Id
+  int32_t sseq[HCAP];  // last op index (>= 0) or -(old entry + 2)
+  uint32_t sstate[HCAP];
+  int64_t claim[64];
+};
+
+__device__ __forceinline__ uint32_t tk_hash(int64_t id) {
+  return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 37);
+}
+
+template <int HCAP>
+__device__ __forceinline__ uint32_t tk_slot(TopkLds<HCAP>& L, int64_t id, bool active) {
+  // find or claim the slot of `id` (lanes of one wave insert concurrently)
+  const int lane = lane_id();
+  L.claim[lane] = id;
+  __syncthreads();
+  uint32_t h = tk_hash(id) & (HCAP - 1);
+  bool done = !active;
+  uint32_t slot = 0;
+  while (ballot(!done)) {
+    if (!done) {
+      const uint32_t s = L.sstate[h];
+      if (s == 0u) {
+        if (atomicCAS(&L.sstate[h], 0u, 0x80000000u | (uint32_t)lane) == 0u) {
+          L.sid[h] = id;
+          slot = h;
+          done = true;
+        }
+      } else if (s & 0x80000000u) {
+        if (L.claim[s & 63u] == id) {
+          slot = h;
+          done = true;
+        } else {
+          h = (h + 1) & (HCAP - 1);
+        }
+      } else if (L.sid[h] == id) {
+        slot = h;
+        done = true;
+      } else {
+        h = (h + 1) & (HCAP - 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (active) L.sstate[slot] = 1u;  // published (claims resolved)
+  __syncthreads();
+  return slot;
+}
+
+template <int HCAP>
+__global__ __launch_bounds__(64) void topk_apply_kernel(TopkArgs a) {
+  __shared__ TopkLds<HCAP> L;
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list ? a.key_list[w] : (uint32_t)w;
+  const int lane = lane_id();
+  const uint64_t i0 = a.key_ptr[k], i1 = a.key_ptr[k + 1];
+  const uint32_t nold = a.fresh ? 0u : a.cnt_in[k];
+  const uint64_t off_old = a.fresh ? 0u : a.off_in[k];
+  if ((uint64_t)nold + (i1 - i0) > (uint64_t)(HCAP / 2)) {  // next class
+    if (lane == 0) a.ovf_list[atomicAdd(&a.status[0], 1u)] = k;
+    return;
+  }
+  for (int i = lane; i < HCAP; i += 64) {
+    L.sstate[i] = 0;
+    L.sseq[i] = INT32_MIN;
+  }
+  __syncthreads();
+  for (uint32_t b = 0; b < nold; b += 64) {
+    const uint32_t j = b + lane;
+    const bool act = j < nold;
+    const int64_t id = act ? a.id_in[off_old + j] : 0;
+    const uint32_t s = tk_slot<HCAP>(L, id, act);
+    if (act) L.sseq[s] = -(int32_t)j - 2;
+  }
+  __syncthreads();
+  for (uint64_t b = i0; b < i1; b += 64) {
+    const uint64_t i = b + lane;
+    const bool act = i < i1;
+    const int64_t id = act ? a.op_id[i] : 0;
+    const uint32_t s = tk_slot<HCAP>(L, id, act);
+    if (act) atomicMax(&L.sseq[s], (int32_t)(i - i0));
+  }
+  __syncthreads();
+  // compact surviving entries into the new segment
+  const uint64_t off_new = a.off_out[k];
+  uint32_t n = 0;
+  for (int b = 0; b < HCAP; b += 64) {
+    const int h = b + lane;
+    const bool used = L.sstate[h] != 0u;
+    const uint64_t m = ballot(used);
+    if (used) {
+      const uint64_t dst = off_new + n + mbcnt(m);
+      const int32_t q = L.sseq[h];
+      a.id_out[dst] = L.sid[h];
+      a.score_out[dst] = q >= 0 ? a.op_score[i0 + q] : a.score_in[off_old + (uint32_t)(-q - 2)];
+    }
+    n += (uint32_t)__builtin_popcountll(m);
+  }
+  if (lane == 0) a.cnt_out[k] = n;
+}
+
+// value/1 (topk.erl:81-83): lists:sort by Score desc, then Id desc, of the
+// whole map (not truncated to Size).  One wave per key, bitonic sort in LDS.
+template <int CAP>
+__global__ __launch_bounds__(64) void topk_value_kernel(TopkValueArgs a) {
+  __shared__ int64_t ks[CAP], kid[CAP];
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list ? a.key_list[w] : (uint32_t)w;
+  const int lane = lane_id();
+  const uint32_t n = a.cnt[k];
+  const uint64_t off = a.off[k];
+  if (n > (uint32_t)CAP) {
+    if (lane == 0) a.ovf_list[atomicAdd(a.status, 1u)] = k;
+    return;
+  }
+  uint32_t p2 = 1;
+  while (p2 < n) p2 <<= 1;
+  for (uint32_t j = lane; j < p2; j += 64) {
+    ks[j] = j < n ? a.score[off + j] : INT64_MIN;
+    kid[j] = j < n ? a.id[off + j] : INT64_MIN;
+  }
+  __syncthreads();
+  // descending by (score, id)
+  for (uint32_t size = 2; size <= p2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = lane; t < p2 / 2; t += 64) {
+        const uint32_t lo = 2 * t - (t & (stride - 1));
+        const uint32_t hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const int64_t s0 = ks[lo], s1 = ks[hi], i0 = kid[lo], i1 = kid[hi];
+        const bool gt = s1 > s0 || (s1 == s0 && i1 > i0);  // [hi] sorts before [lo]
+        if (gt == desc) {
+          ks[lo] = s1;
+          ks[hi] = s0;
+          kid[lo] = i1;
+          kid[hi] = i0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t j = lane; j < n; j += 64) {
+    a.out_score[a.out_ptr[k] + j] = ks[j];
+    a.out_id[a.out_ptr[k] + j] = kid[j];
+  }
+}
+
+// Keys beyond the LDS classes (the map is unbounded, Q10): one 256-thread
+// block per key over an HBM hash of tab_cap slots (a power of two >= twice
+// the entries) plus one spare slot for Id == INT64_MIN, which doubles as the
+// empty marker.  Insertion is a 64-bit CAS on the Id itself (lock-free, no
+// claim protocol); the last writer wins by atomicMax on the op index as in
+// the LDS kernel.
+constexpr int TK_HBM_BLOCK = 256;
+__device__ __forceinline__ uint64_t tk_hbm_slot(int64_t* tid, uint64_t cap, int64_t id) {
+  if (id == INT64_MIN) return cap;
+  uint64_t h = ((uint64_t)id * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
+  while (true) {
+    const unsigned long long prev =
+        atomicCAS((unsigned long long*)&tid[h], (unsigned long long)INT64_MIN, (unsigned long long)id);
+    if (prev == (unsigned long long)INT64_MIN || prev == (unsigned long long)id) return h;
+    h = (h + 1) & (cap - 1);
+  }
+}
+
+__global__ __launch_bounds__(TK_HBM_BLOCK) void topk_apply_hbm_kernel(TopkArgs a) {
+  __shared__ uint32_t n_out;
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list[w];
+  const uint64_t i0 = a.key_ptr[k], i1 = a.key_ptr[k + 1];
+  const uint32_t nold = a.fresh ? 0u : a.cnt_in[k];
+  const uint64_t off_old = a.fresh ? 0u : a.off_in[k];
+  const uint64_t cap = a.tab_cap[w];
+  int64_t* tid = a.g_id + a.tab_off[w] + w;  // cap + 1 slots per key
+  int32_t* tseq = a.g_seq + a.tab_off[w] + w;
+  for (uint64_t i = threadIdx.x; i <= cap; i += TK_HBM_BLOCK) {
+    tid[i] = INT64_MIN;
+    tseq[i] = INT32_MIN;
+  }
+  if (threadIdx.x == 0) n_out = 0;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nold; j += TK_HBM_BLOCK)
+    atomicMax(&tseq[tk_hbm_slot(tid, cap, a.id_in[off_old + j])], -(int32_t)j - 2);
+  for (uint64_t i = i0 + threadIdx.x; i < i1; i += TK_HBM_BLOCK)
+    atomicMax(&tseq[tk_hbm_slot(tid, cap, a.op_id[i])], (int32_t)(i - i0));
+  __syncthreads();
+  const uint64_t off_new = a.off_out[k];
+  for (uint64_t b = 0; b <= cap; b += TK_HBM_BLOCK) {
+    const uint64_t h = b + threadIdx.x;
+    const int32_t q = h <= cap ? tseq[h] : INT32_MIN;
+    const bool used = q != INT32_MIN;
+    const uint64_t m = ballot(used);
+    uint32_t base = 0;
+    if (lane_id() == 0 && m) base = atomicAdd(&n_out, (uint32_t)__builtin_popcountll(m));
+    base = rl32(base, 0);
+    if (used) {
+      const uint64_t dst = off_new + base + mbcnt(m);
+      a.id_out[dst] = h == cap ? INT64_MIN : tid[h];
+      a.score_out[dst] = q >= 0 ? a.op_score[i0 + q] : a.score_in[off_old + (uint32_t)(-q - 2)];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.cnt_out[k] = n_out;
+}
+
+// value/1 of keys beyond 4096 entries: bitonic sort of the padded segment in
+// an HBM region (tab_cap = next power of two), one 1024-thread block per key.
+constexpr int TK_SORT_BLOCK = 1024;
+__global__ __launch_bounds__(TK_SORT_BLOCK) void topk_value_hbm_kernel(TopkValueArgs a) {
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list[w];
+  const uint32_t n = a.cnt[k];
+  const uint64_t off = a.off[k];
+  const uint64_t p2 = a.tab_cap[w];
+  int64_t* ks = a.g_score + a.tab_off[w];
+  int64_t* kid = a.g_id + a.tab_off[w];
+  for (uint64_t j = threadIdx.x; j < p2; j += TK_SORT_BLOCK) {
+    ks[j] = j < n ? a.score[off + j] : INT64_MIN;
+    kid[j] = j < n ? a.id[off + j] : INT64_MIN;
+  }
+  __syncthreads();
+  for (uint64_t size = 2; size <= p2; size <<= 1) {
+    for (uint64_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint64_t t = threadIdx.x; t < p2 / 2; t += TK_SORT_BLOCK) {
+        const uint64_t lo = 2 * t - (t & (stride - 1));
+        const uint64_t hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const int64_t s0 = ks[lo], s1 = ks[hi], i0 = kid[lo], i1 = kid[hi];
+        const bool gt = s1 > s0 || (s1 == s0 && i1 > i0);
+        if (gt == desc) {
+          ks[lo] = s1;
+          ks[hi] = s0;
+          kid[lo] = i1;
+          kid[hi] = i0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint64_t j = threadIdx.x; j < n; j += TK_SORT_BLOCK) {
+    a.out_score[a.out_ptr[k] + j] = ks[j];
+    a.out_id[a.out_ptr[k] + j] = kid[j];
+  }
+}
+
+// Per listed key: need[w] = ops of the key + cnt[k * stride] (old entries).
+__global__ void ovf_need_kernel(const uint32_t* list, uint64_t n, const uint64_t* key_ptr, const uint32_t* cnt,
+                                uint32_t stride, uint64_t* need) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n) return;
+  const uint32_t k = list[w];
+  need[w] = (key_ptr ? key_ptr[k + 1] - key_ptr[k] : 0) + (cnt ? cnt[(uint64_t)k * stride] : 0u);
+}
+int launch_ovf_need(const uint32_t* list, uint64_t n, const uint64_t* key_ptr, const uint32_t* cnt,
+                    uint32_t stride, uint64_t* need, hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  hipLaunchKernelGGL(ovf_need_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, list, n, key_ptr,
+                     cnt, stride, need);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// ================================================================ leaderboard
+// update/2 (src/antidote_ccrdt_leaderboard.erl:128-134): add/3 (:215-261)
+// and ban/2 (:264-286) replayed in stream order, one wave per board.  The
+// board's players live in LDS as entries (Id, Score, status) with status
+// Observed / Masked / banned — the reference keeps Observed, Masked and Bans
+// disjoint by Id (Masked non-empty implies Observed full, so the not-full
+// insert of :252-258 never meets a Masked Id) — plus an LDS hash Id -> entry.
+// Min is an entry index; min/1 (:297-303) and get_largest/1 (:306-312) are
+// wave reductions over the entries.
+__device__ __forceinline__ bool lb_cmp(int64_t i1, int64_t s1, int64_t i2, int64_t s2) {
+  return s1 > s2 || (s1 == s2 && i1 > i2);  // cmp/2 (:289-294)
+}
+
+template <int E>
+struct LbLds {
+  int64_t eid[E];
+  int64_t esc[E];
+  uint8_t est[E];
+  uint32_t hslot[2 * E];  // entry + 1, 0 = empty
+};
+
+// The board's storage: LDS (classes 0/1) or an HBM scratch region (class 2,
+// boards beyond 2048 entries); E is a power of two, the hash has 2E slots.
+struct LbView {
+  int64_t* eid;
+  int64_t* esc;
+  uint8_t* est;
+  uint32_t* hslot;
+  uint32_t hmask;  // 2E - 1
+};
+
+__device__ __forceinline__ uint32_t lb_hash(int64_t id) {
+  return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 32);
+}
+
+// wave-uniform lookup: entry index of id or NONE
+__device__ __forceinline__ uint32_t lb_find(const LbView& L, int64_t id, uint32_t& slot_out) {
+  const int lane = lane_id();
+  uint32_t h = lb_hash(id) & L.hmask;
+  while (true) {
+    const uint32_t sl = (h + lane) & L.hmask;
+    const uint32_t s = L.hslot[sl];
+    const uint64_t hit = ballot(s != 0u && L.eid[s - 1] == id);
+    const uint64_t emp = ballot(s == 0u);
+    const int fh = hit ? __builtin_ctzll(hit) : 64, fe = emp ? __builtin_ctzll(emp) : 64;
+    if (fh < fe) {
+      slot_out = (h + fh) & L.hmask;
+      return rl32(s, fh) - 1;
+    }
+    if (fe < 64) {
+      slot_out = (h + fe) & L.hmask;
+      return 0xFFFFFFFFu;
+    }
+    h = (h + 64) & L.hmask;
+  }
+}
+
+__device__ __forceinline__ void lb_recompute_min(const LbView& L, uint32_t n, uint32_t& minq) {
+  const int lane = lane_id();
+  int64_t bs = INT64_MAX, bi = INT64_MAX;
+  uint32_t be = 0xFFFFFFFFu;
+  for (uint32_t j = lane; j < n; j += 64) {
+    if (L.est[j] == LB_OBS) {
+      const int64_t s = L.esc[j], i = L.eid[j];
+      if (be == 0xFFFFFFFFu || lb_cmp(bi, bs, i, s)) {
+        bs = s;
+        bi = i;
+        be = j;
+      }
+    }
+  }
+  const bool has = be != 0xFFFFFFFFu;
+  if (!ballot(has)) {
+    minq = 0xFFFFFFFFu;
+    return;
+  }
+  const int64_t ms = wave_min_i64(has ? bs : INT64_MAX);
+  const int64_t mi = wave_min_i64(has && bs == ms ? bi : INT64_MAX);
+  const uint64_t hit = ballot(has && bs == ms && bi == mi);
+  minq = rl32(be, __builtin_ctzll(hit));
+}
+
+// One board: old entries into L, replay the ops, write the new segment.
+__device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMeta& om, const LbView& L) {
+  const int lane = lane_id();
+  const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
+  for (uint32_t i = lane; i <= L.hmask; i += 64) L.hslot[i] = 0;
+  __syncthreads();
+  for (uint32_t j = lane; j < om.n; j += 64) {
+    const int64_t id = a.id_in[om.off + j];
+    L.eid[j] = id;
+    L.esc[j] = a.score_in[om.off + j];
+    L.est[j] = a.st_in[om.off + j];
+    uint32_t h = lb_hash(id) & L.hmask;
+    while (atomicCAS(&L.hslot[h], 0u, j + 1) != 0u) h = (h + 1) & L.hmask;
+  }
+  __syncthreads();
+  uint32_t n = om.n, nobs = om.nobs, minq = om.minq, nex = 0;
+  for (uint64_t base = op0; base < op1; base += 64) {
+    const uint64_t i = base + lane;
+    const bool v = i < op1;
+    const uint32_t kd = v ? a.kind[i] : 0u;
+    const int64_t oid = v ? a.id[i] : 0, osc = v ? a.score[i] : 0;
+    if (ballot(v && kd > 2)) {
+      if (lane == 0) atomicOr(&a.status[1], LB_ERR_KIND);
+      return;
+    }
+    const int cnt = (int)((op1 - base) < 64 ? (op1 - base) : 64);
+    for (int j = 0; j < cnt; ++j) {
+      const uint32_t kind = rl32(kd, j);
+      const int64_t id = rl64(oid, j);
+      uint32_t slot;
+      uint32_t e = lb_find(L, id, slot);
+      const uint8_t st = e != 0xFFFFFFFFu ? L.est[e] : (uint8_t)0xFF;
+      auto create = [&](uint8_t status, int64_t sc) {
+        e = n++;
+        if (lane == 0) {
+          L.eid[e] = id;
+          L.esc[e] = sc;
+          L.est[e] = status;
+          L.hslot[slot] = e + 1;
+        }
+      };
+      if (kind == 2) {  // ban/2 (:264-286)
+        const bool was_obs = st == LB_OBS;
+        if (e == 0xFFFFFFFFu) create(LB_BANNED, 0);
+        else if (lane == 0) L.est[e] = LB_BANNED;
+        __syncthreads();
+        if (was_obs) {
+          --nobs;
+          // get_largest(Masked) (:306-312)
+          int64_t bs = INT64_MIN, bi = INT64_MIN;
+          uint32_t be = 0xFFFFFFFFu;
+          for (uint32_t q = lane; q < n; q += 64)
+            if (L.est[q] == LB_MASKED && (be == 0xFFFFFFFFu || lb_cmp(L.eid[q], L.esc[q], bi, bs))) {
+              bs = L.esc[q];
+              bi = L.eid[q];
+              be = q;
+            }
+          const bool has = be != 0xFFFFFFFFu;
+          if (ballot(has)) {
+            const int64_t ms = wave_max_i64(has ? bs : INT64_MIN);
+            const int64_t mi = wave_max_i64(has && bs == ms ? bi : INT64_MIN);
+            const uint32_t m = rl32(be, __builtin_ctzll(ballot(has && bs == ms && bi == mi)));
+            if (lane == 0) {
+              L.est[m] = LB_OBS;
+              LbExtraRec r;
+              r.op = (uint32_t)(base + j);
+              r.pad = 0;
+              r.id = mi;
+              r.score = ms;
+              a.ex[op0 + nex] = r;
+            }
+            ++nex;
+            ++nobs;
+            minq = m;  // Min := promoted element (:282, Q15)
+          } else if (minq == e) {
+            __syncthreads();
+            lb_recompute_min(L, n, minq);
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      // add/3 (:215-261)
+      const int64_t sc = rl64(osc, j);
+      if (st == LB_BANNED) continue;
+      if (st == LB_OBS) {
+        if (sc > L.esc[e]) {
+          if (lane == 0) L.esc[e] = sc;
+          __syncthreads();
+          if (minq == e) lb_recompute_min(L, n, minq);
+        }
+        continue;
+      }
+      if (nobs == a.k) {
+        const int64_t mid = L.eid[minq], msc = L.esc[minq];
+        if (lb_cmp(id, sc, mid, msc)) {  // evict Min into Masked (:235-242)
+          if (e == 0xFFFFFFFFu) create(LB_OBS, sc);
+          else if (lane == 0) {
+            L.est[e] = LB_OBS;
+            L.esc[e] = sc;
+          }
+          if (lane == 0) L.est[minq] = LB_MASKED;
+          __syncthreads();
+          lb_recompute_min(L, n, minq);
+        } else if (e == 0xFFFFFFFFu) {  // Masked[Id] := max (:243-250)
+          create(LB_MASKED, sc);
+        } else if (sc > L.esc[e]) {
+          if (lane == 0) L.esc[e] = sc;
+        }
+      } else {  // not full (:252-258)
+        if (e == 0xFFFFFFFFu) create(LB_OBS, sc);
+        else if (lane == 0) {
+          L.est[e] = LB_OBS;
+          L.esc[e] = sc;
+        }
+        ++nobs;
+        if (minq == 0xFFFFFFFFu || lb_cmp(L.eid[minq], L.esc[minq], id, sc)) minq = e;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const uint32_t noff = (uint32_t)a.off_out[k];
+  for (uint32_t j = lane; j < n; j += 64) {
+    a.id_out[noff + j] = L.eid[j];
+    a.score_out[noff + j] = L.esc[j];
+    a.st_out[noff + j] = L.est[j];
+  }
+  if (lane == 0) {
+    LbMeta m{noff, n, nobs, minq};
+    a.meta_out[k] = m;
+    a.ex_cnt[k] = nex;
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
+  __shared__ LbLds<E> S;
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list ? a.key_list[w] : (uint32_t)w;
+  LbMeta om{0, 0, 0, 0xFFFFFFFFu};
+  if (!a.fresh) om = a.meta_in[k];
+  if ((uint64_t)om.n + (a.key_ptr[k + 1] - a.key_ptr[k]) > (uint64_t)E) {
+    if (lane_id() == 0) a.ovf_list[atomicAdd(&a.status[0], 1u)] = k;
+    return;
+  }
+  lb_board(a, k, om, LbView{S.eid, S.esc, S.est, S.hslot, 2 * E - 1});
+}
+
+// Boards beyond the LDS classes: the same replay over an HBM scratch region
+// (entries at tab_off[w], capacity tab_cap[w] >= entries, a power of two).
+__global__ __launch_bounds__(64) void lb_apply_hbm_kernel(LbArgs a) {
+  const uint64_t w = blockIdx.x;
+  const uint32_t k = a.key_list[w];
+  LbMeta om{0, 0, 0, 0xFFFFFFFFu};
+  if (!a.fresh) om = a.meta_in[k];
+  const uint64_t o = a.tab_off[w];
+  const uint32_t E = a.tab_cap[w];
+  lb_board(a, k, om, LbView{a.g_eid + o, a.g_esc + o, a.g_est + o, a.g_hslot + 2 * o, 2 * E - 1});
+}
+
+// downstream/2 (leaderboard.erl:93-116), one wave per request, read-only.
+__global__ __launch_bounds__(64) void lb_downstream_kernel(LbDownArgs a) {
+  const uint64_t r = blockIdx.x;
+  const int lane = lane_id();
+  const uint64_t k = a.key[r];
+  LbMeta m{0, 0, 0, 0xFFFFFFFFu};
+  if (!a.fresh) m = a.meta[k];
+  const int64_t id = a.id[r], sc = a.score[r];
+  uint32_t e = 0xFFFFFFFFu;
+  for (uint32_t b = 0; b < m.n && e == 0xFFFFFFFFu; b += 64) {
+    const uint64_t hit = ballot(b + lane < m.n && a.eid[m.off + b + lane] == id);
+    if (hit) e = b + __builtin_ctzll(hit);
+  }
+  const uint8_t st = e == 0xFFFFFFFFu ? 0xFF : a.est[m.off + e];
+  uint8_t out;
+  if (a.op[r] == 1) {
+    out = st == LB_BANNED ? 255 : 2;
+  } else if (st == LB_BANNED) {
+    out = 255;
+  } else if (st == LB_OBS) {
+    out = sc > a.escore[m.off + e] ? 0 : 255;
+  } else if (st == LB_MASKED && !(sc > a.escore[m.off + e])) {
+    out = 255;
+  } else {
+    bool better = m.minq == 0xFFFFFFFFu;  // cmp(_, {nil,nil}) = true
+    if (!better)
+      better = lb_cmp(id, sc, a.eid[m.off + m.minq], a.escore[m.off + m.minq]);
+    out = (m.nobs < a.k || better) ? 0 : 1;
+  }
+  if (lane == 0) a.out[r] = out;
+}
+
+int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
+  if (n_work == 0) return CCRDT_OK;
+  if (cls == 0)
+    hipLaunchKernelGGL(lb_apply_kernel<512>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 1)
+    hipLaunchKernelGGL(lb_apply_kernel<2048>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(lb_apply_hbm_kernel, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
+  if (a.n == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(lb_downstream_kernel, dim3((unsigned)a.n), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// ===================================================== wordcount / wdc
+// add/2 (src/antidote_ccrdt_wordcount.erl:76-85, worddocumentcount.erl:76-86):
+// binary:split(File, [<<"\n">>, <<" ">>], [global]) — tokens start at the
+// document start and after every 0x0A / 0x20 byte, empty tokens included
+// (Q13); wordcount adds 1 per token, worddocumentcount 1 per distinct token
+// of the document.  One wave per document; each lane owns a 64-byte segment
+// of a 4 KiB tile and handles the tokens that start in it (reading past its
+// segment when a token does).  Words are keyed by h = mix(FNV-1a(bytes),
+// key, len); a per-document LDS table aggregates counts (wordcount: the Zipf
+// head costs one global atomic per document) or de-duplicates
+// (worddocumentcount); misses go to the global table (CAS on h).  Exactness
+// does not rest on the hash: wc_verify_kernel byte-compares every token with
+// its word's representative and flags any collision.
+constexpr int WC_LDS = 512;  // per-document LDS table entries
+constexpr int WC_PROBE = 8;
+
+__device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
+
+__device__ __forceinline__ uint64_t wc_mix(uint64_t fnv, uint64_t key, uint64_t len) {
+  uint64_t x = fnv ^ (key * 0x9E3779B97F4A7C15ull) ^ (len * 0xC2B2AE3D27D4EB4Full);
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  return x ? x : 1;
+}
+
+// Token starting at s (byte index in the document): returns its end.
+__device__ __forceinline__ uint64_t wc_token(const uint8_t* doc, uint64_t len, uint64_t s, uint64_t& fnv) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  uint64_t e = s;
+  while (e < len) {
+    const uint8_t c = doc[e];
+    if (wc_sep(c)) break;
+    h = (h ^ c) * 0x100000001B3ull;
+    ++e;
+  }
+  fnv = h;
+  return e;
+}
+
+__device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
+                                                     uint64_t pos) {
+  uint64_t sl = h & a.t_mask;
+  for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&a.t_hash[sl], 0ull, (unsigned long long)h);
+    if (prev == 0ull) {  // new word: this token is its representative
+      a.t_key[sl] = key;
+      a.t_len[sl] = len;
+      a.t_pos[sl] = pos;
+      a.t_arena[sl] = ~0ull;
+      return sl;
+    }
+    if (prev == h) return sl;
+    sl = (sl + 1) & a.t_mask;
+  }
+  atomicOr(&a.status[0], 1u);  // table full
+  return ~0ull;
+}
+
+__device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t h, uint64_t doc) {
+  // worddocumentcount: first occurrence of (doc, word) in the global dedupe table
+  const uint64_t dh = wc_mix(h, doc + 1, 0x5151);
+  uint64_t sl = dh & a.d_mask;
+  for (uint64_t probe = 0; probe <= a.d_mask; ++probe) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], 0ull, (unsigned long long)dh);
+    if (prev == 0ull) return true;
+    if (prev == dh) return false;
+    sl = (sl + 1) & a.d_mask;
+  }
+  atomicOr(&a.status[0], 2u);
+  return false;
+}
+
+__global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
+  __shared__ unsigned long long lh[WC_LDS];
+  __shared__ uint32_t lc[WC_LDS];
+  __shared__ uint32_t llen[WC_LDS];
+  __shared__ uint64_t lpos[WC_LDS];
+  const uint64_t d = blockIdx.x;
+  const int lane = lane_id();
+  const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
+  const uint32_t key = (uint32_t)a.doc_key[d];
+  const uint8_t* doc = a.bytes + b0;
+  for (int i = lane; i < WC_LDS; i += 64) {
+    lh[i] = 0ull;
+    lc[i] = 0u;
+  }
+  __syncthreads();
+  for (uint64_t tile = 0; tile <= len; tile += 4096) {
+    const uint64_t s0 = tile + (uint64_t)lane * 64;
+    for (uint64_t s = s0; s < s0 + 64 && s <= len; ++s) {
+      if (!(s == 0 || wc_sep(doc[s - 1]))) continue;  // not a token start
+      uint64_t fnv;
+      const uint64_t e = wc_token(doc, len, s, fnv);
+      const uint32_t tl = (uint32_t)(e - s);
+      const uint64_t h = wc_mix(fnv, key, tl);
+      // per-document LDS table
+      uint32_t sl = (uint32_t)(h >> 17) & (WC_LDS - 1);
+      int where = -1;  // 0: counted in LDS, 1: global
+      for (int p = 0; p < WC_PROBE; ++p) {
+        const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
+        if (prev == 0ull) {
+          llen[sl] = tl;
+          lpos[sl] = b0 + s;
+          where = 0;
+          if (!a.wdc) atomicAdd(&lc[sl], 1u);
+          else lc[sl] = 1u;
+          break;
+        }
+        if (prev == h) {  // same word already seen in this document
+          where = 0;
+          if (!a.wdc) atomicAdd(&lc[sl], 1u);
+          break;
+        }
+        sl = (sl + 1) & (WC_LDS - 1);
+      }
+      if (where < 0) {  // LDS table full: global path
+        if (a.wdc && !wc_doc_first(a, h, d)) continue;
+        const uint64_t g = wc_global_insert(a, h, key, tl, b0 + s);
+        if (g != ~0ull) atomicAdd(&a.t_cnt[g], 1ull);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < WC_LDS; i += 64) {
+    const uint64_t h = lh[i];
+    if (h == 0ull) continue;
+    // a word takes the same path (LDS or global) for the whole document: LDS
+    // slots are never freed, so a word that once missed them always misses
+    const uint64_t g = wc_global_insert(a, h, key, llen[i], lpos[i]);
+    if (g != ~0ull) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
+  }
+}
+
+// Exactness: every token must equal its word's representative byte-for-byte.
+__global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
+  const uint64_t d = blockIdx.x;
+  const int lane = lane_id();
+  const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
+  const uint32_t key = (uint32_t)a.doc_key[d];
+  const uint8_t* doc = a.bytes + b0;
+  for (uint64_t tile = 0; tile <= len; tile += 4096) {
+    const uint64_t s0 = tile + (uint64_t)lane * 64;
+    for (uint64_t s = s0; s < s0 + 64 && s <= len; ++s) {
+      if (!(s == 0 || wc_sep(doc[s - 1]))) continue;
+      uint64_t fnv;
+      const uint64_t e = wc_token(doc, len, s, fnv);
+      const uint32_t tl = (uint32_t)(e - s);
+      const uint64_t h = wc_mix(fnv, key, tl);
+      uint64_t sl = h & a.t_mask;
+      while (a.t_hash[sl] != h && a.t_hash[sl] != 0ull) sl = (sl + 1) & a.t_mask;
+      if (a.t_hash[sl] != h) {
+        atomicOr(&a.status[1], 2u);  // lost token (table overflow)
+        continue;
+      }
+      const uint8_t* rep = a.t_arena[sl] != ~0ull ? a.arena + a.t_arena[sl] : a.bytes + a.t_pos[sl];
+      bool eq = a.t_key[sl] == key && a.t_len[sl] == tl;
+      for (uint32_t j = 0; eq && j < tl; ++j) eq = rep[j] == doc[s + j];
+      if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+    }
+  }
+}
+
+// New words of this batch: copy their bytes into the persistent arena.
+// arena_top[1] counts the table's words.
+__global__ void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* arena_top) {
+  const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
+  atomicAdd(&arena_top[1], 1ull);
+  if (a.t_arena[sl] != ~0ull) return;
+  const uint32_t n = a.t_len[sl];
+  const uint64_t at = atomicAdd(arena_top, (unsigned long long)n);
+  const uint8_t* src = a.bytes + a.t_pos[sl];
+  for (uint32_t j = 0; j < n; ++j) arena[at + j] = src[j];
+  a.t_arena[sl] = at;
+}
+
+// token count of every document (sizes the worddocumentcount dedupe table)
+__global__ __launch_bounds__(64) void wc_count_kernel(const uint64_t* doc_off, const uint8_t* bytes,
+                                                      uint64_t* ntok) {
+  const uint64_t d = blockIdx.x;
+  const uint64_t b0 = doc_off[d], b1 = doc_off[d + 1];
+  uint32_t c = 0;
+  for (uint64_t i = b0 + lane_id(); i < b1; i += 64) c += wc_sep(bytes[i]);
+  uint32_t tot;
+  (void)wave_excl_scan_u32(c, tot);
+  if (lane_id() == 0) ntok[d] = (uint64_t)tot + 1;
+}
+// key of every document from the key -> documents CSR
+__global__ void wc_doc_key_kernel(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_keys) return;
+  for (uint64_t d = key_ptr[k]; d < key_ptr[k + 1]; ++d) doc_key[d] = k;
+}
+
+int wc_launch_count(const uint64_t* doc_off, const uint8_t* bytes, uint64_t n_docs, uint64_t* ntok,
+                    hipStream_t st) {
+  if (!n_docs) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_count_kernel, dim3((unsigned)n_docs), dim3(64), 0, st, doc_off, bytes, ntok);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key, hipStream_t st) {
+  if (!n_keys) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_doc_key_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0, st, key_ptr,
+                     n_keys, doc_key);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_insert(const WcArgs& a, hipStream_t st) {
+  if (!a.n_docs) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_insert_kernel, dim3((unsigned)a.n_docs), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_verify(const WcArgs& a, hipStream_t st) {
+  if (!a.n_docs) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_verify_kernel, dim3((unsigned)a.n_docs), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st) {
+  const uint64_t n = a.t_mask + 1;
+  hipLaunchKernelGGL(wc_persist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, arena, top);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// Re-insert the words of an old table into a fresh (larger) table.
+__global__ void wc_rehash_kernel(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen,
+                                 const uint64_t* oarena, const unsigned long long* ocnt, uint64_t on,
+                                 WcArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= on || oh[i] == 0ull) return;
+  uint64_t sl = oh[i] & a.t_mask;
+  while (atomicCAS((unsigned long long*)&a.t_hash[sl], 0ull, (unsigned long long)oh[i]) != 0ull)
+    sl = (sl + 1) & a.t_mask;
+  a.t_key[sl] = okey[i];
+  a.t_len[sl] = olen[i];
+  a.t_pos[sl] = 0;
+  a.t_arena[sl] = oarena[i];
+  a.t_cnt[sl] = ocnt[i];
+}
+int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
+                     const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st) {
+  if (!on) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_rehash_kernel, dim3((unsigned)((on + 255) / 256)), dim3(256), 0, st, oh, okey, olen,
+                     oarena, ocnt, on, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// ------------------------------------------------- segment capacities + scan
+// caps[k] = cnt[k*stride] (0 if cnt == nullptr) + ops of key k; then an
+// exclusive scan of caps into off[0..n], off[n] = total.
+__global__ void caps_kernel(const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stride,
+                            uint64_t n, uint64_t* caps) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  caps[k] = (key_ptr ? key_ptr[k + 1] - key_ptr[k] : 0) + (cnt ? cnt[k * stride] : 0u);
+}
+
+constexpr int SC_BLOCK = 256;
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
+  __shared__ uint64_t ws[SC_BLOCK / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t o = (uint64_t)shfl64((int64_t)inc, lane >= off ? lane - off : lane);
+    if (lane >= off) inc += o;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  for (int j = 0; j < SC_BLOCK / 64; ++j) {
+    if (j < w) pre += ws[j];
+    tot += ws[j];
+  }
+  __syncthreads();
+  total = tot;
+  return pre + inc - v;
+}
+__global__ __launch_bounds__(SC_BLOCK) void scan_partials_kernel(const uint64_t* in, uint64_t n,
+                                                                 uint64_t* part) {
+  const uint64_t i = (uint64_t)blockIdx.x * SC_BLOCK + threadIdx.x;
+  uint64_t tot;
+  (void)block_excl_scan(i < n ? in[i] : 0, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(SC_BLOCK) void scan_tops_kernel(uint64_t* part, uint64_t nb) {
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < nb; b0 += SC_BLOCK) {
+    const uint64_t b = b0 + threadIdx.x;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(b < nb ? part[b] : 0, tot);
+    if (b < nb) part[b] = ex + carry;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[nb] = carry;
+}
+__global__ __launch_bounds__(SC_BLOCK) void scan_apply_kernel(const uint64_t* in, uint64_t n,
+                                                              const uint64_t* part, uint64_t* out,
+                                                              uint64_t nb) {
+  const uint64_t i = (uint64_t)blockIdx.x * SC_BLOCK + threadIdx.x;
+  uint64_t tot;
+  const uint64_t ex = block_excl_scan(i < n ? in[i] : 0, tot);
+  if (i < n) out[i] = part[blockIdx.x] + ex;
+  if (i == 0) out[n] = part[nb];
+}
+
+int launch_caps_scan(const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stride, uint64_t n,
+                     uint64_t* caps, uint64_t* off, uint64_t* part, hipStream_t st) {
+  const uint64_t nb = (n + SC_BLOCK - 1) / SC_BLOCK;
+  if (n) {
+    hipLaunchKernelGGL(caps_kernel, dim3((unsigned)nb), dim3(SC_BLOCK), 0, st, key_ptr, cnt, stride, n,
+                       caps);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3((unsigned)nb), dim3(SC_BLOCK), 0, st, caps, n, part);
+  }
+  hipLaunchKernelGGL(scan_tops_kernel, dim3(1), dim3(SC_BLOCK), 0, st, part, nb);
+  if (n)
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(SC_BLOCK), 0, st, caps, n, part, off,
+                       nb);
+  else
+    CCRDT_HIP(hipMemsetAsync(off, 0, 8, st));
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// ------------------------------------------------------------- launchers
+int avg_launch_apply(const AvgArgs& a, hipStream_t st) {
+  if (a.n_keys == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(avg_apply_kernel, dim3((unsigned)a.n_keys), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int avg_launch_value(const int64_t* sum, const int64_t* num, int64_t n_keys, int fresh, double* out,
+                     uint8_t* defined, hipStream_t st) {
+  if (n_keys == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(avg_value_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0, st, sum,
+                     num, n_keys, fresh, out, defined);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+// cls 0: <= 512 entries per key (LDS hash 1024), 1: <= 4096 (hash 8192)
+int topk_launch_apply(const TopkArgs& a, int cls, uint64_t n_work, hipStream_t st) {
+  if (n_work == 0) return CCRDT_OK;
+  if (cls == 0)
+    hipLaunchKernelGGL(topk_apply_kernel<1024>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 1)
+    hipLaunchKernelGGL(topk_apply_kernel<8192>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(topk_apply_hbm_kernel, dim3((unsigned)n_work), dim3(TK_HBM_BLOCK), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int topk_launch_value(const TopkValueArgs& a, int cls, uint64_t n_work, hipStream_t st) {
+  if (n_work == 0) return CCRDT_OK;
+  if (cls == 0)
+    hipLaunchKernelGGL(topk_value_kernel<512>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 1)
+    hipLaunchKernelGGL(topk_value_kernel<4096>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(topk_value_hbm_kernel, dim3((unsigned)n_work), dim3(TK_SORT_BLOCK), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+}  // namespace ccrdt

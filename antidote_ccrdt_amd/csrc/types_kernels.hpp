@@ -1,0 +1,152 @@
+// types_kernels.hpp — argument blocks of the average / topk / leaderboard /
+// wordcount kernels and the generic segment scan.
+#pragma once
+#include <cstdint>
+
+namespace ccrdt {
+
+enum : uint32_t { AVG_ERR_NEG = 1u, AVG_ERR_RANGE = 2u };
+
+struct AvgArgs {
+  int64_t n_keys;
+  const uint64_t* key_ptr;
+  const int64_t* v;
+  const int64_t* n;
+  const int64_t* sum_in;
+  const int64_t* num_in;
+  int64_t* sum_out;
+  int64_t* num_out;
+  int32_t fresh;
+  uint32_t* status;
+};
+
+// topk: per key a segment of (id, score) entries (any order)
+struct TopkArgs {
+  int64_t n_keys;
+  const uint64_t* key_ptr;
+  const int64_t* op_id;
+  const int64_t* op_score;
+  const uint64_t* off_in;
+  const uint32_t* cnt_in;
+  const int64_t* id_in;
+  const int64_t* score_in;
+  const uint64_t* off_out;  // precomputed by the scan
+  uint32_t* cnt_out;
+  int64_t* id_out;
+  int64_t* score_out;
+  int32_t fresh;
+  const uint32_t* key_list;
+  uint32_t* ovf_list;
+  uint32_t* status;
+  // HBM class: per listed key a hash region at tab_off[w], tab_cap[w] slots
+  const uint64_t* tab_off;
+  const uint32_t* tab_cap;
+  int64_t* g_id;
+  int32_t* g_seq;
+};
+
+struct TopkValueArgs {
+  const uint64_t* off;
+  const uint32_t* cnt;
+  const int64_t* id;
+  const int64_t* score;
+  const uint64_t* out_ptr;
+  int64_t* out_id;
+  int64_t* out_score;
+  const uint32_t* key_list;
+  uint32_t* ovf_list;
+  uint32_t* status;
+  // HBM class: per listed key a sort region at tab_off[w], tab_cap[w] slots
+  const uint64_t* tab_off;
+  const uint32_t* tab_cap;
+  int64_t* g_id;
+  int64_t* g_score;
+};
+
+// leaderboard: per board a segment of entries (id, score, status) + meta
+enum : uint8_t { LB_OBS = 0, LB_MASKED = 1, LB_BANNED = 2 };
+struct alignas(16) LbMeta {
+  uint32_t off;    // segment start (entries)
+  uint32_t n;      // entries
+  uint32_t nobs;   // |Observed|
+  uint32_t minq;   // entry index of Min, 0xFFFFFFFF = {nil,nil}
+};
+struct alignas(16) LbExtraRec {
+  uint32_t op;
+  uint32_t pad;
+  int64_t id;
+  int64_t score;
+};
+struct LbArgs {
+  int64_t n_keys;
+  uint32_t k;
+  const uint64_t* key_ptr;
+  const uint8_t* kind;
+  const int64_t* id;
+  const int64_t* score;
+  const LbMeta* meta_in;
+  const int64_t* id_in;
+  const int64_t* score_in;
+  const uint8_t* st_in;
+  LbMeta* meta_out;
+  const uint64_t* off_out;  // new segment starts (scan)
+  int64_t* id_out;
+  int64_t* score_out;
+  uint8_t* st_out;
+  int32_t fresh;
+  uint32_t* ex_cnt;
+  LbExtraRec* ex;
+  const uint32_t* key_list;
+  uint32_t* ovf_list;
+  uint32_t* status;  // [0] overflow count, [1] error flags
+  // HBM class: per listed board entries at tab_off[w] (tab_cap[w] of them),
+  // hash slots at 2 * tab_off[w]
+  const uint64_t* tab_off;
+  const uint32_t* tab_cap;
+  int64_t* g_eid;
+  int64_t* g_esc;
+  uint8_t* g_est;
+  uint32_t* g_hslot;
+};
+enum : uint32_t { LB_ERR_KIND = 1u };
+
+struct LbDownArgs {
+  int64_t n;
+  uint32_t k;
+  const uint64_t* key;
+  const uint8_t* op;
+  const int64_t* id;
+  const int64_t* score;
+  uint8_t* out;
+  const LbMeta* meta;
+  const int64_t* eid;
+  const int64_t* escore;
+  const uint8_t* est;
+  int32_t fresh;
+};
+
+// wordcount / worddocumentcount
+struct WcArgs {
+  int64_t n_keys;
+  int64_t n_docs;
+  const uint64_t* doc_key;   // [n_docs] key of each document
+  const uint64_t* doc_off;   // [n_docs+1] byte offsets
+  const uint8_t* bytes;
+  uint64_t n_bytes;
+  int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)
+  // word table (persistent across batches)
+  uint64_t* t_hash;          // 0 = empty
+  uint32_t* t_key;
+  uint32_t* t_len;
+  uint64_t* t_pos;           // batch byte position of first occurrence (this batch)
+  uint64_t* t_arena;         // arena offset (persistent words) or ~0
+  unsigned long long* t_cnt;
+  uint64_t t_mask;
+  const uint8_t* arena;
+  // per-document dedupe table (worddocumentcount)
+  uint64_t* d_hash;
+  uint64_t d_mask;
+  uint32_t* status;          // [0] table overflow, [1] hash collision
+};
+
+}  // namespace ccrdt

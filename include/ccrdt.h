@@ -200,6 +200,114 @@ int ccrdt_trmv_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const
                           const int64_t* id, const int64_t* score, const uint8_t* dc,
                           const int64_t* ts, uint8_t* out_kind, int64_t* out_vc);
 
+
+/* ---------------------------------------------------------------- average */
+
+/* {add, {V, N}} effects (src/antidote_ccrdt_average.erl:88-94); {add, V} is
+ * N = 1 (downstream/2 :77-81).  CSR by key. */
+typedef struct {
+  int64_t n_ops;
+  const uint64_t* key_ptr; /* [n_keys+1] */
+  const int64_t* value;    /* [n_ops] V */
+  const int64_t* n;        /* [n_ops] N (0 = no-op, < 0 = EINVAL) */
+} ccrdt_avg_ops;
+/* update/2 over a batch (host arrays).  Sums that leave int64 give ERANGE. */
+int ccrdt_avg_apply(ccrdt_engine* e, const ccrdt_avg_ops* ops);
+int ccrdt_avg_apply_device(ccrdt_engine* e, const ccrdt_avg_ops* dev_ops);
+/* State {Sum, Num} of every key (to_binary/from_binary analogues). */
+int ccrdt_avg_export(ccrdt_engine* e, int64_t* sum, int64_t* num);
+int ccrdt_avg_import(ccrdt_engine* e, const int64_t* sum, const int64_t* num);
+/* value/1 (:68-70): Sum / Num in IEEE double; defined[k] = 0 where Num = 0
+ * (the reference raises badarith). */
+int ccrdt_avg_value(ccrdt_engine* e, double* value, uint8_t* defined);
+
+/* ------------------------------------------------------------------- topk */
+
+/* {add, {Id, Score}} effects (src/antidote_ccrdt_topk.erl:100-104); an
+ * {add_map, Map} effect is its entries in any order (maps:merge). */
+typedef struct {
+  int64_t n_ops;
+  const uint64_t* key_ptr; /* [n_keys+1] */
+  const int64_t* id;       /* [n_ops] (binary Ids interned by the host in term order) */
+  const int64_t* score;    /* [n_ops] */
+} ccrdt_topk_ops;
+int ccrdt_topk_apply(ccrdt_engine* e, const ccrdt_topk_ops* ops);
+int ccrdt_topk_apply_device(ccrdt_engine* e, const ccrdt_topk_ops* dev_ops);
+int ccrdt_topk_size(ccrdt_engine* e, int64_t* n_entries);
+/* The map of every key, sorted by Id: ptr[n_keys+1], id/score[n_entries]. */
+int ccrdt_topk_export(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score);
+int ccrdt_topk_import(ccrdt_engine* e, const uint64_t* ptr, const int64_t* id, const int64_t* score);
+/* value/1 (:81-83): every key's entries sorted by Score desc, Id desc (GPU
+ * segmented sort). */
+int ccrdt_topk_value(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score);
+/* downstream/2 (:89-94, changes_state :164-166): out[i] = CCRDT_TRMV_ADD if
+ * score[i] > Size else CCRDT_NOOP. */
+int ccrdt_topk_downstream(ccrdt_engine* e, int64_t n, const int64_t* score, uint8_t* out_kind);
+
+/* ------------------------------------------------------------ leaderboard */
+
+#define CCRDT_LB_ADD 0
+#define CCRDT_LB_ADD_R 1
+#define CCRDT_LB_BAN 2
+/* {add|add_r, {Id, Score}} and {ban, Id} effects
+ * (src/antidote_ccrdt_leaderboard.erl:128-134). */
+typedef struct {
+  int64_t n_ops;
+  const uint64_t* key_ptr; /* [n_keys+1] */
+  const uint8_t* kind;     /* [n_ops] CCRDT_LB_* */
+  const int64_t* id;       /* [n_ops] */
+  const int64_t* score;    /* [n_ops] (ignored for ban) */
+} ccrdt_lb_ops;
+/* Extra effects, op-indexed: kind CCRDT_LB_ADD = {add, {Id, Score}} from a
+ * ban that promoted a Masked player (:279-283), CCRDT_NOOP = none. */
+typedef struct {
+  uint8_t* kind;
+  int64_t* id;
+  int64_t* score;
+} ccrdt_lb_extra;
+int ccrdt_lb_apply(ccrdt_engine* e, const ccrdt_lb_ops* ops, ccrdt_lb_extra* extra);
+int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* dev_ops);
+int ccrdt_lb_fetch_extra(ccrdt_engine* e, ccrdt_lb_extra* extra);
+/* leaderboard() = {Observed, Masked, Bans, Min, Size} (:62-68), canonical
+ * (each list sorted by Id). */
+typedef struct {
+  uint64_t* obs_ptr;
+  int64_t *obs_id, *obs_score;
+  uint64_t* m_ptr;
+  int64_t *m_id, *m_score;
+  uint64_t* b_ptr;
+  int64_t* b_id;
+  uint8_t* min_valid;
+  int64_t *min_id, *min_score;
+} ccrdt_lb_state;
+int ccrdt_lb_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans);
+int ccrdt_lb_export(ccrdt_engine* e, ccrdt_lb_state* out);
+int ccrdt_lb_import(ccrdt_engine* e, const ccrdt_lb_state* in);
+/* downstream/2 (:93-116): op 0 = {add, {Id, Score}}, 1 = {ban, Id};
+ * out_kind CCRDT_LB_ADD / _ADD_R / _BAN / CCRDT_NOOP. */
+int ccrdt_lb_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,
+                        const int64_t* id, const int64_t* score, uint8_t* out_kind);
+
+/* ------------------------------------------- wordcount / worddocumentcount */
+
+/* {add, File} effects (src/antidote_ccrdt_wordcount.erl:53-54,
+ * worddocumentcount.erl:53-54): documents CSR by key. */
+typedef struct {
+  int64_t n_docs;
+  const uint64_t* key_ptr; /* [n_keys+1] over documents */
+  const uint64_t* doc_off; /* [n_docs+1] over bytes */
+  const uint8_t* bytes;
+  uint64_t n_bytes;
+} ccrdt_wc_docs;
+int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs);
+int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* dev_docs);
+int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes);
+/* value/1 (:47-48) = the map word -> count; per key, words sorted by bytes
+ * (Erlang binary order): key_ptr[n_keys+1] over words, word_off[n_words+1]
+ * over word_bytes. */
+int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint8_t* word_bytes,
+                    int64_t* count);
+
 #ifdef __cplusplus
 }
 #endif

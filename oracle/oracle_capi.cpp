@@ -166,3 +166,195 @@ void orc_trmv_downstream(void* h, int64_t n, const uint64_t* key, const uint8_t*
 }
 
 }  // extern "C"
+
+// ================================================================ others
+extern "C" {
+
+// ---------------------------------------------------------------- average
+// update/2 over a CSR batch; sum/num are in-out [n_keys].  Returns 1 if an op
+// would crash the reference (N < 0: no function clause), else 0.
+int orc_avg_apply(int64_t n_keys, const uint64_t* key_ptr, const int64_t* v, const int64_t* n,
+                  int64_t* sum, int64_t* num) {
+  for (int64_t k = 0; k < n_keys; ++k) {
+    Average a;
+    a.sum = sum[k];
+    a.num = num[k];
+    for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i)
+      if (!a.add(v[i], n[i])) return 1;
+    sum[k] = a.sum;
+    num[k] = a.num;
+  }
+  return 0;
+}
+double orc_avg_value(int64_t sum, int64_t num) {
+  Average a;
+  a.sum = sum;
+  a.num = num;
+  return a.value();
+}
+
+// ------------------------------------------------------------------- topk
+void* orc_topk_create(int64_t n_keys, int64_t k) { return new TkSet{std::vector<Topk>(n_keys, Topk(k))}; }
+void orc_topk_destroy(void* h) { delete (TkSet*)h; }
+void orc_topk_apply(void* h, const uint64_t* key_ptr, const int64_t* id, const int64_t* score) {
+  auto* s = (TkSet*)h;
+  for (size_t k = 0; k < s->keys.size(); ++k)
+    for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i) s->keys[k].add(id[i], score[i]);
+}
+int64_t orc_topk_size(void* h) {
+  int64_t n = 0;
+  for (auto& t : ((TkSet*)h)->keys) n += t.top.size();
+  return n;
+}
+// state sorted by id (sorted=0) or value/1 order (sorted=1)
+void orc_topk_export(void* h, int value_order, uint64_t* ptr, int64_t* id, int64_t* score) {
+  auto* s = (TkSet*)h;
+  uint64_t p = 0;
+  ptr[0] = 0;
+  for (size_t k = 0; k < s->keys.size(); ++k) {
+    auto v = value_order ? s->keys[k].value()
+                         : std::vector<std::pair<i64, i64>>(s->keys[k].top.begin(), s->keys[k].top.end());
+    for (auto& [i, sc] : v) {
+      id[p] = i;
+      score[p] = sc;
+      ++p;
+    }
+    ptr[k + 1] = p;
+  }
+}
+
+// ------------------------------------------------------------ leaderboard
+void* orc_lb_create(int64_t n_keys, int64_t k) { return new LbSet{std::vector<Leaderboard>(n_keys, Leaderboard(k))}; }
+void orc_lb_destroy(void* h) { delete (LbSet*)h; }
+// kind 0 add, 1 add_r, 2 ban; ex_kind 255 none / 0 {add, {Id, Score}}
+void orc_lb_apply(void* h, const uint64_t* key_ptr, const uint8_t* kind, const int64_t* id,
+                  const int64_t* score, uint8_t* ex_kind, int64_t* ex_id, int64_t* ex_score) {
+  auto* s = (LbSet*)h;
+  for (size_t k = 0; k < s->keys.size(); ++k)
+    for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i) {
+      LExtra x = kind[i] == 2 ? s->keys[k].ban(id[i]) : s->keys[k].add(id[i], score[i]);
+      if (ex_kind) ex_kind[i] = x.kind == L_ADD ? 0 : 255;
+      if (x.kind == L_ADD) {
+        if (ex_id) ex_id[i] = x.elem.id;
+        if (ex_score) ex_score[i] = x.elem.score;
+      }
+    }
+}
+void orc_lb_sizes(void* h, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans) {
+  int64_t o = 0, m = 0, b = 0;
+  for (auto& l : ((LbSet*)h)->keys) {
+    o += l.obs.size();
+    m += l.masked.size();
+    b += l.bans.size();
+  }
+  *n_obs = o;
+  *n_masked = m;
+  *n_bans = b;
+}
+void orc_lb_export(void* h, uint64_t* obs_ptr, int64_t* obs_id, int64_t* obs_score, uint64_t* m_ptr,
+                   int64_t* m_id, int64_t* m_score, uint64_t* b_ptr, int64_t* b_id, uint8_t* min_valid,
+                   int64_t* min_id, int64_t* min_score) {
+  auto* s = (LbSet*)h;
+  uint64_t po = 0, pm = 0, pb = 0;
+  obs_ptr[0] = m_ptr[0] = b_ptr[0] = 0;
+  for (size_t k = 0; k < s->keys.size(); ++k) {
+    const Leaderboard& l = s->keys[k];
+    for (auto& [i, sc] : l.obs) {
+      obs_id[po] = i;
+      obs_score[po++] = sc;
+    }
+    for (auto& [i, sc] : l.masked) {
+      m_id[pm] = i;
+      m_score[pm++] = sc;
+    }
+    for (auto i : l.bans) b_id[pb++] = i;
+    obs_ptr[k + 1] = po;
+    m_ptr[k + 1] = pm;
+    b_ptr[k + 1] = pb;
+    min_valid[k] = l.min ? 1 : 0;
+    min_id[k] = l.min ? l.min->id : 0;
+    min_score[k] = l.min ? l.min->score : 0;
+  }
+}
+// op 0 add, 1 ban; out 0 add, 1 add_r, 2 ban, 255 noop
+void orc_lb_downstream(void* h, int64_t n, const uint64_t* key, const uint8_t* op, const int64_t* id,
+                       const int64_t* score, uint8_t* out) {
+  auto* s = (LbSet*)h;
+  for (int64_t i = 0; i < n; ++i) {
+    const Leaderboard& l = s->keys[key[i]];
+    const int r = op[i] == 0 ? l.downstream_add(id[i], score[i]) : l.downstream_ban(id[i]);
+    out[i] = r == L_NOOP ? 255 : (uint8_t)r;
+  }
+}
+// cmp/2, min/1, get_largest/1 on explicit arguments (golden vectors)
+int orc_lb_cmp(int a_nil, int64_t a_id, int64_t a_sc, int b_nil, int64_t b_id, int64_t b_sc) {
+  std::optional<LPair> a, b;
+  if (!a_nil) a = LPair{a_id, a_sc};
+  if (!b_nil) b = LPair{b_id, b_sc};
+  return lb_cmp(a, b) ? 1 : 0;
+}
+int orc_lb_minmax(int largest, int64_t n, const int64_t* id, const int64_t* sc, int64_t* out_id,
+                  int64_t* out_sc) {
+  std::map<i64, i64> m;
+  for (int64_t i = 0; i < n; ++i) m[id[i]] = sc[i];
+  auto r = largest ? Leaderboard::get_largest(m) : Leaderboard::lb_min(m);
+  if (!r) return 0;
+  *out_id = r->id;
+  *out_sc = r->score;
+  return 1;
+}
+
+// ------------------------------------------------ wordcount / worddocumentcount
+struct WcSet {
+  int wdc;
+  std::vector<std::map<std::string, i64>> keys;
+};
+void* orc_wc_create(int64_t n_keys, int wdc) { return new WcSet{wdc, std::vector<std::map<std::string, i64>>(n_keys)}; }
+void orc_wc_destroy(void* h) { delete (WcSet*)h; }
+// key_ptr[n_keys+1] over docs; doc_off[n_docs+1] over bytes
+void orc_wc_apply(void* h, const uint64_t* key_ptr, const uint64_t* doc_off, const uint8_t* bytes) {
+  auto* s = (WcSet*)h;
+  for (size_t k = 0; k < s->keys.size(); ++k)
+    for (uint64_t d = key_ptr[k]; d < key_ptr[k + 1]; ++d) {
+      std::string f((const char*)bytes + doc_off[d], doc_off[d + 1] - doc_off[d]);
+      if (s->wdc) {
+        WordDocCount w;
+        w.counts.swap(s->keys[k]);
+        w.add(f);
+        w.counts.swap(s->keys[k]);
+      } else {
+        Wordcount w;
+        w.counts.swap(s->keys[k]);
+        w.add(f);
+        w.counts.swap(s->keys[k]);
+      }
+    }
+}
+void orc_wc_sizes(void* h, int64_t* n_words, int64_t* n_bytes) {
+  int64_t w = 0, b = 0;
+  for (auto& m : ((WcSet*)h)->keys)
+    for (auto& [s, c] : m) {
+      ++w;
+      b += (int64_t)s.size();
+    }
+  *n_words = w;
+  *n_bytes = b;
+}
+// words sorted by bytes (std::string order = Erlang binary order) per key
+void orc_wc_export(void* h, uint64_t* key_ptr, uint64_t* word_off, uint8_t* bytes, int64_t* count) {
+  auto* s = (WcSet*)h;
+  uint64_t w = 0, b = 0;
+  key_ptr[0] = 0;
+  word_off[0] = 0;
+  for (size_t k = 0; k < s->keys.size(); ++k) {
+    for (auto& [str, c] : s->keys[k]) {
+      memcpy(bytes + b, str.data(), str.size());
+      b += str.size();
+      count[w] = c;
+      word_off[++w] = b;
+    }
+    key_ptr[k + 1] = w;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,244 @@
+"""average / topk / leaderboard / wordcount / worddocumentcount on the GPU vs
+the oracle, bit-exact (through the C-ABI)."""
+import numpy as np
+import pytest
+
+import oracle as orc
+from antidote_ccrdt_amd import _lib
+from antidote_ccrdt_amd.types import (AverageEngine, LeaderboardEngine, TopkEngine,
+                                      WordcountEngine, WordDocumentCountEngine, _csr)
+from types_helpers import FIX, avg_fixture_ops, lb_batch, lb_state_key, run_lb_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+# ---------------------------------------------------------------- leaderboard
+class LbEngineBackend:
+    def apply(self, size, effects):
+        e = LeaderboardEngine(1, size)
+        x = e.apply(*lb_batch(effects)) if effects else None
+        ex = None
+        if x is not None and x["kind"][-1] == 0:
+            ex = ["add", int(x["id"][-1]), int(x["score"][-1])]
+        return lb_state_key(e.export()), ex
+
+    def downstream(self, size, effects, op, id, score):
+        e = LeaderboardEngine(1, size)
+        if effects:
+            e.apply(*lb_batch(effects), want_extra=False)
+        return int(e.downstream([0], [op], [id], [score])[0])
+
+
+LB = [f for f in FIX["leaderboard"] if "steps" in f]
+
+
+@pytest.mark.parametrize("fx", LB, ids=[f["name"] for f in LB])
+def test_leaderboard_golden(gpu, fx):
+    run_lb_fixture(fx, LbEngineBackend())
+
+
+def _lb_stream(rng, n, nk, n_players, smax, ban_frac):
+    keys = rng.integers(0, nk, n)
+    kind = np.where(rng.random(n) < ban_frac, 2, rng.integers(0, 2, n)).astype(np.uint8)
+    pid = rng.integers(0, n_players, n)
+    sc = rng.integers(0, smax, n)
+    order, kp = _csr(keys, nk)
+    return kp, kind[order], pid[order], sc[order]
+
+
+@pytest.mark.parametrize("cfg", [(20000, 40, 300, 10**6, 0.01, 100), (20000, 50, 30, 10, 0.05, 5),
+                                 (8000, 8, 1500, 1000, 0.02, 100), (3000, 30, 8, 4, 0.2, 1)])
+def test_leaderboard_random(gpu, cfg):
+    n, nk, npl, smax, bf, K = cfg
+    rng = np.random.default_rng(n + nk)
+    e, o = LeaderboardEngine(nk, K), orc.LbOracle(nk, K)
+    for _ in range(2):  # two batches: state carried over
+        b = _lb_stream(rng, n, nk, npl, smax, bf)
+        xe, xo = e.apply(*b), o.apply(*b)
+        assert np.array_equal(xe["kind"], xo["kind"])
+        m = xo["kind"] == 0
+        assert np.array_equal(xe["id"][m], xo["id"][m])
+        assert np.array_equal(xe["score"][m], xo["score"][m])
+        assert not e.export().diff(o.export())
+    keys = rng.integers(0, nk, 2000)
+    op = rng.integers(0, 2, 2000)
+    pid, sc = rng.integers(0, npl, 2000), rng.integers(0, smax, 2000)
+    assert np.array_equal(e.downstream(keys, op, pid, sc), o.downstream(keys, op, pid, sc))
+    st = e.export()
+    e2 = LeaderboardEngine(nk, K)
+    e2.import_state(st)
+    assert not e2.export().diff(st)
+
+
+# ----------------------------------------------------------------------- topk
+def test_topk_golden(gpu):
+    for f in FIX["topk"]:
+        if "state" in f:
+            e = TopkEngine(1, f["size"])
+            st = f["state"]
+            e.apply([0, len(st)], [s[0] for s in st], [s[1] for s in st])
+            if "value" in f:
+                p, i, s = e.value()
+                assert [[int(a), int(b)] for a, b in zip(i, s)] == f["value"]
+            for (pid, sc), want in f.get("downstream", []):
+                assert ("add" if e.downstream([sc])[0] == 0 else "noop") == want
+        if "ops" in f:
+            e = TopkEngine(1, f["size"])
+            ops = f["ops"]
+            e.apply([0, len(ops)], [x[0] for x in ops], [x[1] for x in ops])
+            p, i, s = e.value()
+            assert [[int(a), int(b)] for a, b in zip(i, s)] == f["value"]
+
+
+@pytest.mark.parametrize("cfg", [(50000, 500, 1000, 10**6), (30000, 100, 50, 5),
+                                 (20000, 4, 3000, 100)])
+def test_topk_random(gpu, cfg):
+    n, nk, nid, smax = cfg
+    rng = np.random.default_rng(n + nk + nid)
+    e, o = TopkEngine(nk, 100), orc.TopkOracle(nk, 100)
+    for _ in range(2):
+        keys = rng.integers(0, nk, n)
+        order, kp = _csr(keys, nk)
+        pid = rng.integers(0, nid, n)[order]
+        sc = rng.integers(0, smax, n)[order]
+        e.apply(kp, pid, sc)
+        o.apply(kp, pid, sc)
+        for a, b in zip(e.export(), o.export()):
+            assert np.array_equal(a, b)
+        for a, b in zip(e.value(), o.export(value_order=True)):
+            assert np.array_equal(a, b)
+    e2 = TopkEngine(nk, 100)
+    e2.import_state(*e.export())
+    for a, b in zip(e2.value(), o.export(value_order=True)):
+        assert np.array_equal(a, b)
+
+
+# -------------------------------------------------------------------- average
+def test_average_golden(gpu):
+    for f in FIX["average"]:
+        if "equal" in f:
+            continue
+        e = AverageEngine(1)
+        init = f.get("init")
+        if init:
+            e.import_state([init[0]], [init[1]])
+        kp, v, n = avg_fixture_ops(f)
+        e.apply(kp, v, n)
+        s, m = e.export()
+        assert [int(s[0]), int(m[0])] == f["state"]
+        if "value" in f:
+            val, ok = e.value()
+            assert ok[0] and val[0] == f["value"]  # bit-exact fp64
+
+
+def test_average_random_and_errors(gpu):
+    rng = np.random.default_rng(7)
+    nk, n = 1000, 200000
+    keys = rng.integers(0, nk, n)
+    order, kp = _csr(keys, nk)
+    v = rng.integers(-2**40, 2**40, n)[order]
+    nn = rng.integers(0, 5, n)[order]  # includes the {add,{X,0}} no-op (Q14)
+    e = AverageEngine(nk)
+    e.apply(kp, v, nn)
+    s, m, crashed = orc.avg_apply(kp, v, nn, np.zeros(nk), np.zeros(nk))
+    es, em = e.export()
+    assert not crashed and np.array_equal(es, s) and np.array_equal(em, m)
+    val, ok = e.value()
+    want = np.array([orc.avg_value(a, b) if b else 0.0 for a, b in zip(s, m)])
+    assert np.array_equal(ok, m != 0) and np.array_equal(val[ok], want[ok])
+    before = e.export()
+    with pytest.raises(_lib.CcrdtError) as ei:  # N < 0: no function clause
+        e.apply([0] + [1] * nk, [1], [-1])
+    assert ei.value.code == _lib.EINVAL
+    with pytest.raises(_lib.CcrdtError) as ei:  # leaves int64 (Erlang bignum)
+        e.apply([0] + [2] * nk, [2**62, 2**62], [1, 1])
+    assert ei.value.code == _lib.ERANGE
+    assert all(np.array_equal(a, b) for a, b in zip(e.export(), before))
+
+
+# ------------------------------------------------ wordcount / worddocumentcount
+@pytest.mark.parametrize("fx", FIX["wordcount"], ids=[f["name"] for f in FIX["wordcount"]])
+def test_wordcount_golden(gpu, fx):
+    E = WordDocumentCountEngine if fx["type"] == "worddocumentcount" else WordcountEngine
+    e = E(1)
+    e.apply_docs([[d.encode() for d in fx["docs"]]])
+    assert e.value() == {k.encode(): v for k, v in fx["expect"].items()}
+    if "then" in fx:
+        e.apply_docs([[d.encode() for d in fx["then"]["docs"]]])
+        assert e.value() == {k.encode(): v for k, v in fx["then"]["expect"].items()}
+
+
+def _zipf_docs(rng, n_docs, words_per_doc, vocab=2000):
+    words = [("w%d" % i).encode() * (1 + i % 3) for i in range(vocab)]
+    p = 1.0 / np.arange(1, vocab + 1)
+    p /= p.sum()
+    docs = []
+    for _ in range(n_docs):
+        idx = rng.choice(vocab, rng.integers(0, words_per_doc), p=p)
+        seps = rng.choice([b" ", b"\n", b"  "], len(idx), p=[0.85, 0.1, 0.05])
+        docs.append(b"".join(words[i] + s for i, s in zip(idx, seps))[:-1] if len(idx) else b"")
+    return docs
+
+
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_random(gpu, wdc):
+    rng = np.random.default_rng(11 + wdc)
+    nk = 5
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    e, o = E(nk), orc.WcOracle(nk, wdc)
+    for _ in range(3):
+        batch = [_zipf_docs(rng, int(rng.integers(0, 6)), 3000) for _ in range(nk)]
+        batch[0].append(b"")  # empty document: one empty token
+        batch[1].append(b" \n" * 3)
+        e.apply_docs(batch)
+        o.apply_docs(batch)
+        for a, b in zip(e.export(), o.export()):
+            assert np.array_equal(a, b)
+
+
+def test_wordcount_lds_overflow_path(gpu):
+    """A document with far more distinct words than the per-document LDS
+    table (512) exercises the global path (and the wdc dedupe table)."""
+    docs = [b" ".join(b"x%05d" % (i % 3000) for i in range(9000))]
+    for E, wdc in ((WordcountEngine, False), (WordDocumentCountEngine, True)):
+        e, o = E(1), orc.WcOracle(1, wdc)
+        e.apply_docs([docs])
+        o.apply_docs([docs])
+        assert e.value() == o.value()
+
+
+# ------------------------------------------------- HBM classes (beyond LDS)
+def test_topk_hbm_class(gpu):
+    """A key with 30000 ops / 9000 distinct Ids goes through the HBM hash and
+    the HBM bitonic value/1; INT64_MIN (the hash's empty marker) is an Id."""
+    rng = np.random.default_rng(3)
+    n = 30000
+    pid = rng.integers(0, 9000, n)
+    pid[::977] = np.iinfo(np.int64).min
+    sc = rng.integers(-5, 10**6, n)
+    kp = [0, 100, n]
+    e, o = TopkEngine(2, 100), orc.TopkOracle(2, 100)
+    for _ in range(2):
+        e.apply(kp, pid, sc)
+        o.apply(kp, pid, sc)
+        for a, b in zip(e.export(), o.export()):
+            assert np.array_equal(a, b)
+        for a, b in zip(e.value(), o.export(value_order=True)):
+            assert np.array_equal(a, b)
+        pid = rng.integers(0, 12000, n)
+        sc = rng.integers(0, 10**6, n)
+
+
+def test_leaderboard_hbm_class(gpu):
+    rng = np.random.default_rng(4)
+    n = 12000
+    kind = np.where(rng.random(n) < 0.03, 2, rng.integers(0, 2, n)).astype(np.uint8)
+    pid, sc = rng.integers(0, 5000, n), rng.integers(0, 10**5, n)
+    kp = [0, 50, n]
+    e, o = LeaderboardEngine(2, 100), orc.LbOracle(2, 100)
+    for _ in range(2):
+        xe, xo = e.apply(kp, kind, pid, sc), o.apply(kp, kind, pid, sc)
+        assert np.array_equal(xe["kind"], xo["kind"])
+        m = xo["kind"] == 0
+        assert np.array_equal(xe["id"][m], xo["id"][m]) and np.array_equal(xe["score"][m], xo["score"][m])
+        assert not e.export().diff(o.export())
