@@ -41,10 +41,11 @@ def _term(e, names, n_dc):
 def test_eunit_replay(gpu, mocks, fx):
     n_dc = fx["n_dc"]
     names = mocks(n_dc)
-    states = {"Top": trmv.new(fx["size"])}
+    states = {}
+    get = lambda name: states[name] if name in states else trmv.new(fx["size"])  # unnamed = new()
     for step in fx["steps"]:
         if "update" in step:
-            res = trmv.update(_effect(step["update"], names), states[step["on"]])
+            res = trmv.update(_effect(step["update"], names), get(step["on"]))
             assert res[0] == "ok"
             extra = _term(res[2][0], names, n_dc) if len(res) == 3 else None
             assert extra == step["extra"], (fx["name"], step)
@@ -56,7 +57,7 @@ def test_eunit_replay(gpu, mocks, fx):
                 assert got == step["expect"], (fx["name"], step, got)
         elif "downstream" in step:
             req = step["downstream"]
-            on = states[step["on"]]
+            on = get(step["on"])
             if req[0] == "add":
                 terms.TIME.state = step["ts"] - 1  # the mock's next tick is Ts
                 terms.DC_META_DATA.set_my_dc_id((names[step["dc"]], 0))
