@@ -31,6 +31,8 @@ int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStrea
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
 static constexpr uint32_t TRMV_MAX_ROWS = 8u * 2u * 16u;  // removal rows per key
+static constexpr int TRMV_STATUS_WORDS = 16;
+static constexpr uint32_t TRMV_LATER_GRID = 2048;  // workgroups of the tiers after the first
 
 }  // namespace ccrdt
 
@@ -149,6 +151,7 @@ int ccrdt_engine_create(int type, int64_t k, int64_t n_keys, int n_dc, int devic
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
       hipEventCreate(&e->evk0) != hipSuccess || hipEventCreate(&e->evk1) != hipSuccess ||
+      !e->create_tier_events() ||
       hipHostMalloc((void**)&e->h_status, 64, hipHostMallocDefault) != hipSuccess) {
     set_error("engine_create: stream/event/pinned allocation failed");
     delete e;
@@ -173,6 +176,8 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->evk0) (void)hipEventDestroy(e->evk0);
   if (e->evk1) (void)hipEventDestroy(e->evk1);
+  for (hipEvent_t& v : e->evt)
+    if (v) (void)hipEventDestroy(v);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return CCRDT_OK;
@@ -258,6 +263,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   const int D = E.n_dc;
   const uint64_t nk = (uint64_t)E.n_keys;
   const int out = 1 - E.cur;
+  const uint64_t n_ops = (uint64_t)ops->n_ops;
   TrmvApplyArgs a{};
   a.n_keys = E.n_keys;
   a.n_dc = D;
@@ -276,38 +282,51 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.new_s = E.trmv_side(out);
   const uint64_t nb = (nk + 1023) / 1024;
   CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t)));
-  CCRDT_TRY(E.status.ensure(64));
-  a.status = E.status.as<uint32_t>();
-  CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
+  // status words: [0..1] scan, [2+2t, 3+2t] tier t (overflow count, errors)
+  CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4));
+  uint32_t* status = E.status.as<uint32_t>();
+  CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
+  a.status = status;
   // 1) capacities -> segment offsets of the new state
   CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
-  uint64_t tot[3] = {0, 0, 0};
-  if (nk) {
+  // Sizes of the new side.  Its totals are sum(old counts + ops per key) <=
+  // (old side's totals) + n_ops, known on the host without waiting for the
+  // scan; only when that bound outgrows the buffers does the host read the
+  // exact totals (one stream sync) and grow them.
+  uint64_t tot[3];
+  for (int x = 0; x < 3; ++x) tot[x] = (E.fresh ? 0 : E.trmv_tot[E.cur][x]) + n_ops;
+  TrmvBufs& ob = E.trmv[out];
+  auto fits = [&](const TrmvBufs& b) {
+    return b.pl_id.bytes >= tot[0] * 8 && b.m_score.bytes >= tot[1] * 8 &&
+           b.r_vc.bytes >= tot[2] * 8 * D && b.vc.bytes >= nk * 8 * D;
+  };
+  if (nk && !fits(ob)) {
     CCRDT_HIP(hipMemcpyAsync(E.h_status, E.partials.as<uint64_t>() + nb * 3, 3 * sizeof(uint64_t),
                              hipMemcpyDeviceToHost, E.stream));
-    CCRDT_HIP(hipMemcpyAsync((char*)E.h_status + 32, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
     memcpy(tot, E.h_status, sizeof(tot));
-    if (((uint32_t*)((char*)E.h_status + 32))[1] & TRMV_ERR_SEG) {
-      set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
-      return CCRDT_ENOMEM;
-    }
   }
   if (tot[0] >= 0xFFFFFFFFull || tot[1] >= 0xFFFFFFFFull || tot[2] >= 0xFFFFFFFFull) {
     set_error("trmv_apply: resident state would exceed 2^32 elements");
     return CCRDT_ENOMEM;
   }
-  TrmvBufs& ob = E.trmv[out];
-  CCRDT_TRY(ob.pl_id.ensure(tot[0] * 8));
-  CCRDT_TRY(ob.pl_info.ensure(tot[0] * 4));
-  CCRDT_TRY(ob.pl_slab.ensure(tot[0] * 4));
-  CCRDT_TRY(ob.m_score.ensure(tot[1] * 8));
-  CCRDT_TRY(ob.m_ts.ensure(tot[1] * 8));
-  CCRDT_TRY(ob.m_dc.ensure(tot[1]));
-  CCRDT_TRY(ob.r_vc.ensure(tot[2] * 8 * D));
-  CCRDT_TRY(ob.vc.ensure(nk * 8 * D));
+  auto grow = [&](TrmvBufs& b) -> int {
+    CCRDT_TRY(b.meta.ensure(nk * sizeof(KeyMeta)));
+    CCRDT_TRY(b.pl_id.ensure(tot[0] * 8));
+    CCRDT_TRY(b.pl_info.ensure(tot[0] * 4));
+    CCRDT_TRY(b.pl_slab.ensure(tot[0] * 4));
+    CCRDT_TRY(b.m_score.ensure(tot[1] * 8));
+    CCRDT_TRY(b.m_ts.ensure(tot[1] * 8));
+    CCRDT_TRY(b.m_dc.ensure(tot[1]));
+    CCRDT_TRY(b.r_vc.ensure(tot[2] * 8 * D));
+    CCRDT_TRY(b.vc.ensure(nk * 8 * D));
+    return CCRDT_OK;
+  };
+  CCRDT_TRY(grow(ob));
+  // The current side holds nothing live after reset(): size it too, so the
+  // next batch (which writes it) does not allocate.
+  if (E.fresh) CCRDT_TRY(grow(E.trmv[E.cur]));
   a.new_s = E.trmv_side(out);
-  const uint64_t n_ops = (uint64_t)ops->n_ops;
   CCRDT_TRY(E.ex_cnt.ensure(nk * 4));
   CCRDT_TRY(E.ex.ensure(n_ops * sizeof(TrmvExtraRec)));
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
@@ -317,21 +336,47 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
-  // 2) per-player-parallel pass over every key, then the sequential kernel
-  //    (escalating register classes) for the keys it hands back
+  // 2) per-player-parallel tiers over every key, then the sequential kernel
+  //    (escalating register classes) for the keys each tier hands on.  Every
+  //    later tier reads its list length from the device, so the whole chain is
+  //    queued without a host round trip; one sync at the end reads the status.
+  // CCRDT_TRMV_FIRST_TIER (tuning knob, default 0): 1 skips the all-LDS tier,
+  // 2 sends every key to the sequential kernel.
+  static const int first_tier = [] {
+    const char* v = getenv("CCRDT_TRMV_FIRST_TIER");
+    return v ? atoi(v) : 0;
+  }();
+  constexpr int N_TIERS = 2 + (int)(sizeof(TRMV_SLOT_CLASSES) / sizeof(int));
+  const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
   DevBuf* work = nullptr;
-  uint64_t n_work = nk;
-  float kernel_ms = 0.f;
-  E.trmv_overflow_keys.clear();
-  E.trmv_tier_ms.clear();
-  auto read_status = [&](uint32_t& n_ovf, uint32_t& err) -> int {
-    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, 8, hipMemcpyDeviceToHost, E.stream));
-    CCRDT_HIP(hipStreamSynchronize(E.stream));
-    n_ovf = ((uint32_t*)E.h_status)[0];
-    err = ((uint32_t*)E.h_status)[1];
-    return CCRDT_OK;
-  };
-  auto fail_err = [&](uint32_t err) -> int {
+  const uint32_t* n_dev = nullptr;
+  int ev = 0;
+  CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+  for (int t = first_tier; t < N_TIERS && nk; ++t) {
+    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
+    a.key_list = work ? work->as<uint32_t>() : nullptr;
+    a.n_list = work ? 0u : (uint32_t)nk;
+    a.n_list_dev = n_dev;
+    a.ovf_list = ovf->as<uint32_t>();
+    a.status = status + 2 + 2 * t;
+    const uint64_t grid = work ? later_grid : nk;
+    if (t < 2) CCRDT_TRY(trmv_launch_fast(a, t, grid, E.stream));
+    else CCRDT_TRY(trmv_launch_apply(a, TRMV_SLOT_CLASSES[t - 2], grid, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    work = ovf;
+    n_dev = a.status;
+  }
+  CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost,
+                           E.stream));
+  CCRDT_HIP(hipStreamSynchronize(E.stream));
+  const uint32_t* hs = (const uint32_t*)E.h_status;
+  if (hs[1] & TRMV_ERR_SEG) {
+    set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
+    return CCRDT_ENOMEM;
+  }
+  uint32_t err = 0;
+  for (int t = first_tier; t < N_TIERS; ++t) err |= hs[3 + 2 * t];
+  if (err) {
     std::string m = "trmv_apply: invalid op in batch:";
     if (err & TRMV_ERR_KIND) m += " kind>3";
     if (err & TRMV_ERR_DC) m += " dc>=n_dc";
@@ -342,61 +387,26 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
                ? CCRDT_ERANGE
                : CCRDT_EINVAL;
-  };
-  // CCRDT_TRMV_FIRST_TIER (tuning knob, default 0): 1 skips the all-LDS tier,
-  // 2 sends every key to the sequential kernel.
-  static const int first_tier = [] {
-    const char* v = getenv("CCRDT_TRMV_FIRST_TIER");
-    return v ? atoi(v) : 0;
-  }();
-  for (int tier = first_tier; tier < 2 && n_work; ++tier) {
-    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
-    a.key_list = work ? work->as<uint32_t>() : nullptr;
-    a.n_list = (uint32_t)n_work;
-    a.ovf_list = ovf->as<uint32_t>();
-    CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
-    CCRDT_TRY(trmv_launch_fast(a, tier, n_work, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
-    uint32_t n_ovf = 0, err = 0;
-    CCRDT_TRY(read_status(n_ovf, err));
-    float ms = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
-    kernel_ms += ms;
-    E.trmv_tier_ms[tier] = ms;
-    E.trmv_overflow_keys[tier] = n_ovf;
-    if (err) return fail_err(err);
-    work = ovf;
-    n_work = n_ovf;
   }
-  for (int cls : TRMV_SLOT_CLASSES) {
-    if (n_work == 0) break;
-    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
-    a.key_list = work->as<uint32_t>();
-    a.n_list = (uint32_t)n_work;
-    a.ovf_list = ovf->as<uint32_t>();
-    CCRDT_HIP(hipMemsetAsync(E.status.p, 0, 8, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evk0, E.stream));
-    CCRDT_TRY(trmv_launch_apply(a, cls, n_work, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evk1, E.stream));
-    uint32_t n_ovf = 0, err = 0;
-    CCRDT_TRY(read_status(n_ovf, err));
-    float ms = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&ms, E.evk0, E.evk1));
-    kernel_ms += ms;
-    if (err) return fail_err(err);
-    E.trmv_overflow_keys[cls] = n_ovf;
-    E.trmv_tier_ms[cls] = ms;
-    work = ovf;
-    n_work = n_ovf;
-  }
-  if (n_work) {
+  if (nk && hs[2 + 2 * (N_TIERS - 1)]) {
     set_error("trmv_apply: a key exceeds the per-key capacity (1024 Ids or Masked elements, "
               "256 Removals entries)");
     return CCRDT_ENOMEM;
   }
+  E.trmv_overflow_keys.clear();
+  E.trmv_tier_ms.clear();
+  float kernel_ms = 0.f;
+  for (int t = first_tier, i = 1; t < N_TIERS && nk; ++t, ++i) {
+    const int key = t < 2 ? t : TRMV_SLOT_CLASSES[t - 2];
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[i - 1], E.evt[i]));
+    E.trmv_tier_ms[key] = ms;
+    E.trmv_overflow_keys[key] = hs[2 + 2 * t];
+  }
+  if (nk && ev > 1) CCRDT_HIP(hipEventElapsedTime(&kernel_ms, E.evt[0], E.evt[ev - 1]));
   CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
                            E.stream));
+  for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
   E.cur = out;
   E.fresh = false;
   E.last_n_ops = n_ops;
@@ -808,6 +818,9 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   }
   if (!h.r_vc.empty())
     CCRDT_HIP(hipMemcpy(b.r_vc.p, h.r_vc.data(), h.r_vc.size() * 8, hipMemcpyHostToDevice));
+  E.trmv_tot[E.cur][0] = h.pl_id.size();
+  E.trmv_tot[E.cur][1] = h.m_score.size();
+  E.trmv_tot[E.cur][2] = h.r_vc.size() / D;
   E.fresh = false;
   return CCRDT_OK;
 }

@@ -46,6 +46,12 @@ struct ccrdt_engine {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the main apply kernel
+  hipEvent_t evt[8] = {};                      // topk_rmv tier boundaries
+  bool create_tier_events() {
+    for (hipEvent_t& v : evt)
+      if (hipEventCreate(&v) != hipSuccess) return false;
+    return true;
+  }
   float last_kernel_ms = 0.f;
   void* h_status = nullptr;  // pinned, 64 bytes
   bool fresh = true;         // every key == new(k); resident arrays ignored
@@ -55,6 +61,7 @@ struct ccrdt_engine {
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, ovf_a, ovf_b, status;
   uint64_t last_n_ops = 0;
+  uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held
   std::map<int, uint32_t> trmv_overflow_keys;  // per tier / slot class, last apply
   std::map<int, float> trmv_tier_ms;
   // host-API staging

@@ -87,6 +87,7 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
   fresh = src.fresh;
   if (type == CCRDT_TOPK_RMV) {
     cur = src.cur;
+    for (int x = 0; x < 3; ++x) trmv_tot[cur][x] = src.trmv_tot[src.cur][x];
     const TrmvBufs& s = src.trmv[src.cur];
     TrmvBufs& d = trmv[cur];
     CCRDT_TRY(copy_buf(d.meta, s.meta, stream));

@@ -524,13 +524,18 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
 template <bool SMALL>
 __global__ __launch_bounds__(64) void trmv_fast_kernel(TrmvApplyArgs a) {
   __shared__ FastLds<SMALL> lds;
-  const uint64_t w = blockIdx.x;
-  const uint32_t key = a.key_list ? a.key_list[w] : (uint32_t)w;
-  if (!trmv_fast_key<SMALL>(a, key, lds)) {
-    if (lane_id() == 0) {
-      const uint32_t pos = atomicAdd(&a.status[0], 1u);
-      a.ovf_list[pos] = key;
+  // grid-stride over the work list; its length may only be known on the
+  // device (overflow count of the previous tier), so the host never waits
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t key = a.key_list ? a.key_list[w] : w;
+    if (!trmv_fast_key<SMALL>(a, key, lds)) {
+      if (lane_id() == 0) {
+        const uint32_t pos = atomicAdd(&a.status[0], 1u);
+        a.ovf_list[pos] = key;
+      }
     }
+    __syncthreads();  // LDS is reused by the next key
   }
 }
 
@@ -541,6 +546,7 @@ int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStrea
     hipLaunchKernelGGL(trmv_fast_kernel<true>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(trmv_fast_kernel<false>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  // (n_work is the grid: all keys for the first tier, a bound for later ones)
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -662,9 +662,12 @@ overflow:
 template <int S>
 __global__ __launch_bounds__(64) void trmv_apply_kernel(TrmvApplyArgs a) {
   __shared__ SeqLds<S> lds;
-  const uint64_t w = blockIdx.x;
-  const uint32_t key = a.key_list ? a.key_list[w] : (uint32_t)w;
-  trmv_process_key<S>(a, key, lds);
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t key = a.key_list ? a.key_list[w] : w;
+    trmv_process_key<S>(a, key, lds);
+    __syncthreads();  // LDS is reused by the next key
+  }
 }
 
 // ------------------------------------------------------------- capacity scan

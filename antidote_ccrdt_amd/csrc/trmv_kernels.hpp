@@ -89,6 +89,8 @@ struct TrmvApplyArgs {
   // work list (nullptr = all keys) and overflow list
   const uint32_t* key_list;
   uint32_t n_list;
+  const uint32_t* n_list_dev;  // non-null: the list length lives on the device
+                               // (the previous tier's overflow count)
   uint32_t* ovf_list;
   uint32_t* status;  // [0] overflow count, [1] error flags
 };
