@@ -12,7 +12,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libccrdt.so")
+# CCRDT_LIB selects another build of the same library (e.g. the diagnostic
+# -DTRMV_PROF build of tools/prof_phases.py); the default is the in-tree one.
+LIB_PATH = os.environ.get("CCRDT_LIB") or os.path.join(_HERE, "lib", "libccrdt.so")
 
 OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS = range(6)
 AVERAGE, TOPK, TOPK_RMV, LEADERBOARD, WORDCOUNT, WORDDOCUMENTCOUNT = range(6)

@@ -98,6 +98,32 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, uint32_t& tot
   total = rl32(inc, 63);
   return inc - v;
 }
+// Inclusive prefix sum over the 64 lanes in 6 DPP adds (no LDS crossbar):
+// row_shr 1/2/4/8 scan each 16-lane row, row_bcast:15/31 carry the row
+// totals into the rows above.  Lanes a DPP source cannot reach add `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+// Exclusive DPP scan; `total` = wave sum (wave-uniform).
+__device__ __forceinline__ uint32_t wave_excl_scan_dpp(uint32_t v, uint32_t& total) {
+  const uint32_t inc = wave_incl_scan_dpp(v);
+  total = rl32(inc, 63);
+  return inc - v;
+}
+// Orders one wavefront's LDS accesses across lanes without a workgroup
+// barrier (the LDS executes a wave's DS instructions in issue order; this
+// only stops the compiler from moving them across the point).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {

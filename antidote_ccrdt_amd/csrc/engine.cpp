@@ -27,6 +27,7 @@ int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st)
 int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st);
+int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
@@ -360,7 +361,8 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     a.ovf_list = ovf->as<uint32_t>();
     a.status = status + 2 + 2 * t;
     const uint64_t grid = work ? later_grid : nk;
-    if (t < 2) CCRDT_TRY(trmv_launch_fast(a, t, grid, E.stream));
+    if (t == 0) CCRDT_TRY(trmv_launch_wave(a, grid, E.stream));
+    else if (t == 1) CCRDT_TRY(trmv_launch_fast(a, 1, grid, E.stream));
     else CCRDT_TRY(trmv_launch_apply(a, TRMV_SLOT_CLASSES[t - 2], grid, E.stream));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     work = ovf;

@@ -1,0 +1,564 @@
+// trmv_wave.hip — tier 0 of the topk_rmv apply: one wavefront per key, four
+// independent keys per 256-thread workgroup, ~6.3 KB of LDS per key.
+//
+// Exactness argument: the per-player decomposition of trmv_fast.hip (P <= K
+// players => recompute_observed/5 never evicts, promotion candidates of rmv/3
+// are the removed player's own survivors; src/antidote_ccrdt_topk_rmv.erl
+// :231-334).  Keys outside this tier's caps go to the next tier.
+//
+// What differs from the LDS tier of trmv_fast.hip is the mapping onto gfx950:
+//  * occupancy: LDS per key is cut to ~6.3 KB (elements are addressed by
+//    index, Masked slabs are u8 index lists, removal clocks are one shared
+//    table of 16 rows) and the kernel is held to <= 80 VGPRs, so six keys
+//    are resident per SIMD instead of three;
+//  * latency: every global load a key needs is issued before its first use
+//    (ops, old players, old rows), the removal clocks of the batch are
+//    fetched in one cooperative pass (8 lanes per clock row) while the hash
+//    table is built;
+//  * no workgroup barriers: the four keys of a workgroup are independent and
+//    each wave orders its own LDS accesses (wave_lds_sync);
+//  * grouping: 64-bit LDS compare-and-swap on the Id itself (one probe loop,
+//    no claim protocol); players are numbered in hash-slot order (new ones
+//    after the old ones), so the device layout is deterministic;
+//  * scans are DPP (wave_excl_scan_dpp), not LDS-crossbar shuffles.
+//
+// Element index space of a key: [0, nops) = this batch's ops (stream order),
+// [nops, nops + old |Masked|) = the key's old Masked elements.
+#include "common.hpp"
+#include "trmv_kernels.hpp"
+
+namespace ccrdt {
+
+namespace {
+constexpr int W_HCAP = 256;  // hash slots (Ids)
+constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
+constexpr int W_PCAP = 128;  // players
+constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
+constexpr int W_WAVES = 4;   // keys per workgroup
+constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
+constexpr uint32_t NONE8 = 0xFFu;
+
+struct alignas(16) WaveLds {
+  unsigned long long htab[W_HCAP];  // Ids (W_EMPTY = free)
+  int64_t esc[W_ECAP];              // element score (rmv op: its clock row in `rows`)
+  int64_t ets[W_ECAP];              // element ts    (rmv op: its row of rmv_vc)
+  int64_t rows[W_RCAP][TRMV_DPAD];  // [0, old nr) old Removals rows, then rmv clocks
+  unsigned long long vc[TRMV_DPAD]; // replica Vc
+  uint16_t ekd[W_ECAP];             // kind | dc << 2 | player << 8
+  uint8_t hp[W_HCAP];               // hash slot -> player
+  uint8_t pslot[W_PCAP];            // player -> hash slot
+  uint8_t sorted[W_ECAP];           // ops grouped by player (stream order inside a player)
+  uint8_t slab[W_ECAP];             // working Masked slabs (element indices)
+  uint8_t fin[W_ECAP];              // final pool: element of every output position
+  uint8_t pstart[W_PCAP];           // first `sorted` position of each player
+  uint32_t pcnt2[W_PCAP / 2];       // ops per player (two u16 counters per word)
+  uint32_t rsrc[W_RCAP];            // rmv_vc row of each staged rmv clock
+  uint8_t rl[W_RCAP];               // clock row of each output Removals row (player order)
+  uint8_t pobs[W_PCAP];             // Obs[Id] of each player (element), NONE8 = not observed
+  uint32_t nex;                     // extra effects emitted by the key
+};
+
+__device__ __forceinline__ uint32_t whash(int64_t id) {
+  const uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(x >> 56);  // 8 bits = W_HCAP slots
+}
+
+__device__ __forceinline__ uint32_t pcnt_of(const WaveLds& L, uint32_t p) {
+  return (L.pcnt2[p >> 1] >> (16 * (p & 1))) & 0xFFFFu;
+}
+
+// One extra effect (the {ok, S, [Effect]} of topk_rmv.erl:236-237 / :294-295).
+__device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, WaveLds& L, uint64_t op0,
+                                          uint64_t op, uint8_t kind, int64_t id, int64_t sc,
+                                          uint32_t dc, int64_t ts, uint32_t row) {
+  const uint32_t pos = atomicAdd(&L.nex, 1u);
+  TrmvExtraRec r;
+  r.op = (uint32_t)op;
+  r.kind = kind;
+  r.dc = (uint8_t)dc;
+  r.pad = 0;
+  r.id = id;
+  r.score = sc;
+  r.ts = ts;
+  a.ex[op0 + pos] = r;
+  if (kind == CCRDT_TRMV_RMV)
+    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
+}
+
+// Returns false (having written nothing to HBM) if the key must take the next tier.
+__device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, WaveLds& L) {
+  const int lane = lane_id();
+  const int D = a.n_dc;
+  const uint64_t op0 = a.key_ptr[key];
+  const uint64_t op1 = a.key_ptr[key + 1];
+  const uint32_t nops = (uint32_t)(op1 - op0);
+  const KeyMeta nmeta = a.new_s.meta[key];
+  KeyMeta om;
+  if (a.fresh) {
+    om.p_off = om.m_off = om.r_off = 0;
+    om.np = om.nm = om.nr = om.nobs = 0;
+    om.minq = NONE32;
+  } else {
+    om = a.old_s.meta[key];
+  }
+  const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
+  if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
+      om.nr > (uint32_t)W_RCAP)
+    return false;
+
+  // ---- 1. issue every load of the key: ops, old players, old clock rows
+  int64_t xid[2], xsc[2], xts[2];
+  uint32_t xkd[2];
+  bool xv[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t l = s * 64 + lane;
+    xv[s] = l < nops;
+    const uint64_t i = op0 + (xv[s] ? l : 0u);
+    xid[s] = xv[s] ? a.id[i] : 0;
+    xsc[s] = xv[s] ? a.score[i] : 0;
+    xts[s] = xv[s] ? a.ts[i] : 0;
+    xkd[s] = xv[s] ? ((uint32_t)a.kind[i] | ((uint32_t)a.dc[i] << 8)) : 0u;
+  }
+  int64_t pid[2] = {0, 0};
+  uint32_t pinfo[2] = {NONE32, NONE32}, pslab[2] = {0u, 0u};
+  if (!a.fresh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      if (p < om.np) {
+        pid[s] = a.old_s.pl_id[om.p_off + p];
+        pinfo[s] = a.old_s.pl_info[om.p_off + p];
+        pslab[s] = a.old_s.pl_slab[om.p_off + p];
+      }
+    }
+  }
+  // LDS init (overlaps the loads)
+  for (int i = lane; i < W_HCAP; i += 64) L.htab[i] = W_EMPTY;
+  reinterpret_cast<uint32_t*>(L.hp)[lane] = 0xFFFFFFFFu;  // 256 B
+  L.pcnt2[lane] = 0u;
+  if (lane == 0) L.nex = 0u;
+  if (lane < TRMV_DPAD)
+    L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+  if (!a.fresh) {  // old Removals rows -> clock rows [0, om.nr)
+    for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
+      const uint32_t r = r0 + (lane >> 3), d = lane & 7;
+      if (r < om.nr)
+        L.rows[r][d] = (int)d < D ? a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d] : 0;
+    }
+  }
+
+  // ---- 2. validate ops, stage element fields, rank the rmv ops
+  uint32_t err = 0;
+  bool xr[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t kind = xkd[s] & 0xFFu, dc = xkd[s] >> 8;
+    xr[s] = xv[s] && kind >= 2;
+    if (xv[s]) {
+      if (kind > 3) err |= TRMV_ERR_KIND;
+      else if (kind < 2) {
+        if ((int)dc >= D) err |= TRMV_ERR_DC;
+        if (xts[s] < 1) err |= TRMV_ERR_TS;
+      } else if (xts[s] < 0 || xts[s] >= a.n_rmv_rows) {
+        err |= TRMV_ERR_ROW;
+      }
+    }
+  }
+  if (ballot(err != 0)) {
+    if (err) atomicOr(&a.status[1], err);
+    return true;  // the host rejects the batch
+  }
+  const uint64_t rb0 = ballot(xr[0]), rb1 = ballot(xr[1]);
+  const uint32_t nr0 = (uint32_t)__builtin_popcountll(rb0);
+  const uint32_t nrmv = nr0 + (uint32_t)__builtin_popcountll(rb1);
+  if (om.nr + nrmv > (uint32_t)W_RCAP) return false;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t l = s * 64 + lane;
+    if (xv[s]) {
+      int64_t sc = xsc[s];
+      if (xr[s]) {
+        const uint32_t r = (s == 0 ? 0u : nr0) + mbcnt(s == 0 ? rb0 : rb1);
+        L.rsrc[r] = (uint32_t)xts[s];
+        sc = om.nr + r;  // clock row of this rmv
+      }
+      L.esc[l] = sc;
+      L.ets[l] = xts[s];
+    }
+  }
+  wave_lds_sync();
+  // rmv clocks: 8 lanes per row, coalesced (issued before the hash build)
+  int64_t rv[W_RCAP / 8];
+#pragma unroll
+  for (int s = 0; s < W_RCAP / 8; ++s) {
+    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+    rv[s] = (r < nrmv && (int)d < D) ? a.rmv_vc[(uint64_t)L.rsrc[r] * D + d] : 0;
+  }
+
+  // ---- 3. hash build: old players, then ops (64-bit CAS on the Id)
+  uint32_t hs[4];
+  bool pend[4];
+  int64_t hid[4] = {pid[0], pid[1], xid[0], xid[1]};
+  pend[0] = !a.fresh && (uint32_t)lane < om.np;
+  pend[1] = !a.fresh && (uint32_t)(64 + lane) < om.np;
+  pend[2] = xv[0];
+  pend[3] = xv[1];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hs[j] = whash(hid[j]);
+    bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
+  }
+  if (ballot(bad)) return false;
+  while (ballot(pend[0] || pend[1] || pend[2] || pend[3])) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (pend[j]) {
+        const unsigned long long prev =
+            atomicCAS(&L.htab[hs[j]], W_EMPTY, (unsigned long long)hid[j]);
+        if (prev == W_EMPTY || prev == (unsigned long long)hid[j]) pend[j] = false;
+        else hs[j] = (hs[j] + 1) & (W_HCAP - 1);
+      }
+    }
+  }
+  // old players keep their index
+  if (!a.fresh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      if (p < om.np) {
+        L.hp[hs[s]] = (uint8_t)p;
+        L.pslot[p] = (uint8_t)hs[s];
+        // every player with Masked elements must be in Observed (P <= K states)
+        bad |= ((pslab[s] >> 16) != 0) != ((pinfo[s] & 0xFFFFu) != NONE16);
+      }
+    }
+    if (ballot(bad)) return false;
+  }
+  // write the staged rmv clocks (loads were in flight during the build)
+#pragma unroll
+  for (int s = 0; s < W_RCAP / 8; ++s) {
+    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+    if (r < nrmv) {
+      if (rv[s] < 0) err |= TRMV_ERR_VC;
+      L.rows[om.nr + r][d] = rv[s];
+    }
+  }
+  if (ballot(err != 0)) {
+    if (err) atomicOr(&a.status[1], err);
+    return true;
+  }
+  wave_lds_sync();
+  // new players numbered after the old ones, in hash-slot order
+  uint32_t np;
+  {
+    uint32_t c = 0, newm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i = (uint32_t)lane * 4 + q;
+      const bool nw = L.htab[i] != W_EMPTY && L.hp[i] == NONE8;
+      newm |= (nw ? 1u : 0u) << q;
+      c += nw ? 1u : 0u;
+    }
+    const uint64_t b0 = ballot(c & 1), b1 = ballot(c & 2), b2 = ballot(c & 4);
+    uint32_t idx = om.np + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
+    np = om.np + (uint32_t)__builtin_popcountll(b0) + 2 * (uint32_t)__builtin_popcountll(b1) +
+         4 * (uint32_t)__builtin_popcountll(b2);
+    if (np > pmax) return false;  // Observed could fill: next tier
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (newm & (1u << q)) {
+        const uint32_t i = (uint32_t)lane * 4 + q;
+        L.hp[i] = (uint8_t)idx;
+        L.pslot[idx] = (uint8_t)i;
+        ++idx;
+      }
+    }
+  }
+  wave_lds_sync();
+
+  // ---- 4. player of every op, Vc, counting sort by player
+  uint32_t xrank[2], xp[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    xp[s] = 0;
+    xrank[s] = 0;
+    if (xv[s]) {
+      const uint32_t kind = xkd[s] & 0xFFu, dc = xkd[s] >> 8;
+      const uint32_t p = L.hp[hs[2 + s]];
+      xp[s] = p;
+      L.ekd[s * 64 + lane] = (uint16_t)(kind | (dc << 2) | (p << 8));
+      if (kind < 2) atomicMax(&L.vc[dc], (unsigned long long)xts[s]);  // vc_update (:233)
+      const uint32_t sh = 16 * (p & 1);
+      xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    }
+  }
+  wave_lds_sync();
+  // per player (lane, lane + 64): first position of its ops in `sorted`
+  {
+    uint32_t tot0, tot1;
+    const uint32_t c0 = (uint32_t)lane < np ? pcnt_of(L, lane) : 0u;
+    const uint32_t c1 = (uint32_t)(64 + lane) < np ? pcnt_of(L, 64 + lane) : 0u;
+    const uint32_t st0 = wave_excl_scan_dpp(c0, tot0);
+    const uint32_t st1 = wave_excl_scan_dpp(c1, tot1);
+    if ((uint32_t)lane < np) L.pstart[lane] = (uint8_t)st0;
+    if ((uint32_t)(64 + lane) < np) L.pstart[64 + lane] = (uint8_t)(tot0 + st1);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    if (xv[s]) L.sorted[L.pstart[xp[s]] + xrank[s]] = (uint8_t)(s * 64 + lane);
+  // old Masked elements -> elements [nops, nops + om.nm), player by player
+  if (!a.fresh) {
+    uint32_t ebase = nops;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      const uint32_t oc = p < om.np ? (pslab[s] >> 16) : 0u;
+      uint32_t tot;
+      const uint32_t eb = ebase + wave_excl_scan_dpp(oc, tot);
+      ebase += tot;
+      for (uint32_t j = 0; j < oc; ++j) {
+        const uint64_t go = (uint64_t)om.m_off + (pslab[s] & 0xFFFFu) + j;
+        const uint32_t e = eb + j;
+        L.esc[e] = a.old_s.m_score[go];
+        L.ets[e] = a.old_s.m_ts[go];
+        L.ekd[e] = (uint16_t)(((uint32_t)a.old_s.m_dc[go] << 2) | (p << 8));
+      }
+    }
+  }
+  wave_lds_sync();
+
+  // ---- 5. replay every player's ops (lane = player; players lane, lane + 64)
+  uint32_t fbase = 0, rbase = 0, nobs = 0, mbase = 0, ebase = nops;
+#pragma unroll 1
+  for (int s = 0; s < 2; ++s) {
+    if (s * 64 >= (int)np) break;  // wave-uniform
+    const uint32_t p = s * 64 + lane;
+    const bool act = p < np;
+    const uint32_t pinfo_s = s ? pinfo[1] : pinfo[0];
+    const uint32_t ocnt = (act && p < om.np) ? ((s ? pslab[1] : pslab[0]) >> 16) : 0u;
+    const uint32_t c = act ? pcnt_of(L, p) : 0u;
+    const uint32_t st = act ? L.pstart[p] : 0u;
+    uint32_t tot;
+    const uint32_t moff = mbase + wave_excl_scan_dpp(c + ocnt, tot);  // slab capacity
+    mbase += tot;
+    const uint32_t eb = ebase + wave_excl_scan_dpp(ocnt, tot);        // old elements
+    ebase += tot;
+    // stable order: insertion sort of this player's op list (ranks came from
+    // LDS atomics, whose order inside one instruction is not specified)
+    for (uint32_t x = 1; x < c; ++x) {
+      const uint32_t v = L.sorted[st + x];
+      uint32_t y = x;
+      while (y > 0 && L.sorted[st + y - 1] > v) {
+        L.sorted[st + y] = L.sorted[st + y - 1];
+        --y;
+      }
+      L.sorted[st + y] = (uint8_t)v;
+    }
+    // initial player state
+    uint32_t cnt = ocnt;
+    int64_t maxts = 0;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      L.slab[moff + j] = (uint8_t)(eb + j);
+      const int64_t t = L.ets[eb + j];
+      maxts = t > maxts ? t : maxts;
+    }
+    uint32_t o = NONE8, prow = NONE8;
+    int64_t osc = 0, ots = 0;
+    if (act && !a.fresh && p < om.np) {
+      const uint32_t oi = pinfo_s & 0xFFFFu, ri = pinfo_s >> 16;
+      if (oi != NONE16) {
+        o = eb + oi;
+        osc = L.esc[o];
+        ots = L.ets[o];
+      }
+      if (ri != NONE16) prow = ri;
+    }
+    const int64_t id = act ? (int64_t)L.htab[L.pslot[p]] : 0;
+    for (uint32_t x = 0; x < c; ++x) {
+      const uint32_t e = L.sorted[st + x];
+      const uint32_t kd = L.ekd[e];
+      const int64_t sc = L.esc[e];
+      const int64_t t = L.ets[e];
+      const uint32_t kind = kd & 3u, dc = (kd >> 2) & 7u;
+      const uint64_t gop = op0 + e;
+      if (kind < 2) {  // add/4 (:231-249)
+        if (prow != NONE8 && L.rows[prow][dc] >= t) {  // dominated (:234-237)
+          wave_emit(a, L, op0, gop, CCRDT_TRMV_RMV, id, 0, 0, 0, prow);
+          continue;
+        }
+        // gb_sets:add_element: set semantics (a ts above every ts ever in the
+        // slab cannot duplicate an element)
+        uint32_t ee = e;
+        if (t <= maxts) {
+          for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t e2 = L.slab[moff + j];
+            if (L.ets[e2] == t && ((L.ekd[e2] >> 2) & 7u) == dc && L.esc[e2] == sc) {
+              ee = e2;
+              break;
+            }
+          }
+        }
+        maxts = t > maxts ? t : maxts;
+        if (ee == e) L.slab[moff + cnt++] = (uint8_t)e;
+        // recompute_observed (:301-324; never full in this tier)
+        if (o == NONE8 || sc > osc || (sc == osc && t > ots)) {
+          o = ee;
+          osc = sc;
+          ots = t;
+        }
+      } else {  // rmv/3 (:252-298)
+        const uint32_t vs = (uint32_t)sc;  // this rmv's clock row
+        if (prow == NONE8) {
+          prow = vs;  // Removals[Id] := VcRmv
+        } else {
+          for (int d = 0; d < D; ++d) {  // merge_vc (:369-386)
+            const int64_t u = L.rows[vs][d], w0 = L.rows[prow][d];
+            L.rows[prow][d] = u > w0 ? u : w0;
+          }
+        }
+        // keep Masked[Id] elements with Ts > VcRmv[DcId] (:255-266)
+        uint32_t w = 0, be = NONE8, bdc = 0;
+        bool alive = false;
+        int64_t bsc = 0, bts = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t e2 = L.slab[moff + j];
+          const int64_t t2 = L.ets[e2];
+          const uint32_t d2 = (L.ekd[e2] >> 2) & 7u;
+          if (t2 > L.rows[vs][d2]) {
+            L.slab[moff + w++] = (uint8_t)e2;
+            alive |= e2 == o;
+            const int64_t s2 = L.esc[e2];
+            if (be == NONE8 || s2 > bsc || (s2 == bsc && (d2 > bdc || (d2 == bdc && t2 > bts)))) {
+              be = e2;
+              bsc = s2;
+              bdc = d2;
+              bts = t2;
+            }
+          }
+        }
+        cnt = w;
+        if (o != NONE8 && !alive) {  // impacts Observed (:267-272)
+          if (cnt == 0) {
+            o = NONE8;
+          } else {  // promote gb_sets:largest of the survivors (:291-295)
+            o = be;
+            osc = bsc;
+            ots = bts;
+            wave_emit(a, L, op0, gop, CCRDT_TRMV_ADD, id, bsc, bdc, bts, prow);
+          }
+        }
+      }
+    }
+    // final slab -> compact pool positions; the player record
+    uint32_t ftot;
+    const uint32_t goff = fbase + wave_excl_scan_dpp(act ? cnt : 0u, ftot);
+    fbase += ftot;
+    uint32_t opos = NONE16;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint32_t e2 = L.slab[moff + j];
+      L.fin[goff + j] = (uint8_t)e2;
+      if (e2 == o) opos = j;
+    }
+    const uint64_t rm = ballot(act && prow != NONE8);
+    const uint32_t rix = rbase + mbcnt(rm);
+    rbase += (uint32_t)__builtin_popcountll(rm);
+    if (act) {
+      if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
+      a.new_s.pl_id[nmeta.p_off + p] = id;
+      a.new_s.pl_info[nmeta.p_off + p] = opos | ((prow != NONE8 ? rix : NONE16) << 16);
+      a.new_s.pl_slab[nmeta.p_off + p] = goff | (cnt << 16);
+    }
+    if (act) L.pobs[p] = (uint8_t)o;
+    nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
+  }
+  wave_lds_sync();
+
+  // ---- 6. Masked pool, Removals rows, Vc, Min, metadata
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t q = s * 64 + lane;
+    if (q < fbase) {
+      const uint32_t e = L.fin[q];
+      const uint64_t g = (uint64_t)nmeta.m_off + q;
+      a.new_s.m_score[g] = L.esc[e];
+      a.new_s.m_ts[g] = L.ets[e];
+      a.new_s.m_dc[g] = (uint8_t)((L.ekd[e] >> 2) & 7u);
+    }
+  }
+  for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
+    const uint32_t r = r0 + (lane >> 3), d = lane & 7;
+    if (r < rbase && (int)d < D)
+      a.new_s.r_vc[((uint64_t)nmeta.r_off + r) * D + d] = L.rows[L.rl[r]][d];
+  }
+  if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+  // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
+  uint32_t best_q = NONE32;
+  {
+    int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      const uint32_t o = p < np ? L.pobs[p] : NONE8;
+      if (o != NONE8) {
+        const int64_t sc = L.esc[o], id = (int64_t)L.htab[L.pslot[p]];
+        if (best_q == NONE32 || sc < best_sc || (sc == best_sc && id < best_id)) {
+          best_q = p;
+          best_sc = sc;
+          best_id = id;
+        }
+      }
+    }
+    const bool has = best_q != NONE32;
+    if (ballot(has)) {
+      const int64_t ms = wave_min_i64(has ? best_sc : INT64_MAX);
+      const int64_t mi = wave_min_i64(has && best_sc == ms ? best_id : INT64_MAX);
+      const uint64_t hit = ballot(has && best_sc == ms && best_id == mi);
+      best_q = rl32(best_q, (int)__builtin_ctzll(hit));
+    } else {
+      best_q = NONE32;
+    }
+  }
+  if (lane == 0) {
+    KeyMeta out = nmeta;
+    out.np = np;
+    out.nm = fbase;
+    out.nr = rbase;
+    out.nobs = nobs;
+    out.minq = best_q;
+    a.new_s.meta[key] = out;
+    a.ex_cnt[key] = L.nex;
+  }
+  return true;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void trmv_wave_kernel(TrmvApplyArgs a) {
+  __shared__ WaveLds lds[W_WAVES];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveLds& L = lds[wv];
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x * W_WAVES + wv; w < n; w += gridDim.x * W_WAVES) {
+    const uint32_t key = a.key_list ? a.key_list[w] : w;
+    if (!trmv_wave_key(a, key, L)) {
+      if (lane_id() == 0) {
+        const uint32_t pos = atomicAdd(&a.status[0], 1u);
+        a.ovf_list[pos] = key;
+      }
+    }
+    wave_lds_sync();  // LDS is reused by the wave's next key
+  }
+}
+
+// grid_keys = keys the grid covers (all keys for the first tier)
+int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
+  if (grid_keys == 0) return CCRDT_OK;
+  const uint64_t blocks = (grid_keys + W_WAVES - 1) / W_WAVES;
+  hipLaunchKernelGGL(trmv_wave_kernel, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+}  // namespace ccrdt
