@@ -33,28 +33,6 @@
 #include "common.hpp"
 #include "trmv_kernels.hpp"
 
-// Diagnostic build only (-DTRMV_PROF): per-phase s_memtime stamps summed
-// over keys; read with ccrdt_debug_trmv_prof().  No stamp in the real build.
-#ifdef TRMV_PROF
-__device__ unsigned long long g_trmv_prof[16];
-#define PROF_STAMP(v)                                                        \
-  do {                                                                       \
-    __builtin_amdgcn_sched_barrier(0);                                       \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                       \
-  } while (0)
-#define PROF_MARK(i)                                                         \
-  do {                                                                       \
-    unsigned long long _t;                                                   \
-    PROF_STAMP(_t);                                                          \
-    if (lane_id() == 0 && (key & 63u) == 0) atomicAdd(&g_trmv_prof[i], _t - prof_t);             \
-    prof_t = _t;                                                             \
-  } while (0)
-#else
-#define PROF_STAMP(v) (void)0
-#define PROF_MARK(i) (void)0
-#endif
-
 namespace ccrdt {
 
 constexpr uint32_t F_CLAIM = 1u << 31;
@@ -157,10 +135,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
   using C = FastCfg<SMALL>;
   const int lane = lane_id();
   const int D = a.n_dc;
-#ifdef TRMV_PROF
-  unsigned long long prof_t;
-  PROF_STAMP(prof_t);
-#endif
   const KeyMeta nmeta = a.new_s.meta[key];
   KeyMeta om;
   if (a.fresh) {
@@ -207,7 +181,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
   }
   if (ballot(bad)) return false;
   __syncthreads();
-  PROF_MARK(0);
 
   // ---- 2. load ops, player of every op (new Ids claimed in lane order)
   int64_t* claim_id = SMALL ? L.msc : L.msc;  // LDS scratch, 64 entries
@@ -297,7 +270,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
     return true;  // the host rejects the batch
   }
 
-  PROF_MARK(1);
   // ---- 3. counting sort of ops by player
   {
     uint32_t base = 0;
@@ -318,7 +290,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
   }
   __syncthreads();
 
-  PROF_MARK(2);
   // ---- 4. replay each player's ops (lane = player)
   uint32_t slab_base = 0, row_base = 0, nm = 0, nobs = 0;
   int64_t best_sc = 0, best_id = 0;
@@ -503,7 +474,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
       best_id = id;
     }
   }
-  PROF_MARK(3);
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct
   {
     const bool has = best_q != NONE32;
@@ -548,7 +518,6 @@ __device__ __forceinline__ bool trmv_fast_key(const TrmvApplyArgs& a, uint32_t k
     a.new_s.meta[key] = out;
     a.ex_cnt[key] = L.nex;
   }
-  PROF_MARK(4);
   return true;
 }
 
@@ -584,13 +553,3 @@ int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStrea
 
 }  // namespace ccrdt
 
-#ifdef TRMV_PROF
-extern "C" int ccrdt_debug_trmv_prof(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_trmv_prof), 16 * 8) != hipSuccess) return 4;
-  if (reset) {
-    unsigned long long z[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trmv_prof), z, sizeof(z)) != hipSuccess) return 4;
-  }
-  return 0;
-}
-#endif

@@ -20,12 +20,40 @@
 //  * grouping: 64-bit LDS compare-and-swap on the Id itself (one probe loop,
 //    no claim protocol); players are numbered in hash-slot order (new ones
 //    after the old ones), so the device layout is deterministic;
-//  * scans are DPP (wave_excl_scan_dpp), not LDS-crossbar shuffles.
+//  * scans are DPP (wave_excl_scan_dpp), not LDS-crossbar shuffles;
+//  * each wave runs W_KPW consecutive keys and issues the next key's loads
+//    (bounds, metadata, ops) before the current key's write-out, so the
+//    first HBM round trip of a key overlaps the previous key's stores;
+//  * op elements are stored at their position in player order, so the replay
+//    reads an op with one LDS round trip.
 //
-// Element index space of a key: [0, nops) = this batch's ops (stream order),
-// [nops, nops + old |Masked|) = the key's old Masked elements.
+// Element index space of a key: [0, nops) = this batch's ops, grouped by player
+// (stream order inside a player), [nops, nops + old |Masked|) = the key's old
+// Masked elements.
 #include "common.hpp"
 #include "trmv_kernels.hpp"
+
+// Diagnostic build only (-DTRMV_PROF): per-phase s_memtime stamps summed
+// over keys; read with ccrdt_debug_trmv_prof().  No stamp in the real build.
+#ifdef TRMV_PROF
+__device__ unsigned long long g_trmv_prof[16];
+#define PROF_STAMP(v)                                                        \
+  do {                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+  } while (0)
+#define PROF_MARK(i)                                                         \
+  do {                                                                       \
+    unsigned long long _t;                                                   \
+    PROF_STAMP(_t);                                                          \
+    if (lane_id() == 0 && (key & 63u) == 0) atomicAdd(&g_trmv_prof[i], _t - prof_t);             \
+    prof_t = _t;                                                             \
+  } while (0)
+#else
+#define PROF_STAMP(v) (void)0
+#define PROF_MARK(i) (void)0
+#endif
 
 namespace ccrdt {
 
@@ -34,20 +62,21 @@ constexpr int W_HCAP = 256;  // hash slots (Ids)
 constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
-constexpr int W_WAVES = 4;   // keys per workgroup
+constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
+constexpr int W_KPW = 8;     // consecutive keys per wave
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
 constexpr uint32_t NONE8 = 0xFFu;
 
 struct alignas(16) WaveLds {
   unsigned long long htab[W_HCAP];  // Ids (W_EMPTY = free)
   int64_t esc[W_ECAP];              // element score (rmv op: its clock row in `rows`)
-  int64_t ets[W_ECAP];              // element ts    (rmv op: its row of rmv_vc)
+  int64_t ets[W_ECAP];              // element ts
   int64_t rows[W_RCAP][TRMV_DPAD];  // [0, old nr) old Removals rows, then rmv clocks
   unsigned long long vc[TRMV_DPAD]; // replica Vc
   uint16_t ekd[W_ECAP];             // kind | dc << 2 | player << 8
   uint8_t hp[W_HCAP];               // hash slot -> player
   uint8_t pslot[W_PCAP];            // player -> hash slot
-  uint8_t sorted[W_ECAP];           // ops grouped by player (stream order inside a player)
+  uint8_t sorted[W_ECAP];           // op index (stream position) of every op element
   uint8_t slab[W_ECAP];             // working Masked slabs (element indices)
   uint8_t fin[W_ECAP];              // final pool: element of every output position
   uint8_t pstart[W_PCAP];           // first `sorted` position of each player
@@ -85,14 +114,55 @@ __device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, WaveLds& L, ui
     for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
 }
 
-// Returns false (having written nothing to HBM) if the key must take the next tier.
-__device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, WaveLds& L) {
+// What a key needs before anything else: bounds, new-side metadata, its ops.
+struct KeyIn {
+  uint64_t op0;
+  uint32_t nops;
+  KeyMeta nmeta;
+  int64_t id[2], sc[2], ts[2];
+  uint32_t kd[2];  // kind | dc << 8
+};
+
+__device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, uint32_t key, KeyIn& in) {
+  const int lane = lane_id();
+  in.op0 = a.key_ptr[key];
+  in.nops = (uint32_t)(a.key_ptr[key + 1] - in.op0);
+  in.nmeta = a.new_s.meta[key];
+  // wave-uniform bases + 32-bit lane offsets (saddr addressing, no 64-bit
+  // per-lane address arithmetic)
+  const int64_t* idp = a.id + in.op0;
+  const int64_t* scp = a.score + in.op0;
+  const int64_t* tsp = a.ts + in.op0;
+  const uint8_t* kp = a.kind + in.op0;
+  const uint8_t* dp = a.dc + in.op0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t l = s * 64 + lane;
+    const bool v = l < in.nops;
+    in.id[s] = v ? idp[l] : 0;
+    in.sc[s] = v ? scp[l] : 0;
+    in.ts[s] = v ? tsp[l] : 0;
+    in.kd[s] = v ? ((uint32_t)kp[l] | ((uint32_t)dp[l] << 8)) : 0u;
+  }
+}
+
+// Outcome of one key.  Only W_DONE has already issued the loads of the wave's
+// next key (just before the write-out); the rare other paths leave that to the
+// caller, which keeps the prefetched registers out of the early phases.
+enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
+#define WAVE_RETURN(v) return (v)
+
+__device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
+                                              WaveLds& L, bool has_next, uint32_t nkey, KeyIn& nxt) {
   const int lane = lane_id();
   const int D = a.n_dc;
-  const uint64_t op0 = a.key_ptr[key];
-  const uint64_t op1 = a.key_ptr[key + 1];
-  const uint32_t nops = (uint32_t)(op1 - op0);
-  const KeyMeta nmeta = a.new_s.meta[key];
+#ifdef TRMV_PROF
+  unsigned long long prof_t;
+  PROF_STAMP(prof_t);
+#endif
+  const uint64_t op0 = in.op0;
+  const uint32_t nops = in.nops;
+  const KeyMeta nmeta = in.nmeta;
   KeyMeta om;
   if (a.fresh) {
     om.p_off = om.m_off = om.r_off = 0;
@@ -104,22 +174,12 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
   const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
   if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
       om.nr > (uint32_t)W_RCAP)
-    return false;
+    WAVE_RETURN(W_NEXT_TIER);
 
-  // ---- 1. issue every load of the key: ops, old players, old clock rows
-  int64_t xid[2], xsc[2], xts[2];
-  uint32_t xkd[2];
-  bool xv[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const uint32_t l = s * 64 + lane;
-    xv[s] = l < nops;
-    const uint64_t i = op0 + (xv[s] ? l : 0u);
-    xid[s] = xv[s] ? a.id[i] : 0;
-    xsc[s] = xv[s] ? a.score[i] : 0;
-    xts[s] = xv[s] ? a.ts[i] : 0;
-    xkd[s] = xv[s] ? ((uint32_t)a.kind[i] | ((uint32_t)a.dc[i] << 8)) : 0u;
-  }
+  // ---- 1. the ops are in `in`; issue the old-state loads
+  int64_t xid[2] = {in.id[0], in.id[1]}, xsc[2] = {in.sc[0], in.sc[1]}, xts[2] = {in.ts[0], in.ts[1]};
+  const uint32_t xkd[2] = {in.kd[0], in.kd[1]};
+  const bool xv[2] = {(uint32_t)lane < nops, (uint32_t)(64 + lane) < nops};
   int64_t pid[2] = {0, 0};
   uint32_t pinfo[2] = {NONE32, NONE32}, pslab[2] = {0u, 0u};
   if (!a.fresh) {
@@ -127,9 +187,9 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
       if (p < om.np) {
-        pid[s] = a.old_s.pl_id[om.p_off + p];
-        pinfo[s] = a.old_s.pl_info[om.p_off + p];
-        pslab[s] = a.old_s.pl_slab[om.p_off + p];
+        pid[s] = (a.old_s.pl_id + om.p_off)[p];
+        pinfo[s] = (a.old_s.pl_info + om.p_off)[p];
+        pslab[s] = (a.old_s.pl_slab + om.p_off)[p];
       }
     }
   }
@@ -144,10 +204,11 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7;
       if (r < om.nr)
-        L.rows[r][d] = (int)d < D ? a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d] : 0;
+        L.rows[r][d] = (int)d < D ? (a.old_s.r_vc + (uint64_t)om.r_off * D)[r * D + d] : 0;
     }
   }
 
+  PROF_MARK(0);
   // ---- 2. validate ops, stage element fields, rank the rmv ops
   uint32_t err = 0;
   bool xr[2];
@@ -167,24 +228,18 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
-    return true;  // the host rejects the batch
+    WAVE_RETURN(W_REJECT);  // the host rejects the batch
   }
   const uint64_t rb0 = ballot(xr[0]), rb1 = ballot(xr[1]);
   const uint32_t nr0 = (uint32_t)__builtin_popcountll(rb0);
   const uint32_t nrmv = nr0 + (uint32_t)__builtin_popcountll(rb1);
-  if (om.nr + nrmv > (uint32_t)W_RCAP) return false;
+  if (om.nr + nrmv > (uint32_t)W_RCAP) WAVE_RETURN(W_NEXT_TIER);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const uint32_t l = s * 64 + lane;
-    if (xv[s]) {
-      int64_t sc = xsc[s];
-      if (xr[s]) {
-        const uint32_t r = (s == 0 ? 0u : nr0) + mbcnt(s == 0 ? rb0 : rb1);
-        L.rsrc[r] = (uint32_t)xts[s];
-        sc = om.nr + r;  // clock row of this rmv
-      }
-      L.esc[l] = sc;
-      L.ets[l] = xts[s];
+    if (xr[s]) {
+      const uint32_t r = (s == 0 ? 0u : nr0) + mbcnt(s == 0 ? rb0 : rb1);
+      L.rsrc[r] = (uint32_t)xts[s];
+      xsc[s] = om.nr + r;  // clock row of this rmv (stored as its "score")
     }
   }
   wave_lds_sync();
@@ -196,6 +251,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     rv[s] = (r < nrmv && (int)d < D) ? a.rmv_vc[(uint64_t)L.rsrc[r] * D + d] : 0;
   }
 
+  PROF_MARK(1);
   // ---- 3. hash build: old players, then ops (64-bit CAS on the Id)
   uint32_t hs[4];
   bool pend[4];
@@ -210,7 +266,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     hs[j] = whash(hid[j]);
     bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
   }
-  if (ballot(bad)) return false;
+  if (ballot(bad)) WAVE_RETURN(W_NEXT_TIER);
   while (ballot(pend[0] || pend[1] || pend[2] || pend[3])) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -234,7 +290,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
         bad |= ((pslab[s] >> 16) != 0) != ((pinfo[s] & 0xFFFFu) != NONE16);
       }
     }
-    if (ballot(bad)) return false;
+    if (ballot(bad)) WAVE_RETURN(W_NEXT_TIER);
   }
   // write the staged rmv clocks (loads were in flight during the build)
 #pragma unroll
@@ -247,7 +303,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
-    return true;
+    WAVE_RETURN(W_REJECT);
   }
   wave_lds_sync();
   // new players numbered after the old ones, in hash-slot order
@@ -265,7 +321,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     uint32_t idx = om.np + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
     np = om.np + (uint32_t)__builtin_popcountll(b0) + 2 * (uint32_t)__builtin_popcountll(b1) +
          4 * (uint32_t)__builtin_popcountll(b2);
-    if (np > pmax) return false;  // Observed could fill: next tier
+    if (np > pmax) WAVE_RETURN(W_NEXT_TIER);  // Observed could fill: next tier
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (newm & (1u << q)) {
@@ -278,7 +334,8 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
   }
   wave_lds_sync();
 
-  // ---- 4. player of every op, Vc, counting sort by player
+  PROF_MARK(2);
+  // ---- 4. player of every op, Vc, op elements in player order
   uint32_t xrank[2], xp[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -288,14 +345,13 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
       const uint32_t kind = xkd[s] & 0xFFu, dc = xkd[s] >> 8;
       const uint32_t p = L.hp[hs[2 + s]];
       xp[s] = p;
-      L.ekd[s * 64 + lane] = (uint16_t)(kind | (dc << 2) | (p << 8));
       if (kind < 2) atomicMax(&L.vc[dc], (unsigned long long)xts[s]);  // vc_update (:233)
       const uint32_t sh = 16 * (p & 1);
       xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
     }
   }
   wave_lds_sync();
-  // per player (lane, lane + 64): first position of its ops in `sorted`
+  // per player (lane, lane + 64): first position of its ops
   {
     uint32_t tot0, tot1;
     const uint32_t c0 = (uint32_t)lane < np ? pcnt_of(L, lane) : 0u;
@@ -307,8 +363,54 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
   }
   wave_lds_sync();
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
-    if (xv[s]) L.sorted[L.pstart[xp[s]] + xrank[s]] = (uint8_t)(s * 64 + lane);
+  for (int s = 0; s < 2; ++s) {
+    if (xv[s]) {
+      const uint32_t q = L.pstart[xp[s]] + xrank[s];
+      L.esc[q] = xsc[s];
+      L.ets[q] = xts[s];
+      L.ekd[q] = (uint16_t)((xkd[s] & 0xFFu) | ((xkd[s] >> 8) << 2) | (xp[s] << 8));
+      L.sorted[q] = (uint8_t)(s * 64 + lane);
+    }
+  }
+  wave_lds_sync();
+  // The ranks came from LDS atomics, whose order inside one instruction is
+  // not specified: check that every player's ops are in stream order, and
+  // restore it (insertion sort per player) where they are not.
+  {
+    bool bad_order = false;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t q = s * 64 + lane;
+      if (q < nops && q > 0) {
+        const uint32_t p = L.ekd[q] >> 8;
+        bad_order |= q != L.pstart[p] && L.sorted[q - 1] > L.sorted[q];
+      }
+    }
+    if (ballot(bad_order)) {
+#pragma unroll 1
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t p = s * 64 + lane;
+        const uint32_t c = p < np ? pcnt_of(L, p) : 0u, st = p < np ? L.pstart[p] : 0u;
+        for (uint32_t x = 1; x < c; ++x) {
+          const uint32_t v = L.sorted[st + x];
+          const int64_t vs = L.esc[st + x], vt = L.ets[st + x];
+          const uint16_t vk = L.ekd[st + x];
+          uint32_t y = x;
+          while (y > 0 && L.sorted[st + y - 1] > v) {
+            L.sorted[st + y] = L.sorted[st + y - 1];
+            L.esc[st + y] = L.esc[st + y - 1];
+            L.ets[st + y] = L.ets[st + y - 1];
+            L.ekd[st + y] = L.ekd[st + y - 1];
+            --y;
+          }
+          L.sorted[st + y] = (uint8_t)v;
+          L.esc[st + y] = vs;
+          L.ets[st + y] = vt;
+          L.ekd[st + y] = vk;
+        }
+      }
+    }
+  }
   // old Masked elements -> elements [nops, nops + om.nm), player by player
   if (!a.fresh) {
     uint32_t ebase = nops;
@@ -320,16 +422,17 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
       const uint32_t eb = ebase + wave_excl_scan_dpp(oc, tot);
       ebase += tot;
       for (uint32_t j = 0; j < oc; ++j) {
-        const uint64_t go = (uint64_t)om.m_off + (pslab[s] & 0xFFFFu) + j;
+        const uint32_t go = (pslab[s] & 0xFFFFu) + j;
         const uint32_t e = eb + j;
-        L.esc[e] = a.old_s.m_score[go];
-        L.ets[e] = a.old_s.m_ts[go];
-        L.ekd[e] = (uint16_t)(((uint32_t)a.old_s.m_dc[go] << 2) | (p << 8));
+        L.esc[e] = (a.old_s.m_score + om.m_off)[go];
+        L.ets[e] = (a.old_s.m_ts + om.m_off)[go];
+        L.ekd[e] = (uint16_t)(((uint32_t)(a.old_s.m_dc + om.m_off)[go] << 2) | (p << 8));
       }
     }
   }
   wave_lds_sync();
 
+  PROF_MARK(3);
   // ---- 5. replay every player's ops (lane = player; players lane, lane + 64)
   uint32_t fbase = 0, rbase = 0, nobs = 0, mbase = 0, ebase = nops;
 #pragma unroll 1
@@ -346,17 +449,6 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     mbase += tot;
     const uint32_t eb = ebase + wave_excl_scan_dpp(ocnt, tot);        // old elements
     ebase += tot;
-    // stable order: insertion sort of this player's op list (ranks came from
-    // LDS atomics, whose order inside one instruction is not specified)
-    for (uint32_t x = 1; x < c; ++x) {
-      const uint32_t v = L.sorted[st + x];
-      uint32_t y = x;
-      while (y > 0 && L.sorted[st + y - 1] > v) {
-        L.sorted[st + y] = L.sorted[st + y - 1];
-        --y;
-      }
-      L.sorted[st + y] = (uint8_t)v;
-    }
     // initial player state
     uint32_t cnt = ocnt;
     int64_t maxts = 0;
@@ -378,15 +470,14 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     }
     const int64_t id = act ? (int64_t)L.htab[L.pslot[p]] : 0;
     for (uint32_t x = 0; x < c; ++x) {
-      const uint32_t e = L.sorted[st + x];
+      const uint32_t e = st + x;  // op element (player order)
       const uint32_t kd = L.ekd[e];
       const int64_t sc = L.esc[e];
       const int64_t t = L.ets[e];
       const uint32_t kind = kd & 3u, dc = (kd >> 2) & 7u;
-      const uint64_t gop = op0 + e;
       if (kind < 2) {  // add/4 (:231-249)
         if (prow != NONE8 && L.rows[prow][dc] >= t) {  // dominated (:234-237)
-          wave_emit(a, L, op0, gop, CCRDT_TRMV_RMV, id, 0, 0, 0, prow);
+          wave_emit(a, L, op0, op0 + L.sorted[e], CCRDT_TRMV_RMV, id, 0, 0, 0, prow);
           continue;
         }
         // gb_sets:add_element: set semantics (a ts above every ts ever in the
@@ -447,7 +538,7 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
             o = be;
             osc = bsc;
             ots = bts;
-            wave_emit(a, L, op0, gop, CCRDT_TRMV_ADD, id, bsc, bdc, bts, prow);
+            wave_emit(a, L, op0, op0 + L.sorted[e], CCRDT_TRMV_ADD, id, bsc, bdc, bts, prow);
           }
         }
       }
@@ -467,31 +558,32 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     rbase += (uint32_t)__builtin_popcountll(rm);
     if (act) {
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      a.new_s.pl_id[nmeta.p_off + p] = id;
-      a.new_s.pl_info[nmeta.p_off + p] = opos | ((prow != NONE8 ? rix : NONE16) << 16);
-      a.new_s.pl_slab[nmeta.p_off + p] = goff | (cnt << 16);
+      (a.new_s.pl_id + nmeta.p_off)[p] = id;
+      (a.new_s.pl_info + nmeta.p_off)[p] = opos | ((prow != NONE8 ? rix : NONE16) << 16);
+      (a.new_s.pl_slab + nmeta.p_off)[p] = goff | (cnt << 16);
     }
     if (act) L.pobs[p] = (uint8_t)o;
     nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
   }
   wave_lds_sync();
 
+  PROF_MARK(4);
+  if (has_next) wave_load_key(a, nkey, nxt);  // overlaps this key's write-out
   // ---- 6. Masked pool, Removals rows, Vc, Min, metadata
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t q = s * 64 + lane;
     if (q < fbase) {
       const uint32_t e = L.fin[q];
-      const uint64_t g = (uint64_t)nmeta.m_off + q;
-      a.new_s.m_score[g] = L.esc[e];
-      a.new_s.m_ts[g] = L.ets[e];
-      a.new_s.m_dc[g] = (uint8_t)((L.ekd[e] >> 2) & 7u);
+      (a.new_s.m_score + nmeta.m_off)[q] = L.esc[e];
+      (a.new_s.m_ts + nmeta.m_off)[q] = L.ets[e];
+      (a.new_s.m_dc + nmeta.m_off)[q] = (uint8_t)((L.ekd[e] >> 2) & 7u);
     }
   }
   for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
     if (r < rbase && (int)d < D)
-      a.new_s.r_vc[((uint64_t)nmeta.r_off + r) * D + d] = L.rows[L.rl[r]][d];
+      (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = L.rows[L.rl[r]][d];
   }
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
@@ -531,34 +623,59 @@ __device__ __forceinline__ bool trmv_wave_key(const TrmvApplyArgs& a, uint32_t k
     a.new_s.meta[key] = out;
     a.ex_cnt[key] = L.nex;
   }
-  return true;
+  PROF_MARK(5);
+  return W_DONE;
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void trmv_wave_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
-  for (uint32_t w = blockIdx.x * W_WAVES + wv; w < n; w += gridDim.x * W_WAVES) {
-    const uint32_t key = a.key_list ? a.key_list[w] : w;
-    if (!trmv_wave_key(a, key, L)) {
-      if (lane_id() == 0) {
-        const uint32_t pos = atomicAdd(&a.status[0], 1u);
-        a.ovf_list[pos] = key;
+  for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * W_KPW; c0 < n; c0 += gridDim.x * W_WAVES * W_KPW) {
+    const uint32_t c1 = c0 + W_KPW < n ? c0 + W_KPW : n;
+    uint32_t key = a.key_list ? a.key_list[c0] : c0;
+    KeyIn cur;
+    wave_load_key(a, key, cur);
+    for (uint32_t w = c0; w < c1; ++w) {
+      const bool has_next = w + 1 < c1;
+      const uint32_t nkey = has_next ? (a.key_list ? a.key_list[w + 1] : w + 1) : 0u;
+      KeyIn nxt;
+      const int r = trmv_wave_key(a, key, cur, L, has_next, nkey, nxt);
+      if (r != W_DONE) {
+        if (r == W_NEXT_TIER && lane_id() == 0) {
+          const uint32_t pos = atomicAdd(&a.status[0], 1u);
+          a.ovf_list[pos] = key;
+        }
+        if (has_next) wave_load_key(a, nkey, nxt);
       }
+      wave_lds_sync();  // LDS is reused by the wave's next key
+      key = nkey;
+      cur = nxt;
     }
-    wave_lds_sync();  // LDS is reused by the wave's next key
   }
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
-  const uint64_t blocks = (grid_keys + W_WAVES - 1) / W_WAVES;
+  const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
+  const uint64_t blocks = (grid_keys + per_block - 1) / per_block;
   hipLaunchKernelGGL(trmv_wave_kernel, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
 
 }  // namespace ccrdt
+
+#ifdef TRMV_PROF
+extern "C" int ccrdt_debug_trmv_prof(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_trmv_prof), 16 * 8) != hipSuccess) return 4;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trmv_prof), z, sizeof(z)) != hipSuccess) return 4;
+  }
+  return 0;
+}
+#endif

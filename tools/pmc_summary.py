@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of rocprofv3 PMC passes (tools/profile.sh output).
+
+    python tools/pmc_summary.py gpurun_out/prof [--json out.json] [--kernel NAME]
+
+Counter values are summed over a dispatch's rows (rocprofv3 writes one row per
+dispatch and counter, already summed over XCDs/SEs), then averaged over
+dispatches of the same kernel.  FETCH_SIZE/WRITE_SIZE are KiB; `hbm_bytes`
+applies the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE counts
+half of a wide coalesced read, so bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(prof_dir):
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> dispatch -> value
+    meta = {}
+    for f in glob.glob(os.path.join(prof_dir, "*", "*_counter_collection.csv")):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k, c, d = r["Kernel_Name"], r["Counter_Name"], (f, r["Dispatch_Id"])
+                per[k][c][d] += float(r["Counter_Value"])
+                meta[k] = {"vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                           "lds": int(r["LDS_Block_Size"]), "wg": int(r["Workgroup_Size"])}
+    out = {}
+    for k, cs in per.items():
+        out[k] = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+        out[k].update(meta.get(k, {}))
+        if "FETCH_SIZE" in out[k] and "WRITE_SIZE" in out[k]:
+            out[k]["hbm_bytes"] = (2 * out[k]["FETCH_SIZE"] + out[k]["WRITE_SIZE"]) * 1024
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("--json")
+    ap.add_argument("--kernel", default="")
+    a = ap.parse_args()
+    out = load(a.prof_dir)
+    for k, v in sorted(out.items()):
+        if a.kernel not in k:
+            continue
+        print(k)
+        waves = v.get("SQ_WAVES", 0) or 1
+        for c in sorted(v):
+            x = v[c]
+            extra = f"   ({x / waves:.1f}/wave)" if c.startswith("SQ_INSTS") or c in ("SQ_WAVE_CYCLES",) else ""
+            print(f"   {c:24s} {x:18.1f}{extra}")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

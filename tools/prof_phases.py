@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase shares of the topk_rmv tier-0 kernel (diagnostic build, -DTRMV_PROF).
+"""Phase shares of the topk_rmv tier-0 kernel (trmv_wave.hip) (diagnostic build, -DTRMV_PROF).
 
 Build first (CPU side):  make -C antidote_ccrdt_amd/csrc OUT=../lib/libccrdt_prof.so \
     OBJDIR=../../build/objprof EXTRA=-DTRMV_PROF
@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 from antidote_ccrdt_amd import _lib  # noqa: E402
 from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv  # noqa: E402
 
-NAMES = ["meta+clear+old players", "op load + claim", "counting sort", "replay", "min+writes"]
+NAMES = ["loads issue + LDS init", "validate + rmv rank (load wait)", "clocks + hash + numbering",
+         "player/op + counting sort", "replay", "pool/rows/min/meta writes"]
 n_ops = int(os.environ.get("N_OPS", 100_000_000))
 b = gen_trmv(n_ops, 1 << 20, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64)
 db = DeviceTrmvBatch(b)
@@ -27,7 +28,7 @@ eng.reset(); eng.apply_device(db); eng.sync()
 f(buf, 1)
 eng.reset(); eng.apply_device(db); eng.sync()
 f(buf, 1)
-tot = sum(buf[i] for i in range(5))
+tot = sum(buf[i] for i in range(len(NAMES)))
 for i, n in enumerate(NAMES):
     print(f"{n:28s} {buf[i] / tot * 100:6.1f} %   {buf[i] / (1 << 14):9.0f} cyc/key (1/64 of keys sampled)")
 print("kernel ms (stamped build):", eng.last_kernel_ms())
