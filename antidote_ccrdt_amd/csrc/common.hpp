@@ -110,6 +110,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
 }
+// Wave minimum of an int64 in 6 DPP steps (same row_shr / row_bcast pattern
+// as wave_incl_scan_dpp); lanes without a DPP source see INT64_MAX.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int64_t dpp_min_step_i64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)(uint32_t)v, CTRL,
+                                                            ROWMASK, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(
+      (int)0x7FFFFFFF, (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROWMASK, 0xf, false);
+  const int64_t o = (int64_t)(((uint64_t)hi << 32) | lo);
+  return o < v ? o : v;
+}
+__device__ __forceinline__ int64_t wave_min_i64_dpp(int64_t v) {
+  v = dpp_min_step_i64<0x111, 0xf>(v);
+  v = dpp_min_step_i64<0x112, 0xf>(v);
+  v = dpp_min_step_i64<0x114, 0xf>(v);
+  v = dpp_min_step_i64<0x118, 0xf>(v);
+  v = dpp_min_step_i64<0x142, 0xa>(v);
+  v = dpp_min_step_i64<0x143, 0xc>(v);
+  return rl64(v, 63);
+}
 // Exclusive DPP scan; `total` = wave sum (wave-uniform).
 __device__ __forceinline__ uint32_t wave_excl_scan_dpp(uint32_t v, uint32_t& total) {
   const uint32_t inc = wave_incl_scan_dpp(v);

@@ -47,7 +47,7 @@ __device__ unsigned long long g_trmv_prof[16];
   do {                                                                       \
     unsigned long long _t;                                                   \
     PROF_STAMP(_t);                                                          \
-    if (lane_id() == 0 && (key & 63u) == 0) atomicAdd(&g_trmv_prof[i], _t - prof_t);             \
+    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_trmv_prof[i], _t - prof_t);             \
     prof_t = _t;                                                             \
   } while (0)
 #else
@@ -123,11 +123,36 @@ struct KeyIn {
   uint32_t kd[2];  // kind | dc << 8
 };
 
-__device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, uint32_t key, KeyIn& in) {
+// Bounds and new-side metadata of a wave's W_KPW keys, loaded once per chunk
+// into lanes (key j: lane j holds its key and op range, lanes 8j..8j+7 the
+// eight dwords of its KeyMeta), so a key's op loads never wait on a scalar
+// load of its own bounds.
+struct ChunkHdr {
+  uint32_t key;     // lane j < n: key j
+  uint64_t lo, hi;  // lane j < n: key_ptr[key j], key_ptr[key j + 1]
+  uint32_t meta;    // lane 8j + d: dword d of new_s.meta[key j]
+};
+
+__device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t c0, uint32_t n,
+                                                ChunkHdr& h) {
   const int lane = lane_id();
-  in.op0 = a.key_ptr[key];
-  in.nops = (uint32_t)(a.key_ptr[key + 1] - in.op0);
-  in.nmeta = a.new_s.meta[key];
+  const uint32_t j = (uint32_t)lane < n ? (uint32_t)lane : 0u;
+  h.key = a.key_list ? a.key_list[c0 + j] : c0 + j;
+  h.lo = a.key_ptr[h.key];
+  h.hi = a.key_ptr[h.key + 1];
+  const uint32_t jm = (uint32_t)(lane >> 3) < n ? (uint32_t)(lane >> 3) : 0u;
+  const uint32_t km = a.key_list ? a.key_list[c0 + jm] : c0 + jm;
+  h.meta = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
+}
+
+__device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const ChunkHdr& h, uint32_t j,
+                                              KeyIn& in) {
+  const int lane = lane_id();
+  in.op0 = (uint64_t)rl64((int64_t)h.lo, (int)j);
+  in.nops = (uint32_t)((uint64_t)rl64((int64_t)h.hi, (int)j) - in.op0);
+  uint32_t* m = reinterpret_cast<uint32_t*>(&in.nmeta);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) m[d] = rl32(h.meta, (int)(8 * j + d));
   // wave-uniform bases + 32-bit lane offsets (saddr addressing, no 64-bit
   // per-lane address arithmetic)
   const int64_t* idp = a.id + in.op0;
@@ -153,7 +178,8 @@ enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
 #define WAVE_RETURN(v) return (v)
 
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
-                                              WaveLds& L, bool has_next, uint32_t nkey, KeyIn& nxt) {
+                                              WaveLds& L, bool has_next, const ChunkHdr& hdr,
+                                              uint32_t nj, KeyIn& nxt) {
   const int lane = lane_id();
   const int D = a.n_dc;
 #ifdef TRMV_PROF
@@ -162,6 +188,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #endif
   const uint64_t op0 = in.op0;
   const uint32_t nops = in.nops;
+  (void)key;
   const KeyMeta nmeta = in.nmeta;
   KeyMeta om;
   if (a.fresh) {
@@ -568,7 +595,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
 
   PROF_MARK(4);
-  if (has_next) wave_load_key(a, nkey, nxt);  // overlaps this key's write-out
+  if (has_next) wave_load_key(a, hdr, nj, nxt);  // overlaps this key's write-out
   // ---- 6. Masked pool, Removals rows, Vc, Min, metadata
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -605,8 +632,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
     const bool has = best_q != NONE32;
     if (ballot(has)) {
-      const int64_t ms = wave_min_i64(has ? best_sc : INT64_MAX);
-      const int64_t mi = wave_min_i64(has && best_sc == ms ? best_id : INT64_MAX);
+      const int64_t ms = wave_min_i64_dpp(has ? best_sc : INT64_MAX);
+      const int64_t mi = wave_min_i64_dpp(has && best_sc == ms ? best_id : INT64_MAX);
       const uint64_t hit = ballot(has && best_sc == ms && best_id == mi);
       best_q = rl32(best_q, (int)__builtin_ctzll(hit));
     } else {
@@ -634,24 +661,24 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
   WaveLds& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * W_KPW; c0 < n; c0 += gridDim.x * W_WAVES * W_KPW) {
-    const uint32_t c1 = c0 + W_KPW < n ? c0 + W_KPW : n;
-    uint32_t key = a.key_list ? a.key_list[c0] : c0;
+    const uint32_t cn = c0 + W_KPW < n ? W_KPW : n - c0;
+    ChunkHdr hdr;
+    wave_load_chunk(a, c0, cn, hdr);
     KeyIn cur;
-    wave_load_key(a, key, cur);
-    for (uint32_t w = c0; w < c1; ++w) {
-      const bool has_next = w + 1 < c1;
-      const uint32_t nkey = has_next ? (a.key_list ? a.key_list[w + 1] : w + 1) : 0u;
+    wave_load_key(a, hdr, 0, cur);
+    for (uint32_t j = 0; j < cn; ++j) {
+      const uint32_t key = rl32(hdr.key, (int)j);
+      const bool has_next = j + 1 < cn;
       KeyIn nxt;
-      const int r = trmv_wave_key(a, key, cur, L, has_next, nkey, nxt);
+      const int r = trmv_wave_key(a, key, cur, L, has_next, hdr, j + 1, nxt);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&a.status[0], 1u);
           a.ovf_list[pos] = key;
         }
-        if (has_next) wave_load_key(a, nkey, nxt);
+        if (has_next) wave_load_key(a, hdr, j + 1, nxt);
       }
       wave_lds_sync();  // LDS is reused by the wave's next key
-      key = nkey;
       cur = nxt;
     }
   }
