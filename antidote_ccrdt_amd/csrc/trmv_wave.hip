@@ -25,7 +25,17 @@
 //    (bounds, metadata, ops) before the current key's write-out, so the
 //    first HBM round trip of a key overlaps the previous key's stores;
 //  * op elements are stored at their position in player order, so the replay
-//    reads an op with one LDS round trip.
+//    reads an op with one LDS round trip;
+//  * players split into "simple" and "complex".  A simple player has only
+//    adds in the batch, no old state, and strictly increasing Ts across its
+//    adds (so no add can duplicate a Masked element): its Masked set is all
+//    its adds and Obs[Id] is the first add with the largest (Score, Ts) --
+//    recompute_observed/5's strict cmp/2 keeps the first arrival on a tie --
+//    which every op lane decides for itself by scanning its player's
+//    positions.  Only complex players (a rmv in the batch, old state, or a Ts
+//    that does not rise) are replayed op by op, one lane per player, packed
+//    into as few passes as there are 64-player groups.  Old state exists
+//    only when the engine is not fresh (template FRESH).
 //
 // Element index space of a key: [0, nops) = this batch's ops, grouped by player
 // (stream order inside a player), [nops, nops + old |Masked|) = the key's old
@@ -84,6 +94,12 @@ struct alignas(16) WaveLds {
   uint32_t rsrc[W_RCAP];            // rmv_vc row of each staged rmv clock
   uint8_t rl[W_RCAP];               // clock row of each output Removals row (player order)
   uint8_t pobs[W_PCAP];             // Obs[Id] of each player (element), NONE8 = not observed
+  uint8_t pflag[W_PCAP];            // 1 = complex player (op-by-op replay)
+  uint8_t pcntf[W_PCAP];            // complex player: final |Masked[Id]|
+  uint8_t pmoff[W_PCAP];            // complex player: its working slab in `slab`
+  uint8_t prow[W_PCAP];             // complex player: its clock row (Removals[Id]) or NONE8
+  uint8_t peb[W_PCAP];              // old player: first element of its old Masked slab
+  uint8_t cpl[W_PCAP];              // complex players, packed
   uint32_t nex;                     // extra effects emitted by the key
 };
 
@@ -175,8 +191,8 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
 // next key (just before the write-out); the rare other paths leave that to the
 // caller, which keeps the prefetched registers out of the early phases.
 enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
-#define WAVE_RETURN(v) return (v)
 
+template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
                                               WaveLds& L, bool has_next, const ChunkHdr& hdr,
                                               uint32_t nj, KeyIn& nxt) {
@@ -188,10 +204,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #endif
   const uint64_t op0 = in.op0;
   const uint32_t nops = in.nops;
-  (void)key;
   const KeyMeta nmeta = in.nmeta;
   KeyMeta om;
-  if (a.fresh) {
+  if (FRESH) {
     om.p_off = om.m_off = om.r_off = 0;
     om.np = om.nm = om.nr = om.nobs = 0;
     om.minq = NONE32;
@@ -201,15 +216,16 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
   if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
       om.nr > (uint32_t)W_RCAP)
-    WAVE_RETURN(W_NEXT_TIER);
+    return W_NEXT_TIER;
 
   // ---- 1. the ops are in `in`; issue the old-state loads
-  int64_t xid[2] = {in.id[0], in.id[1]}, xsc[2] = {in.sc[0], in.sc[1]}, xts[2] = {in.ts[0], in.ts[1]};
+  int64_t xsc[2] = {in.sc[0], in.sc[1]};
+  const int64_t xts[2] = {in.ts[0], in.ts[1]};
   const uint32_t xkd[2] = {in.kd[0], in.kd[1]};
   const bool xv[2] = {(uint32_t)lane < nops, (uint32_t)(64 + lane) < nops};
   int64_t pid[2] = {0, 0};
   uint32_t pinfo[2] = {NONE32, NONE32}, pslab[2] = {0u, 0u};
-  if (!a.fresh) {
+  if (!FRESH) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
@@ -224,10 +240,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   for (int i = lane; i < W_HCAP; i += 64) L.htab[i] = W_EMPTY;
   reinterpret_cast<uint32_t*>(L.hp)[lane] = 0xFFFFFFFFu;  // 256 B
   L.pcnt2[lane] = 0u;
+  if (lane < W_PCAP / 4) reinterpret_cast<uint32_t*>(L.pflag)[lane] = 0u;
   if (lane == 0) L.nex = 0u;
   if (lane < TRMV_DPAD)
-    L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
-  if (!a.fresh) {  // old Removals rows -> clock rows [0, om.nr)
+    L.vc[lane] = (!FRESH && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+  if (!FRESH) {  // old Removals rows -> clock rows [0, om.nr)
     for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7;
       if (r < om.nr)
@@ -236,7 +253,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
 
   PROF_MARK(0);
-  // ---- 2. validate ops, stage element fields, rank the rmv ops
+  // ---- 2. validate ops, rank the rmv ops, issue their clock loads
   uint32_t err = 0;
   bool xr[2];
 #pragma unroll
@@ -255,12 +272,12 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
-    WAVE_RETURN(W_REJECT);  // the host rejects the batch
+    return W_REJECT;  // the host rejects the batch
   }
   const uint64_t rb0 = ballot(xr[0]), rb1 = ballot(xr[1]);
   const uint32_t nr0 = (uint32_t)__builtin_popcountll(rb0);
   const uint32_t nrmv = nr0 + (uint32_t)__builtin_popcountll(rb1);
-  if (om.nr + nrmv > (uint32_t)W_RCAP) WAVE_RETURN(W_NEXT_TIER);
+  if (om.nr + nrmv > (uint32_t)W_RCAP) return W_NEXT_TIER;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (xr[s]) {
@@ -270,7 +287,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
   }
   wave_lds_sync();
-  // rmv clocks: 8 lanes per row, coalesced (issued before the hash build)
+  // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
   int64_t rv[W_RCAP / 8];
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
@@ -282,9 +299,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // ---- 3. hash build: old players, then ops (64-bit CAS on the Id)
   uint32_t hs[4];
   bool pend[4];
-  int64_t hid[4] = {pid[0], pid[1], xid[0], xid[1]};
-  pend[0] = !a.fresh && (uint32_t)lane < om.np;
-  pend[1] = !a.fresh && (uint32_t)(64 + lane) < om.np;
+  const int64_t hid[4] = {pid[0], pid[1], in.id[0], in.id[1]};
+  pend[0] = !FRESH && (uint32_t)lane < om.np;
+  pend[1] = !FRESH && (uint32_t)(64 + lane) < om.np;
   pend[2] = xv[0];
   pend[3] = xv[1];
   bool bad = false;
@@ -293,7 +310,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     hs[j] = whash(hid[j]);
     bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
   }
-  if (ballot(bad)) WAVE_RETURN(W_NEXT_TIER);
+  if (ballot(bad)) return W_NEXT_TIER;
   while (ballot(pend[0] || pend[1] || pend[2] || pend[3])) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -306,7 +323,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
   }
   // old players keep their index
-  if (!a.fresh) {
+  if (!FRESH) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
@@ -317,7 +334,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         bad |= ((pslab[s] >> 16) != 0) != ((pinfo[s] & 0xFFFFu) != NONE16);
       }
     }
-    if (ballot(bad)) WAVE_RETURN(W_NEXT_TIER);
+    if (ballot(bad)) return W_NEXT_TIER;
   }
   // write the staged rmv clocks (loads were in flight during the build)
 #pragma unroll
@@ -330,7 +347,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
-    WAVE_RETURN(W_REJECT);
+    return W_REJECT;
   }
   wave_lds_sync();
   // new players numbered after the old ones, in hash-slot order
@@ -348,7 +365,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     uint32_t idx = om.np + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
     np = om.np + (uint32_t)__builtin_popcountll(b0) + 2 * (uint32_t)__builtin_popcountll(b1) +
          4 * (uint32_t)__builtin_popcountll(b2);
-    if (np > pmax) WAVE_RETURN(W_NEXT_TIER);  // Observed could fill: next tier
+    if (np > pmax) return W_NEXT_TIER;  // Observed could fill: next tier
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (newm & (1u << q)) {
@@ -373,6 +390,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t p = L.hp[hs[2 + s]];
       xp[s] = p;
       if (kind < 2) atomicMax(&L.vc[dc], (unsigned long long)xts[s]);  // vc_update (:233)
+      else L.pflag[p] = 1;  // a rmv: complex player
       const uint32_t sh = 16 * (p & 1);
       xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
     }
@@ -389,10 +407,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if ((uint32_t)(64 + lane) < np) L.pstart[64 + lane] = (uint8_t)(tot0 + st1);
   }
   wave_lds_sync();
+  uint32_t xq[2], xst[2], xc[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
+    xq[s] = 0;
+    xst[s] = 0;
+    xc[s] = 0;
     if (xv[s]) {
-      const uint32_t q = L.pstart[xp[s]] + xrank[s];
+      xst[s] = L.pstart[xp[s]];
+      xc[s] = pcnt_of(L, xp[s]);
+      const uint32_t q = xst[s] + xrank[s];
+      xq[s] = q;
       L.esc[q] = xsc[s];
       L.ets[q] = xts[s];
       L.ekd[q] = (uint16_t)((xkd[s] & 0xFFu) | ((xkd[s] >> 8) << 2) | (xp[s] << 8));
@@ -406,13 +431,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   {
     bool bad_order = false;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const uint32_t q = s * 64 + lane;
-      if (q < nops && q > 0) {
-        const uint32_t p = L.ekd[q] >> 8;
-        bad_order |= q != L.pstart[p] && L.sorted[q - 1] > L.sorted[q];
-      }
-    }
+    for (int s = 0; s < 2; ++s)
+      if (xv[s] && xq[s] > xst[s]) bad_order |= L.sorted[xq[s] - 1] > (uint32_t)(s * 64 + lane);
     if (ballot(bad_order)) {
 #pragma unroll 1
       for (int s = 0; s < 2; ++s) {
@@ -436,10 +456,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
           L.ekd[st + y] = vk;
         }
       }
+      wave_lds_sync();
+      // positions moved: every op lane finds its own again
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        if (xv[s])
+          for (uint32_t x = 0; x < xc[s]; ++x)
+            if (L.sorted[xst[s] + x] == (uint32_t)(s * 64 + lane)) xq[s] = xst[s] + x;
     }
   }
   // old Masked elements -> elements [nops, nops + om.nm), player by player
-  if (!a.fresh) {
+  if (!FRESH) {
     uint32_t ebase = nops;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -448,6 +475,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       uint32_t tot;
       const uint32_t eb = ebase + wave_excl_scan_dpp(oc, tot);
       ebase += tot;
+      if (p < om.np) {
+        L.peb[p] = (uint8_t)eb;
+        L.pflag[p] = 1;  // old state: complex player
+      }
       for (uint32_t j = 0; j < oc; ++j) {
         const uint32_t go = (pslab[s] & 0xFFFFu) + j;
         const uint32_t e = eb + j;
@@ -460,22 +491,63 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
 
   PROF_MARK(3);
-  // ---- 5. replay every player's ops (lane = player; players lane, lane + 64)
-  uint32_t fbase = 0, rbase = 0, nobs = 0, mbase = 0, ebase = nops;
-#pragma unroll 1
+  // the next key's loads land during the replay; the explicit wait below
+  // retires them before this key's stores, so the next key never waits on
+  // (and its vmcnt never counts) this key's stores
+  if (has_next) wave_load_key(a, hdr, nj, nxt);
+  // ---- 5a. simple players, op-parallel: each add decides whether it is its
+  // player's Obs[Id] and whether its Ts rises over every earlier add's
+#pragma unroll
   for (int s = 0; s < 2; ++s) {
-    if (s * 64 >= (int)np) break;  // wave-uniform
-    const uint32_t p = s * 64 + lane;
-    const bool act = p < np;
-    const uint32_t pinfo_s = s ? pinfo[1] : pinfo[0];
-    const uint32_t ocnt = (act && p < om.np) ? ((s ? pslab[1] : pslab[0]) >> 16) : 0u;
+    if (xv[s] && !L.pflag[xp[s]]) {
+      const uint32_t me = xq[s] - xst[s];
+      bool beaten = false, risk = false;
+      for (uint32_t x = 0; x < xc[s]; ++x) {
+        if (x == me) continue;
+        const int64_t sx = L.esc[xst[s] + x], tx = L.ets[xst[s] + x];
+        const int64_t sm = xsc[s], tm = xts[s];
+        if (x < me) {
+          risk |= tx >= tm;
+          beaten |= sx > sm || (sx == sm && tx >= tm);
+        } else {
+          beaten |= sx > sm || (sx == sm && tx > tm);
+        }
+      }
+      if (risk) L.pflag[xp[s]] = 1;
+      if (!beaten) L.pobs[xp[s]] = (uint8_t)xq[s];
+    }
+  }
+  wave_lds_sync();
+
+  // ---- 5b. complex players, one lane per player, replayed op by op
+  uint32_t ncx;
+  {
+    const bool c0 = (uint32_t)lane < np && L.pflag[lane];
+    const bool c1 = (uint32_t)(64 + lane) < np && L.pflag[64 + lane];
+    const uint64_t m0 = ballot(c0), m1 = ballot(c1);
+    const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
+    ncx = n0 + (uint32_t)__builtin_popcountll(m1);
+    if (c0) L.cpl[mbcnt(m0)] = (uint8_t)lane;
+    if (c1) L.cpl[n0 + mbcnt(m1)] = (uint8_t)(64 + lane);
+  }
+  wave_lds_sync();
+  uint32_t mbase = 0;
+#pragma unroll 1
+  for (uint32_t b = 0; b < ncx; b += 64) {
+    const uint32_t k = b + lane;
+    const bool act = k < ncx;
+    const uint32_t p = act ? L.cpl[k] : 0u;
+    uint32_t ocnt = 0, pinfo_p = NONE32, eb = 0;
+    if (!FRESH && act && p < om.np) {
+      pinfo_p = (a.old_s.pl_info + om.p_off)[p];
+      ocnt = (a.old_s.pl_slab + om.p_off)[p] >> 16;
+      eb = L.peb[p];
+    }
     const uint32_t c = act ? pcnt_of(L, p) : 0u;
     const uint32_t st = act ? L.pstart[p] : 0u;
     uint32_t tot;
     const uint32_t moff = mbase + wave_excl_scan_dpp(c + ocnt, tot);  // slab capacity
     mbase += tot;
-    const uint32_t eb = ebase + wave_excl_scan_dpp(ocnt, tot);        // old elements
-    ebase += tot;
     // initial player state
     uint32_t cnt = ocnt;
     int64_t maxts = 0;
@@ -486,8 +558,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
     uint32_t o = NONE8, prow = NONE8;
     int64_t osc = 0, ots = 0;
-    if (act && !a.fresh && p < om.np) {
-      const uint32_t oi = pinfo_s & 0xFFFFu, ri = pinfo_s >> 16;
+    if (!FRESH && act && p < om.np) {
+      const uint32_t oi = pinfo_p & 0xFFFFu, ri = pinfo_p >> 16;
       if (oi != NONE16) {
         o = eb + oi;
         osc = L.esc[o];
@@ -570,33 +642,59 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         }
       }
     }
-    // final slab -> compact pool positions; the player record
-    uint32_t ftot;
-    const uint32_t goff = fbase + wave_excl_scan_dpp(act ? cnt : 0u, ftot);
-    fbase += ftot;
-    uint32_t opos = NONE16;
-    for (uint32_t j = 0; j < cnt; ++j) {
-      const uint32_t e2 = L.slab[moff + j];
-      L.fin[goff + j] = (uint8_t)e2;
-      if (e2 == o) opos = j;
-    }
-    const uint64_t rm = ballot(act && prow != NONE8);
-    const uint32_t rix = rbase + mbcnt(rm);
-    rbase += (uint32_t)__builtin_popcountll(rm);
     if (act) {
-      if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      (a.new_s.pl_id + nmeta.p_off)[p] = id;
-      (a.new_s.pl_info + nmeta.p_off)[p] = opos | ((prow != NONE8 ? rix : NONE16) << 16);
-      (a.new_s.pl_slab + nmeta.p_off)[p] = goff | (cnt << 16);
+      L.pobs[p] = (uint8_t)o;
+      L.pcntf[p] = (uint8_t)cnt;
+      L.pmoff[p] = (uint8_t)moff;
+      L.prow[p] = (uint8_t)prow;
     }
-    if (act) L.pobs[p] = (uint8_t)o;
-    nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
   }
   wave_lds_sync();
 
   PROF_MARK(4);
-  if (has_next) wave_load_key(a, hdr, nj, nxt);  // overlaps this key's write-out
-  // ---- 6. Masked pool, Removals rows, Vc, Min, metadata
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next key's ops are in registers
+  // ---- 6. player records, final pool order, Removals rows
+  uint32_t fbase = 0, rbase = 0, nobs = 0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t p = s * 64 + lane;
+    const bool act = p < np;
+    const bool cx = act && L.pflag[p];
+    const uint32_t c = act ? pcnt_of(L, p) : 0u;
+    const uint32_t st = act ? L.pstart[p] : 0u;
+    const uint32_t cnt = cx ? L.pcntf[p] : c;  // simple: every add is in Masked[Id]
+    const uint32_t o = act ? L.pobs[p] : NONE8;
+    const uint32_t prow = cx ? L.prow[p] : NONE8;
+    const uint32_t moff = cx ? L.pmoff[p] : 0u;
+    uint32_t ftot;
+    const uint32_t goff = fbase + wave_excl_scan_dpp(cnt, ftot);
+    fbase += ftot;
+    uint32_t opos = NONE16;
+    if (cx) {
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t e2 = L.slab[moff + j];
+        L.fin[goff + j] = (uint8_t)e2;
+        if (e2 == o) opos = j;
+      }
+    } else {
+      for (uint32_t j = 0; j < cnt; ++j) L.fin[goff + j] = (uint8_t)(st + j);
+      if (act) opos = o - st;
+    }
+    const uint64_t rm = ballot(prow != NONE8);
+    const uint32_t rix = rbase + mbcnt(rm);
+    rbase += (uint32_t)__builtin_popcountll(rm);
+    if (act) {
+      if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
+      (a.new_s.pl_id + nmeta.p_off)[p] = (int64_t)L.htab[L.pslot[p]];
+      (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : opos) |
+                                           ((prow != NONE8 ? rix : NONE16) << 16);
+      (a.new_s.pl_slab + nmeta.p_off)[p] = goff | (cnt << 16);
+    }
+    nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
+  }
+  wave_lds_sync();
+
+  // ---- 7. Masked pool, Removals rows, Vc, Min, metadata
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t q = s * 64 + lane;
@@ -655,6 +753,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
+template <bool FRESH>
 __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -670,7 +769,7 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
       const uint32_t key = rl32(hdr.key, (int)j);
       const bool has_next = j + 1 < cn;
       KeyIn nxt;
-      const int r = trmv_wave_key(a, key, cur, L, has_next, hdr, j + 1, nxt);
+      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&a.status[0], 1u);
@@ -689,7 +788,10 @@ int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st)
   if (grid_keys == 0) return CCRDT_OK;
   const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
   const uint64_t blocks = (grid_keys + per_block - 1) / per_block;
-  hipLaunchKernelGGL(trmv_wave_kernel, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+  if (a.fresh)
+    hipLaunchKernelGGL(trmv_wave_kernel<true>, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+  else
+    hipLaunchKernelGGL(trmv_wave_kernel<false>, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
