@@ -102,6 +102,7 @@ SIGNATURES = {
     "ccrdt_engine_last_kernel_ms": (INT, [P, C.POINTER(C.c_float)]),
     "ccrdt_engine_overflow_keys": (INT, [P, INT, C.POINTER(I64)]),
     "ccrdt_engine_tier_ms": (INT, [P, INT, C.POINTER(C.c_float)]),
+    "ccrdt_engine_handed_on": (INT, [P, INT, P, I64, C.POINTER(I64)]),
     "ccrdt_timer_start": (INT, [P]),
     "ccrdt_timer_stop": (INT, [P, C.POINTER(C.c_float)]),
     "ccrdt_trmv_apply": (INT, [P, C.POINTER(TrmvOps), C.POINTER(TrmvExtra)]),
@@ -109,6 +110,7 @@ SIGNATURES = {
     "ccrdt_trmv_extra_count": (INT, [P, C.POINTER(I64)]),
     "ccrdt_trmv_fetch_extra": (INT, [P, C.POINTER(TrmvExtra)]),
     "ccrdt_trmv_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+    "ccrdt_trmv_key_sizes": (INT, [P, P, P, P, P]),
     "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),

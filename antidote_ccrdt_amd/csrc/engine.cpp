@@ -66,7 +66,8 @@ void ccrdt_engine::release_all() {
     b.r_vc.release();
     b.vc.release();
   }
-  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &ovf_a, &ovf_b, &status, &st_kp,
+  for (DevBuf& d : tier_ovf) d.release();
+  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
   release_types();
@@ -332,8 +333,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex.ensure(n_ops * sizeof(TrmvExtraRec)));
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
-  CCRDT_TRY(E.ovf_a.ensure(nk * 4));
-  CCRDT_TRY(E.ovf_b.ensure(nk * 4));
+  for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
@@ -354,7 +354,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   int ev = 0;
   CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
   for (int t = first_tier; t < N_TIERS && nk; ++t) {
-    DevBuf* ovf = (work == &E.ovf_a) ? &E.ovf_b : &E.ovf_a;
+    DevBuf* ovf = &E.tier_ovf[t];
     a.key_list = work ? work->as<uint32_t>() : nullptr;
     a.n_list = work ? 0u : (uint32_t)nk;
     a.n_list_dev = n_dev;
@@ -397,6 +397,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   }
   E.trmv_overflow_keys.clear();
   E.trmv_tier_ms.clear();
+  E.trmv_first_tier = first_tier;
   float kernel_ms = 0.f;
   for (int t = first_tier, i = 1; t < N_TIERS && nk; ++t, ++i) {
     const int key = t < 2 ? t : TRMV_SLOT_CLASSES[t - 2];
@@ -578,6 +579,45 @@ int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, i
   if (n_obs) *n_obs = o;
   if (n_masked) *n_masked = m;
   if (n_rows) *n_rows = r;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* nr, uint32_t* nobs) {
+  CCRDT_TRY(check_trmv(e));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  std::vector<KeyMeta> meta(nk);
+  if (!e->fresh && nk) {
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.p, nk * sizeof(KeyMeta),
+                        hipMemcpyDeviceToHost));
+  }
+  for (uint64_t k = 0; k < nk; ++k) {
+    const KeyMeta m = e->fresh ? KeyMeta{} : meta[k];
+    if (np) np[k] = m.np;
+    if (nm) nm[k] = m.nm;
+    if (nr) nr[k] = m.nr;
+    if (nobs) nobs[k] = m.nobs;
+  }
+  return CCRDT_OK;
+}
+
+int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, int64_t* n) {
+  if (!e || !n || cap < 0) return CCRDT_EINVAL;
+  static constexpr int tiers[] = {0, 1, 2, 4, 8, 16};
+  int ti = -1;
+  for (int i = 0; i < 6; ++i)
+    if (tiers[i] == t) ti = i;
+  auto it = e->trmv_overflow_keys.find(t);
+  if (ti < 0 || e->type != CCRDT_TOPK_RMV || it == e->trmv_overflow_keys.end()) {
+    *n = 0;
+    return ti < 0 ? CCRDT_EINVAL : CCRDT_OK;
+  }
+  *n = it->second;
+  const int64_t m = std::min<int64_t>(cap, *n);
+  if (m > 0 && keys) {
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    CCRDT_HIP(hipMemcpy(keys, e->tier_ovf[ti].p, (size_t)m * 4, hipMemcpyDeviceToHost));
+  }
   return CCRDT_OK;
 }
 

@@ -59,7 +59,9 @@ struct ccrdt_engine {
   // topk_rmv
   ccrdt::TrmvBufs trmv[2];
   int cur = 0;
-  ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, ovf_a, ovf_b, status;
+  ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status;
+  ccrdt::DevBuf tier_ovf[6];  // keys each topk_rmv tier handed on (last batch)
+  int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held
   std::map<int, uint32_t> trmv_overflow_keys;  // per tier / slot class, last apply

@@ -215,6 +215,14 @@ class _Engine:
         check(lib.ccrdt_engine_overflow_keys(self.h, slot_class, C.byref(n)), "overflow_keys")
         return int(n.value)
 
+    def handed_on(self, tier: int) -> np.ndarray:
+        """Keys tier `tier` handed on in the last topk_rmv batch."""
+        n = C.c_int64()
+        check(lib.ccrdt_engine_handed_on(self.h, tier, None, 0, C.byref(n)), "handed_on")
+        out = np.empty(n.value, np.uint32)
+        check(lib.ccrdt_engine_handed_on(self.h, tier, ptr(out), n.value, C.byref(n)), "handed_on")
+        return out
+
     def close(self):
         if getattr(self, "h", None):
             lib.ccrdt_engine_destroy(self.h)
@@ -268,6 +276,13 @@ class TopkRmvEngine(_Engine):
         a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
         check(lib.ccrdt_trmv_state_sizes(self.h, C.byref(a), C.byref(b), C.byref(c)), "sizes")
         return int(a.value), int(b.value), int(c.value)
+
+    def key_sizes(self) -> dict:
+        """Per-key (players, masked, rows, observed) counts of the resident state."""
+        out = {k: np.zeros(self.n_keys, np.uint32) for k in ("np", "nm", "nr", "nobs")}
+        check(lib.ccrdt_trmv_key_sizes(self.h, *(ptr(out[k]) for k in ("np", "nm", "nr", "nobs"))),
+              "key_sizes")
+        return out
 
     def export(self) -> TrmvState:
         """Canonical image of every key (to_binary/1 analogue, topk_rmv.erl:156-158)."""

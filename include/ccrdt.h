@@ -106,6 +106,9 @@ int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms);
 int ccrdt_engine_overflow_keys(ccrdt_engine* e, int t, int64_t* n);
 /* Kernel time (HIP events) of tier `t` in the last topk_rmv batch. */
 int ccrdt_engine_tier_ms(ccrdt_engine* e, int t, float* ms);
+/* The keys tier `t` handed on in the last topk_rmv batch (up to `cap` of
+ * them into `keys`; *n = how many there were).  Diagnostics / bench. */
+int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, int64_t* n);
 
 /* Event timing on the engine stream (for bench.py; HIP events). */
 int ccrdt_timer_start(ccrdt_engine* e);
@@ -184,6 +187,9 @@ typedef struct {
 
 /* Totals for sizing a ccrdt_trmv_state. */
 int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows);
+/* Per-key counts of the resident state (players, Masked elements, Removals
+ * rows, |Observed|); any output may be NULL.  For bench.py's byte accounting. */
+int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* nr, uint32_t* nobs);
 /* to_binary/1 analogue (topk_rmv.erl:156-158): canonical image of every key. */
 int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out);
 /* from_binary/1 analogue (topk_rmv.erl:161-163).  Arrays as in export
