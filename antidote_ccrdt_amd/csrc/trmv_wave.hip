@@ -76,31 +76,36 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 constexpr int W_KPW = 8;     // consecutive keys per wave
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
 constexpr uint32_t NONE8 = 0xFFu;
+// Sink entries: a lane with nothing to read reads the extra entry of the
+// array, so the hot phases issue their LDS reads back to back without
+// per-lane branches.  (Stores and atomics stay exec-masked: many lanes on one
+// sink address would serialize.)
+constexpr uint32_t HSINK = W_HCAP, ESINK = W_ECAP, PSINK = W_PCAP;
 
 struct alignas(16) WaveLds {
-  unsigned long long htab[W_HCAP];  // Ids (W_EMPTY = free)
-  int64_t esc[W_ECAP];              // element score (rmv op: its clock row in `rows`)
-  int64_t ets[W_ECAP];              // element ts
-  int64_t rows[W_RCAP][TRMV_DPAD];  // [0, old nr) old Removals rows, then rmv clocks
-  unsigned long long vc[TRMV_DPAD]; // replica Vc
-  uint16_t ekd[W_ECAP];             // kind | dc << 2 | player << 8
-  uint8_t hp[W_HCAP];               // hash slot -> player
-  uint8_t pslot[W_PCAP];            // player -> hash slot
-  uint8_t sorted[W_ECAP];           // op index (stream position) of every op element
-  uint8_t slab[W_ECAP];             // working Masked slabs (element indices)
-  uint8_t fin[W_ECAP];              // final pool: element of every output position
-  uint8_t pstart[W_PCAP];           // first `sorted` position of each player
-  uint32_t pcnt2[W_PCAP / 2];       // ops per player (two u16 counters per word)
-  uint32_t rsrc[W_RCAP];            // rmv_vc row of each staged rmv clock
-  uint8_t rl[W_RCAP];               // clock row of each output Removals row (player order)
-  uint8_t pobs[W_PCAP];             // Obs[Id] of each player (element), NONE8 = not observed
-  uint8_t pflag[W_PCAP];            // 1 = complex player (op-by-op replay)
-  uint8_t pcntf[W_PCAP];            // complex player: final |Masked[Id]|
-  uint8_t pmoff[W_PCAP];            // complex player: its working slab in `slab`
-  uint8_t prow[W_PCAP];             // complex player: its clock row (Removals[Id]) or NONE8
-  uint8_t peb[W_PCAP];              // old player: first element of its old Masked slab
-  uint8_t cpl[W_PCAP];              // complex players, packed
-  uint32_t nex;                     // extra effects emitted by the key
+  unsigned long long htab[W_HCAP + 2];   // Ids (W_EMPTY = free); [HSINK]
+  int64_t esc[W_ECAP + 2];               // element score (rmv op: its clock row in `rows`)
+  int64_t ets[W_ECAP + 2];               // element ts
+  int64_t rows[W_RCAP][TRMV_DPAD];       // [0, old nr) old Removals rows, then rmv clocks
+  unsigned long long vc[TRMV_DPAD + 2];  // replica Vc; [TRMV_DPAD] sink
+  uint32_t pcnt2[W_PCAP / 2 + 4];        // ops per player (two u16 counters per word)
+  uint32_t rsrc[W_RCAP + 4];             // rmv_vc row of each staged rmv clock
+  uint16_t ekd[W_ECAP + 8];              // kind | dc << 2 | player << 8
+  uint8_t hp[W_HCAP];                    // hash slot -> player
+  uint8_t pslot[W_PCAP + 8];             // player -> hash slot
+  uint8_t sorted[W_ECAP + 8];            // op index (stream position) of every op element
+  uint8_t slab[W_ECAP];                  // working Masked slabs (element indices)
+  uint8_t fin[W_ECAP + 8];               // final pool: element of every output position
+  uint8_t pstart[W_PCAP + 8];            // first position of each player's ops
+  uint8_t pobs[W_PCAP + 8];              // Obs[Id] of each player (element), NONE8 = none
+  uint8_t pflag[W_PCAP + 8];             // 1 = complex player (op-by-op replay)
+  uint8_t pcntf[W_PCAP + 8];             // complex player: final |Masked[Id]|
+  uint8_t pmoff[W_PCAP + 8];             // complex player: its working slab in `slab`
+  uint8_t prow[W_PCAP + 8];              // complex player: its clock row or NONE8
+  uint8_t peb[W_PCAP + 8];               // old player: first element of its old slab
+  uint8_t cpl[W_PCAP + 8];               // complex players, packed
+  uint8_t rl[W_RCAP + 8];                // clock row of each output Removals row
+  uint32_t nex;                          // extra effects emitted by the key
 };
 
 __device__ __forceinline__ uint32_t whash(int64_t id) {
@@ -221,7 +226,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // ---- 1. the ops are in `in`; issue the old-state loads
   int64_t xsc[2] = {in.sc[0], in.sc[1]};
   const int64_t xts[2] = {in.ts[0], in.ts[1]};
-  const uint32_t xkd[2] = {in.kd[0], in.kd[1]};
+  const uint32_t xkind[2] = {in.kd[0] & 0xFFu, in.kd[1] & 0xFFu};
+  const uint32_t xdc[2] = {in.kd[0] >> 8, in.kd[1] >> 8};
   const bool xv[2] = {(uint32_t)lane < nops, (uint32_t)(64 + lane) < nops};
   int64_t pid[2] = {0, 0};
   uint32_t pinfo[2] = {NONE32, NONE32}, pslab[2] = {0u, 0u};
@@ -237,11 +243,15 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
   }
   // LDS init (overlaps the loads)
-  for (int i = lane; i < W_HCAP; i += 64) L.htab[i] = W_EMPTY;
+#pragma unroll
+  for (int i = 0; i < W_HCAP / 64; ++i) L.htab[i * 64 + lane] = W_EMPTY;
+  if (lane == 0) {
+    L.htab[HSINK] = W_EMPTY;
+    L.nex = 0u;
+  }
   reinterpret_cast<uint32_t*>(L.hp)[lane] = 0xFFFFFFFFu;  // 256 B
   L.pcnt2[lane] = 0u;
   if (lane < W_PCAP / 4) reinterpret_cast<uint32_t*>(L.pflag)[lane] = 0u;
-  if (lane == 0) L.nex = 0u;
   if (lane < TRMV_DPAD)
     L.vc[lane] = (!FRESH && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
   if (!FRESH) {  // old Removals rows -> clock rows [0, om.nr)
@@ -253,22 +263,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
 
   PROF_MARK(0);
-  // ---- 2. validate ops, rank the rmv ops, issue their clock loads
+  // ---- 2. validate ops (predicated), rank the rmv ops, issue their clock loads
   uint32_t err = 0;
-  bool xr[2];
+  bool xr[2], xa[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const uint32_t kind = xkd[s] & 0xFFu, dc = xkd[s] >> 8;
-    xr[s] = xv[s] && kind >= 2;
-    if (xv[s]) {
-      if (kind > 3) err |= TRMV_ERR_KIND;
-      else if (kind < 2) {
-        if ((int)dc >= D) err |= TRMV_ERR_DC;
-        if (xts[s] < 1) err |= TRMV_ERR_TS;
-      } else if (xts[s] < 0 || xts[s] >= a.n_rmv_rows) {
-        err |= TRMV_ERR_ROW;
-      }
-    }
+    xa[s] = xv[s] && xkind[s] < 2;
+    xr[s] = xv[s] && (xkind[s] == 2 || xkind[s] == 3);
+    err |= (xv[s] && xkind[s] > 3) ? TRMV_ERR_KIND : 0u;
+    err |= (xa[s] && (int)xdc[s] >= D) ? TRMV_ERR_DC : 0u;
+    err |= (xa[s] && xts[s] < 1) ? TRMV_ERR_TS : 0u;
+    err |= (xr[s] && (xts[s] < 0 || xts[s] >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
@@ -278,48 +283,60 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   const uint32_t nr0 = (uint32_t)__builtin_popcountll(rb0);
   const uint32_t nrmv = nr0 + (uint32_t)__builtin_popcountll(rb1);
   if (om.nr + nrmv > (uint32_t)W_RCAP) return W_NEXT_TIER;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (xr[s]) {
-      const uint32_t r = (s == 0 ? 0u : nr0) + mbcnt(s == 0 ? rb0 : rb1);
-      L.rsrc[r] = (uint32_t)xts[s];
-      xsc[s] = om.nr + r;  // clock row of this rmv (stored as its "score")
-    }
+  {
+    const uint32_t r0 = mbcnt(rb0), r1 = nr0 + mbcnt(rb1);
+    if (xr[0]) L.rsrc[r0] = (uint32_t)xts[0];
+    if (xr[1]) L.rsrc[r1] = (uint32_t)xts[1];
+    xsc[0] = xr[0] ? (int64_t)(om.nr + r0) : xsc[0];  // a rmv's "score": its clock row
+    xsc[1] = xr[1] ? (int64_t)(om.nr + r1) : xsc[1];
   }
   wave_lds_sync();
   // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
-  int64_t rv[W_RCAP / 8];
+  int64_t rv[W_RCAP / 8] = {};
+  if (nrmv) {
 #pragma unroll
-  for (int s = 0; s < W_RCAP / 8; ++s) {
-    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    rv[s] = (r < nrmv && (int)d < D) ? a.rmv_vc[(uint64_t)L.rsrc[r] * D + d] : 0;
+    for (int s = 0; s < W_RCAP / 8; ++s) {
+      const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+      const uint32_t row = L.rsrc[r < nrmv ? r : 0u];
+      const int64_t v = a.rmv_vc[(uint64_t)row * D + ((int)d < D ? d : 0u)];
+      rv[s] = (r < nrmv && (int)d < D) ? v : 0;
+    }
   }
 
   PROF_MARK(1);
-  // ---- 3. hash build: old players, then ops (64-bit CAS on the Id)
+  // ---- 3. hash build: old players, then ops (64-bit CAS on the Id; idle
+  // lanes CAS the sink slot, which stays empty)
+  constexpr int NS = FRESH ? 2 : 4;
   uint32_t hs[4];
   bool pend[4];
-  const int64_t hid[4] = {pid[0], pid[1], in.id[0], in.id[1]};
-  pend[0] = !FRESH && (uint32_t)lane < om.np;
-  pend[1] = !FRESH && (uint32_t)(64 + lane) < om.np;
-  pend[2] = xv[0];
-  pend[3] = xv[1];
+  const int64_t hid[4] = {in.id[0], in.id[1], pid[0], pid[1]};
+  pend[0] = xv[0];
+  pend[1] = xv[1];
+  pend[2] = !FRESH && (uint32_t)lane < om.np;
+  pend[3] = !FRESH && (uint32_t)(64 + lane) < om.np;
   bool bad = false;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NS; ++j) {
     hs[j] = whash(hid[j]);
     bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
   }
   if (ballot(bad)) return W_NEXT_TIER;
-  while (ballot(pend[0] || pend[1] || pend[2] || pend[3])) {
+  for (;;) {
+    bool any = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (pend[j]) {
-        const unsigned long long prev =
-            atomicCAS(&L.htab[hs[j]], W_EMPTY, (unsigned long long)hid[j]);
-        if (prev == W_EMPTY || prev == (unsigned long long)hid[j]) pend[j] = false;
-        else hs[j] = (hs[j] + 1) & (W_HCAP - 1);
-      }
+    for (int j = 0; j < NS; ++j) any |= pend[j];
+    if (!ballot(any)) break;
+    unsigned long long prev[4];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      prev[j] = W_EMPTY;
+      if (pend[j]) prev[j] = atomicCAS(&L.htab[hs[j]], W_EMPTY, (unsigned long long)hid[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const bool done = prev[j] == W_EMPTY || prev[j] == (unsigned long long)hid[j];
+      hs[j] = (pend[j] && !done) ? ((hs[j] + 1) & (W_HCAP - 1)) : hs[j];
+      pend[j] = pend[j] && !done;
     }
   }
   // old players keep their index
@@ -328,8 +345,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
       if (p < om.np) {
-        L.hp[hs[s]] = (uint8_t)p;
-        L.pslot[p] = (uint8_t)hs[s];
+        L.hp[hs[2 + s]] = (uint8_t)p;
+        L.pslot[p] = (uint8_t)hs[2 + s];
         // every player with Masked elements must be in Observed (P <= K states)
         bad |= ((pslab[s] >> 16) != 0) != ((pinfo[s] & 0xFFFFu) != NONE16);
       }
@@ -340,41 +357,40 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
     const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    if (r < nrmv) {
-      if (rv[s] < 0) err |= TRMV_ERR_VC;
-      L.rows[om.nr + r][d] = rv[s];
-    }
+    err |= (r < nrmv && rv[s] < 0) ? TRMV_ERR_VC : 0u;
+    if (r < nrmv) L.rows[om.nr + r][d] = rv[s];
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
     return W_REJECT;
   }
   wave_lds_sync();
-  // new players numbered after the old ones, in hash-slot order
+  // new players numbered after the old ones, in hash-slot order (branch-free:
+  // each lane owns four consecutive slots)
   uint32_t np;
   {
-    uint32_t c = 0, newm = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t i = (uint32_t)lane * 4 + q;
-      const bool nw = L.htab[i] != W_EMPTY && L.hp[i] == NONE8;
-      newm |= (nw ? 1u : 0u) << q;
-      c += nw ? 1u : 0u;
-    }
+    const unsigned long long* h4 = &L.htab[lane * 4];
+    const unsigned long long t0 = h4[0], t1 = h4[1], t2 = h4[2], t3 = h4[3];
+    const uint32_t hp4 = reinterpret_cast<const uint32_t*>(L.hp)[lane];
+    const uint32_t n0 = (t0 != W_EMPTY && (hp4 & 0xFFu) == NONE8) ? 1u : 0u;
+    const uint32_t n1 = (t1 != W_EMPTY && ((hp4 >> 8) & 0xFFu) == NONE8) ? 1u : 0u;
+    const uint32_t n2 = (t2 != W_EMPTY && ((hp4 >> 16) & 0xFFu) == NONE8) ? 1u : 0u;
+    const uint32_t n3 = (t3 != W_EMPTY && (hp4 >> 24) == NONE8) ? 1u : 0u;
+    const uint32_t c = n0 + n1 + n2 + n3;
     const uint64_t b0 = ballot(c & 1), b1 = ballot(c & 2), b2 = ballot(c & 4);
-    uint32_t idx = om.np + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
+    const uint32_t base = om.np + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2);
     np = om.np + (uint32_t)__builtin_popcountll(b0) + 2 * (uint32_t)__builtin_popcountll(b1) +
          4 * (uint32_t)__builtin_popcountll(b2);
     if (np > pmax) return W_NEXT_TIER;  // Observed could fill: next tier
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (newm & (1u << q)) {
-        const uint32_t i = (uint32_t)lane * 4 + q;
-        L.hp[i] = (uint8_t)idx;
-        L.pslot[idx] = (uint8_t)i;
-        ++idx;
-      }
-    }
+    const uint32_t i0 = base, i1 = i0 + n0, i2 = i1 + n1, i3 = i2 + n2;
+    const uint32_t nhp = (n0 ? i0 : (hp4 & 0xFFu)) | ((n1 ? i1 : ((hp4 >> 8) & 0xFFu)) << 8) |
+                         ((n2 ? i2 : ((hp4 >> 16) & 0xFFu)) << 16) |
+                         ((n3 ? i3 : (hp4 >> 24)) << 24);
+    reinterpret_cast<uint32_t*>(L.hp)[lane] = nhp;
+    if (n0) L.pslot[i0] = (uint8_t)(lane * 4 + 0);
+    if (n1) L.pslot[i1] = (uint8_t)(lane * 4 + 1);
+    if (n2) L.pslot[i2] = (uint8_t)(lane * 4 + 2);
+    if (n3) L.pslot[i3] = (uint8_t)(lane * 4 + 3);
   }
   wave_lds_sync();
 
@@ -383,17 +399,13 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   uint32_t xrank[2], xp[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    xp[s] = 0;
+    const uint32_t p = xv[s] ? (uint32_t)L.hp[hs[s]] : PSINK;
+    xp[s] = p;
+    if (xa[s]) atomicMax(&L.vc[xdc[s]], (unsigned long long)xts[s]);  // vc_update (:233)
+    if (xr[s]) L.pflag[p] = 1;                                        // a rmv: complex player
+    const uint32_t sh = 16 * (p & 1);
     xrank[s] = 0;
-    if (xv[s]) {
-      const uint32_t kind = xkd[s] & 0xFFu, dc = xkd[s] >> 8;
-      const uint32_t p = L.hp[hs[2 + s]];
-      xp[s] = p;
-      if (kind < 2) atomicMax(&L.vc[dc], (unsigned long long)xts[s]);  // vc_update (:233)
-      else L.pflag[p] = 1;  // a rmv: complex player
-      const uint32_t sh = 16 * (p & 1);
-      xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    }
+    if (xv[s]) xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
   }
   wave_lds_sync();
   // per player (lane, lane + 64): first position of its ops
@@ -403,25 +415,21 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const uint32_t c1 = (uint32_t)(64 + lane) < np ? pcnt_of(L, 64 + lane) : 0u;
     const uint32_t st0 = wave_excl_scan_dpp(c0, tot0);
     const uint32_t st1 = wave_excl_scan_dpp(c1, tot1);
-    if ((uint32_t)lane < np) L.pstart[lane] = (uint8_t)st0;
-    if ((uint32_t)(64 + lane) < np) L.pstart[64 + lane] = (uint8_t)(tot0 + st1);
+    L.pstart[lane] = (uint8_t)st0;
+    L.pstart[64 + lane] = (uint8_t)(tot0 + st1);
   }
   wave_lds_sync();
   uint32_t xq[2], xst[2], xc[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    xq[s] = 0;
-    xst[s] = 0;
-    xc[s] = 0;
+    xst[s] = L.pstart[xp[s]];
+    xc[s] = pcnt_of(L, xp[s]);
+    xq[s] = xv[s] ? xst[s] + xrank[s] : ESINK;
     if (xv[s]) {
-      xst[s] = L.pstart[xp[s]];
-      xc[s] = pcnt_of(L, xp[s]);
-      const uint32_t q = xst[s] + xrank[s];
-      xq[s] = q;
-      L.esc[q] = xsc[s];
-      L.ets[q] = xts[s];
-      L.ekd[q] = (uint16_t)((xkd[s] & 0xFFu) | ((xkd[s] >> 8) << 2) | (xp[s] << 8));
-      L.sorted[q] = (uint8_t)(s * 64 + lane);
+      L.esc[xq[s]] = xsc[s];
+      L.ets[xq[s]] = xts[s];
+      L.ekd[xq[s]] = (uint16_t)(xkind[s] | (xdc[s] << 2) | (xp[s] << 8));
+      L.sorted[xq[s]] = (uint8_t)(s * 64 + lane);
     }
   }
   wave_lds_sync();
@@ -431,8 +439,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   {
     bool bad_order = false;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      if (xv[s] && xq[s] > xst[s]) bad_order |= L.sorted[xq[s] - 1] > (uint32_t)(s * 64 + lane);
+    for (int s = 0; s < 2; ++s) {
+      const bool has_prev = xv[s] && xq[s] > xst[s];
+      bad_order |= has_prev && L.sorted[has_prev ? xq[s] - 1 : ESINK] > (uint32_t)(s * 64 + lane);
+    }
     if (ballot(bad_order)) {
 #pragma unroll 1
       for (int s = 0; s < 2; ++s) {
@@ -497,24 +507,32 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   if (has_next) wave_load_key(a, hdr, nj, nxt);
   // ---- 5a. simple players, op-parallel: each add decides whether it is its
   // player's Obs[Id] and whether its Ts rises over every earlier add's
+  {
+    bool simple[2], beaten[2] = {false, false}, risk[2] = {false, false};
+    uint32_t me[2], cl[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (xv[s] && !L.pflag[xp[s]]) {
-      const uint32_t me = xq[s] - xst[s];
-      bool beaten = false, risk = false;
-      for (uint32_t x = 0; x < xc[s]; ++x) {
-        if (x == me) continue;
-        const int64_t sx = L.esc[xst[s] + x], tx = L.ets[xst[s] + x];
+    for (int s = 0; s < 2; ++s) {
+      simple[s] = xa[s] && !L.pflag[xp[s]];
+      me[s] = xq[s] - xst[s];
+      cl[s] = simple[s] ? xc[s] : 0u;
+    }
+    const uint32_t maxc = wave_max_u32_dpp(cl[0] > cl[1] ? cl[0] : cl[1]);
+    for (uint32_t x = 0; x < maxc; ++x) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bool valid = x < cl[s] && x != me[s];
+        const uint32_t pos = x < cl[s] ? xst[s] + x : (uint32_t)ESINK;
+        const int64_t sx = L.esc[pos], tx = L.ets[pos];
         const int64_t sm = xsc[s], tm = xts[s];
-        if (x < me) {
-          risk |= tx >= tm;
-          beaten |= sx > sm || (sx == sm && tx >= tm);
-        } else {
-          beaten |= sx > sm || (sx == sm && tx > tm);
-        }
+        const bool before = x < me[s];
+        risk[s] |= valid && before && tx >= tm;
+        beaten[s] |= valid && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
       }
-      if (risk) L.pflag[xp[s]] = 1;
-      if (!beaten) L.pobs[xp[s]] = (uint8_t)xq[s];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (risk[s]) L.pflag[xp[s]] = 1;
+      if (simple[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
     }
   }
   wave_lds_sync();
@@ -655,42 +673,54 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next key's ops are in registers
   // ---- 6. player records, final pool order, Removals rows
   uint32_t fbase = 0, rbase = 0, nobs = 0;
+  uint32_t po[2];
+  {
+    uint32_t cnt[2], st[2], moff[2], goff[2], prow[2], opos[2];
+    bool act[2], cx[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const uint32_t p = s * 64 + lane;
-    const bool act = p < np;
-    const bool cx = act && L.pflag[p];
-    const uint32_t c = act ? pcnt_of(L, p) : 0u;
-    const uint32_t st = act ? L.pstart[p] : 0u;
-    const uint32_t cnt = cx ? L.pcntf[p] : c;  // simple: every add is in Masked[Id]
-    const uint32_t o = act ? L.pobs[p] : NONE8;
-    const uint32_t prow = cx ? L.prow[p] : NONE8;
-    const uint32_t moff = cx ? L.pmoff[p] : 0u;
-    uint32_t ftot;
-    const uint32_t goff = fbase + wave_excl_scan_dpp(cnt, ftot);
-    fbase += ftot;
-    uint32_t opos = NONE16;
-    if (cx) {
-      for (uint32_t j = 0; j < cnt; ++j) {
-        const uint32_t e2 = L.slab[moff + j];
-        L.fin[goff + j] = (uint8_t)e2;
-        if (e2 == o) opos = j;
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      act[s] = p < np;
+      const uint32_t pp = act[s] ? p : PSINK;
+      cx[s] = act[s] && L.pflag[pp];
+      const uint32_t c = pcnt_of(L, pp);
+      st[s] = L.pstart[pp];
+      po[s] = act[s] ? L.pobs[pp] : NONE8;
+      cnt[s] = act[s] ? (cx[s] ? (uint32_t)L.pcntf[pp] : c) : 0u;  // simple: every add is in Masked[Id]
+      prow[s] = cx[s] ? L.prow[pp] : NONE8;
+      moff[s] = cx[s] ? L.pmoff[pp] : 0u;
+      uint32_t ftot;
+      goff[s] = fbase + wave_excl_scan_dpp(cnt[s], ftot);
+      fbase += ftot;
+      opos[s] = (act[s] && !cx[s]) ? po[s] - st[s] : NONE16;
+    }
+    // final pool order: complex players' slabs, simple players' op runs
+    const uint32_t maxcnt = wave_max_u32_dpp(cnt[0] > cnt[1] ? cnt[0] : cnt[1]);
+    for (uint32_t j = 0; j < maxcnt; ++j) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bool in = j < cnt[s];
+        const uint32_t e = cx[s] ? (uint32_t)L.slab[in ? moff[s] + j : 0u] : st[s] + j;
+        if (in) L.fin[goff[s] + j] = (uint8_t)e;
+        opos[s] = (cx[s] && in && e == po[s]) ? j : opos[s];
       }
-    } else {
-      for (uint32_t j = 0; j < cnt; ++j) L.fin[goff + j] = (uint8_t)(st + j);
-      if (act) opos = o - st;
     }
-    const uint64_t rm = ballot(prow != NONE8);
-    const uint32_t rix = rbase + mbcnt(rm);
-    rbase += (uint32_t)__builtin_popcountll(rm);
-    if (act) {
-      if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      (a.new_s.pl_id + nmeta.p_off)[p] = (int64_t)L.htab[L.pslot[p]];
-      (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : opos) |
-                                           ((prow != NONE8 ? rix : NONE16) << 16);
-      (a.new_s.pl_slab + nmeta.p_off)[p] = goff | (cnt << 16);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      const uint64_t rm = ballot(prow[s] != NONE8);
+      const uint32_t rix = rbase + mbcnt(rm);
+      rbase += (uint32_t)__builtin_popcountll(rm);
+      if (prow[s] != NONE8) L.rl[rix] = (uint8_t)prow[s];
+      const int64_t id = (int64_t)L.htab[L.pslot[act[s] ? p : PSINK]];
+      if (act[s]) {
+        (a.new_s.pl_id + nmeta.p_off)[p] = id;
+        (a.new_s.pl_info + nmeta.p_off)[p] = (po[s] == NONE8 ? NONE16 : opos[s]) |
+                                             ((prow[s] != NONE8 ? rix : NONE16) << 16);
+        (a.new_s.pl_slab + nmeta.p_off)[p] = goff[s] | (cnt[s] << 16);
+      }
+      nobs += (uint32_t)__builtin_popcountll(ballot(act[s] && po[s] != NONE8));
     }
-    nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
   }
   wave_lds_sync();
 
@@ -698,17 +728,20 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t q = s * 64 + lane;
+    const uint32_t e0 = L.fin[q < fbase ? q : (uint32_t)ESINK];
+    const uint32_t e = e0 < (uint32_t)W_ECAP ? e0 : (uint32_t)ESINK;
+    const int64_t sc = L.esc[e], ts = L.ets[e];
+    const uint8_t dc = (uint8_t)((L.ekd[e] >> 2) & 7u);
     if (q < fbase) {
-      const uint32_t e = L.fin[q];
-      (a.new_s.m_score + nmeta.m_off)[q] = L.esc[e];
-      (a.new_s.m_ts + nmeta.m_off)[q] = L.ets[e];
-      (a.new_s.m_dc + nmeta.m_off)[q] = (uint8_t)((L.ekd[e] >> 2) & 7u);
+      (a.new_s.m_score + nmeta.m_off)[q] = sc;
+      (a.new_s.m_ts + nmeta.m_off)[q] = ts;
+      (a.new_s.m_dc + nmeta.m_off)[q] = dc;
     }
   }
   for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
-    if (r < rbase && (int)d < D)
-      (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = L.rows[L.rl[r]][d];
+    const int64_t v = L.rows[L.rl[r < rbase ? r : 0u]][d];
+    if (r < rbase && (int)d < D) (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
   }
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
@@ -718,15 +751,13 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
-      const uint32_t o = p < np ? L.pobs[p] : NONE8;
-      if (o != NONE8) {
-        const int64_t sc = L.esc[o], id = (int64_t)L.htab[L.pslot[p]];
-        if (best_q == NONE32 || sc < best_sc || (sc == best_sc && id < best_id)) {
-          best_q = p;
-          best_sc = sc;
-          best_id = id;
-        }
-      }
+      const uint32_t o = po[s];
+      const int64_t sc = L.esc[o != NONE8 ? o : (uint32_t)ESINK];
+      const int64_t id = (int64_t)L.htab[L.pslot[o != NONE8 ? p : (uint32_t)PSINK]];
+      const bool better = o != NONE8 && (best_q == NONE32 || sc < best_sc || (sc == best_sc && id < best_id));
+      best_q = better ? p : best_q;
+      best_sc = better ? sc : best_sc;
+      best_id = better ? id : best_id;
     }
     const bool has = best_q != NONE32;
     if (ballot(has)) {
