@@ -28,11 +28,13 @@ int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStr
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
+int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st);
 
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
 static constexpr uint32_t TRMV_MAX_ROWS = 8u * 2u * 16u;  // removal rows per key
-static constexpr int TRMV_STATUS_WORDS = 16;
+static constexpr int TRMV_STATUS_WORDS = 32;  // [0,14) scan + main tiers, [16,26) side chain
+static constexpr int TRMV_SIDE = 16;
 static constexpr uint32_t TRMV_LATER_GRID = 2048;  // workgroups of the tiers after the first
 
 }  // namespace ccrdt
@@ -67,6 +69,7 @@ void ccrdt_engine::release_all() {
     b.vc.release();
   }
   for (DevBuf& d : tier_ovf) d.release();
+  for (DevBuf& d : tier_ovf_b) d.release();
   for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -154,7 +157,7 @@ int ccrdt_engine_create(int type, int64_t k, int64_t n_keys, int n_dc, int devic
       hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
       hipEventCreate(&e->evk0) != hipSuccess || hipEventCreate(&e->evk1) != hipSuccess ||
       !e->create_tier_events() ||
-      hipHostMalloc((void**)&e->h_status, 64, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&e->h_status, 256, hipHostMallocDefault) != hipSuccess) {
     set_error("engine_create: stream/event/pinned allocation failed");
     delete e;
     return CCRDT_EDEVICE;
@@ -178,8 +181,8 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->evk0) (void)hipEventDestroy(e->evk0);
   if (e->evk1) (void)hipEventDestroy(e->evk1);
-  for (hipEvent_t& v : e->evt)
-    if (v) (void)hipEventDestroy(v);
+  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
+  e->destroy_tier_events();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return CCRDT_OK;
@@ -334,6 +337,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
   for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
+  for (DevBuf& d : E.tier_ovf_b) CCRDT_TRY(d.ensure(nk * 4));
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
@@ -349,6 +353,34 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   }();
   constexpr int N_TIERS = 2 + (int)(sizeof(TRMV_SLOT_CLASSES) / sizeof(int));
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
+  constexpr int N_CLS = (int)(sizeof(TRMV_SLOT_CLASSES) / sizeof(int));
+  // Side chain (stream2, after the scan): keys with more ops than tier 0
+  // takes go straight to the sequential kernel's classes, concurrently with
+  // tier 0, which skips them.
+  const bool side = first_tier == 0 && nk;
+  if (side) {
+    CCRDT_HIP(hipEventRecord(E.ev_scan, E.stream));
+    CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.ev_scan, 0));
+    TrmvApplyArgs b = a;
+    CCRDT_HIP(hipEventRecord(E.evb[0], E.stream2));
+    b.key_list = nullptr;
+    b.n_list = (uint32_t)nk;
+    b.n_list_dev = nullptr;
+    b.ovf_list = E.tier_ovf_b[0].as<uint32_t>();
+    b.status = status + TRMV_SIDE;
+    CCRDT_TRY(trmv_launch_classify(b, E.stream2));
+    CCRDT_HIP(hipEventRecord(E.evb[1], E.stream2));
+    for (int i = 0; i < N_CLS; ++i) {
+      b.key_list = E.tier_ovf_b[i].as<uint32_t>();
+      b.n_list_dev = status + TRMV_SIDE + 2 * i;
+      b.ovf_list = E.tier_ovf_b[i + 1].as<uint32_t>();
+      b.status = status + TRMV_SIDE + 2 + 2 * i;
+      CCRDT_TRY(trmv_launch_apply(b, TRMV_SLOT_CLASSES[i], later_grid, E.stream2));
+      CCRDT_HIP(hipEventRecord(E.evb[i + 2], E.stream2));
+    }
+    CCRDT_HIP(hipEventRecord(E.ev_side, E.stream2));
+  }
+  a.skip_big = side ? 1 : 0;
   DevBuf* work = nullptr;
   const uint32_t* n_dev = nullptr;
   int ev = 0;
@@ -368,6 +400,10 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     work = ovf;
     n_dev = a.status;
   }
+  if (side) {
+    CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_side, 0));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+  }
   CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost,
                            E.stream));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
@@ -378,6 +414,8 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   }
   uint32_t err = 0;
   for (int t = first_tier; t < N_TIERS; ++t) err |= hs[3 + 2 * t];
+  if (side)
+    for (int i = 0; i < N_CLS; ++i) err |= hs[TRMV_SIDE + 3 + 2 * i];
   if (err) {
     std::string m = "trmv_apply: invalid op in batch:";
     if (err & TRMV_ERR_KIND) m += " kind>3";
@@ -390,7 +428,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
                ? CCRDT_ERANGE
                : CCRDT_EINVAL;
   }
-  if (nk && hs[2 + 2 * (N_TIERS - 1)]) {
+  if (nk && (hs[2 + 2 * (N_TIERS - 1)] || (side && hs[TRMV_SIDE + 2 * N_CLS]))) {
     set_error("trmv_apply: a key exceeds the per-key capacity (1024 Ids or Masked elements, "
               "256 Removals entries)");
     return CCRDT_ENOMEM;
@@ -405,6 +443,18 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[i - 1], E.evt[i]));
     E.trmv_tier_ms[key] = ms;
     E.trmv_overflow_keys[key] = hs[2 + 2 * t];
+  }
+  if (side) {  // side chain: 1000 = keys sent to it, 1000 + class = its hand-ons / times
+    E.trmv_overflow_keys[1000] = hs[TRMV_SIDE];
+    for (int i = 0; i < N_CLS; ++i) {
+      float ms = 0.f;
+      CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[i + 1], E.evb[i + 2]));
+      E.trmv_tier_ms[1000 + TRMV_SLOT_CLASSES[i]] = ms;
+      E.trmv_overflow_keys[1000 + TRMV_SLOT_CLASSES[i]] = hs[TRMV_SIDE + 2 + 2 * i];
+    }
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[0], E.evb[1]));
+    E.trmv_tier_ms[1000] = ms;
   }
   if (nk && ev > 1) CCRDT_HIP(hipEventElapsedTime(&kernel_ms, E.evt[0], E.evt[ev - 1]));
   CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
@@ -603,9 +653,9 @@ int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* 
 
 int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, int64_t* n) {
   if (!e || !n || cap < 0) return CCRDT_EINVAL;
-  static constexpr int tiers[] = {0, 1, 2, 4, 8, 16};
+  static constexpr int tiers[] = {0, 1, 2, 4, 8, 16, 1000, 1002, 1004, 1008, 1016};
   int ti = -1;
-  for (int i = 0; i < 6; ++i)
+  for (int i = 0; i < 11; ++i)
     if (tiers[i] == t) ti = i;
   auto it = e->trmv_overflow_keys.find(t);
   if (ti < 0 || e->type != CCRDT_TOPK_RMV || it == e->trmv_overflow_keys.end()) {
@@ -615,8 +665,9 @@ int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, 
   *n = it->second;
   const int64_t m = std::min<int64_t>(cap, *n);
   if (m > 0 && keys) {
+    const DevBuf& src = ti < 6 ? e->tier_ovf[ti] : e->tier_ovf_b[ti - 6];
     CCRDT_HIP(hipStreamSynchronize(e->stream));
-    CCRDT_HIP(hipMemcpy(keys, e->tier_ovf[ti].p, (size_t)m * 4, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(keys, src.p, (size_t)m * 4, hipMemcpyDeviceToHost));
   }
   return CCRDT_OK;
 }

@@ -47,20 +47,37 @@ struct ccrdt_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the main apply kernel
   hipEvent_t evt[8] = {};                      // topk_rmv tier boundaries
+  // topk_rmv side chain: keys too large for tier 0 run the sequential kernel
+  // on a second stream, concurrently with tier 0
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_scan = nullptr, ev_side = nullptr, evb[6] = {};
   bool create_tier_events() {
     for (hipEvent_t& v : evt)
       if (hipEventCreate(&v) != hipSuccess) return false;
-    return true;
+    for (hipEvent_t& v : evb)
+      if (hipEventCreate(&v) != hipSuccess) return false;
+    return hipEventCreate(&ev_scan) == hipSuccess && hipEventCreate(&ev_side) == hipSuccess &&
+           hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) == hipSuccess;
+  }
+  void destroy_tier_events() {
+    for (hipEvent_t& v : evt)
+      if (v) (void)hipEventDestroy(v);
+    for (hipEvent_t& v : evb)
+      if (v) (void)hipEventDestroy(v);
+    if (ev_scan) (void)hipEventDestroy(ev_scan);
+    if (ev_side) (void)hipEventDestroy(ev_side);
+    if (stream2) (void)hipStreamDestroy(stream2);
   }
   float last_kernel_ms = 0.f;
-  void* h_status = nullptr;  // pinned, 64 bytes
+  void* h_status = nullptr;  // pinned, 256 bytes
   bool fresh = true;         // every key == new(k); resident arrays ignored
 
   // topk_rmv
   ccrdt::TrmvBufs trmv[2];
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status;
-  ccrdt::DevBuf tier_ovf[6];  // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf tier_ovf[6];    // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf tier_ovf_b[5];  // side chain: big keys, then each class's hand-ons
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held

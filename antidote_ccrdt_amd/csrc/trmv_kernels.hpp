@@ -93,6 +93,7 @@ struct TrmvApplyArgs {
                                // (the previous tier's overflow count)
   uint32_t* ovf_list;
   uint32_t* status;  // [0] overflow count, [1] error flags
+  int32_t skip_big;  // tier 0: keys with more ops than it takes run on the side chain
 };
 
 enum : uint32_t {

@@ -195,7 +195,7 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
 // Outcome of one key.  Only W_DONE has already issued the loads of the wave's
 // next key (just before the write-out); the rare other paths leave that to the
 // caller, which keeps the prefetched registers out of the early phases.
-enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
+enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2, W_SIDE = 3 };
 
 template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
@@ -219,6 +219,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     om = a.old_s.meta[key];
   }
   const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
+  if (nops > (uint32_t)W_ECAP && a.skip_big) return W_SIDE;  // the side chain has it
   if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
       om.nr > (uint32_t)W_RCAP)
     return W_NEXT_TIER;
@@ -801,7 +802,9 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
       const bool has_next = j + 1 < cn;
       KeyIn nxt;
       const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
-      if (r != W_DONE) {
+      if (r == W_SIDE) {
+        if (has_next) wave_load_key(a, hdr, j + 1, nxt);
+      } else if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&a.status[0], 1u);
           a.ovf_list[pos] = key;
@@ -812,6 +815,26 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
       cur = nxt;
     }
   }
+}
+
+// The side chain's work list: every key with more ops than tier 0 takes.
+__global__ __launch_bounds__(256) void trmv_classify_kernel(TrmvApplyArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool big = k < (uint64_t)a.n_keys && a.key_ptr[k + 1] - a.key_ptr[k] > (uint64_t)W_ECAP;
+  const uint64_t m = ballot(big);
+  if (m) {
+    uint32_t base = 0;
+    if (lane_id() == (int)__builtin_ctzll(m)) base = atomicAdd(&a.status[0], (uint32_t)__builtin_popcountll(m));
+    base = rl32(base, (int)__builtin_ctzll(m));
+    if (big) a.ovf_list[base + mbcnt(m)] = (uint32_t)k;
+  }
+}
+
+int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st) {
+  if (a.n_keys == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_classify_kernel, dim3((unsigned)((a.n_keys + 255) / 256)), dim3(256), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)

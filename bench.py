@@ -139,8 +139,9 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    overflow = {c: eng.overflow_keys(c) for c in (0, 1, 2, 4, 8)}
-    tier_ms = {c: round(eng.tier_ms(c), 4) for c in (0, 1, 2, 4, 8)}
+    tiers = (0, 1, 2, 4, 8, 16, 1000, 1002, 1004, 1008, 1016)  # 1000+: side chain (big keys)
+    overflow = {c: eng.overflow_keys(c) for c in tiers}
+    tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
     cpu = None
     if rank == 0 and args.cpu_sample_keys > 0:
