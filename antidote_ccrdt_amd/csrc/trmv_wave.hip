@@ -141,7 +141,7 @@ struct KeyIn {
   uint32_t nops;
   KeyMeta nmeta;
   int64_t id[2], sc[2], ts[2];
-  uint32_t kd[2];  // kind | dc << 8
+  uint32_t kind[2], dc[2];  // kept apart: combining them would force a wait at the load
 };
 
 // Bounds and new-side metadata of a wave's W_KPW keys, loaded once per chunk
@@ -188,7 +188,8 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
     in.id[s] = v ? idp[l] : 0;
     in.sc[s] = v ? scp[l] : 0;
     in.ts[s] = v ? tsp[l] : 0;
-    in.kd[s] = v ? ((uint32_t)kp[l] | ((uint32_t)dp[l] << 8)) : 0u;
+    in.kind[s] = v ? (uint32_t)kp[l] : 0u;
+    in.dc[s] = v ? (uint32_t)dp[l] : 0u;
   }
 }
 
@@ -227,8 +228,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // ---- 1. the ops are in `in`; issue the old-state loads
   int64_t xsc[2] = {in.sc[0], in.sc[1]};
   const int64_t xts[2] = {in.ts[0], in.ts[1]};
-  const uint32_t xkind[2] = {in.kd[0] & 0xFFu, in.kd[1] & 0xFFu};
-  const uint32_t xdc[2] = {in.kd[0] >> 8, in.kd[1] >> 8};
+  const uint32_t xkind[2] = {in.kind[0], in.kind[1]};
+  const uint32_t xdc[2] = {in.dc[0], in.dc[1]};
   const bool xv[2] = {(uint32_t)lane < nops, (uint32_t)(64 + lane) < nops};
   int64_t pid[2] = {0, 0};
   uint32_t pinfo[2] = {NONE32, NONE32}, pslab[2] = {0u, 0u};
@@ -293,15 +294,16 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   wave_lds_sync();
   // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
+  // (raw values: masked only where they are written, after the hash build,
+  // so no use forces an early wait)
   int64_t rv[W_RCAP / 8] = {};
   if (nrmv) {
+    const uint32_t rw[W_RCAP / 8] = {L.rsrc[(lane >> 3) < (int)nrmv ? (lane >> 3) : 0],
+                                     L.rsrc[8 + (lane >> 3) < (int)nrmv ? 8 + (lane >> 3) : 0],
+                                     L.rsrc[16 + (lane >> 3) < (int)nrmv ? 16 + (lane >> 3) : 0]};
+    const uint32_t d = (lane & 7) < D ? (lane & 7) : 0u;
 #pragma unroll
-    for (int s = 0; s < W_RCAP / 8; ++s) {
-      const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-      const uint32_t row = L.rsrc[r < nrmv ? r : 0u];
-      const int64_t v = a.rmv_vc[(uint64_t)row * D + ((int)d < D ? d : 0u)];
-      rv[s] = (r < nrmv && (int)d < D) ? v : 0;
-    }
+    for (int s = 0; s < W_RCAP / 8; ++s) rv[s] = a.rmv_vc[(uint64_t)rw[s] * D + d];
   }
 
   PROF_MARK(1);
@@ -358,8 +360,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
     const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    err |= (r < nrmv && rv[s] < 0) ? TRMV_ERR_VC : 0u;
-    if (r < nrmv) L.rows[om.nr + r][d] = rv[s];
+    const int64_t v = (int)d < D ? rv[s] : 0;
+    err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
+    if (r < nrmv) L.rows[om.nr + r][d] = v;
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&a.status[1], err);
@@ -538,6 +541,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   wave_lds_sync();
 
+  PROF_MARK(6);
   // ---- 5b. complex players, one lane per player, replayed op by op
   uint32_t ncx;
   {
@@ -797,19 +801,21 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
     wave_load_chunk(a, c0, cn, hdr);
     KeyIn cur;
     wave_load_key(a, hdr, 0, cur);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load is pending at the loop head
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
       const bool has_next = j + 1 < cn;
       KeyIn nxt;
       const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
-      if (r == W_SIDE) {
-        if (has_next) wave_load_key(a, hdr, j + 1, nxt);
-      } else if (r != W_DONE) {
+      if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&a.status[0], 1u);
           a.ovf_list[pos] = key;
         }
         if (has_next) wave_load_key(a, hdr, j + 1, nxt);
+        // retire these loads here, as the common path does before its
+        // stores: otherwise every key would wait on the previous key's stores
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       }
       wave_lds_sync();  // LDS is reused by the wave's next key
       cur = nxt;
