@@ -293,22 +293,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     xsc[1] = xr[1] ? (int64_t)(om.nr + r1) : xsc[1];
   }
   wave_lds_sync();
-  // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
-  // (raw values: masked only where they are written, after the hash build,
-  // so no use forces an early wait)
-  int64_t rv[W_RCAP / 8] = {};
-  if (nrmv) {
-    const uint32_t rw[W_RCAP / 8] = {L.rsrc[(lane >> 3) < (int)nrmv ? (lane >> 3) : 0],
-                                     L.rsrc[8 + (lane >> 3) < (int)nrmv ? 8 + (lane >> 3) : 0],
-                                     L.rsrc[16 + (lane >> 3) < (int)nrmv ? 16 + (lane >> 3) : 0]};
-    const uint32_t d = (lane & 7) < D ? (lane & 7) : 0u;
-#pragma unroll
-    for (int s = 0; s < W_RCAP / 8; ++s) rv[s] = a.rmv_vc[(uint64_t)rw[s] * D + d];
-  }
-
-  PROF_MARK(1);
-  // ---- 3. hash build: old players, then ops (64-bit CAS on the Id; idle
-  // lanes CAS the sink slot, which stays empty)
+  // ---- 3 (set-up). hash slots; an Id equal to the empty marker takes tier 1
   constexpr int NS = FRESH ? 2 : 4;
   uint32_t hs[4];
   bool pend[4];
@@ -324,6 +309,21 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
   }
   if (ballot(bad)) return W_NEXT_TIER;
+  // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
+  // (raw values: masked only where they are written, after the hash build,
+  // so no use forces an early wait)
+  int64_t rv[W_RCAP / 8] = {};
+  if (nrmv) {
+    const uint32_t rw[W_RCAP / 8] = {L.rsrc[(lane >> 3) < (int)nrmv ? (lane >> 3) : 0],
+                                     L.rsrc[8 + (lane >> 3) < (int)nrmv ? 8 + (lane >> 3) : 0],
+                                     L.rsrc[16 + (lane >> 3) < (int)nrmv ? 16 + (lane >> 3) : 0]};
+    const uint32_t d = (lane & 7) < D ? (lane & 7) : 0u;
+#pragma unroll
+    for (int s = 0; s < W_RCAP / 8; ++s) rv[s] = a.rmv_vc[(uint64_t)rw[s] * D + d];
+  }
+
+  PROF_MARK(1);
+  // ---- 3. hash build: ops, then old players (64-bit CAS on the Id)
   for (;;) {
     bool any = false;
 #pragma unroll
@@ -342,6 +342,18 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       pend[j] = pend[j] && !done;
     }
   }
+  // write the staged rmv clocks (loads were in flight during the build)
+#pragma unroll
+  for (int s = 0; s < W_RCAP / 8; ++s) {
+    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+    const int64_t v = (int)d < D ? rv[s] : 0;
+    err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
+    if (r < nrmv) L.rows[om.nr + r][d] = v;
+  }
+  if (ballot(err != 0)) {
+    if (err) atomicOr(&a.status[1], err);
+    return W_REJECT;
+  }
   // old players keep their index
   if (!FRESH) {
 #pragma unroll
@@ -355,18 +367,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
     }
     if (ballot(bad)) return W_NEXT_TIER;
-  }
-  // write the staged rmv clocks (loads were in flight during the build)
-#pragma unroll
-  for (int s = 0; s < W_RCAP / 8; ++s) {
-    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    const int64_t v = (int)d < D ? rv[s] : 0;
-    err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
-    if (r < nrmv) L.rows[om.nr + r][d] = v;
-  }
-  if (ballot(err != 0)) {
-    if (err) atomicOr(&a.status[1], err);
-    return W_REJECT;
   }
   wave_lds_sync();
   // new players numbered after the old ones, in hash-slot order (branch-free:
