@@ -554,6 +554,50 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (c1) L.cpl[n0 + mbcnt(m1)] = (uint8_t)(64 + lane);
   }
   wave_lds_sync();
+  // FRESH: every player's Masked slab lives at its own op positions
+  // [pstart, pstart + |Masked[Id]|) of the key's pool segment (|Masked[Id]|
+  // <= its adds), so no pool order has to be built: simple players' elements
+  // are written by their op lanes, complex players' by their replay lanes.
+  // The next key's ops (issued at 5a) are retired before this key's first
+  // store, so the next key never waits on (and its vmcnt never counts) them.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  uint32_t f_nm = 0, f_nobs = 0, f_nr = 0;       // FRESH totals (wave-uniform)
+  uint32_t best_q = NONE32;                      // Min candidate of this lane
+  int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
+  auto min_cand = [&](bool has, int64_t sc, int64_t id, uint32_t p) {
+    const bool better = has && (best_q == NONE32 || sc < best_sc || (sc == best_sc && id < best_id));
+    best_q = better ? p : best_q;
+    best_sc = better ? sc : best_sc;
+    best_id = better ? id : best_id;
+  };
+  if (FRESH) {
+    // every op position as if its player were simple (coalesced); complex
+    // players rewrite their own ranges below, in program order after these
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t q = s * 64 + lane;
+      const uint32_t qq = q < nops ? q : (uint32_t)ESINK;
+      const int64_t sc = L.esc[qq], ts = L.ets[qq];
+      const uint32_t kd = L.ekd[qq];
+      if (q < nops) {
+        (a.new_s.m_score + nmeta.m_off)[q] = sc;
+        (a.new_s.m_ts + nmeta.m_off)[q] = ts;
+        (a.new_s.m_dc + nmeta.m_off)[q] = (uint8_t)((kd >> 2) & 7u);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      const uint32_t pp = p < np ? p : (uint32_t)PSINK;
+      const uint32_t st = L.pstart[pp], c = pcnt_of(L, pp), o = L.pobs[pp];
+      const int64_t id = (int64_t)L.htab[L.pslot[pp]];
+      if (p < np) {  // (complex players' records are rewritten below)
+        (a.new_s.pl_id + nmeta.p_off)[p] = id;
+        (a.new_s.pl_slab + nmeta.p_off)[p] = st | (c << 16);
+        (a.new_s.pl_info + nmeta.p_off)[p] = (o - st) | (NONE16 << 16);
+      }
+    }
+  }
   uint32_t mbase = 0;
 #pragma unroll 1
   for (uint32_t b = 0; b < ncx; b += 64) {
@@ -665,20 +709,57 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         }
       }
     }
-    if (act) {
+    if (FRESH) {
+      uint32_t opos = NONE16;
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t e2 = L.slab[moff + j];
+        (a.new_s.m_score + nmeta.m_off)[st + j] = L.esc[e2];
+        (a.new_s.m_ts + nmeta.m_off)[st + j] = L.ets[e2];
+        (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)((L.ekd[e2] >> 2) & 7u);
+        opos = e2 == o ? j : opos;
+      }
+      const uint64_t rm = ballot(act && prow != NONE8);
+      const uint32_t rix = f_nr + mbcnt(rm);
+      f_nr += (uint32_t)__builtin_popcountll(rm);
+      if (act) {
+        (a.new_s.pl_id + nmeta.p_off)[p] = id;
+        (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : opos) |
+                                             ((prow != NONE8 ? rix : NONE16) << 16);
+        (a.new_s.pl_slab + nmeta.p_off)[p] = st | (cnt << 16);
+        if (prow != NONE8)
+          for (int d = 0; d < D; ++d)
+            (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[rix * D + d] = L.rows[prow][d];
+      }
+      uint32_t ctot;
+      (void)wave_excl_scan_dpp(act ? cnt : 0u, ctot);
+      f_nm += ctot;
+      f_nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
+      min_cand(act && o != NONE8, osc, id, p);
+    } else if (act) {
       L.pobs[p] = (uint8_t)o;
       L.pcntf[p] = (uint8_t)cnt;
       L.pmoff[p] = (uint8_t)moff;
       L.prow[p] = (uint8_t)prow;
     }
   }
+  if (FRESH) {
+    // simple players (their final status: 5a may have made some complex)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool simple = xa[s] && !L.pflag[xp[s]];
+      const bool win = simple && L.pobs[xp[s]] == xq[s];
+      f_nm += (uint32_t)__builtin_popcountll(ballot(simple));
+      f_nobs += (uint32_t)__builtin_popcountll(ballot(win));
+      min_cand(win, xsc[s], in.id[s], xp[s]);
+    }
+  }
   wave_lds_sync();
 
   PROF_MARK(4);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next key's ops are in registers
-  // ---- 6. player records, final pool order, Removals rows
-  uint32_t fbase = 0, rbase = 0, nobs = 0;
-  uint32_t po[2];
+  // ---- 6. (not FRESH) player records, final pool order, Removals rows
+  uint32_t fbase = f_nm, rbase = f_nr, nobs = f_nobs;
+  uint32_t po[2] = {NONE8, NONE8};
+  if (!FRESH) {
   {
     uint32_t cnt[2], st[2], moff[2], goff[2], prow[2], opos[2];
     bool act[2], cx[2];
@@ -748,21 +829,19 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const int64_t v = L.rows[L.rl[r < rbase ? r : 0u]][d];
     if (r < rbase && (int)d < D) (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
   }
+  }  // !FRESH
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
-  uint32_t best_q = NONE32;
   {
-    int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
+    if (!FRESH) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const uint32_t p = s * 64 + lane;
-      const uint32_t o = po[s];
-      const int64_t sc = L.esc[o != NONE8 ? o : (uint32_t)ESINK];
-      const int64_t id = (int64_t)L.htab[L.pslot[o != NONE8 ? p : (uint32_t)PSINK]];
-      const bool better = o != NONE8 && (best_q == NONE32 || sc < best_sc || (sc == best_sc && id < best_id));
-      best_q = better ? p : best_q;
-      best_sc = better ? sc : best_sc;
-      best_id = better ? id : best_id;
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t p = s * 64 + lane;
+        const uint32_t o = po[s];
+        const int64_t sc = L.esc[o != NONE8 ? o : (uint32_t)ESINK];
+        const int64_t id = (int64_t)L.htab[L.pslot[o != NONE8 ? p : (uint32_t)PSINK]];
+        min_cand(o != NONE8, sc, id, p);
+      }
     }
     const bool has = best_q != NONE32;
     if (ballot(has)) {
