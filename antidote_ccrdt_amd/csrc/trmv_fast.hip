@@ -542,10 +542,13 @@ __global__ __launch_bounds__(64) void trmv_fast_kernel(TrmvApplyArgs a) {
 // tier 0 = SMALL (all-LDS), tier 1 = LARGE (slabs in HBM)
 int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st) {
   if (n_work == 0) return CCRDT_OK;
-  if (tier == 0)
-    hipLaunchKernelGGL(trmv_fast_kernel<true>, dim3((unsigned)n_work), dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(trmv_fast_kernel<false>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  // tier 0 is trmv_wave.hip; this file's LDS variant is kept only as the
+  // reference formulation the wave kernel was derived from (not launched)
+  if (tier != 1) {
+    set_error("trmv_launch_fast: only the HBM-slab tier (1) is launched from here");
+    return CCRDT_EINVAL;
+  }
+  hipLaunchKernelGGL(trmv_fast_kernel<false>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   // (n_work is the grid: all keys for the first tier, a bound for later ones)
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
