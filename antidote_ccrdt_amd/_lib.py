@@ -111,6 +111,8 @@ SIGNATURES = {
     "ccrdt_trmv_fetch_extra": (INT, [P, C.POINTER(TrmvExtra)]),
     "ccrdt_trmv_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_trmv_key_sizes": (INT, [P, P, P, P, P]),
+    "ccrdt_trmv_replica_vc_device": (INT, [P, P]),
+    "ccrdt_trmv_extras_device": (INT, [P, P, I64, P]),
     "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),
@@ -144,6 +146,7 @@ SIGNATURES = {
     # ccrdt_gen.h
     "ccrdt_splitmix64": (U64, [U64]),
     "ccrdt_gen_trmv_count": (I64, [I64, U64, INT]),
+    "ccrdt_gen_corpus": (INT, [I64, I64, I64, U64, INT, P, P]),
     "ccrdt_gen_trmv": (INT, [I64, I64, INT, I64, I64, INT, INT, INT, INT, U64,
                              P, P, P, P, P, P, P]),
 }

@@ -29,6 +29,11 @@ int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st);
+int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
+                           hipStream_t st);
+int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
+                            const int64_t* ex_vc, uint64_t n_keys, int n_dc, int64_t* rows,
+                            int64_t cap, uint32_t* count, hipStream_t st);
 
 static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
 static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
@@ -465,6 +470,23 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   E.last_n_ops = n_ops;
   E.last_kernel_ms = kernel_ms;
   return CCRDT_OK;
+}
+
+int ccrdt_trmv_replica_vc_device(ccrdt_engine* e, int64_t* d_out) {
+  CCRDT_TRY(check_trmv(e));
+  if (!d_out) return CCRDT_EINVAL;
+  const TrmvBufs& b = e->trmv[e->cur];
+  return trmv_launch_replica_vc(e->fresh ? nullptr : b.vc.as<int64_t>(), (uint64_t)e->n_keys,
+                                e->n_dc, d_out, e->stream);
+}
+
+int ccrdt_trmv_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, uint32_t* d_count) {
+  CCRDT_TRY(check_trmv(e));
+  if (!d_rows || !d_count || cap_rows < 0) return CCRDT_EINVAL;
+  const bool have = e->last_n_ops > 0 && e->ex_cnt.p;
+  return trmv_launch_pack_extras(e->ex_key_ptr.as<uint64_t>(), have ? e->ex_cnt.as<uint32_t>() : nullptr,
+                                 e->ex.as<TrmvExtraRec>(), e->ex_vc.as<int64_t>(),
+                                 (uint64_t)e->n_keys, e->n_dc, d_rows, cap_rows, d_count, e->stream);
 }
 
 int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n) {

@@ -5,6 +5,7 @@
 // order the host batcher hands to ccrdt_*_apply).  This is input generation,
 // not a compute path of the engine.
 #include <algorithm>
+#include <thread>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -145,3 +146,79 @@ int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, i
 }
 
 }  // extern "C"
+
+namespace {
+// Walker alias table for O(1) Zipf(1) rank draws.
+struct Alias {
+  std::vector<double> prob;
+  std::vector<uint32_t> alias;
+  explicit Alias(int64_t n) : prob(n), alias(n) {
+    std::vector<double> w(n);
+    double sum = 0;
+    for (int64_t r = 0; r < n; ++r) sum += (w[r] = 1.0 / (double)(r + 1));
+    std::vector<int64_t> small, large;
+    for (int64_t r = 0; r < n; ++r) {
+      prob[r] = w[r] * (double)n / sum;
+      (prob[r] < 1.0 ? small : large).push_back(r);
+    }
+    while (!small.empty() && !large.empty()) {
+      const int64_t s = small.back(), l = large.back();
+      small.pop_back();
+      alias[s] = (uint32_t)l;
+      prob[l] -= 1.0 - prob[s];
+      if (prob[l] < 1.0) {
+        large.pop_back();
+        small.push_back(l);
+      }
+    }
+    for (int64_t r : small) prob[r] = 1.0;
+    for (int64_t r : large) prob[r] = 1.0;
+  }
+};
+}  // namespace
+
+extern "C" int ccrdt_gen_corpus(int64_t n_docs, int64_t doc_bytes, int64_t vocab, uint64_t seed,
+                                int threads, uint8_t* bytes, uint64_t* doc_off) {
+  if (n_docs < 0 || doc_bytes < 0 || vocab < 1 || vocab > (int64_t)0xFFFFFFFF || !doc_off ||
+      (n_docs * doc_bytes > 0 && !bytes))
+    return CCRDT_EINVAL;
+  // vocabulary: word r = 1..12 lowercase letters from its hash
+  std::vector<uint64_t> woff(vocab + 1);
+  std::vector<uint8_t> wchars;
+  wchars.reserve((size_t)vocab * 7);
+  for (int64_t r = 0; r < vocab; ++r) {
+    woff[r] = wchars.size();
+    uint64_t x = splitmix64(seed ^ (0xC0FFEEull + (uint64_t)r * 0x9E3779B97F4A7C15ull));
+    const int len = 1 + (int)(x % 12);
+    for (int c = 0; c < len; ++c) {
+      x = splitmix64(x);
+      wchars.push_back((uint8_t)('a' + x % 26));
+    }
+  }
+  woff[vocab] = wchars.size();
+  const Alias al(vocab);
+  for (int64_t d = 0; d <= n_docs; ++d) doc_off[d] = (uint64_t)(d * doc_bytes);
+  if (threads < 1) threads = 1;
+  auto work = [&](int t) {
+    for (int64_t d = t; d < n_docs; d += threads) {
+      uint8_t* out = bytes + d * doc_bytes;
+      uint64_t x = splitmix64(seed * 0x100000001B3ull + (uint64_t)d);
+      int64_t pos = 0;
+      while (pos < doc_bytes) {
+        x = splitmix64(x);
+        const uint64_t i = x % (uint64_t)vocab;
+        const double u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
+        const uint64_t r = u < al.prob[i] ? i : al.alias[i];
+        for (uint64_t c = woff[r]; c < woff[r + 1] && pos < doc_bytes; ++c) out[pos++] = wchars[c];
+        x = splitmix64(x);
+        if (pos < doc_bytes) out[pos++] = (x % 12 == 0) ? (uint8_t)'\n' : (uint8_t)' ';
+        if (pos < doc_bytes && (x >> 32) % 100 == 0) out[pos++] = (uint8_t)' ';
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  return CCRDT_OK;
+}

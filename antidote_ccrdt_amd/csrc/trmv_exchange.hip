@@ -1,0 +1,91 @@
+// trmv_exchange.hip — device side of the two per-batch exchange steps of the
+// key-sharded topk_rmv cluster; the collectives themselves are
+// RCCL calls of the host (bench.py, cluster.py).
+//
+//  * replica Vc: the elementwise max of every key's Vc on this shard, the
+//    dense-vector form of merge_vcs/2 (src/antidote_ccrdt_topk_rmv.erl:378-386),
+//    so that a MAX all-reduce over the shards gives the replica-wide Vc;
+//  * extra effects: the {ok, S, [Effect]} effects of the last batch
+//    (:236-237, :294-295) packed as int64 rows [op, kind, id, score, dc, ts,
+//    vc[0..n_dc)] for the all-gather; rows come out grouped by key (the
+//    receiver orders them by op, which is unique).
+#include <algorithm>
+
+#include "common.hpp"
+#include "trmv_kernels.hpp"
+
+namespace ccrdt {
+
+__global__ __launch_bounds__(256) void trmv_replica_vc_kernel(const int64_t* vc, uint64_t n_keys,
+                                                              int n_dc, unsigned long long* out) {
+  __shared__ unsigned long long m[TRMV_DPAD];
+  if (threadIdx.x < TRMV_DPAD) m[threadIdx.x] = 0ull;
+  __syncthreads();
+  unsigned long long loc[TRMV_DPAD] = {};
+  // Vc entries are >= 0 (0 = absent), so unsigned max is the int64 max
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_keys * (uint64_t)n_dc;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = (unsigned long long)vc[i];
+    const int d = (int)(i % (uint64_t)n_dc);
+#pragma unroll
+    for (int k = 0; k < TRMV_DPAD; ++k) loc[k] = (k == d && v > loc[k]) ? v : loc[k];
+  }
+#pragma unroll
+  for (int k = 0; k < TRMV_DPAD; ++k)
+    if (k < n_dc && loc[k]) atomicMax(&m[k], loc[k]);
+  __syncthreads();
+  if ((int)threadIdx.x < n_dc && m[threadIdx.x]) atomicMax(&out[threadIdx.x], m[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void trmv_pack_extras_kernel(const uint64_t* key_ptr,
+                                                               const uint32_t* ex_cnt,
+                                                               const TrmvExtraRec* ex,
+                                                               const int64_t* ex_vc, uint64_t n_keys,
+                                                               int n_dc, int64_t* rows, int64_t cap,
+                                                               uint32_t* count) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = k < n_keys ? ex_cnt[k] : 0u;
+  if (c == 0) return;
+  const uint32_t pos = atomicAdd(count, c);
+  const uint64_t op0 = key_ptr[k];
+  const int w = 6 + n_dc;
+  for (uint32_t j = 0; j < c; ++j) {
+    const int64_t r = (int64_t)pos + j;
+    if (r >= cap) break;
+    const TrmvExtraRec e = ex[op0 + j];
+    int64_t* row = rows + r * w;
+    row[0] = e.op;
+    row[1] = e.kind;
+    row[2] = e.id;
+    row[3] = e.score;
+    row[4] = e.dc;
+    row[5] = e.ts;
+    for (int d = 0; d < n_dc; ++d)
+      row[6 + d] = e.kind == CCRDT_TRMV_RMV ? ex_vc[(op0 + j) * n_dc + d] : 0;
+  }
+}
+
+int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
+                           hipStream_t st) {
+  CCRDT_HIP(hipMemsetAsync(out, 0, (size_t)n_dc * 8, st));
+  if (n_keys == 0 || !vc) return CCRDT_OK;
+  const uint64_t n = n_keys * (uint64_t)n_dc;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(trmv_replica_vc_kernel, dim3(blocks), dim3(256), 0, st, vc, n_keys, n_dc,
+                     (unsigned long long*)out);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
+                            const int64_t* ex_vc, uint64_t n_keys, int n_dc, int64_t* rows,
+                            int64_t cap, uint32_t* count, hipStream_t st) {
+  CCRDT_HIP(hipMemsetAsync(count, 0, 4, st));
+  if (n_keys == 0 || !ex_cnt) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_pack_extras_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0,
+                     st, key_ptr, ex_cnt, ex, ex_vc, n_keys, n_dc, rows, cap, count);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+}  // namespace ccrdt

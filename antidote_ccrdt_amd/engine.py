@@ -277,6 +277,15 @@ class TopkRmvEngine(_Engine):
         check(lib.ccrdt_trmv_state_sizes(self.h, C.byref(a), C.byref(b), C.byref(c)), "sizes")
         return int(a.value), int(b.value), int(c.value)
 
+    def replica_vc_device(self, d_out: int) -> None:
+        """Enqueue the shard's elementwise-max Vc into device int64[n_dc] at d_out."""
+        check(lib.ccrdt_trmv_replica_vc_device(self.h, d_out), "replica_vc_device")
+
+    def extras_device(self, d_rows: int, cap_rows: int, d_count: int) -> None:
+        """Enqueue the last apply's extras as device int64 rows [cap, 6 + n_dc]
+        (op, kind, id, score, dc, ts, vc...) and their count (device uint32)."""
+        check(lib.ccrdt_trmv_extras_device(self.h, d_rows, cap_rows, d_count), "extras_device")
+
     def key_sizes(self) -> dict:
         """Per-key (players, masked, rows, observed) counts of the resident state."""
         out = {k: np.zeros(self.n_keys, np.uint32) for k in ("np", "nm", "nr", "nobs")}

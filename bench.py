@@ -39,7 +39,75 @@ def parse():
     ap.add_argument("--cpu-sample-keys", type=int, default=1 << 18,
                     help="keys of the batch the CPU baseline replays (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "trmv_pmc.json"))
+    ap.add_argument("--dist-backend", default=None,
+                    help="N > 1: nccl (RCCL, default on GPUs) or gloo (host-staged; tests)")
     return ap.parse_args()
+
+
+class Exchange:
+    """The two per-batch exchange steps of the key-sharded cluster (SURVEY
+    §8(e), cluster.py): the shard's extra effects are packed on the device and
+    all-gathered (every replica ends with the same effect list), and the
+    shard's elementwise-max Vc is MAX-all-reduced.  nccl = RCCL on device
+    tensors; gloo (tests on a one-GPU box) stages through the host."""
+
+    ROWS_CAP = 1 << 20  # extra effects per rank and batch (the bench stream makes ~46)
+
+    def __init__(self, eng, n_dc, world, backend, device, dist):
+        import numpy as np
+        import torch
+        from antidote_ccrdt_amd.engine import DeviceArray
+        self.eng, self.world, self.dist, self.np, self.torch = eng, world, dist, np, torch
+        self.w = 6 + n_dc
+        self.on_dev = backend == "nccl"
+        if self.on_dev:
+            dev = torch.device("cuda", device)
+            self.rows = torch.zeros((self.ROWS_CAP, self.w), dtype=torch.int64, device=dev)
+            self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.vc = torch.zeros(n_dc, dtype=torch.int64, device=dev)
+            self.p_rows, self.p_cnt, self.p_vc = (self.rows.data_ptr(), self.cnt.data_ptr(),
+                                                  self.vc.data_ptr())
+        else:
+            self.d_rows = DeviceArray(np.zeros((self.ROWS_CAP, self.w), np.int64))
+            self.d_cnt = DeviceArray(np.zeros(1, np.int32))
+            self.d_vc = DeviceArray(np.zeros(n_dc, np.int64))
+            self.p_rows, self.p_cnt, self.p_vc = self.d_rows.p, self.d_cnt.p, self.d_vc.p
+            self.h_cnt, self.h_vc = np.zeros(1, np.int32), np.zeros(n_dc, np.int64)
+        self.n_gathered = 0
+        self.replica_vc = None
+
+    def _d2h(self, host, dptr, nbytes):
+        from antidote_ccrdt_amd import _lib
+        _lib.check(_lib.lib.ccrdt_memcpy_d2h(_lib.ptr(host), dptr, nbytes), "d2h")
+
+    def run(self):
+        torch, dist = self.torch, self.dist
+        self.eng.extras_device(self.p_rows, self.ROWS_CAP, self.p_cnt)
+        self.eng.replica_vc_device(self.p_vc)
+        self.eng.sync()
+        if self.on_dev:
+            cnt, vc = self.cnt, self.vc
+        else:
+            self._d2h(self.h_cnt, self.p_cnt, 4)
+            self._d2h(self.h_vc, self.p_vc, self.h_vc.nbytes)
+            cnt, vc = torch.from_numpy(self.h_cnt), torch.from_numpy(self.h_vc)
+        dist.all_reduce(vc, op=dist.ReduceOp.MAX)
+        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt)
+        m = max(int(c.item()) for c in counts)
+        if m > self.ROWS_CAP:
+            raise RuntimeError(f"bench exchange: {m} extra effects > {self.ROWS_CAP} rows")
+        m = max(m, 1)
+        if self.on_dev:
+            mine = self.rows[:m]
+        else:
+            h = self.np.zeros((m, self.w), self.np.int64)
+            self._d2h(h, self.p_rows, h.nbytes)
+            mine = torch.from_numpy(h)
+        outs = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(outs, mine)
+        self.n_gathered = sum(int(c.item()) for c in counts)
+        self.replica_vc = vc
 
 
 def cpu_model():
@@ -62,13 +130,18 @@ def main():
     from antidote_ccrdt_amd import _lib
     from antidote_ccrdt_amd.engine import (DeviceTrmvBatch, TopkRmvEngine, TrmvBatch, gen_trmv,
                                            trmv_algorithmic_bytes)
+    # one process per GPU (on a box with fewer GPUs than ranks, ranks share)
+    device = local % max(1, _lib.device_count())
+    _lib.check(_lib.lib.ccrdt_set_device(device), "set_device")
     dist = None
+    backend = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        # gloo on the host: barrier + max-over-ranks timing only (the apply
-        # step has no data-path collective; keys are sharded).
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        backend = args.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(device)  # RCCL over xGMI
+        dist.init_process_group(backend, rank=rank, world_size=world)
 
     def barrier():
         if dist is not None:
@@ -80,11 +153,14 @@ def main():
                  lag_max=64, seed=seed)
     t_gen = time.perf_counter() - t_gen
     db = DeviceTrmvBatch(b)
-    eng = TopkRmvEngine(args.n_keys, args.k, args.n_dc, device=local)
+    eng = TopkRmvEngine(args.n_keys, args.k, args.n_dc, device=device)
+    xchg = Exchange(eng, args.n_dc, world, backend, device, dist) if world > 1 else None
 
     def step():
         eng.reset()            # every key back to new(K): O(1), no traffic
         eng.apply_device(db)   # scan -> apply kernel(s) -> status
+        if xchg is not None:   # the batch's two exchange steps
+            xchg.run()
 
     for _ in range(args.warmup):
         step()
@@ -99,7 +175,8 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device=torch.device("cuda", device) if backend == "nccl" else None)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1000.0 / args.steps
@@ -185,7 +262,8 @@ def main():
                             f"players/key, score U[1,1e6], rmv lag U[0,64)) CSR-grouped over "
                             f"{args.n_keys} fresh keys per GPU, ops resident in HBM",
                 "n_ops_per_gpu": args.n_ops, "n_keys_per_gpu": args.n_keys, "K": args.k,
-                "n_dc": args.n_dc, "parallelism": f"key-sharded x{world}",
+                "n_dc": args.n_dc,
+                "parallelism": f"key-sharded x{world}" + (f", {backend} exchange per step" if world > 1 else ""),
                 "seed": "0xCC0DE+2 (+1000003*rank)",
             },
             "roofline": {
@@ -209,6 +287,10 @@ def main():
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),
+                "exchange": (None if xchg is None else
+                             {"backend": backend, "extras_all_gathered": xchg.n_gathered,
+                              "replica_vc": [int(v) for v in xchg.replica_vc.cpu().tolist()],
+                              "in_step": "extras pack + all_gather, Vc max + all_reduce"}),
             },
         }
         print(json.dumps(out), flush=True)

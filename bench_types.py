@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench_types.py — the secondary kernels of SURVEY §8 on one MI355X.
+
+One JSON line per workload (BASELINE.json configs; inputs resident in HBM,
+one step = reset + one apply of the whole batch, HIP-event kernel time on the
+engine stream):
+
+  topk         100M add ops over 2^20 keys (id U[0,1000), score U[1,1e6])    configs[1]
+  topk_value   value/1 of every key of that state (segmented full sort)
+  leaderboard  50M ops over 100k boards, 99% add / 1% ban, K=100               configs[3]
+  wordcount    8 GiB Zipf corpus (8192 docs of 1 MiB, 1M-word vocabulary)  configs[4] / 8 GPUs
+  wdc          worddocumentcount on the same corpus
+  average      1M adds over 10k keys                                        configs[0]
+
+Each line carries a `roofline` object (algorithmic bytes per launch / kernel
+time vs 8 TB/s).  Algorithmic bytes: ops in + final state out, counted from
+the engine's own state sizes.  The main metric line is
+bench.py; this file is the measurement record of the other §8 rows.
+
+    python bench_types.py [--types topk,leaderboard,...] [--steps K --warmup W] [--corpus-gib G]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def csr_counts(rng, n_ops, n_keys):
+    """key_ptr of n_ops ops spread uniformly over n_keys keys (multinomial)."""
+    counts = rng.multinomial(n_ops, np.full(n_keys, 1.0 / n_keys))
+    kp = np.zeros(n_keys + 1, np.uint64)
+    np.cumsum(counts, out=kp[1:])
+    return kp
+
+
+def timed(eng, step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(steps):
+        step()
+        kms.append(eng.last_kernel_ms())
+    eng.sync()
+    return (time.perf_counter() - t0) * 1000.0 / steps, sum(kms) / len(kms)
+
+
+def line(name, config, units, unit_name, ms_step, kernel_ms, alg_bytes, extra=None):
+    ach = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    out = {"workload": name, "config": config, "value": units / (ms_step * 1e-3),
+           "unit": unit_name, "ms_per_step": ms_step, "higher_is_better": True,
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
+                        "kernel_ms": kernel_ms}}
+    if extra:
+        out["detail"] = extra
+    print(json.dumps(out), flush=True)
+
+
+def bench_topk(args, rng):
+    from antidote_ccrdt_amd.types import DeviceBatch, TopkEngine
+    n, nk = args.topk_ops, 1 << 20
+    kp = csr_counts(rng, n, nk)
+    pid = rng.integers(0, 1000, n, dtype=np.int64)
+    sc = rng.integers(1, 10**6 + 1, n, dtype=np.int64)
+    d = DeviceBatch(n, key_ptr=kp, id=pid, score=sc)
+    eng = TopkEngine(nk, 100)
+
+    def step():
+        eng.reset()
+        eng.apply_device(d)
+    ms, kms = timed(eng, step, args.steps, args.warmup)
+    entries = eng.size()
+    alg = n * 16 + (nk + 1) * 8 + entries * 16 + nk * 8
+    line("topk", f"antidote_ccrdt_topk update/2: {n} add ops over {nk} keys, id U[0,1000), "
+         "score U[1,1e6], fresh keys, ops in HBM", n, "ops/s", ms, kms, alg,
+         {"entries": entries})
+    # value/1: full segmented sort of every key (Score desc, Id desc)
+    t = time.perf_counter()
+    p, i, s = eng.value()
+    vt = (time.perf_counter() - t) * 1000.0
+    vk = eng.last_kernel_ms()
+    line("topk_value", f"antidote_ccrdt_topk value/1 of all {nk} keys ({entries} entries), "
+         "host copy-out included in ms_per_step", entries, "entries/s", vt, vk, entries * 32 + nk * 16,
+         {"note": "kernel_ms = the sort kernels; ms_per_step includes the D2H copy of the result"})
+    d.close()
+
+
+def bench_leaderboard(args, rng):
+    from antidote_ccrdt_amd.types import DeviceBatch, LeaderboardEngine
+    n, nk = args.lb_ops, 100_000
+    kp = csr_counts(rng, n, nk)
+    ban = rng.random(n) < 0.01
+    kind = np.where(ban, 2, rng.integers(0, 2, n)).astype(np.uint8)
+    pid = rng.integers(0, 10**4, n, dtype=np.int64)
+    sc = rng.integers(0, 10**6 + 1, n, dtype=np.int64)
+    d = DeviceBatch(n, key_ptr=kp, kind=kind, id=pid, score=sc)
+    eng = LeaderboardEngine(nk, 100)
+
+    def step():
+        eng.reset()
+        eng.apply_device(d)
+    ms, kms = timed(eng, step, args.steps, args.warmup)
+    no, nm, nb = eng.sizes()
+    n_ban = int(ban.sum())
+    alg = (n - n_ban) * 17 + n_ban * 9 + (nk + 1) * 8 + (no + nm) * 16 + nb * 8 + nk * 16
+    line("leaderboard", f"antidote_ccrdt_leaderboard update/2: {n} ops over {nk} boards, 99% add / "
+         "1% ban, id U[0,1e4), score U[0,1e6], K=100, fresh boards, ops in HBM", n, "ops/s", ms, kms,
+         alg, {"observed": no, "masked": nm, "bans": nb})
+    d.close()
+
+
+def bench_wordcount(args, rng, wdc):
+    from antidote_ccrdt_amd import _lib
+    from antidote_ccrdt_amd.types import DeviceBatch, WordcountEngine, WordDocumentCountEngine
+    doc = 1 << 20
+    n_docs = int(args.corpus_gib * 1024)
+    key = ("wdc" if wdc else "wc")
+    if key not in CORPUS:
+        b = np.empty(n_docs * doc, np.uint8)
+        off = np.empty(n_docs + 1, np.uint64)
+        t = time.perf_counter()
+        _lib.check(_lib.lib.ccrdt_gen_corpus(n_docs, doc, 10**6, 0xCC0DE + 4, 16, _lib.ptr(b),
+                                             _lib.ptr(off)), "gen_corpus")
+        CORPUS["gen_s"] = time.perf_counter() - t
+        CORPUS["data"] = (b, off)
+    b, off = CORPUS["data"]
+    kp = np.array([0, n_docs], np.uint64)
+    d = DeviceBatch(n_docs, key_ptr=kp, doc_off=off, bytes=b)
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    eng = E(1)
+
+    def step():
+        eng.reset()
+        eng.apply_device(d, b.shape[0])
+    ms, kms = timed(eng, step, args.steps, args.warmup)
+    nw, nb = eng.sizes()
+    alg = b.shape[0] + (n_docs + 1) * 8 + nw * 24 + nb
+    name = "worddocumentcount" if wdc else "wordcount"
+    line("wdc" if wdc else "wordcount",
+         f"antidote_ccrdt_{name} update/2: {b.shape[0] / 2**30:.0f} GiB Zipf(1) corpus, {n_docs} docs "
+         "of 1 MiB, 1M-word vocabulary (1/8 of the 64 GB 8-GPU config), one object, corpus in HBM",
+         b.shape[0], "bytes/s", ms, kms, alg,
+         {"distinct_words": nw, "word_bytes": nb, "gen_s": round(CORPUS.get("gen_s", 0), 1)})
+    d.close()
+    del eng
+
+
+def bench_average(args, rng):
+    from antidote_ccrdt_amd.types import AverageEngine, DeviceBatch
+    n, nk = 1_000_000, 10_000
+    kp = csr_counts(rng, n, nk)
+    v = rng.integers(0, 1 << 20, n, dtype=np.int64)
+    nn = np.ones(n, np.int64)
+    d = DeviceBatch(n, key_ptr=kp, value=v, n=nn)
+    eng = AverageEngine(nk)
+
+    def step():
+        eng.reset()
+        eng.apply_device(d)
+    ms, kms = timed(eng, step, args.steps, args.warmup)
+    alg = n * 16 + (nk + 1) * 8 + nk * 16
+    line("average", f"antidote_ccrdt_average update/2: {n} adds over {nk} keys (V U[0,2^20), N=1), "
+         "ops in HBM", n, "ops/s", ms, kms, alg)
+    d.close()
+
+
+CORPUS = {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--types", default="topk,leaderboard,wordcount,wdc,average")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--topk-ops", type=int, default=100_000_000)
+    ap.add_argument("--lb-ops", type=int, default=50_000_000)
+    ap.add_argument("--corpus-gib", type=float, default=8.0)
+    args = ap.parse_args()
+    from antidote_ccrdt_amd import _lib
+    if _lib.device_count() < 1:
+        raise SystemExit("bench_types: no HIP device")
+    rng = np.random.default_rng(0xCC0DE + 1)
+    for t in args.types.split(","):
+        {"topk": bench_topk, "leaderboard": bench_leaderboard, "average": bench_average,
+         "wordcount": lambda a, r: bench_wordcount(a, r, False),
+         "wdc": lambda a, r: bench_wordcount(a, r, True)}[t](args, rng)
+
+
+if __name__ == "__main__":
+    main()

@@ -162,6 +162,19 @@ int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n);
 /* Copy the last apply's extra effects into op-indexed host arrays. */
 int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* extra);
 
+/* Device side of the cluster's two exchange steps (the
+ * collectives are the caller's, e.g. RCCL).  Both are enqueued on the engine
+ * stream (ccrdt_engine_stream) and do not wait.
+ * Replica Vc: d_out[n_dc] (device) := elementwise max of every key's Vc, the
+ * dense form of merge_vcs/2 (topk_rmv.erl:378-386); a MAX all-reduce of it
+ * over the shards is the replica-wide Vc. */
+int ccrdt_trmv_replica_vc_device(ccrdt_engine* e, int64_t* d_out);
+/* Extra effects of the last apply (topk_rmv.erl:236-237, :294-295) packed
+ * into device rows d_rows[cap_rows][6 + n_dc] = {op, kind, id, score, dc, ts,
+ * vc...}, grouped by key (order by op to get stream order); *d_count
+ * (device) = how many there were (rows past cap_rows are not written). */
+int ccrdt_trmv_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, uint32_t* d_count);
+
 /* Canonical state image (host arrays), used by export/import:
  *   vc[n_keys*n_dc]                                   replica Vc
  *   obs_ptr[n_keys+1], obs_{id,score,dc,ts}           Observed, sorted by id

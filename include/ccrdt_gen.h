@@ -21,6 +21,16 @@ int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, i
                    uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score, uint8_t* dc,
                    int64_t* ts, int64_t* rmv_vc);
 
+/* Synthetic Zipf text corpus (wordcount / worddocumentcount):
+ * a vocabulary of `vocab` lowercase words of length 1..12, word ranks drawn
+ * with Zipf(s = 1) frequencies, ' ' between words, '\n' instead after ~1 in
+ * 12 words, a doubled space after ~1 in 100 (empty tokens).  `n_docs`
+ * documents of `doc_bytes` bytes each (the last word of a document is cut at
+ * its end), written to bytes[n_docs * doc_bytes]; doc_off[n_docs + 1] gets
+ * the document offsets.  Deterministic in `seed` for any thread count. */
+int ccrdt_gen_corpus(int64_t n_docs, int64_t doc_bytes, int64_t vocab, uint64_t seed, int threads,
+                     uint8_t* bytes, uint64_t* doc_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -144,6 +144,42 @@ def test_invalid_ops_leave_state(gpu):
     assert not eng.export().diff(before)
 
 
+def test_exchange_device_side(gpu):
+    """Device halves of the cluster exchange: the packed extras equal the
+    op-indexed extras of the same apply, and the replica Vc equals the max of
+    every key's exported Vc."""
+    from antidote_ccrdt_amd.engine import DeviceArray
+    nk, D = 200, 8
+    b = gen_trmv(20000, nk, D, 12, 20, 150, 8, 50, 30, seed=5)  # churn: many extras
+    eng = TopkRmvEngine(nk, 4, D)
+    x = eng.apply(b)
+    want = np.nonzero(x.kind != 255)[0]
+    assert want.shape[0] > 10
+    cap = want.shape[0] + 5
+    rows = DeviceArray(np.zeros((cap, 6 + D), np.int64))
+    cnt = DeviceArray(np.zeros(1, np.uint32))
+    vc = DeviceArray(np.zeros(D, np.int64))
+    eng.extras_device(rows.p, cap, cnt.p)
+    eng.replica_vc_device(vc.p)
+    eng.sync()
+    h_rows = np.zeros((cap, 6 + D), np.int64)
+    h_cnt, h_vc = np.zeros(1, np.uint32), np.zeros(D, np.int64)
+    for h, d in ((h_rows, rows), (h_cnt, cnt), (h_vc, vc)):
+        _lib.check(_lib.lib.ccrdt_memcpy_d2h(_lib.ptr(h), d.p, h.nbytes), "d2h")
+    assert int(h_cnt[0]) == want.shape[0]
+    got = h_rows[: want.shape[0]]
+    got = got[np.argsort(got[:, 0])]
+    assert np.array_equal(got[:, 0], want)
+    assert np.array_equal(got[:, 1], x.kind[want])
+    assert np.array_equal(got[:, 2], x.id[want])
+    add = x.kind[want] == 0
+    assert np.array_equal(got[add, 3], x.score[want][add])
+    assert np.array_equal(got[add, 4], x.dc[want][add])
+    assert np.array_equal(got[add, 5], x.ts[want][add])
+    assert np.array_equal(got[~add, 6:], x.vc[want][~add])
+    assert np.array_equal(h_vc, eng.export().vc.max(axis=0))
+
+
 def test_empty_batch_and_reset(gpu):
     nk, D = 64, 8
     eng = TopkRmvEngine(nk, 100, D)

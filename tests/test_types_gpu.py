@@ -196,6 +196,23 @@ def test_wordcount_random(gpu, wdc):
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_generated_corpus(gpu, wdc):
+    """The bench corpus generator's text (Zipf words, '\\n', double spaces,
+    words cut at document ends), two keys, vs the oracle."""
+    n_docs, db = 12, 200_000
+    b, off = np.empty(n_docs * db, np.uint8), np.empty(n_docs + 1, np.uint64)
+    _lib.check(_lib.lib.ccrdt_gen_corpus(n_docs, db, 50_000, 99, 4, _lib.ptr(b), _lib.ptr(off)),
+               "gen_corpus")
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    e, o = E(2), orc.WcOracle(2, wdc)
+    kp = np.array([0, 5, n_docs], np.uint64)
+    e.apply(kp, off, b)
+    o.apply(kp, off, b)
+    for x, y in zip(e.export(), o.export()):
+        assert np.array_equal(x, y)
+
+
 def test_wordcount_lds_overflow_path(gpu):
     """A document with far more distinct words than the per-document LDS
     table (512) exercises the global path (and the wdc dedupe table)."""
