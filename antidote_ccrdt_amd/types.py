@@ -252,7 +252,7 @@ class WordDocumentCountEngine(WordcountEngine):
 class DeviceBatch:
     """Named device copies of numpy arrays (inputs resident in HBM)."""
 
-    def __init__(self, n: int, **arrays):
+    def __init__(self, n: int, /, **arrays):
         from .engine import DeviceArray
         self.n = n
         self.bufs = {k: DeviceArray(np.ascontiguousarray(v)) for k, v in arrays.items()}
