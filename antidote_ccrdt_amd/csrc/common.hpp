@@ -161,21 +161,29 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    int64_t o = shfl64(v, lane_id() ^ off);
-    v = o < v ? o : v;
-  }
-  return rl64(v, 0);
+// Wave maximum of an int64 (DPP, identity INT64_MIN), wave-uniform result.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int64_t dpp_max_step_i64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROWMASK, 0xf,
+                                                            false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(
+      (int)0x80000000, (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROWMASK, 0xf, false);
+  const int64_t o = (int64_t)(((uint64_t)hi << 32) | lo);
+  return o > v ? o : v;
 }
-__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    int64_t o = shfl64(v, lane_id() ^ off);
-    v = o > v ? o : v;
-  }
-  return rl64(v, 0);
+__device__ __forceinline__ int64_t wave_max_i64_dpp(int64_t v) {
+  v = dpp_max_step_i64<0x111, 0xf>(v);
+  v = dpp_max_step_i64<0x112, 0xf>(v);
+  v = dpp_max_step_i64<0x114, 0xf>(v);
+  v = dpp_max_step_i64<0x118, 0xf>(v);
+  v = dpp_max_step_i64<0x142, 0xa>(v);
+  v = dpp_max_step_i64<0x143, 0xc>(v);
+  return rl64(v, 63);
 }
+
+// Wave min / max over all 64 lanes (every lane active), wave-uniform result:
+// six DPP steps, no LDS-crossbar round trips on the reduction's latency chain.
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) { return wave_min_i64_dpp(v); }
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return wave_max_i64_dpp(v); }
 
 }  // namespace ccrdt

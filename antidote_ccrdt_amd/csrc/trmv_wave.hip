@@ -1,5 +1,5 @@
 // trmv_wave.hip — tier 0 of the topk_rmv apply: one wavefront per key, four
-// independent keys per 256-thread workgroup, ~6.3 KB of LDS per key.
+// independent keys per 256-thread workgroup, ~8.5 KB of LDS per key.
 //
 // Exactness argument: the per-player decomposition of trmv_fast.hip (P <= K
 // players => recompute_observed/5 never evicts, promotion candidates of rmv/3
@@ -7,14 +7,12 @@
 // :231-334).  Keys outside this tier's caps go to the next tier.
 //
 // What differs from the LDS tier of trmv_fast.hip is the mapping onto gfx950:
-//  * occupancy: LDS per key is cut to ~6.3 KB (elements are addressed by
-//    index, Masked slabs are u8 index lists, removal clocks are one shared
-//    table of 16 rows) and the kernel is held to <= 80 VGPRs, so six keys
-//    are resident per SIMD instead of three;
-//  * latency: every global load a key needs is issued before its first use
-//    (ops, old players, old rows), the removal clocks of the batch are
-//    fetched in one cooperative pass (8 lanes per clock row) while the hash
-//    table is built;
+//  * occupancy: elements are addressed by index, Masked slabs are u8 index
+//    lists, removal clocks are one shared table of 24 rows, so four keys fit
+//    per SIMD;
+//  * latency: every global load a key needs is issued before its first use:
+//    a key's ops, and then its removal clocks (8 lanes per clock row,
+//    coalesced), are loaded while the wave still works on the previous key;
 //  * no workgroup barriers: the four keys of a workgroup are independent and
 //    each wave orders its own LDS accesses (wave_lds_sync);
 //  * grouping: 64-bit LDS compare-and-swap on the Id itself (one probe loop,
@@ -22,20 +20,23 @@
 //    after the old ones), so the device layout is deterministic;
 //  * scans are DPP (wave_excl_scan_dpp), not LDS-crossbar shuffles;
 //  * each wave runs W_KPW consecutive keys and issues the next key's loads
-//    (bounds, metadata, ops) before the current key's write-out, so the
-//    first HBM round trip of a key overlaps the previous key's stores;
-//  * op elements are stored at their position in player order, so the replay
-//    reads an op with one LDS round trip;
-//  * players split into "simple" and "complex".  A simple player has only
-//    adds in the batch, no old state, and strictly increasing Ts across its
-//    adds (so no add can duplicate a Masked element): its Masked set is all
-//    its adds and Obs[Id] is the first add with the largest (Score, Ts) --
-//    recompute_observed/5's strict cmp/2 keeps the first arrival on a tie --
-//    which every op lane decides for itself by scanning its player's
-//    positions.  Only complex players (a rmv in the batch, old state, or a Ts
-//    that does not rise) are replayed op by op, one lane per player, packed
-//    into as few passes as there are 64-player groups.  Old state exists
-//    only when the engine is not fresh (template FRESH).
+//    (bounds, metadata, ops, clocks) before the current key's write-out, so
+//    the first HBM round trip of a key overlaps the previous key's stores;
+//  * op elements are stored at their position in player order, so every op
+//    lane reads its player's ops with one LDS round trip each;
+//  * players are decided op-parallel wherever the history allows it (step 5):
+//    every op lane scans its player's positions once.
+//    A player's rmvs cut its ops into segments.  When (a) no add is dominated
+//    by an earlier rmv, (b) every add that has a later rmv is removed by the
+//    first of them, and (c) the adds after the last rmv have strictly
+//    increasing Ts, every rmv empties Masked[Id] and drops the Id from
+//    Observed without a promotion, so Masked[Id] is the last segment, Obs[Id]
+//    its first add with the largest (Score, Ts) (recompute_observed/5's
+//    strict cmp/2 keeps the first arrival on a tie), Removals[Id] the
+//    elementwise max of its rmv clocks, and the player emits no extra effect.
+//    A player without rmvs is the case of one segment.  Only the players that
+//    fail a test (and, outside FRESH, every player with old state or a rmv)
+//    are replayed op by op, one lane per player.
 //
 // Element index space of a key: [0, nops) = this batch's ops, grouped by player
 // (stream order inside a player), [nops, nops + old |Masked|) = the key's old
@@ -89,7 +90,7 @@ struct alignas(16) WaveLds {
   int64_t rows[W_RCAP][TRMV_DPAD];       // [0, old nr) old Removals rows, then rmv clocks
   unsigned long long vc[TRMV_DPAD + 2];  // replica Vc; [TRMV_DPAD] sink
   uint32_t pcnt2[W_PCAP / 2 + 4];        // ops per player (two u16 counters per word)
-  uint32_t rsrc[W_RCAP + 4];             // rmv_vc row of each staged rmv clock
+  uint32_t rsrc[W_RCAP + 4];             // rmv_vc row of each rmv op of the key being prefetched
   uint16_t ekd[W_ECAP + 8];              // kind | dc << 2 | player << 8
   uint8_t hp[W_HCAP];                    // hash slot -> player
   uint8_t pslot[W_PCAP + 8];             // player -> hash slot
@@ -98,12 +99,13 @@ struct alignas(16) WaveLds {
   uint8_t fin[W_ECAP + 8];               // final pool: element of every output position
   uint8_t pstart[W_PCAP + 8];            // first position of each player's ops
   uint8_t pobs[W_PCAP + 8];              // Obs[Id] of each player (element), NONE8 = none
-  uint8_t pflag[W_PCAP + 8];             // 1 = complex player (op-by-op replay)
-  uint8_t pcntf[W_PCAP + 8];             // complex player: final |Masked[Id]|
-  uint8_t pmoff[W_PCAP + 8];             // complex player: its working slab in `slab`
-  uint8_t prow[W_PCAP + 8];              // complex player: its clock row or NONE8
+  uint8_t pflag[W_PCAP + 8];             // 1 = player replayed op by op
+  uint8_t pcntf[W_PCAP + 8];             // replayed player: final |Masked[Id]|
+  uint8_t pmoff[W_PCAP + 8];             // replayed player: its working slab in `slab`
+  uint8_t prow[W_PCAP + 8];              // the player's clock row (Removals[Id]) or NONE8
+  uint8_t plr[W_PCAP + 8];               // FRESH: 1 + position of the player's last rmv, 0 = none
   uint8_t peb[W_PCAP + 8];               // old player: first element of its old slab
-  uint8_t cpl[W_PCAP + 8];               // complex players, packed
+  uint8_t cpl[W_PCAP + 8];               // replayed players, packed
   uint8_t rl[W_RCAP + 8];                // clock row of each output Removals row
   uint32_t nex;                          // extra effects emitted by the key
 };
@@ -135,13 +137,15 @@ __device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, WaveLds& L, ui
     for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
 }
 
-// What a key needs before anything else: bounds, new-side metadata, its ops.
+// What a key needs before anything else: bounds, new-side metadata, its ops,
+// and the removal clocks of its rmv ops.
 struct KeyIn {
   uint64_t op0;
   uint32_t nops;
   KeyMeta nmeta;
   int64_t id[2], sc[2], ts[2];
   uint32_t kind[2], dc[2];  // kept apart: combining them would force a wait at the load
+  int64_t rv[W_RCAP / 8];   // clock of the (lane/8 + 8s)-th rmv op, entry lane%8
 };
 
 // Bounds and new-side metadata of a wave's W_KPW keys, loaded once per chunk
@@ -193,9 +197,41 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
   }
 }
 
+// Issue the loads of a key's removal clocks (rmv ops in stream order, 8 lanes
+// per clock row, coalesced) once its ops are in registers; they are consumed
+// after the key's hash build.  A row outside [0, n_rmv_rows) reads row 0: the
+// key's validation rejects the batch before any value is used.
+__device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, WaveLds& L, KeyIn& in) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int s = 0; s < W_RCAP / 8; ++s) in.rv[s] = 0;
+  bool r[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    r[s] = (uint32_t)(s * 64 + lane) < in.nops && (in.kind[s] == 2 || in.kind[s] == 3);
+  const uint64_t b0 = ballot(r[0]), b1 = ballot(r[1]);
+  const uint32_t n0 = (uint32_t)__builtin_popcountll(b0);
+  const uint32_t n = n0 + (uint32_t)__builtin_popcountll(b1);
+  if (n == 0 || a.n_rmv_rows <= 0) return;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t k = s ? n0 + mbcnt(b1) : mbcnt(b0);
+    if (r[s] && k < (uint32_t)W_RCAP)
+      L.rsrc[k] = (in.ts[s] >= 0 && in.ts[s] < a.n_rmv_rows) ? (uint32_t)in.ts[s] : 0u;
+  }
+  wave_lds_sync();
+  const uint32_t d = (lane & 7) < a.n_dc ? (lane & 7) : 0u;
+#pragma unroll
+  for (int s = 0; s < W_RCAP / 8; ++s) {
+    const uint32_t k = s * 8 + (lane >> 3);
+    const uint32_t row = k < n ? L.rsrc[k] : 0u;
+    in.rv[s] = a.rmv_vc[(uint64_t)row * a.n_dc + d];
+  }
+  wave_lds_sync();  // rsrc is rewritten for the next key
+}
+
 // Outcome of one key.  Only W_DONE has already issued the loads of the wave's
-// next key (just before the write-out); the rare other paths leave that to the
-// caller, which keeps the prefetched registers out of the early phases.
+// next key; the rare other paths leave that to the caller.
 enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2, W_SIDE = 3 };
 
 template <bool FRESH>
@@ -254,6 +290,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   reinterpret_cast<uint32_t*>(L.hp)[lane] = 0xFFFFFFFFu;  // 256 B
   L.pcnt2[lane] = 0u;
   if (lane < W_PCAP / 4) reinterpret_cast<uint32_t*>(L.pflag)[lane] = 0u;
+  if (FRESH && lane < (W_PCAP + 8) / 4) {  // step 5's per-player results
+    reinterpret_cast<uint32_t*>(L.pobs)[lane] = 0xFFFFFFFFu;
+    reinterpret_cast<uint32_t*>(L.prow)[lane] = 0xFFFFFFFFu;
+    reinterpret_cast<uint32_t*>(L.plr)[lane] = 0u;
+  }
   if (lane < TRMV_DPAD)
     L.vc[lane] = (!FRESH && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
   if (!FRESH) {  // old Removals rows -> clock rows [0, om.nr)
@@ -265,7 +306,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
 
   PROF_MARK(0);
-  // ---- 2. validate ops (predicated), rank the rmv ops, issue their clock loads
+  // ---- 2. validate ops (predicated), rank the rmv ops
   uint32_t err = 0;
   bool xr[2], xa[2];
 #pragma unroll
@@ -286,10 +327,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   const uint32_t nrmv = nr0 + (uint32_t)__builtin_popcountll(rb1);
   if (om.nr + nrmv > (uint32_t)W_RCAP) return W_NEXT_TIER;
   {
+    // a rmv's "score": its clock row (the order wave_load_rows staged them in)
     const uint32_t r0 = mbcnt(rb0), r1 = nr0 + mbcnt(rb1);
-    if (xr[0]) L.rsrc[r0] = (uint32_t)xts[0];
-    if (xr[1]) L.rsrc[r1] = (uint32_t)xts[1];
-    xsc[0] = xr[0] ? (int64_t)(om.nr + r0) : xsc[0];  // a rmv's "score": its clock row
+    xsc[0] = xr[0] ? (int64_t)(om.nr + r0) : xsc[0];
     xsc[1] = xr[1] ? (int64_t)(om.nr + r1) : xsc[1];
   }
   wave_lds_sync();
@@ -309,18 +349,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     bad |= pend[j] && (unsigned long long)hid[j] == W_EMPTY;
   }
   if (ballot(bad)) return W_NEXT_TIER;
-  // rmv clocks: 8 lanes per row, coalesced (in flight during the hash build)
-  // (raw values: masked only where they are written, after the hash build,
-  // so no use forces an early wait)
-  int64_t rv[W_RCAP / 8] = {};
-  if (nrmv) {
-    const uint32_t rw[W_RCAP / 8] = {L.rsrc[(lane >> 3) < (int)nrmv ? (lane >> 3) : 0],
-                                     L.rsrc[8 + (lane >> 3) < (int)nrmv ? 8 + (lane >> 3) : 0],
-                                     L.rsrc[16 + (lane >> 3) < (int)nrmv ? 16 + (lane >> 3) : 0]};
-    const uint32_t d = (lane & 7) < D ? (lane & 7) : 0u;
-#pragma unroll
-    for (int s = 0; s < W_RCAP / 8; ++s) rv[s] = a.rmv_vc[(uint64_t)rw[s] * D + d];
-  }
 
   PROF_MARK(1);
   // ---- 3. hash build: ops, then old players (64-bit CAS on the Id)
@@ -342,11 +370,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       pend[j] = pend[j] && !done;
     }
   }
-  // write the staged rmv clocks (loads were in flight during the build)
+  // write the rmv clocks (their loads were issued with the key's ops)
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
     const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    const int64_t v = (int)d < D ? rv[s] : 0;
+    const int64_t v = (int)d < D ? in.rv[s] : 0;
     err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
     if (r < nrmv) L.rows[om.nr + r][d] = v;
   }
@@ -397,6 +425,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (n3) L.pslot[i3] = (uint8_t)(lane * 4 + 3);
   }
   wave_lds_sync();
+  // the next key's op loads go out here, after the last early return: they
+  // land during steps 4-5; the explicit wait before this key's stores
+  // retires them, so the next key never waits on (and its vmcnt never
+  // counts) this key's stores
+  if (has_next) wave_load_key(a, hdr, nj, nxt);
 
   PROF_MARK(2);
   // ---- 4. player of every op, Vc, op elements in player order
@@ -406,7 +439,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const uint32_t p = xv[s] ? (uint32_t)L.hp[hs[s]] : PSINK;
     xp[s] = p;
     if (xa[s]) atomicMax(&L.vc[xdc[s]], (unsigned long long)xts[s]);  // vc_update (:233)
-    if (xr[s]) L.pflag[p] = 1;                                        // a rmv: complex player
+    if (!FRESH && xr[s]) L.pflag[p] = 1;                              // a rmv: replayed
     const uint32_t sh = 16 * (p & 1);
     xrank[s] = 0;
     if (xv[s]) xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
@@ -491,7 +524,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       ebase += tot;
       if (p < om.np) {
         L.peb[p] = (uint8_t)eb;
-        L.pflag[p] = 1;  // old state: complex player
+        L.pflag[p] = 1;  // old state: replayed
       }
       for (uint32_t j = 0; j < oc; ++j) {
         const uint32_t go = (pslab[s] & 0xFFFFu) + j;
@@ -505,13 +538,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
 
   PROF_MARK(3);
-  // the next key's loads land during the replay; the explicit wait below
-  // retires them before this key's stores, so the next key never waits on
-  // (and its vmcnt never counts) this key's stores
-  if (has_next) wave_load_key(a, hdr, nj, nxt);
-  // ---- 5a. simple players, op-parallel: each add decides whether it is its
-  // player's Obs[Id] and whether its Ts rises over every earlier add's
-  {
+  if (!FRESH) {
+    // ---- 5a. players without rmv or old state, op-parallel: each add
+    // decides whether it is its player's Obs[Id] and whether its Ts rises
+    // over every earlier add's
     bool simple[2], beaten[2] = {false, false}, risk[2] = {false, false};
     uint32_t me[2], cl[2];
 #pragma unroll
@@ -538,11 +568,65 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       if (risk[s]) L.pflag[xp[s]] = 1;
       if (simple[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
     }
+    wave_lds_sync();
+  } else {
+    // ---- 5. every op lane scans its player's positions once (header: tests
+    // (a)-(c)).  A rmv at a position ends the segments before it, so the
+    // Obs/Ts bookkeeping restarts there and ends with the last segment's.
+    bool fb[2] = {false, false}, beaten[2] = {false, false}, risk[2] = {false, false};
+    bool seen[2] = {false, false}, first[2] = {true, true};
+    uint32_t me[2], cl[2], adc[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      me[s] = xq[s] - xst[s];
+      cl[s] = xv[s] ? xc[s] : 0u;
+      adc[s] = xa[s] ? xdc[s] : 0u;
+    }
+    const uint32_t maxc = wave_max_u32_dpp(cl[0] > cl[1] ? cl[0] : cl[1]);
+    for (uint32_t x = 0; x < maxc; ++x) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bool valid = x < cl[s] && x != me[s];
+        const uint32_t pos = x < cl[s] ? xst[s] + x : (uint32_t)ESINK;
+        const int64_t sx = L.esc[pos], tx = L.ets[pos];
+        const bool isr = valid && (L.ekd[pos] & 2u) != 0;
+        const bool before = x < me[s];
+        const bool need = xa[s] && isr && (before || !seen[s]);
+        const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc[s]];
+        const int64_t sm = xsc[s], tm = xts[s];
+        fb[s] |= need && (before ? rt >= tm : rt < tm);
+        seen[s] |= isr && !before;
+        first[s] &= !(isr && before);
+        risk[s] = risk[s] && !isr;
+        beaten[s] = beaten[s] && !isr;
+        const bool both = xa[s] && valid && !isr;
+        risk[s] |= both && before && tx >= tm;
+        beaten[s] |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (xv[s] && (fb[s] || risk[s])) L.pflag[xp[s]] = 1;
+      if (xa[s] && !seen[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
+      if (xr[s] && first[s]) L.prow[xp[s]] = (uint8_t)xsc[s];
+      if (xr[s] && !seen[s]) L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
+    }
+    wave_lds_sync();
+    // Removals[Id]: the player's later rmv clocks merge into its first rmv's
+    // row (merge_vc, :369-386); replayed players merge their own
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (xr[s] && !first[s] && !L.pflag[xp[s]]) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(L.rows[L.prow[xp[s]]]);
+        const int64_t* src = L.rows[(uint32_t)xsc[s]];
+        for (int d = 0; d < D; ++d) atomicMax(dst + d, (unsigned long long)src[d]);
+      }
+    }
+    wave_lds_sync();
   }
-  wave_lds_sync();
 
   PROF_MARK(6);
-  // ---- 5b. complex players, one lane per player, replayed op by op
+  // ---- 5b. replayed players, one lane per player, op by op
   uint32_t ncx;
   {
     const bool c0 = (uint32_t)lane < np && L.pflag[lane];
@@ -554,14 +638,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (c1) L.cpl[n0 + mbcnt(m1)] = (uint8_t)(64 + lane);
   }
   wave_lds_sync();
-  // FRESH: every player's Masked slab lives at its own op positions
-  // [pstart, pstart + |Masked[Id]|) of the key's pool segment (|Masked[Id]|
-  // <= its adds), so no pool order has to be built: simple players' elements
-  // are written by their op lanes, complex players' by their replay lanes.
-  // The next key's ops (issued at 5a) are retired before this key's first
-  // store, so the next key never waits on (and its vmcnt never counts) them.
+  // The next key's ops are retired before this key's first store, so the
+  // next key never waits on (and its vmcnt never counts) these stores.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  uint32_t f_nm = 0, f_nobs = 0, f_nr = 0;       // FRESH totals (wave-uniform)
+  PROF_MARK(7);
   uint32_t best_q = NONE32;                      // Min candidate of this lane
   int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
   auto min_cand = [&](bool has, int64_t sc, int64_t id, uint32_t p) {
@@ -571,8 +651,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     best_id = better ? id : best_id;
   };
   if (FRESH) {
-    // every op position as if its player were simple (coalesced); complex
-    // players rewrite their own ranges below, in program order after these
+    // FRESH: every player's Masked slab lives inside its own op positions
+    // [pstart, pstart + ops) of the key's pool segment (|Masked[Id]| <= its
+    // adds), so no pool order has to be built: every op position is written
+    // as its op's element (coalesced); replayed players rewrite their own
+    // ranges below, in program order after these
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t q = s * 64 + lane;
@@ -583,18 +666,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         (a.new_s.m_score + nmeta.m_off)[q] = sc;
         (a.new_s.m_ts + nmeta.m_off)[q] = ts;
         (a.new_s.m_dc + nmeta.m_off)[q] = (uint8_t)((kd >> 2) & 7u);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const uint32_t p = s * 64 + lane;
-      const uint32_t pp = p < np ? p : (uint32_t)PSINK;
-      const uint32_t st = L.pstart[pp], c = pcnt_of(L, pp), o = L.pobs[pp];
-      const int64_t id = (int64_t)L.htab[L.pslot[pp]];
-      if (p < np) {  // (complex players' records are rewritten below)
-        (a.new_s.pl_id + nmeta.p_off)[p] = id;
-        (a.new_s.pl_slab + nmeta.p_off)[p] = st | (c << 16);
-        (a.new_s.pl_info + nmeta.p_off)[p] = (o - st) | (NONE16 << 16);
       }
     }
   }
@@ -710,6 +781,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
     }
     if (FRESH) {
+      // the player's slab at [pstart, pstart + cnt); its record is written
+      // with every other player's below
       uint32_t opos = NONE16;
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t e2 = L.slab[moff + j];
@@ -718,22 +791,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)((L.ekd[e2] >> 2) & 7u);
         opos = e2 == o ? j : opos;
       }
-      const uint64_t rm = ballot(act && prow != NONE8);
-      const uint32_t rix = f_nr + mbcnt(rm);
-      f_nr += (uint32_t)__builtin_popcountll(rm);
       if (act) {
-        (a.new_s.pl_id + nmeta.p_off)[p] = id;
-        (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : opos) |
-                                             ((prow != NONE8 ? rix : NONE16) << 16);
-        (a.new_s.pl_slab + nmeta.p_off)[p] = st | (cnt << 16);
-        if (prow != NONE8)
-          for (int d = 0; d < D; ++d)
-            (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[rix * D + d] = L.rows[prow][d];
+        L.pobs[p] = (uint8_t)(o == NONE8 ? NONE8 : st + opos);
+        L.pcntf[p] = (uint8_t)cnt;
+        L.prow[p] = (uint8_t)prow;
       }
-      uint32_t ctot;
-      (void)wave_excl_scan_dpp(act ? cnt : 0u, ctot);
-      f_nm += ctot;
-      f_nobs += (uint32_t)__builtin_popcountll(ballot(act && o != NONE8));
       min_cand(act && o != NONE8, osc, id, p);
     } else if (act) {
       L.pobs[p] = (uint8_t)o;
@@ -742,24 +804,47 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       L.prow[p] = (uint8_t)prow;
     }
   }
-  if (FRESH) {
-    // simple players (their final status: 5a may have made some complex)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool simple = xa[s] && !L.pflag[xp[s]];
-      const bool win = simple && L.pobs[xp[s]] == xq[s];
-      f_nm += (uint32_t)__builtin_popcountll(ballot(simple));
-      f_nobs += (uint32_t)__builtin_popcountll(ballot(win));
-      min_cand(win, xsc[s], in.id[s], xp[s]);
-    }
-  }
   wave_lds_sync();
+  // the next key's clock loads (after the replay: its registers are free)
+  if (has_next) wave_load_rows(a, L, nxt);
 
   PROF_MARK(4);
-  // ---- 6. (not FRESH) player records, final pool order, Removals rows
-  uint32_t fbase = f_nm, rbase = f_nr, nobs = f_nobs;
+  // ---- 6. player records, final pool order, Removals rows
+  uint32_t fbase = 0, rbase = 0, nobs = 0;
   uint32_t po[2] = {NONE8, NONE8};
-  if (!FRESH) {
+  if (FRESH) {
+    // slab of a decided player: its last segment (every op if it has no
+    // rmv); of a replayed player: [pstart, pstart + final count)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = s * 64 + lane;
+      const bool act = p < np;
+      const uint32_t pp = act ? p : (uint32_t)PSINK;
+      const uint32_t st = L.pstart[pp], c = pcnt_of(L, pp), lrp = L.plr[pp];
+      const bool replayed = L.pflag[pp] != 0;
+      const uint32_t off = (replayed || lrp == 0) ? st : lrp;
+      const uint32_t cnt = act ? (replayed ? (uint32_t)L.pcntf[pp] : st + c - off) : 0u;
+      const uint32_t o = act ? (uint32_t)L.pobs[pp] : NONE8;
+      const uint32_t prow = act ? (uint32_t)L.prow[pp] : NONE8;
+      const uint64_t rm = ballot(prow != NONE8);
+      const uint32_t rix = rbase + mbcnt(rm);
+      rbase += (uint32_t)__builtin_popcountll(rm);
+      if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
+      const int64_t id = (int64_t)L.htab[L.pslot[pp]];
+      if (act) {
+        (a.new_s.pl_id + nmeta.p_off)[p] = id;
+        (a.new_s.pl_slab + nmeta.p_off)[p] = off | (cnt << 16);
+        (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : o - off) |
+                                             ((prow != NONE8 ? rix : NONE16) << 16);
+      }
+      uint32_t ctot;
+      (void)wave_excl_scan_dpp(cnt, ctot);
+      fbase += ctot;
+      nobs += (uint32_t)__builtin_popcountll(ballot(o != NONE8));
+      min_cand(!replayed && o != NONE8, L.esc[o != NONE8 ? o : (uint32_t)ESINK], id, p);
+    }
+    wave_lds_sync();
+  } else {
   {
     uint32_t cnt[2], st[2], moff[2], goff[2], prow[2], opos[2];
     bool act[2], cx[2];
@@ -780,7 +865,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       fbase += ftot;
       opos[s] = (act[s] && !cx[s]) ? po[s] - st[s] : NONE16;
     }
-    // final pool order: complex players' slabs, simple players' op runs
+    // final pool order: replayed players' slabs, simple players' op runs
     const uint32_t maxcnt = wave_max_u32_dpp(cnt[0] > cnt[1] ? cnt[0] : cnt[1]);
     for (uint32_t j = 0; j < maxcnt; ++j) {
 #pragma unroll
@@ -810,7 +895,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   wave_lds_sync();
 
-  // ---- 7. Masked pool, Removals rows, Vc, Min, metadata
+  // ---- 7. Masked pool (the FRESH pool is already written)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t q = s * 64 + lane;
@@ -824,12 +909,13 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       (a.new_s.m_dc + nmeta.m_off)[q] = dc;
     }
   }
+  }  // !FRESH
+  // Removals rows (8 lanes per row), Vc, Min, metadata
   for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
     const int64_t v = L.rows[L.rl[r < rbase ? r : 0u]][d];
     if (r < rbase && (int)d < D) (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
   }
-  }  // !FRESH
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
   {
@@ -880,7 +966,8 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
     wave_load_chunk(a, c0, cn, hdr);
     KeyIn cur;
     wave_load_key(a, hdr, 0, cur);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load is pending at the loop head
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the ops are in
+    wave_load_rows(a, L, cur);
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
       const bool has_next = j + 1 < cn;
@@ -895,6 +982,7 @@ __global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
         // retire these loads here, as the common path does before its
         // stores: otherwise every key would wait on the previous key's stores
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if (has_next) wave_load_rows(a, L, nxt);
       }
       wave_lds_sync();  // LDS is reused by the wave's next key
       cur = nxt;

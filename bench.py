@@ -221,7 +221,7 @@ def main():
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
     cpu = None
-    if rank == 0 and args.cpu_sample_keys > 0:
+    if rank == 0 and world == 1 and args.cpu_sample_keys > 0:  # reported at N=1 only
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import numpy as np
 

@@ -15,9 +15,10 @@ sys.path.insert(0, ROOT)
 from antidote_ccrdt_amd import _lib  # noqa: E402
 from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv  # noqa: E402
 
-NAMES = ["loads issue + LDS init", "validate + rmv rank (load wait)", "clocks + hash + numbering",
-         "player/op + counting sort", "complex replay (5b)", "records + pool/rows/min/meta",
-         "simple players, op-parallel (5a)"]
+NAMES = ["loads issue + LDS init", "validate + rmv rank", "hash + clocks + numbering",
+         "player/op + counting sort", "pool write + replayed players (5b)",
+         "records + rows/min/meta", "step 5: players decided op-parallel",
+         "wait next key's ops + issue its clock loads"]
 n_ops = int(os.environ.get("N_OPS", 100_000_000))
 b = gen_trmv(n_ops, 1 << 20, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64)
 db = DeviceTrmvBatch(b)
