@@ -56,8 +56,13 @@ struct ccrdt_engine {
       if (hipEventCreate(&v) != hipSuccess) return false;
     for (hipEvent_t& v : evb)
       if (hipEventCreate(&v) != hipSuccess) return false;
+    // the side chain gets the highest stream priority: tier 0 fills every
+    // CU, and without it the side chain's later classes would only start
+    // once tier 0 has drained
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
     return hipEventCreate(&ev_scan) == hipSuccess && hipEventCreate(&ev_side) == hipSuccess &&
-           hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) == hipSuccess;
+           hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, hi) == hipSuccess;
   }
   void destroy_tier_events() {
     for (hipEvent_t& v : evt)

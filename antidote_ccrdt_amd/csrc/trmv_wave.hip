@@ -428,8 +428,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // the next key's op loads go out here, after the last early return: they
   // land during steps 4-5; the explicit wait before this key's stores
   // retires them, so the next key never waits on (and its vmcnt never
-  // counts) this key's stores
-  if (has_next) wave_load_key(a, hdr, nj, nxt);
+  // counts) this key's stores.  (Non-FRESH keys keep more registers live
+  // through step 4: their next key's loads go out at step 5.)
+  if (FRESH && has_next) wave_load_key(a, hdr, nj, nxt);
 
   PROF_MARK(2);
   // ---- 4. player of every op, Vc, op elements in player order
@@ -538,6 +539,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
 
   PROF_MARK(3);
+  if (!FRESH && has_next) wave_load_key(a, hdr, nj, nxt);
   if (!FRESH) {
     // ---- 5a. players without rmv or old state, op-parallel: each add
     // decides whether it is its player's Obs[Id] and whether its Ts rises
@@ -570,56 +572,89 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
     wave_lds_sync();
   } else {
-    // ---- 5. every op lane scans its player's positions once (header: tests
-    // (a)-(c)).  A rmv at a position ends the segments before it, so the
-    // Obs/Ts bookkeeping restarts there and ends with the last segment's.
-    bool fb[2] = {false, false}, beaten[2] = {false, false}, risk[2] = {false, false};
-    bool seen[2] = {false, false}, first[2] = {true, true};
-    uint32_t me[2], cl[2], adc[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      me[s] = xq[s] - xst[s];
-      cl[s] = xv[s] ? xc[s] : 0u;
-      adc[s] = xa[s] ? xdc[s] : 0u;
-    }
-    const uint32_t maxc = wave_max_u32_dpp(cl[0] > cl[1] ? cl[0] : cl[1]);
-    for (uint32_t x = 0; x < maxc; ++x) {
+    // ---- 5. players decided op-parallel (header: tests (a)-(c)).  A player
+    // with one op is decided by it.  The ops of the other players are packed
+    // into as few 64-lane passes as they fill (one, in practice) and each
+    // scans its player's positions once; a rmv at a position ends the
+    // segments before it, so the Obs/Ts bookkeeping restarts there and ends
+    // with the last segment's.  (fin and peb, unused by FRESH keys, hold the
+    // packed positions and the pending Removals merges.)
+    uint8_t* const cq = L.fin;
+    uint8_t* const mrg = L.peb;
+    uint32_t mn0, mn;
+    {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bool valid = x < cl[s] && x != me[s];
-        const uint32_t pos = x < cl[s] ? xst[s] + x : (uint32_t)ESINK;
+        const bool single = xv[s] && xc[s] == 1;
+        if (single && xa[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
+        if (single && xr[s]) {
+          L.prow[xp[s]] = (uint8_t)xsc[s];
+          L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
+        }
+      }
+      const bool mu0 = xv[0] && xc[0] > 1, mu1 = xv[1] && xc[1] > 1;
+      const uint64_t mb0 = ballot(mu0), mb1 = ballot(mu1);
+      mn0 = (uint32_t)__builtin_popcountll(mb0);
+      mn = mn0 + (uint32_t)__builtin_popcountll(mb1);
+      if (mu0) cq[mbcnt(mb0)] = (uint8_t)xq[0];
+      if (mu1) cq[mn0 + mbcnt(mb1)] = (uint8_t)xq[1];
+    }
+    wave_lds_sync();
+    bool any_merge = false;
+#pragma unroll 1
+    for (uint32_t b = 0; b < mn; b += 64) {
+      const uint32_t k = b + lane;
+      const bool act = k < mn;
+      const uint32_t q = act ? (uint32_t)cq[k] : ESINK;
+      const int64_t sm = L.esc[q], tm = L.ets[q];
+      const uint32_t kd = L.ekd[q];
+      const uint32_t p = act ? (kd >> 8) : PSINK;
+      const bool ya = act && (kd & 2u) == 0, yr = act && (kd & 2u) != 0;
+      const uint32_t adc = ya ? ((kd >> 2) & 7u) : 0u;
+      const uint32_t st = L.pstart[p], c = act ? pcnt_of(L, p) : 0u;
+      const uint32_t me = q - st;
+      bool fb = false, beaten = false, risk = false, seen = false, first = true;
+      const uint32_t maxc = wave_max_u32_dpp(c);
+      for (uint32_t x = 0; x < maxc; ++x) {
+        const bool valid = x < c && x != me;
+        const uint32_t pos = x < c ? st + x : (uint32_t)ESINK;
         const int64_t sx = L.esc[pos], tx = L.ets[pos];
         const bool isr = valid && (L.ekd[pos] & 2u) != 0;
-        const bool before = x < me[s];
-        const bool need = xa[s] && isr && (before || !seen[s]);
-        const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc[s]];
-        const int64_t sm = xsc[s], tm = xts[s];
-        fb[s] |= need && (before ? rt >= tm : rt < tm);
-        seen[s] |= isr && !before;
-        first[s] &= !(isr && before);
-        risk[s] = risk[s] && !isr;
-        beaten[s] = beaten[s] && !isr;
-        const bool both = xa[s] && valid && !isr;
-        risk[s] |= both && before && tx >= tm;
-        beaten[s] |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
+        const bool before = x < me;
+        // an add against a rmv of its player: dominated by an earlier one
+        // (:234), or kept by the first later one (:255-266) -> replay
+        const bool need = ya && isr && (before || !seen);
+        const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
+        fb |= need && (before ? rt >= tm : rt < tm);
+        seen |= isr && !before;
+        first &= !(isr && before);
+        risk = risk && !isr;
+        beaten = beaten && !isr;
+        const bool both = ya && valid && !isr;
+        risk |= both && before && tx >= tm;
+        beaten |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
       }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (xv[s] && (fb[s] || risk[s])) L.pflag[xp[s]] = 1;
-      if (xa[s] && !seen[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
-      if (xr[s] && first[s]) L.prow[xp[s]] = (uint8_t)xsc[s];
-      if (xr[s] && !seen[s]) L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
+      if (act && (fb || risk)) L.pflag[p] = 1;
+      if (ya && !seen && !beaten) L.pobs[p] = (uint8_t)q;
+      if (yr && first) L.prow[p] = (uint8_t)sm;  // a rmv's "score" is its clock row
+      if (yr && !seen) L.plr[p] = (uint8_t)(q + 1);
+      if (act) mrg[k] = (uint8_t)(yr && !first);
+      any_merge |= ballot(yr && !first) != 0;
     }
     wave_lds_sync();
     // Removals[Id]: the player's later rmv clocks merge into its first rmv's
     // row (merge_vc, :369-386); replayed players merge their own
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (xr[s] && !first[s] && !L.pflag[xp[s]]) {
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(L.rows[L.prow[xp[s]]]);
-        const int64_t* src = L.rows[(uint32_t)xsc[s]];
-        for (int d = 0; d < D; ++d) atomicMax(dst + d, (unsigned long long)src[d]);
+    if (any_merge) {
+#pragma unroll 1
+      for (uint32_t b = 0; b < mn; b += 64) {
+        const uint32_t k = b + lane;
+        const uint32_t q = k < mn && mrg[k] ? (uint32_t)cq[k] : ESINK;
+        const uint32_t p = q != ESINK ? (uint32_t)(L.ekd[q] >> 8) : PSINK;
+        if (q != ESINK && !L.pflag[p]) {
+          unsigned long long* dst = reinterpret_cast<unsigned long long*>(L.rows[L.prow[p]]);
+          const int64_t* src = L.rows[(uint32_t)L.esc[q]];
+          for (int d = 0; d < D; ++d) atomicMax(dst + d, (unsigned long long)src[d]);
+        }
       }
     }
     wave_lds_sync();
