@@ -615,16 +615,24 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t me = q - st;
       bool fb = false, beaten = false, risk = false, seen = false, first = true;
       const uint32_t maxc = wave_max_u32_dpp(c);
+      // software-pipelined: position x+1 is read while position x's clock
+      // entry (its address depends on x's element) is in flight
+      const uint32_t p0 = c ? st : (uint32_t)ESINK;
+      int64_t sxn = L.esc[p0], txn = L.ets[p0];
+      uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
+        const int64_t sx = sxn, tx = txn;
         const bool valid = x < c && x != me;
-        const uint32_t pos = x < c ? st + x : (uint32_t)ESINK;
-        const int64_t sx = L.esc[pos], tx = L.ets[pos];
-        const bool isr = valid && (L.ekd[pos] & 2u) != 0;
+        const bool isr = valid && (kxn & 2u) != 0;
         const bool before = x < me;
         // an add against a rmv of its player: dominated by an earlier one
         // (:234), or kept by the first later one (:255-266) -> replay
         const bool need = ya && isr && (before || !seen);
         const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
+        const uint32_t pn = x + 1 < c ? st + x + 1 : (uint32_t)ESINK;
+        sxn = L.esc[pn];
+        txn = L.ets[pn];
+        kxn = L.ekd[pn];
         fb |= need && (before ? rt >= tm : rt < tm);
         seen |= isr && !before;
         first &= !(isr && before);
@@ -850,6 +858,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   if (FRESH) {
     // slab of a decided player: its last segment (every op if it has no
     // rmv); of a replayed player: [pstart, pstart + final count)
+    uint32_t csum = 0;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t p = s * 64 + lane;
@@ -872,12 +881,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : o - off) |
                                              ((prow != NONE8 ? rix : NONE16) << 16);
       }
-      uint32_t ctot;
-      (void)wave_excl_scan_dpp(cnt, ctot);
-      fbase += ctot;
+      csum += cnt;
       nobs += (uint32_t)__builtin_popcountll(ballot(o != NONE8));
       min_cand(!replayed && o != NONE8, L.esc[o != NONE8 ? o : (uint32_t)ESINK], id, p);
     }
+    (void)wave_excl_scan_dpp(csum, fbase);  // |Masked| of the key
     wave_lds_sync();
   } else {
   {
