@@ -83,7 +83,12 @@ constexpr uint32_t NONE8 = 0xFFu;
 // sink address would serialize.)
 constexpr uint32_t HSINK = W_HCAP, ESINK = W_ECAP, PSINK = W_PCAP;
 
+// FRESH keys have no old state: the arrays only the steady-state path uses
+// take no space in their instantiation (zero-length), which keeps the FRESH
+// workgroup inside a fifth of the CU's LDS.
+template <bool FRESH>
 struct alignas(16) WaveLds {
+  static constexpr int NS_ = FRESH ? 0 : 1;
   unsigned long long htab[W_HCAP + 2];   // Ids (W_EMPTY = free); [HSINK]
   int64_t esc[W_ECAP + 2];               // element score (rmv op: its clock row in `rows`)
   int64_t ets[W_ECAP + 2];               // element ts
@@ -96,15 +101,15 @@ struct alignas(16) WaveLds {
   uint8_t pslot[W_PCAP + 8];             // player -> hash slot
   uint8_t sorted[W_ECAP + 8];            // op index (stream position) of every op element
   uint8_t slab[W_ECAP];                  // working Masked slabs (element indices)
-  uint8_t fin[W_ECAP + 8];               // final pool: element of every output position
+  uint8_t fin[NS_ * (W_ECAP + 8)];       // final pool: element of every output position
   uint8_t pstart[W_PCAP + 8];            // first position of each player's ops
   uint8_t pobs[W_PCAP + 8];              // Obs[Id] of each player (element), NONE8 = none
   uint8_t pflag[W_PCAP + 8];             // 1 = player replayed op by op
   uint8_t pcntf[W_PCAP + 8];             // replayed player: final |Masked[Id]|
-  uint8_t pmoff[W_PCAP + 8];             // replayed player: its working slab in `slab`
+  uint8_t pmoff[NS_ * (W_PCAP + 8)];     // replayed player: its working slab in `slab`
   uint8_t prow[W_PCAP + 8];              // the player's clock row (Removals[Id]) or NONE8
   uint8_t plr[W_PCAP + 8];               // FRESH: 1 + position of the player's last rmv, 0 = none
-  uint8_t peb[W_PCAP + 8];               // old player: first element of its old slab
+  uint8_t peb[NS_ * (W_PCAP + 8)];       // old player: first element of its old slab
   uint8_t cpl[W_PCAP + 8];               // replayed players, packed
   uint8_t rl[W_RCAP + 8];                // clock row of each output Removals row
   uint32_t nex;                          // extra effects emitted by the key
@@ -115,12 +120,14 @@ __device__ __forceinline__ uint32_t whash(int64_t id) {
   return (uint32_t)(x >> 56);  // 8 bits = W_HCAP slots
 }
 
-__device__ __forceinline__ uint32_t pcnt_of(const WaveLds& L, uint32_t p) {
+template <class W>
+__device__ __forceinline__ uint32_t pcnt_of(const W& L, uint32_t p) {
   return (L.pcnt2[p >> 1] >> (16 * (p & 1))) & 0xFFFFu;
 }
 
 // One extra effect (the {ok, S, [Effect]} of topk_rmv.erl:236-237 / :294-295).
-__device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, WaveLds& L, uint64_t op0,
+template <class W>
+__device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, W& L, uint64_t op0,
                                           uint64_t op, uint8_t kind, int64_t id, int64_t sc,
                                           uint32_t dc, int64_t ts, uint32_t row) {
   const uint32_t pos = atomicAdd(&L.nex, 1u);
@@ -201,7 +208,8 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
 // per clock row, coalesced) once its ops are in registers; they are consumed
 // after the key's hash build.  A row outside [0, n_rmv_rows) reads row 0: the
 // key's validation rejects the batch before any value is used.
-__device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, WaveLds& L, KeyIn& in) {
+template <class W>
+__device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, W& L, KeyIn& in) {
   const int lane = lane_id();
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) in.rv[s] = 0;
@@ -236,7 +244,7 @@ enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2, W_SIDE = 3 };
 
 template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
-                                              WaveLds& L, bool has_next, const ChunkHdr& hdr,
+                                              WaveLds<FRESH>& L, bool has_next, const ChunkHdr& hdr,
                                               uint32_t nj, KeyIn& nxt) {
   const int lane = lane_id();
   const int D = a.n_dc;
@@ -577,10 +585,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     // into as few 64-lane passes as they fill (one, in practice) and each
     // scans its player's positions once; a rmv at a position ends the
     // segments before it, so the Obs/Ts bookkeeping restarts there and ends
-    // with the last segment's.  (fin and peb, unused by FRESH keys, hold the
-    // packed positions and the pending Removals merges.)
-    uint8_t* const cq = L.fin;
-    uint8_t* const mrg = L.peb;
+    // with the last segment's.  (slab and cpl, used by the replay only after
+    // this step, hold the packed positions and the pending Removals merges.)
+    uint8_t* const cq = L.slab;
+    uint8_t* const mrg = L.cpl;
     uint32_t mn0, mn;
     {
 #pragma unroll
@@ -997,11 +1005,14 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
+#ifndef TRMV_FRESH_WAVES
+#define TRMV_FRESH_WAVES 4  // waves per SIMD the FRESH instantiation is built for
+#endif
 template <bool FRESH>
-__global__ __launch_bounds__(256, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
-  __shared__ WaveLds lds[W_WAVES];
+__global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_kernel(TrmvApplyArgs a) {
+  __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  WaveLds& L = lds[wv];
+  WaveLds<FRESH>& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * W_KPW; c0 < n; c0 += gridDim.x * W_WAVES * W_KPW) {
     const uint32_t cn = c0 + W_KPW < n ? W_KPW : n - c0;
