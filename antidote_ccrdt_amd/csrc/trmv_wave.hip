@@ -378,6 +378,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       pend[j] = pend[j] && !done;
     }
   }
+  PROF_MARK(8);
   // write the rmv clocks (their loads were issued with the key's ops)
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
@@ -390,6 +391,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (err) atomicOr(&a.status[1], err);
     return W_REJECT;
   }
+  PROF_MARK(9);
   // old players keep their index
   if (!FRESH) {
 #pragma unroll
@@ -961,6 +963,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
   }
   }  // !FRESH
+  PROF_MARK(10);
   // Removals rows (8 lanes per row), Vc, Min, metadata
   for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
@@ -968,6 +971,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (r < rbase && (int)d < D) (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
   }
   if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+  PROF_MARK(11);
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
   {
     if (!FRESH) {

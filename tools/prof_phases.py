@@ -18,7 +18,9 @@ from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv  
 NAMES = ["loads issue + LDS init", "validate + rmv rank", "hash + clocks + numbering",
          "player/op + counting sort", "pool write + replayed players (5b)",
          "records + rows/min/meta", "step 5: players decided op-parallel",
-         "wait next key's ops + issue its clock loads"]
+         "wait next key's ops + issue its clock loads",
+         "hash build (CAS loop) [split of 2]", "clock rows into LDS (waits their loads) [split of 2]",
+         "records pass [split of 5]", "rows + Vc stores [split of 5]"]
 n_ops = int(os.environ.get("N_OPS", 100_000_000))
 b = gen_trmv(n_ops, 1 << 20, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64)
 db = DeviceTrmvBatch(b)
