@@ -74,7 +74,11 @@ constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
 constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
-constexpr int W_KPW = 8;     // consecutive keys per wave
+#ifndef TRMV_KPW
+#define TRMV_KPW 8
+#endif
+constexpr int W_KPW = TRMV_KPW;  // consecutive keys per wave chunk (a multiple of 8, <= 64)
+constexpr int W_MD = W_KPW / 8;  // metadata registers of a chunk header
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
 constexpr uint32_t NONE8 = 0xFFu;
 // Sink entries: a lane with nothing to read reads the extra entry of the
@@ -156,13 +160,13 @@ struct KeyIn {
 };
 
 // Bounds and new-side metadata of a wave's W_KPW keys, loaded once per chunk
-// into lanes (key j: lane j holds its key and op range, lanes 8j..8j+7 the
-// eight dwords of its KeyMeta), so a key's op loads never wait on a scalar
-// load of its own bounds.
+// into lanes (key j: lane j holds its key and op range; register i, lane
+// 8(j%8) + d: dword d of the KeyMeta of key 8i + j/8... see wave_load_chunk),
+// so a key's op loads never wait on a scalar load of its own bounds.
 struct ChunkHdr {
-  uint32_t key;     // lane j < n: key j
-  uint64_t lo, hi;  // lane j < n: key_ptr[key j], key_ptr[key j + 1]
-  uint32_t meta;    // lane 8j + d: dword d of new_s.meta[key j]
+  uint32_t key;         // lane j < n: key j
+  uint64_t lo, hi;      // lane j < n: key_ptr[key j], key_ptr[key j + 1]
+  uint32_t meta[W_MD];  // meta[i], lane 8m + d: dword d of new_s.meta[key 8i + m]
 };
 
 __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t c0, uint32_t n,
@@ -172,9 +176,13 @@ __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t
   h.key = a.key_list ? a.key_list[c0 + j] : c0 + j;
   h.lo = a.key_ptr[h.key];
   h.hi = a.key_ptr[h.key + 1];
-  const uint32_t jm = (uint32_t)(lane >> 3) < n ? (uint32_t)(lane >> 3) : 0u;
-  const uint32_t km = a.key_list ? a.key_list[c0 + jm] : c0 + jm;
-  h.meta = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
+#pragma unroll
+  for (int i = 0; i < W_MD; ++i) {
+    const uint32_t m = 8 * i + (lane >> 3);
+    const uint32_t jm = m < n ? m : 0u;
+    const uint32_t km = a.key_list ? a.key_list[c0 + jm] : c0 + jm;
+    h.meta[i] = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
+  }
 }
 
 __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const ChunkHdr& h, uint32_t j,
@@ -184,7 +192,13 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
   in.nops = (uint32_t)((uint64_t)rl64((int64_t)h.hi, (int)j) - in.op0);
   uint32_t* m = reinterpret_cast<uint32_t*>(&in.nmeta);
 #pragma unroll
-  for (int d = 0; d < 8; ++d) m[d] = rl32(h.meta, (int)(8 * j + d));
+  for (int d = 0; d < 8; ++d) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < W_MD; ++i)
+      if ((j >> 3) == (uint32_t)i) v = rl32(h.meta[i], (int)(8 * (j & 7) + d));
+    m[d] = v;
+  }
   // wave-uniform bases + 32-bit lane offsets (saddr addressing, no 64-bit
   // per-lane address arithmetic)
   const int64_t* idp = a.id + in.op0;
