@@ -59,6 +59,12 @@ CONFIGS = [
     (5000, 50, 1, 5, 3, 300, 2, 80, 80, 1),              # K=1
     (30000, 30, 8, 600, 10**6, 30, 64, 0, 0, 100),       # big keys -> slot-class escalation
     (3000, 4000, 8, 256, 10**6, 100, 64, 0, 0, 100),     # many empty keys
+    # tier 0's rmv segments: many rmvs per player, each wiping the player
+    # (lag 0), duplicates in earlier segments, multi-rmv Removals merges
+    (20000, 200, 4, 8, 50, 300, 1, 30, 0, 100),
+    # the same with out-of-order delivery: dominated adds and survivors
+    # send players to the replay
+    (20000, 200, 4, 8, 50, 300, 1, 30, 60, 100),
 ]
 
 
