@@ -26,9 +26,10 @@ int launch_caps_scan(const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stri
                      uint64_t* caps, uint64_t* off, uint64_t* part, hipStream_t st);
 int wc_launch_count(const uint64_t* doc_off, const uint8_t* bytes, uint64_t n_docs, uint64_t* ntok,
                     hipStream_t st);
-int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key, hipStream_t st);
-int wc_launch_insert(const WcArgs& a, hipStream_t st);
-int wc_launch_verify(const WcArgs& a, hipStream_t st);
+int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs, uint64_t* doc_key,
+                     hipStream_t st);
+int wc_launch_insert(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
+int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st);
 int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
                      const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st);
@@ -901,12 +902,22 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   // document keys and token counts
   CCRDT_TRY(T.stage[0].ensure(nd * 8 + 8));
   CCRDT_TRY(T.stage[1].ensure(nd * 8 + 8));
-  CCRDT_TRY(wc_launch_doc_key(docs->key_ptr, nk, T.stage[0].as<uint64_t>(), e->stream));
+  CCRDT_TRY(wc_launch_doc_key(docs->key_ptr, nk, nd, T.stage[0].as<uint64_t>(), e->stream));
   CCRDT_TRY(wc_launch_count(docs->doc_off, docs->bytes, nd, T.stage[1].as<uint64_t>(), e->stream));
   std::vector<uint64_t> ntok;
   CCRDT_TRY(d2h(ntok, T.stage[1], nd, e->stream));
   uint64_t tokens = 0;
   for (uint64_t t : ntok) tokens += t;
+  // documents -> chunks of WC_TPW tiles of WC_TILE bytes (one wave each)
+  std::vector<uint64_t> doff(nd + 1), tptr(nd + 1);
+  if (nd) {
+    CCRDT_HIP(hipMemcpyAsync(doff.data(), docs->doc_off, (nd + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+  }
+  tptr[0] = 0;
+  for (uint64_t d = 0; d < nd; ++d)
+    tptr[d + 1] = tptr[d] + ((doff[d + 1] - doff[d]) / WC_TILE + WC_TPW) / WC_TPW;
+  CCRDT_TRY(h2d(T.stage[4], tptr.data(), (nd + 1) * 8, e->stream));
   std::vector<uint64_t> top;
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   const uint64_t words_old = e->fresh ? 0 : top[1], arena_used = e->fresh ? 0 : top[0];
@@ -938,15 +949,18 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     a.bytes = docs->bytes;
     a.n_bytes = docs->n_bytes;
     CCRDT_HIP(hipEventRecord(e->evk0, e->stream));
-    // worddocumentcount: the per-document dedupe table is sized by the
-    // chunk's tokens; documents are processed in chunks of <= 2^27 tokens
+    // worddocumentcount: the (document, word) dedupe table is sized by the
+    // chunk's tokens; documents are processed in chunks of <= 2^28 tokens
+    // (wordcount: one launch)
     uint64_t d0 = 0;
     while (d0 < nd) {
       uint64_t d1 = d0, tk = 0;
-      while (d1 < nd && (d1 == d0 || tk + ntok[d1] <= (1ull << 27))) tk += ntok[d1++];
+      while (d1 < nd && (d1 == d0 || !a.wdc || tk + ntok[d1] <= (1ull << 28))) tk += ntok[d1++];
       a.n_docs = (int64_t)(d1 - d0);
       a.doc_key = T.stage[0].as<uint64_t>() + d0;
       a.doc_off = docs->doc_off + d0;
+      a.tile_ptr = T.stage[4].as<uint64_t>() + d0;
+      a.tile0 = tptr[d0];
       if (a.wdc) {
         const uint64_t ds = pow2_at_least(2 * tk);
         CCRDT_TRY(T.d_hash.ensure(ds * 8));
@@ -954,7 +968,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.d_hash = T.d_hash.as<uint64_t>();
         a.d_mask = ds - 1;
       }
-      CCRDT_TRY(wc_launch_insert(a, e->stream));
+      CCRDT_TRY(wc_launch_insert(a, tptr[d1] - tptr[d0], e->stream));
       d0 = d1;
     }
     CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
@@ -973,7 +987,9 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     a.doc_key = T.stage[0].as<uint64_t>();
     a.doc_off = docs->doc_off;
     a.n_docs = (int64_t)nd;
-    CCRDT_TRY(wc_launch_verify(a, e->stream));
+    a.tile_ptr = T.stage[4].as<uint64_t>();
+    a.tile0 = 0;
+    CCRDT_TRY(wc_launch_verify(a, tptr[nd], e->stream));
     CCRDT_TRY(read_status(e, st));
     if (st[1]) {
       set_error(st[1] & 1 ? "wc_apply: 64-bit word hash collision between distinct words"

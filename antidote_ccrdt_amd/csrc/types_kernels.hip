@@ -654,7 +654,7 @@ int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
 // (worddocumentcount); misses go to the global table (CAS on h).  Exactness
 // does not rest on the hash: wc_verify_kernel byte-compares every token with
 // its word's representative and flags any collision.
-constexpr int WC_LDS = 512;  // per-document LDS table entries
+constexpr int WC_LDS = 512;  // per-tile LDS table entries
 constexpr int WC_PROBE = 8;
 
 __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
@@ -681,10 +681,109 @@ __device__ __forceinline__ uint64_t wc_token(const uint8_t* doc, uint64_t len, u
   return e;
 }
 
+// A tile staged in LDS: bytes [tile - 16 + sh .. ) of the document, read as
+// 16-byte aligned blocks of the batch's byte array (coalesced), so the token
+// scan reads LDS instead of issuing one dependent global byte load per byte.
+// Bytes past the staged window (a token running far past its tile) are read
+// from HBM.
+constexpr int WC_HALO = 256;
+constexpr int WC_STAGE = (int)WC_TILE + WC_HALO + 32;
+struct WcTileView {
+  const uint8_t* lds;  // staged bytes
+  const uint8_t* doc;  // document in HBM
+  uint64_t lo;         // document position of lds[0] (may be "negative": wraps, never read)
+  uint64_t n;          // staged positions [lo, lo + n) that are inside the document
+  __device__ __forceinline__ uint8_t at(uint64_t s) const {
+    const uint64_t i = s - lo;
+    return i < n ? lds[i] : doc[s];
+  }
+};
+
+__device__ __forceinline__ WcTileView wc_stage(const WcArgs& a, uint8_t* buf, uint64_t b0, uint64_t len,
+                                               uint64_t tile) {
+  // window: document positions [tile - 1, tile + WC_TILE + WC_HALO), clipped
+  // to the document, starting at a 16-byte aligned absolute address
+  const uint64_t want0 = b0 + (tile ? tile - 1 : 0);
+  const uint64_t mis = (uint64_t)(uintptr_t)a.bytes & 15u;  // the batch array need not be aligned
+  const uint64_t abs0 = ((want0 + mis) & ~15ull) - mis;    // may wrap below 0: guarded below
+  const uint64_t want1 = b0 + (tile + WC_TILE + WC_HALO < len ? tile + WC_TILE + WC_HALO : len);
+  const int lane = lane_id();
+  for (int i = lane * 16; i < WC_STAGE; i += 64 * 16) {
+    const uint64_t p = abs0 + (uint64_t)i;
+    if ((int64_t)p >= (int64_t)want1) break;
+    if ((int64_t)p >= 0 && p + 16 <= a.n_bytes) {
+      *reinterpret_cast<uint4*>(buf + i) = *reinterpret_cast<const uint4*>(a.bytes + p);
+    } else {
+      for (int j = 0; j < 16; ++j) {
+        const int64_t q = (int64_t)p + j;
+        buf[i + j] = (q >= 0 && (uint64_t)q < a.n_bytes) ? a.bytes[q] : (uint8_t)0;
+      }
+    }
+  }
+  __syncthreads();
+  WcTileView v;
+  v.lds = buf;
+  v.doc = a.bytes + b0;
+  v.lo = abs0 - b0;  // document position of buf[0] (wraps when abs0 < b0)
+  const uint64_t staged_end = abs0 + (uint64_t)WC_STAGE < want1 ? abs0 + (uint64_t)WC_STAGE : want1;
+  // valid window: [want0, staged_end) in absolute terms
+  v.n = staged_end - b0 - v.lo;
+  // positions below want0 (other documents' bytes) are never asked for:
+  // callers only read s in [tile - 1, len)
+  return v;
+}
+
+// Token starting at document position s: returns its end (staged reads).
+__device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len, uint64_t s, uint64_t& fnv) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  uint64_t e = s;
+  while (e < len) {
+    const uint8_t c = v.at(e);
+    if (wc_sep(c)) break;
+    h = (h ^ c) * 0x100000001B3ull;
+    ++e;
+  }
+  fnv = h;
+  return e;
+}
+
+// Token starts of the staged tile, compacted into an LDS list (offsets from
+// the tile start), so the per-token work runs on full waves instead of one
+// lockstep pass per byte position.  Returns the number of tokens.
+__device__ __forceinline__ uint32_t wc_starts(const WcTileView& v, uint64_t len, uint64_t tile,
+                                              uint16_t* list) {
+  const int lane = lane_id();
+  const uint64_t s0 = tile + (uint64_t)lane * (WC_TILE / 64);
+  uint64_t m = 0;
+#pragma unroll 8
+  for (int i = 0; i < (int)(WC_TILE / 64); ++i) {
+    const uint64_t s = s0 + (uint64_t)i;
+    const bool st = s <= len && (s == 0 || wc_sep(v.at(s - 1)));
+    m |= (uint64_t)st << i;
+  }
+  uint32_t tot;
+  uint32_t o = wave_excl_scan_u32((uint32_t)__builtin_popcountll(m), tot);
+  while (m) {
+    const int i = __builtin_ctzll(m);
+    m &= m - 1;
+    list[o++] = (uint16_t)(lane * (WC_TILE / 64) + i);
+  }
+  __syncthreads();
+  return tot;
+}
+
 __device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
                                                      uint64_t pos) {
   uint64_t sl = h & a.t_mask;
   for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
+    // read first: a slot goes 0 -> h once, so a (possibly stale) nonzero
+    // value is final and only an empty-looking slot needs the CAS
+    const uint64_t seen = __hip_atomic_load(&a.t_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == h) return sl;
+    if (seen != 0ull) {
+      sl = (sl + 1) & a.t_mask;
+      continue;
+    }
     const unsigned long long prev = atomicCAS((unsigned long long*)&a.t_hash[sl], 0ull, (unsigned long long)h);
     if (prev == 0ull) {  // new word: this token is its representative
       a.t_key[sl] = key;
@@ -714,13 +813,37 @@ __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t h, uint64
   return false;
 }
 
+// Chunk of the launch -> (document, first byte of the chunk in it).  Wave-
+// uniform binary search over the launch's tile_ptr.  Documents are split
+// into chunks of WC_TPW tiles of WC_TILE bytes, one wave each, so every wave
+// has a bounded share and stays inside one document.
+__device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d, uint64_t& s0) {
+  uint64_t lo = 0, hi = (uint64_t)a.n_docs;  // tile_ptr[lo] <= t < tile_ptr[hi]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a.tile_ptr[mid] <= t) lo = mid;
+    else hi = mid;
+  }
+  d = lo;
+  s0 = (t - a.tile_ptr[lo]) * (uint64_t)(WC_TILE * WC_TPW);
+}
+
+// One wave per tile: the tokens that START in bytes [s0, s0 + WC_TILE) of
+// document d (the position len counts: a document ending in a separator, or
+// an empty one, has a trailing empty token).  Each lane owns 64 bytes.
 __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   __shared__ unsigned long long lh[WC_LDS];
   __shared__ uint32_t lc[WC_LDS];
   __shared__ uint32_t llen[WC_LDS];
   __shared__ uint64_t lpos[WC_LDS];
-  const uint64_t d = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
+  __shared__ uint16_t tlist[WC_TILE];
   const int lane = lane_id();
+  // a wave takes up to WC_TPW consecutive tiles of ONE document and keeps its
+  // LDS table across them (the Zipf head costs one global atomic per word
+  // per WC_TPW tiles)
+  uint64_t d, tile;
+  wc_tile(a, a.tile0 + blockIdx.x, d, tile);
   const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
   const uint32_t key = (uint32_t)a.doc_key[d];
   const uint8_t* doc = a.bytes + b0;
@@ -729,15 +852,17 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
     lc[i] = 0u;
   }
   __syncthreads();
-  for (uint64_t tile = 0; tile <= len; tile += 4096) {
-    const uint64_t s0 = tile + (uint64_t)lane * 64;
-    for (uint64_t s = s0; s < s0 + 64 && s <= len; ++s) {
-      if (!(s == 0 || wc_sep(doc[s - 1]))) continue;  // not a token start
+  for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
+    __syncthreads();  // the previous tile's staged bytes are no longer read
+    const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
+    const uint32_t ntk = wc_starts(v, len, tile, tlist);
+    for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
+      const uint64_t s = tile + tlist[k];
       uint64_t fnv;
-      const uint64_t e = wc_token(doc, len, s, fnv);
+      const uint64_t e = wc_token_v(v, len, s, fnv);
       const uint32_t tl = (uint32_t)(e - s);
       const uint64_t h = wc_mix(fnv, key, tl);
-      // per-document LDS table
+      // per-tile LDS table
       uint32_t sl = (uint32_t)(h >> 17) & (WC_LDS - 1);
       int where = -1;  // 0: counted in LDS, 1: global
       for (int p = 0; p < WC_PROBE; ++p) {
@@ -750,7 +875,7 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
           else lc[sl] = 1u;
           break;
         }
-        if (prev == h) {  // same word already seen in this document
+        if (prev == h) {  // same word already seen in this tile
           where = 0;
           if (!a.wdc) atomicAdd(&lc[sl], 1u);
           break;
@@ -768,8 +893,9 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   for (int i = lane; i < WC_LDS; i += 64) {
     const uint64_t h = lh[i];
     if (h == 0ull) continue;
-    // a word takes the same path (LDS or global) for the whole document: LDS
-    // slots are never freed, so a word that once missed them always misses
+    // worddocumentcount: other tiles of the document may hold the word too;
+    // the (document, word) dedupe table admits one of them
+    if (a.wdc && !wc_doc_first(a, h, d)) continue;
     const uint64_t g = wc_global_insert(a, h, key, llen[i], lpos[i]);
     if (g != ~0ull) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
   }
@@ -777,30 +903,53 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
 
 // Exactness: every token must equal its word's representative byte-for-byte.
 __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
-  const uint64_t d = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
+  __shared__ uint16_t tlist[WC_TILE];
   const int lane = lane_id();
+  uint64_t d, tile;
+  wc_tile(a, a.tile0 + blockIdx.x, d, tile);
   const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
   const uint32_t key = (uint32_t)a.doc_key[d];
   const uint8_t* doc = a.bytes + b0;
-  for (uint64_t tile = 0; tile <= len; tile += 4096) {
-    const uint64_t s0 = tile + (uint64_t)lane * 64;
-    for (uint64_t s = s0; s < s0 + 64 && s <= len; ++s) {
-      if (!(s == 0 || wc_sep(doc[s - 1]))) continue;
-      uint64_t fnv;
-      const uint64_t e = wc_token(doc, len, s, fnv);
-      const uint32_t tl = (uint32_t)(e - s);
-      const uint64_t h = wc_mix(fnv, key, tl);
-      uint64_t sl = h & a.t_mask;
-      while (a.t_hash[sl] != h && a.t_hash[sl] != 0ull) sl = (sl + 1) & a.t_mask;
-      if (a.t_hash[sl] != h) {
-        atomicOr(&a.status[1], 2u);  // lost token (table overflow)
-        continue;
-      }
-      const uint8_t* rep = a.t_arena[sl] != ~0ull ? a.arena + a.t_arena[sl] : a.bytes + a.t_pos[sl];
-      bool eq = a.t_key[sl] == key && a.t_len[sl] == tl;
-      for (uint32_t j = 0; eq && j < tl; ++j) eq = rep[j] == doc[s + j];
-      if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+  for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
+  __syncthreads();
+  const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
+  const uint32_t ntk = wc_starts(v, len, tile, tlist);
+  for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
+    const uint64_t s = tile + tlist[k];
+    uint64_t fnv;
+    const uint64_t e = wc_token_v(v, len, s, fnv);
+    const uint32_t tl = (uint32_t)(e - s);
+    const uint64_t h = wc_mix(fnv, key, tl);
+    // probe: the slot's fields are loaded together with its hash
+    uint64_t sl = h & a.t_mask;
+    uint64_t th, tar, tpos;
+    uint32_t tk, tln;
+    for (;;) {
+      th = a.t_hash[sl];
+      tar = a.t_arena[sl];
+      tpos = a.t_pos[sl];
+      tk = a.t_key[sl];
+      tln = a.t_len[sl];
+      if (th == h || th == 0ull) break;
+      sl = (sl + 1) & a.t_mask;
     }
+    if (th != h) {
+      atomicOr(&a.status[1], 2u);  // lost token (table overflow)
+      continue;
+    }
+    const uint8_t* rep = tar != ~0ull ? a.arena + tar : a.bytes + tpos;
+    bool eq = tk == key && tln == tl;
+    // 8 independent byte loads per step (one latency per 8 bytes)
+    for (uint32_t j0 = 0; eq && j0 < tl; j0 += 8) {
+      uint8_t r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = j0 + j < tl ? rep[j0 + j] : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) eq = eq && (j0 + j >= tl || r[j] == v.at(s + j0 + j));
+    }
+    if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+  }
   }
 }
 
@@ -829,11 +978,19 @@ __global__ __launch_bounds__(64) void wc_count_kernel(const uint64_t* doc_off, c
   (void)wave_excl_scan_u32(c, tot);
   if (lane_id() == 0) ntok[d] = (uint64_t)tot + 1;
 }
-// key of every document from the key -> documents CSR
-__global__ void wc_doc_key_kernel(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_keys) return;
-  for (uint64_t d = key_ptr[k]; d < key_ptr[k + 1]; ++d) doc_key[d] = k;
+// key of every document from the key -> documents CSR (thread per document,
+// binary search: a key may own thousands of documents)
+__global__ void wc_doc_key_kernel(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs,
+                                  uint64_t* doc_key) {
+  const uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  uint64_t lo = 0, hi = n_keys;  // key_ptr[lo] <= d < key_ptr[hi]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (key_ptr[mid] <= d) lo = mid;
+    else hi = mid;
+  }
+  doc_key[d] = lo;
 }
 
 int wc_launch_count(const uint64_t* doc_off, const uint8_t* bytes, uint64_t n_docs, uint64_t* ntok,
@@ -843,22 +1000,23 @@ int wc_launch_count(const uint64_t* doc_off, const uint8_t* bytes, uint64_t n_do
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t* doc_key, hipStream_t st) {
-  if (!n_keys) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_doc_key_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0, st, key_ptr,
-                     n_keys, doc_key);
+int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs, uint64_t* doc_key,
+                     hipStream_t st) {
+  if (!n_keys || !n_docs) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_doc_key_kernel, dim3((unsigned)((n_docs + 255) / 256)), dim3(256), 0, st, key_ptr,
+                     n_keys, n_docs, doc_key);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-int wc_launch_insert(const WcArgs& a, hipStream_t st) {
-  if (!a.n_docs) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_insert_kernel, dim3((unsigned)a.n_docs), dim3(64), 0, st, a);
+int wc_launch_insert(const WcArgs& a, uint64_t n_tiles, hipStream_t st) {
+  if (!a.n_docs || !n_tiles) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_insert_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-int wc_launch_verify(const WcArgs& a, hipStream_t st) {
-  if (!a.n_docs) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_verify_kernel, dim3((unsigned)a.n_docs), dim3(64), 0, st, a);
+int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st) {
+  if (!a.n_docs || !n_tiles) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_verify_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -126,11 +126,16 @@ struct LbDownArgs {
 };
 
 // wordcount / worddocumentcount
+constexpr uint64_t WC_TILE = 4096;  // bytes of a document per wave step (64 per lane)
+constexpr uint64_t WC_TPW = 16;     // tiles per wave (a chunk)
+
 struct WcArgs {
   int64_t n_keys;
   int64_t n_docs;
   const uint64_t* doc_key;   // [n_docs] key of each document
   const uint64_t* doc_off;   // [n_docs+1] byte offsets
+  const uint64_t* tile_ptr;  // [n_docs+1] first chunk (WC_TPW tiles) of each document, global index
+  uint64_t tile0;            // first chunk of this launch (= tile_ptr[0])
   const uint8_t* bytes;
   uint64_t n_bytes;
   int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)

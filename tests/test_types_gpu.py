@@ -213,6 +213,31 @@ def test_wordcount_generated_corpus(gpu, wdc):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_tile_edges(gpu, wdc):
+    """Documents are split into 4 KiB tiles (one wave each): tokens that cross
+    tile boundaries, a token longer than several tiles, separators on the
+    last/first byte of a tile, a document of exactly one tile (its trailing
+    position starts the next tile) and the same words in many tiles of one
+    document (worddocumentcount counts them once)."""
+    T = 4096
+    d1 = bytearray(b"ab " * 5000)
+    d1[T - 1] = 0x20
+    d1[T] = 0x0A
+    d1[2 * T - 1] = 0x0A
+    d2 = b"q" * (3 * T + 17) + b" tail"
+    d3 = b"x" * (T - 1) + b" "          # exactly one tile, ends in a separator
+    d4 = b"y" * T                       # exactly one tile, no separator
+    d5 = b" ".join([b"ab", b"cd"] * 4000) + b"  "
+    docs = [[bytes(d1), d2, d3], [d4, d5, b"", b" "]]
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    e, o = E(2), orc.WcOracle(2, wdc)
+    e.apply_docs(docs)
+    o.apply_docs(docs)
+    for x, y in zip(e.export(), o.export()):
+        assert np.array_equal(x, y)
+
+
 def test_wordcount_lds_overflow_path(gpu):
     """A document with far more distinct words than the per-document LDS
     table (512) exercises the global path (and the wdc dedupe table)."""
