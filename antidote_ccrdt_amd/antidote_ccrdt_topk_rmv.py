@@ -14,11 +14,9 @@ function_clause); integers outside int64 raise the engine's ERANGE error.
 """
 from __future__ import annotations
 
-import io
-
 import numpy as np
 
-from . import terms
+from . import etf, terms
 from ._lib import NOOP
 from .engine import TopkRmvEngine, TrmvState
 
@@ -145,22 +143,56 @@ def equal(a: TopkRmv, b: TopkRmv) -> bool:
     return a.size == b.size and a._export()["obs"] == b._export()["obs"]
 
 
+def _atom(dc):
+    return etf.Atom(dc) if isinstance(dc, str) and not isinstance(dc, etf.Atom) else dc
+
+
 def to_binary(state: TopkRmv) -> bytes:
-    """to_binary/1 (topk_rmv.erl:156-158).  Canonical image, not ETF
-    (the ETF codec is SURVEY §8f rank 2)."""
-    st = state.engine.export()
-    buf = io.BytesIO()
-    np.savez(buf, size=np.int64(state.size), **st.__dict__)
-    return buf.getvalue()
+    """to_binary/1 (topk_rmv.erl:156-158): term_to_binary of the 6-tuple
+    {Observed, Masked, Removals, Vc, Min, Size}; Masked[Id] is a gb_sets set
+    and DcIds are atoms (etf.py)."""
+    obs, masked, rem, vc, mn, size = state.to_term()
+    el = lambda e: (e[0], e[1], (_atom(e[2][0]), e[2][1]))
+    term = ({i: el(e) for i, e in obs.items()},
+            {i: etf.GbSet(el(e) for e in v) for i, v in masked.items()},
+            {i: {_atom(d): t for d, t in v.items()} for i, v in rem.items()},
+            {_atom(d): t for d, t in vc.items()},
+            el(mn) if mn != NIL else (etf.Atom("nil"),) * 3, size)
+    return etf.term_to_binary(term)
 
 
 def from_binary(b: bytes):
-    """from_binary/1 (topk_rmv.erl:161-163)."""
-    with np.load(io.BytesIO(b), allow_pickle=False) as z:
-        size = int(z["size"])
-        d = {k: z[k] for k in z.files if k != "size"}
+    """from_binary/1 (topk_rmv.erl:161-163): decodes any ERTS shape of the
+    6-tuple (gb_sets trees, maps) into an engine-resident state."""
+    t = etf.binary_to_term(b)
+    if not (isinstance(t, tuple) and len(t) == 6 and all(isinstance(x, dict) for x in t[:4])):
+        raise etf.EtfError("not a topkrmv() term")
+    obs, masked, rem, vc, mn, size = t
+    if not (_is_int(size) and size > 0):
+        raise etf.EtfError("topkrmv() Size must be a positive integer")
+    rank = lambda d: terms.DC_REGISTRY.rank(str(d))
+    nd = terms.DC_REGISTRY.capacity
+    el = lambda e: (int(e[1]), int(e[0]), rank(e[2][0]), int(e[2][1]))  # (id, score, dc, ts)
+    o = sorted(el(e) for e in obs.values())
+    m = sorted(el(e) for v in masked.values() for e in etf.gb_set_items(v))
+    r = sorted(rem.items())
+    st = TrmvState.empty(1, nd, len(o), len(m), len(r))
+    for d, ts in vc.items():
+        st.vc[0, rank(d)] = ts
+    st.obs_ptr[1], st.m_ptr[1], st.r_ptr[1] = len(o), len(m), len(r)
+    for j, (i, sc, d, ts) in enumerate(o):
+        st.obs_id[j], st.obs_score[j], st.obs_dc[j], st.obs_ts[j] = i, sc, d, ts
+    for j, (i, sc, d, ts) in enumerate(m):
+        st.m_id[j], st.m_score[j], st.m_dc[j], st.m_ts[j] = i, sc, d, ts
+    for j, (i, v) in enumerate(r):
+        st.r_id[j] = i
+        for d, ts in v.items():
+            st.r_vc[j, rank(d)] = ts
+    if mn != (etf.Atom("nil"),) * 3:
+        i, sc, d, ts = el(mn)
+        st.min_valid[0], st.min_id[0], st.min_score[0], st.min_dc[0], st.min_ts[0] = 1, i, sc, d, ts
     eng = _engine(size)
-    eng.import_state(TrmvState(**d))
+    eng.import_state(st)
     return ("ok", TopkRmv(size, eng))
 
 

@@ -220,7 +220,7 @@ def main():
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_sample_keys > 0:  # reported at N=1 only
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import numpy as np
@@ -240,6 +240,16 @@ def main():
                "sample": f"first {m} keys of the rank-0 batch = {n_s} effect ops, C++ -O3 "
                          f"restatement (oracle/ccrdt_oracle.hpp), 1 thread on {cpu_model()}; "
                          f"CPU restatement, not BEAM (no Erlang runtime in the image)"}
+        del o
+        # the same sample with keys partitioned over the box's CPU share
+        # (single-threaded AND all cores); reported in detail
+        nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        o = orc.TrmvOracle(m, args.k, args.n_dc)
+        tc = time.perf_counter()
+        o.apply(sb, nt, want_extra=True)
+        tc = time.perf_counter() - tc
+        cpu_mt = {"value": n_s / tc, "unit": "ops/s", "cores": nt, "kind": "port",
+                  "sample": f"same sample, keys partitioned statically over {nt} std::threads"}
         del o
 
     if rank == 0:
@@ -284,6 +294,7 @@ def main():
                 "apply_chain": {"kernel_ms": chain_ms, "algorithmic_bytes": alg_bytes,
                                 "achieved_GBs": alg_bytes / (chain_ms * 1e-3) / 1e9},
                 "extra_effects": n_extra,
+                "cpu_baseline_threads": cpu_mt,
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),

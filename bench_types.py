@@ -53,13 +53,38 @@ def timed(eng, step, steps, warmup):
     return (time.perf_counter() - t0) * 1000.0 / steps, sum(kms) / len(kms)
 
 
-def line(name, config, units, unit_name, ms_step, kernel_ms, alg_bytes, extra=None):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_leg(fn, units, unit_name, sample):
+    """cpu_baseline: the C++ oracle (oracle/ccrdt_oracle.hpp, test
+    infrastructure) timed single-threaded on a bounded sample of the same
+    workload.  A CPU restatement, not BEAM (no Erlang runtime in the image)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    t = time.perf_counter()
+    fn()
+    dt = time.perf_counter() - t
+    return {"value": units / dt, "unit": unit_name, "cores": 1, "kind": "port",
+            "sample": f"{sample}; C++ -O3 restatement, 1 thread on {cpu_model()}, {dt:.2f} s"}
+
+
+def line(name, config, units, unit_name, ms_step, kernel_ms, alg_bytes, extra=None, cpu=None):
     ach = alg_bytes / (kernel_ms * 1e-3) / 1e9
     out = {"workload": name, "config": config, "value": units / (ms_step * 1e-3),
            "unit": unit_name, "ms_per_step": ms_step, "higher_is_better": True,
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
                         "kernel_ms": kernel_ms}}
+    if cpu:
+        out["cpu_baseline"] = cpu
     if extra:
         out["detail"] = extra
     print(json.dumps(out), flush=True)
@@ -80,17 +105,30 @@ def bench_topk(args, rng):
     ms, kms = timed(eng, step, args.steps, args.warmup)
     entries = eng.size()
     alg = n * 16 + (nk + 1) * 8 + entries * 16 + nk * 8
+    cpu = None
+    if args.cpu:
+        import oracle as orc
+        ks = nk // 16
+        m = int(kp[ks])
+        o = orc.TopkOracle(ks, 100)
+        cpu = cpu_leg(lambda: o.apply(kp[:ks + 1], pid[:m], sc[:m]), m, "ops/s",
+                      f"first {ks} keys = {m} add ops")
     line("topk", f"antidote_ccrdt_topk update/2: {n} add ops over {nk} keys, id U[0,1000), "
          "score U[1,1e6], fresh keys, ops in HBM", n, "ops/s", ms, kms, alg,
-         {"entries": entries})
+         {"entries": entries}, cpu)
     # value/1: full segmented sort of every key (Score desc, Id desc)
     t = time.perf_counter()
     p, i, s = eng.value()
     vt = (time.perf_counter() - t) * 1000.0
     vk = eng.last_kernel_ms()
+    cpu = None
+    if args.cpu:
+        ne = int(o.export()[0][-1])
+        cpu = cpu_leg(lambda: o.export(value_order=True), ne, "entries/s",
+                      f"value/1 (full sort) of the first {ks} keys' state = {ne} entries")
     line("topk_value", f"antidote_ccrdt_topk value/1 of all {nk} keys ({entries} entries), "
          "host copy-out included in ms_per_step", entries, "entries/s", vt, vk, entries * 32 + nk * 16,
-         {"note": "kernel_ms = the sort kernels; ms_per_step includes the D2H copy of the result"})
+         {"note": "kernel_ms = the sort kernels; ms_per_step includes the D2H copy of the result"}, cpu)
     d.close()
 
 
@@ -112,9 +150,17 @@ def bench_leaderboard(args, rng):
     no, nm, nb = eng.sizes()
     n_ban = int(ban.sum())
     alg = (n - n_ban) * 17 + n_ban * 9 + (nk + 1) * 8 + (no + nm) * 16 + nb * 8 + nk * 16
+    cpu = None
+    if args.cpu:
+        import oracle as orc
+        ks = nk // 10
+        m = int(kp[ks])
+        o = orc.LbOracle(ks, 100)
+        cpu = cpu_leg(lambda: o.apply(kp[:ks + 1], kind[:m], pid[:m], sc[:m]), m, "ops/s",
+                      f"first {ks} boards = {m} ops")
     line("leaderboard", f"antidote_ccrdt_leaderboard update/2: {n} ops over {nk} boards, 99% add / "
          "1% ban, id U[0,1e4), score U[0,1e6], K=100, fresh boards, ops in HBM", n, "ops/s", ms, kms,
-         alg, {"observed": no, "masked": nm, "bans": nb})
+         alg, {"observed": no, "masked": nm, "bans": nb}, cpu)
     d.close()
 
 
@@ -145,11 +191,19 @@ def bench_wordcount(args, rng, wdc):
     nw, nb = eng.sizes()
     alg = b.shape[0] + (n_docs + 1) * 8 + nw * 24 + nb
     name = "worddocumentcount" if wdc else "wordcount"
+    cpu = None
+    if args.cpu:
+        import oracle as orc
+        nd_s = 64
+        nbytes = int(off[nd_s])
+        o = orc.WcOracle(1, wdc)
+        cpu = cpu_leg(lambda: o.apply(np.array([0, nd_s], np.uint64), off[:nd_s + 1], b[:nbytes]),
+                      nbytes, "bytes/s", f"first {nd_s} documents = {nbytes} bytes")
     line("wdc" if wdc else "wordcount",
          f"antidote_ccrdt_{name} update/2: {b.shape[0] / 2**30:.0f} GiB Zipf(1) corpus, {n_docs} docs "
          "of 1 MiB, 1M-word vocabulary (1/8 of the 64 GB 8-GPU config), one object, corpus in HBM",
          b.shape[0], "bytes/s", ms, kms, alg,
-         {"distinct_words": nw, "word_bytes": nb, "gen_s": round(CORPUS.get("gen_s", 0), 1)})
+         {"distinct_words": nw, "word_bytes": nb, "gen_s": round(CORPUS.get("gen_s", 0), 1)}, cpu)
     d.close()
     del eng
 
@@ -168,8 +222,13 @@ def bench_average(args, rng):
         eng.apply_device(d)
     ms, kms = timed(eng, step, args.steps, args.warmup)
     alg = n * 16 + (nk + 1) * 8 + nk * 16
+    cpu = None
+    if args.cpu:
+        import oracle as orc
+        z = np.zeros(nk, np.int64)
+        cpu = cpu_leg(lambda: orc.avg_apply(kp, v, nn, z, z), n, "ops/s", f"the whole batch ({n} adds)")
     line("average", f"antidote_ccrdt_average update/2: {n} adds over {nk} keys (V U[0,2^20), N=1), "
-         "ops in HBM", n, "ops/s", ms, kms, alg)
+         "ops in HBM", n, "ops/s", ms, kms, alg, None, cpu)
     d.close()
 
 
@@ -184,6 +243,8 @@ def main():
     ap.add_argument("--topk-ops", type=int, default=100_000_000)
     ap.add_argument("--lb-ops", type=int, default=50_000_000)
     ap.add_argument("--corpus-gib", type=float, default=8.0)
+    ap.add_argument("--no-cpu", dest="cpu", action="store_false",
+                    help="skip the cpu_baseline legs (oracle timed on a bounded sample)")
     args = ap.parse_args()
     from antidote_ccrdt_amd import _lib
     if _lib.device_count() < 1:

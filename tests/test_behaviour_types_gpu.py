@@ -1,0 +1,146 @@
+"""Behaviour mirrors of average, topk, leaderboard, wordcount and
+worddocumentcount (antidote_ccrdt_amd/behaviours.py) replaying the reference's
+EUnit vectors (tests/golden/) through their callbacks; every update/2 runs
+the type's gfx950 kernel.  Plus to_binary/from_binary round trips in the
+Erlang external term format for all six types."""
+import pytest
+
+from antidote_ccrdt_amd import antidote_ccrdt_topk_rmv as trmv
+from antidote_ccrdt_amd import behaviours as bh
+from antidote_ccrdt_amd import etf, terms
+from trmv_helpers import load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fx", load("average"), ids=[f["name"] for f in load("average")])
+def test_average_golden(gpu, fx):
+    A = bh.average
+    if "equal" in fx:
+        for a, b, want in fx["equal"]:
+            assert A.equal(A.new(*a), A.new(*b)) == want
+        return
+    st = A.new(*fx["init"]) if "init" in fx else A.new()
+    for v, n in fx["ops"]:
+        st = A.update(("add", (v, n)), st)[1]
+    assert st.to_term() == tuple(fx["state"])
+    if "value" in fx:
+        assert A.value(st) == fx["value"]  # bit-exact fp64 (erlang:'/')
+
+
+def test_average_clauses(gpu):
+    A = bh.average
+    st = A.update(("add", 5), A.new())[1]
+    assert A.update(("add", (99, 0)), st)[1].to_term() == (5, 1)  # {add, {_, 0}} (Q14)
+    for bad in [("add", (1, -1)), ("add", 1.5), ("mul", 2)]:
+        with pytest.raises(bh.FunctionClause):
+            A.update(bad, st)
+    with pytest.raises(ZeroDivisionError):
+        A.value(A.new())
+    ok, st2 = A.from_binary(A.to_binary(st))
+    assert ok == "ok" and A.equal(st, st2)
+    assert A.to_binary(A.new(4, 5)).hex() == "83680261046105"
+
+
+def test_topk_golden(gpu):
+    T = bh.topk
+    fx = {f["name"]: f for f in load("topk")}
+    assert T.new().size == fx["new_test"]["new_size"]  # Q8: the source's new(1000)
+    f = fx["value_test"]
+    st = T.new({i: s for i, s in f["state"]}, f["size"])
+    assert T.value(st) == [tuple(x) for x in f["value"]]
+    f = fx["downstream_add_test"]
+    st = T.new({i: s for i, s in f["state"]}, f["size"])
+    for (i, s), want in f["downstream"]:
+        got = T.downstream(("add", (i, s)), st)[1]
+        assert (got if got == "noop" else got[0]) == want
+    f = fx["update_add_test"]
+    st = T.new(f["size"])
+    for i, s in f["ops"]:
+        st = T.update(("add", (i, s)), st)[1]
+    assert T.value(st) == [tuple(x) for x in f["value"]]
+    st = T.update(("add_map", {7: 1, 2: 5}), st)[1]  # maps:merge: the map's scores win
+    assert st.to_term()[0] == {0: 102, 2: 5, 7: 1}
+    ok, st2 = T.from_binary(T.to_binary(st))
+    assert ok == "ok" and T.equal(st, st2)
+
+
+def _lb_term(e):
+    if e == "noop":
+        return ["noop"]
+    tag, p = e
+    return [tag, *p] if isinstance(p, tuple) else [tag, p]
+
+
+@pytest.mark.parametrize("fx", [f for f in load("leaderboard") if "steps" in f],
+                         ids=[f["name"] for f in load("leaderboard") if "steps" in f])
+def test_leaderboard_golden(gpu, fx):
+    L = bh.leaderboard
+    states = {}
+    get = lambda n: states[n] if n in states else L.new(fx["size"])  # unnamed = new()
+    canon = lambda s: {"obs": sorted(s["obs"]), "masked": sorted(s["masked"]),
+                       "bans": sorted(s["bans"]), "min": s["min"]}
+    for step in fx["steps"]:
+        if "update" in step:
+            u = step["update"]
+            eff = (u[0], (u[1], u[2])) if u[0] in ("add", "add_r") else (u[0], u[1])
+            res = L.update(eff, get(step["on"]))
+            assert (_lb_term(res[2][0]) if len(res) == 3 else None) == step["extra"], step
+            states[step["as"]] = res[1]
+            if "expect" in step:
+                assert canon(res[1].key_state()) == canon(step["expect"]), step
+        elif "downstream" in step:
+            d = step["downstream"]
+            op = ("add", (d[1], d[2])) if d[0] == "add" else ("ban", d[1])
+            assert _lb_term(L.downstream(op, get(step["on"]))[1]) == step["expect"], step
+        elif "value" in step:
+            assert sorted(L.value(get(step["value"]))) == sorted(tuple(x) for x in step["expect"])
+        elif "check" in step:
+            assert canon(get(step["check"]).key_state()) == canon(step["expect"])
+    for st in states.values():  # ETF round trip of every state reached
+        ok, st2 = L.from_binary(L.to_binary(st))
+        assert ok == "ok" and st2.key_state() == st.key_state() and L.equal(st, st2)
+
+
+@pytest.mark.parametrize("fx", load("wordcount"), ids=[f["name"] for f in load("wordcount")])
+def test_wordcount_golden(gpu, fx):
+    W = bh.worddocumentcount if fx["type"] == "worddocumentcount" else bh.wordcount
+    st = W.new()
+    for d in fx["docs"]:
+        st = W.update(("add", d.encode()), st)[1]
+    assert W.value(st) == {k.encode(): v for k, v in fx["expect"].items()}
+    if "then" in fx:
+        for d in fx["then"]["docs"]:
+            st = W.update(("add", d.encode()), st)[1]
+        assert W.value(st) == {k.encode(): v for k, v in fx["then"]["expect"].items()}
+    ok, st2 = W.from_binary(W.to_binary(st))
+    assert ok == "ok" and W.equal(st, st2)
+
+
+def test_wordcount_empty_tokens_roundtrip(gpu):
+    for W in (bh.wordcount, bh.worddocumentcount):
+        st = W.update(("add", b"a  b\n\na "), W.new())[1]
+        st = W.update(("add", b"a"), st)[1]
+        want = {b"a": 3, b"b": 1, b"": 3} if W is bh.wordcount else {b"a": 2, b"b": 1, b"": 1}
+        assert W.value(st) == want  # Q13: empty tokens counted
+        assert W.from_binary(W.to_binary(st))[1].to_term() == want
+
+
+def test_topk_rmv_etf_roundtrip(gpu, monkeypatch):
+    names = ("dc1", "dc2", "dc3")
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry(names))
+    t = trmv.new(2)
+    ops = [("add", (1, 10, ("dc2", 5))), ("add", (1, 10, ("dc1", 9))), ("add", (2, 7, ("dc3", 2))),
+           ("add", (3, 8, ("dc1", 11))), ("rmv", (2, {"dc3": 2, "dc1": 1})), ("add", (1, 12, ("dc3", 3)))]
+    for e in ops:
+        t = trmv.update(e, t)[1]
+    b = trmv.to_binary(t)
+    term = etf.binary_to_term(b)
+    obs, masked, rem, vc, mn, size = term
+    assert size == 2 and set(vc) == {"dc1", "dc2", "dc3"} and all(isinstance(d, etf.Atom) for d in vc)
+    assert etf.gb_set_items(masked[1]) == sorted(etf.gb_set_items(masked[1]), key=etf._Ord)
+    ok, t2 = trmv.from_binary(b)
+    assert ok == "ok" and t2.to_term() == t.to_term() and trmv.equal(t, t2)
+    empty = trmv.new(5)
+    assert etf.binary_to_term(trmv.to_binary(empty))[4] == (etf.Atom("nil"),) * 3
+    assert trmv.from_binary(trmv.to_binary(empty))[1].to_term() == empty.to_term()
