@@ -64,11 +64,20 @@ def cpu_model():
     return "unknown CPU"
 
 
+def _oracle():
+    """The parity oracle's ctypes module (test infrastructure; cpu_baseline only)."""
+    p = os.path.join(ROOT, "oracle")
+    if sys.path[0] != p:
+        sys.path.insert(0, p)
+    sys.modules.pop("oracle", None)  # not the repo's oracle/ directory as a namespace package
+    import oracle
+    return oracle
+
+
 def cpu_leg(fn, units, unit_name, sample):
     """cpu_baseline: the C++ oracle (oracle/ccrdt_oracle.hpp, test
     infrastructure) timed single-threaded on a bounded sample of the same
     workload.  A CPU restatement, not BEAM (no Erlang runtime in the image)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     t = time.perf_counter()
     fn()
     dt = time.perf_counter() - t
@@ -107,7 +116,7 @@ def bench_topk(args, rng):
     alg = n * 16 + (nk + 1) * 8 + entries * 16 + nk * 8
     cpu = None
     if args.cpu:
-        import oracle as orc
+        orc = _oracle()
         ks = nk // 16
         m = int(kp[ks])
         o = orc.TopkOracle(ks, 100)
@@ -152,7 +161,7 @@ def bench_leaderboard(args, rng):
     alg = (n - n_ban) * 17 + n_ban * 9 + (nk + 1) * 8 + (no + nm) * 16 + nb * 8 + nk * 16
     cpu = None
     if args.cpu:
-        import oracle as orc
+        orc = _oracle()
         ks = nk // 10
         m = int(kp[ks])
         o = orc.LbOracle(ks, 100)
@@ -193,7 +202,7 @@ def bench_wordcount(args, rng, wdc):
     name = "worddocumentcount" if wdc else "wordcount"
     cpu = None
     if args.cpu:
-        import oracle as orc
+        orc = _oracle()
         nd_s = 64
         nbytes = int(off[nd_s])
         o = orc.WcOracle(1, wdc)
@@ -224,7 +233,7 @@ def bench_average(args, rng):
     alg = n * 16 + (nk + 1) * 8 + nk * 16
     cpu = None
     if args.cpu:
-        import oracle as orc
+        orc = _oracle()
         z = np.zeros(nk, np.int64)
         cpu = cpu_leg(lambda: orc.avg_apply(kp, v, nn, z, z), n, "ops/s", f"the whole batch ({n} adds)")
     line("average", f"antidote_ccrdt_average update/2: {n} adds over {nk} keys (V U[0,2^20), N=1), "
