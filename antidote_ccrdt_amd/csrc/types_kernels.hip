@@ -628,6 +628,8 @@ int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
   if (cls == 0)
     hipLaunchKernelGGL(lb_apply_kernel<512>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   else if (cls == 1)
+    hipLaunchKernelGGL(lb_apply_kernel<1024>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 2)
     hipLaunchKernelGGL(lb_apply_kernel<2048>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(lb_apply_hbm_kernel, dim3((unsigned)n_work), dim3(64), 0, st, a);
