@@ -659,8 +659,13 @@ overflow:
   }
 }
 
+// S = 4 is held to 128 VGPRs (4 waves per SIMD; it spills ~200 B per lane):
+// it runs beside tier 0 on the side chain, and a wave that needs more
+// registers than one retiring tier-0 wave frees is not dispatched until
+// tier 0 has drained (unbounded, 184 VGPRs: the side chain's class 4 took
+// ~1.9 ms instead of 0.22 ms)
 template <int S>
-__global__ __launch_bounds__(64) void trmv_apply_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(64, S == 4 ? 4 : 1) void trmv_apply_kernel(TrmvApplyArgs a) {
   __shared__ SeqLds<S> lds;
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {

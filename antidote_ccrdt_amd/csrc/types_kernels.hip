@@ -848,7 +848,6 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   wc_tile(a, a.tile0 + blockIdx.x, d, tile);
   const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
   const uint32_t key = (uint32_t)a.doc_key[d];
-  const uint8_t* doc = a.bytes + b0;
   for (int i = lane; i < WC_LDS; i += 64) {
     lh[i] = 0ull;
     lc[i] = 0u;
@@ -912,7 +911,6 @@ __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
   wc_tile(a, a.tile0 + blockIdx.x, d, tile);
   const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
   const uint32_t key = (uint32_t)a.doc_key[d];
-  const uint8_t* doc = a.bytes + b0;
   for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
   __syncthreads();
   const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
