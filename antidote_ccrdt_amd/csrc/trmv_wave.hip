@@ -708,6 +708,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // The next key's ops are retired before this key's first store, so the
   // next key never waits on (and its vmcnt never counts) these stores.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // the next key's clock loads go out before this key's first store: a
+  // load's data waits for every older vector-memory op, stores included
+  if (FRESH && has_next) wave_load_rows(a, L, nxt);
   PROF_MARK(7);
   uint32_t best_q = NONE32;                      // Min candidate of this lane
   int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
@@ -872,8 +875,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
   }
   wave_lds_sync();
-  // the next key's clock loads (after the replay: its registers are free)
-  if (has_next) wave_load_rows(a, L, nxt);
+  // non-FRESH keys: the next key's clock loads after the replay (registers)
+  if (!FRESH && has_next) wave_load_rows(a, L, nxt);
 
   PROF_MARK(4);
   // ---- 6. player records, final pool order, Removals rows
