@@ -347,11 +347,11 @@ int ccrdt_topk_apply_device(ccrdt_engine* e, const ccrdt_topk_ops* ops) {
   uint64_t n_work = nk;
   const uint32_t* list = nullptr;
   float total_ms = 0.f;
-  for (int cls = 0; cls < 3 && n_work; ++cls) {
+  for (int cls = 0; cls < 4 && n_work; ++cls) {
     DevBuf* ovf = (list == T.ovf_a.as<uint32_t>()) ? &T.ovf_b : &T.ovf_a;
     a.key_list = list;
     a.ovf_list = ovf->as<uint32_t>();
-    if (cls == 2) {  // HBM hash: cap + 1 slots per key
+    if (cls == 3) {  // HBM hash: cap + 1 slots per key
       uint64_t slots = 0;
       CCRDT_TRY(hbm_regions(e, list, n_work, ops->key_ptr, e->fresh ? nullptr : a.cnt_in, 1, 2, &slots));
       slots += n_work;

@@ -1147,12 +1147,16 @@ int avg_launch_value(const int64_t* sum, const int64_t* num, int64_t n_keys, int
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-// cls 0: <= 512 entries per key (LDS hash 1024), 1: <= 4096 (hash 8192)
+// cls 0: <= 128 entries per key (LDS hash 256: 4 KB, a quarter of the
+// init and compaction passes of the next class), 1: <= 512 (hash 1024),
+// 2: <= 4096 (hash 8192), 3: HBM
 int topk_launch_apply(const TopkArgs& a, int cls, uint64_t n_work, hipStream_t st) {
   if (n_work == 0) return CCRDT_OK;
   if (cls == 0)
-    hipLaunchKernelGGL(topk_apply_kernel<1024>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(topk_apply_kernel<256>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   else if (cls == 1)
+    hipLaunchKernelGGL(topk_apply_kernel<1024>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 2)
     hipLaunchKernelGGL(topk_apply_kernel<8192>, dim3((unsigned)n_work), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(topk_apply_hbm_kernel, dim3((unsigned)n_work), dim3(TK_HBM_BLOCK), 0, st, a);
