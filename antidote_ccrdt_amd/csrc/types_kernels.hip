@@ -361,30 +361,65 @@ __device__ __forceinline__ bool lb_cmp(int64_t i1, int64_t s1, int64_t i2, int64
   return s1 > s2 || (s1 == s2 && i1 > i2);  // cmp/2 (:289-294)
 }
 
-template <int E>
+template <int E, int H>
 struct LbLds {
   int64_t eid[E];
   int64_t esc[E];
   uint8_t est[E];
-  uint32_t hslot[2 * E];  // entry + 1, 0 = empty
+  uint16_t hslot[H];  // entry + 1, 0 = empty (E <= 2048 fits 16 bits); H >= 1.6 E
 };
 
 // The board's storage: LDS (classes 0/1) or an HBM scratch region (class 2,
 // boards beyond 2048 entries); E is a power of two, the hash has 2E slots.
+template <typename HS>
 struct LbView {
   int64_t* eid;
   int64_t* esc;
   uint8_t* est;
-  uint32_t* hslot;
+  HS* hslot;
   uint32_t hmask;  // 2E - 1
+  // Observed as a list of entry indices (LDS, LB_OL slots), so that the Min
+  // rescan after an eviction reads K entries instead of every entry of the
+  // board.  Off when K > LB_OL or entry indices exceed 16 bits.
+  uint16_t* ol;
+  bool use_ol;
 };
+
+constexpr uint32_t LB_OL = 256;
+
+// Claim an empty hash slot (0 -> v).  LDS has no 16-bit CAS: the 16-bit slot
+// is claimed by a 32-bit CAS on its aligned word.
+__device__ __forceinline__ bool lb_claim(uint32_t* p, uint32_t v) { return atomicCAS(p, 0u, v) == 0u; }
+__device__ __forceinline__ bool lb_claim(uint16_t* p, uint32_t v) {
+  uint32_t* w = (uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t sh = ((uintptr_t)p & 2) ? 16u : 0u;
+  uint32_t old = *w;
+  while (true) {
+    if ((old >> sh) & 0xFFFFu) return false;
+    const uint32_t prev = atomicCAS(w, old, old | (v << sh));
+    if (prev == old) return true;
+    old = prev;
+  }
+}
+
+// wave-uniform position of entry e in the Observed list (it is there)
+template <typename V>
+__device__ __forceinline__ uint32_t lb_ol_find(const V& L, uint32_t nol, uint32_t e) {
+  const int lane = lane_id();
+  for (uint32_t b = 0; b < nol; b += 64) {
+    const uint64_t hit = ballot(b + lane < nol && L.ol[b + lane] == e);
+    if (hit) return b + __builtin_ctzll(hit);
+  }
+  return 0;
+}
 
 __device__ __forceinline__ uint32_t lb_hash(int64_t id) {
   return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 32);
 }
 
 // wave-uniform lookup: entry index of id or NONE
-__device__ __forceinline__ uint32_t lb_find(const LbView& L, int64_t id, uint32_t& slot_out) {
+template <typename V>
+__device__ __forceinline__ uint32_t lb_find(const V& L, int64_t id, uint32_t& slot_out) {
   const int lane = lane_id();
   uint32_t h = lb_hash(id) & L.hmask;
   while (true) {
@@ -405,11 +440,24 @@ __device__ __forceinline__ uint32_t lb_find(const LbView& L, int64_t id, uint32_
   }
 }
 
-__device__ __forceinline__ void lb_recompute_min(const LbView& L, uint32_t n, uint32_t& minq) {
+template <typename V>
+__device__ __forceinline__ void lb_recompute_min(const V& L, uint32_t n, uint32_t nol, uint32_t& minq) {
   const int lane = lane_id();
   int64_t bs = INT64_MAX, bi = INT64_MAX;
   uint32_t be = 0xFFFFFFFFu;
-  for (uint32_t j = lane; j < n; j += 64) {
+  // cmp/2 is a total order on (Score, Id) and Ids are unique per board, so
+  // the scan order does not change which entry is Min.
+  if (L.use_ol) {
+    for (uint32_t j = lane; j < nol; j += 64) {
+      const uint32_t q = L.ol[j];
+      const int64_t s = L.esc[q], i = L.eid[q];
+      if (be == 0xFFFFFFFFu || lb_cmp(bi, bs, i, s)) {
+        bs = s;
+        bi = i;
+        be = q;
+      }
+    }
+  } else for (uint32_t j = lane; j < n; j += 64) {
     if (L.est[j] == LB_OBS) {
       const int64_t s = L.esc[j], i = L.eid[j];
       if (be == 0xFFFFFFFFu || lb_cmp(bi, bs, i, s)) {
@@ -431,7 +479,8 @@ __device__ __forceinline__ void lb_recompute_min(const LbView& L, uint32_t n, ui
 }
 
 // One board: old entries into L, replay the ops, write the new segment.
-__device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMeta& om, const LbView& L) {
+template <typename V>
+__device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMeta& om, const V& L) {
   const int lane = lane_id();
   const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
   for (uint32_t i = lane; i <= L.hmask; i += 64) L.hslot[i] = 0;
@@ -442,9 +491,21 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
     L.esc[j] = a.score_in[om.off + j];
     L.est[j] = a.st_in[om.off + j];
     uint32_t h = lb_hash(id) & L.hmask;
-    while (atomicCAS(&L.hslot[h], 0u, j + 1) != 0u) h = (h + 1) & L.hmask;
+    while (!lb_claim(&L.hslot[h], j + 1)) h = (h + 1) & L.hmask;
   }
   __syncthreads();
+  uint32_t nol = 0;
+  if (L.use_ol) {
+    for (uint32_t b = 0; b < om.n; b += 64) {
+      const uint32_t j = b + lane;
+      const bool o = j < om.n && L.est[j] == LB_OBS;
+      const uint64_t m = ballot(o);
+      const uint32_t p = nol + mbcnt(m);
+      if (o && p < LB_OL) L.ol[p] = (uint16_t)j;
+      nol += (uint32_t)__builtin_popcountll(m);
+    }
+    __syncthreads();
+  }
   uint32_t n = om.n, nobs = om.nobs, minq = om.minq, nex = 0;
   for (uint64_t base = op0; base < op1; base += 64) {
     const uint64_t i = base + lane;
@@ -478,6 +539,11 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
         __syncthreads();
         if (was_obs) {
           --nobs;
+          if (L.use_ol) {
+            const uint32_t p = lb_ol_find(L, nol, e);
+            if (lane == 0) L.ol[p] = L.ol[nol - 1];
+            --nol;
+          }
           // get_largest(Masked) (:306-312)
           int64_t bs = INT64_MIN, bi = INT64_MIN;
           uint32_t be = 0xFFFFFFFFu;
@@ -494,6 +560,7 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
             const uint32_t m = rl32(be, __builtin_ctzll(ballot(has && bs == ms && bi == mi)));
             if (lane == 0) {
               L.est[m] = LB_OBS;
+              if (L.use_ol) L.ol[nol] = (uint16_t)m;
               LbExtraRec r;
               r.op = (uint32_t)(base + j);
               r.pad = 0;
@@ -503,10 +570,11 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
             }
             ++nex;
             ++nobs;
+            ++nol;
             minq = m;  // Min := promoted element (:282, Q15)
           } else if (minq == e) {
             __syncthreads();
-            lb_recompute_min(L, n, minq);
+            lb_recompute_min(L, n, nol, minq);
           }
         }
         __syncthreads();
@@ -519,7 +587,7 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
         if (sc > L.esc[e]) {
           if (lane == 0) L.esc[e] = sc;
           __syncthreads();
-          if (minq == e) lb_recompute_min(L, n, minq);
+          if (minq == e) lb_recompute_min(L, n, nol, minq);
         }
         continue;
       }
@@ -531,9 +599,13 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
             L.est[e] = LB_OBS;
             L.esc[e] = sc;
           }
+          if (L.use_ol) {  // e takes Min's place in the Observed list
+            const uint32_t p = lb_ol_find(L, nol, minq);
+            if (lane == 0) L.ol[p] = (uint16_t)e;
+          }
           if (lane == 0) L.est[minq] = LB_MASKED;
           __syncthreads();
-          lb_recompute_min(L, n, minq);
+          lb_recompute_min(L, n, nol, minq);
         } else if (e == 0xFFFFFFFFu) {  // Masked[Id] := max (:243-250)
           create(LB_MASKED, sc);
         } else if (sc > L.esc[e]) {
@@ -545,6 +617,8 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
           L.est[e] = LB_OBS;
           L.esc[e] = sc;
         }
+        if (L.use_ol && lane == 0) L.ol[nol] = (uint16_t)e;
+        ++nol;
         ++nobs;
         if (minq == 0xFFFFFFFFu || lb_cmp(L.eid[minq], L.esc[minq], id, sc)) minq = e;
       }
@@ -565,9 +639,9 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
   }
 }
 
-template <int E>
+template <int E, int H>
 __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
-  __shared__ LbLds<E> S;
+  __shared__ LbLds<E, H> S;
   const uint64_t w = blockIdx.x;
   const uint32_t k = a.key_list ? a.key_list[w] : (uint32_t)w;
   LbMeta om{0, 0, 0, 0xFFFFFFFFu};
@@ -576,7 +650,8 @@ __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
     if (lane_id() == 0) a.ovf_list[atomicAdd(&a.status[0], 1u)] = k;
     return;
   }
-  lb_board(a, k, om, LbView{S.eid, S.esc, S.est, S.hslot, 2 * E - 1});
+  __shared__ uint16_t OL[LB_OL];
+  lb_board(a, k, om, LbView<uint16_t>{S.eid, S.esc, S.est, S.hslot, H - 1, OL, a.k <= LB_OL && om.nobs <= LB_OL});
 }
 
 // Boards beyond the LDS classes: the same replay over an HBM scratch region
@@ -588,7 +663,10 @@ __global__ __launch_bounds__(64) void lb_apply_hbm_kernel(LbArgs a) {
   if (!a.fresh) om = a.meta_in[k];
   const uint64_t o = a.tab_off[w];
   const uint32_t E = a.tab_cap[w];
-  lb_board(a, k, om, LbView{a.g_eid + o, a.g_esc + o, a.g_est + o, a.g_hslot + 2 * o, 2 * E - 1});
+  __shared__ uint16_t OL[LB_OL];
+  lb_board(a, k, om,
+           LbView<uint32_t>{a.g_eid + o, a.g_esc + o, a.g_est + o, a.g_hslot + 2 * o, 2 * E - 1, OL,
+                  a.k <= LB_OL && om.nobs <= LB_OL && E <= 65536u});
 }
 
 // downstream/2 (leaderboard.erl:93-116), one wave per request, read-only.
@@ -625,12 +703,16 @@ __global__ __launch_bounds__(64) void lb_downstream_kernel(LbDownArgs a) {
 
 int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
   if (n_work == 0) return CCRDT_OK;
+  // LDS per board: 17 B per entry + 2 B per hash slot + the Observed list
+  // (11.3 / 13.4 / 21.5 / 43 KB: 14 / 11 / 7 / 3 boards per CU)
   if (cls == 0)
-    hipLaunchKernelGGL(lb_apply_kernel<512>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<512, 1024>), dim3((unsigned)n_work), dim3(64), 0, st, a);
   else if (cls == 1)
-    hipLaunchKernelGGL(lb_apply_kernel<1024>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<640, 1024>), dim3((unsigned)n_work), dim3(64), 0, st, a);
   else if (cls == 2)
-    hipLaunchKernelGGL(lb_apply_kernel<2048>, dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<1024, 2048>), dim3((unsigned)n_work), dim3(64), 0, st, a);
+  else if (cls == 3)
+    hipLaunchKernelGGL((lb_apply_kernel<2048, 4096>), dim3((unsigned)n_work), dim3(64), 0, st, a);
   else
     hipLaunchKernelGGL(lb_apply_hbm_kernel, dim3((unsigned)n_work), dim3(64), 0, st, a);
   CCRDT_HIP(hipGetLastError());

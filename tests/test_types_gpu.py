@@ -47,7 +47,8 @@ def _lb_stream(rng, n, nk, n_players, smax, ban_frac):
 
 
 @pytest.mark.parametrize("cfg", [(20000, 40, 300, 10**6, 0.01, 100), (20000, 50, 30, 10, 0.05, 5),
-                                 (8000, 8, 1500, 1000, 0.02, 100), (3000, 30, 8, 4, 0.2, 1)])
+                                 (8000, 8, 1500, 1000, 0.02, 100), (3000, 30, 8, 4, 0.2, 1),
+                                 (12000, 4, 1500, 10**4, 0.02, 300)])  # K > 256: full-scan Min path
 def test_leaderboard_random(gpu, cfg):
     n, nk, npl, smax, bf, K = cfg
     rng = np.random.default_rng(n + nk)
