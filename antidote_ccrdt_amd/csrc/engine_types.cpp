@@ -589,13 +589,14 @@ int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* ops) {
   uint64_t n_work = nk;
   const uint32_t* list = nullptr;
   float total_ms = 0.f;
-  // LDS classes of 512 / 640 / 1024 / 2048 entries (occupancy 14 / 11 / 7 / 3
-  // boards per CU), then HBM boards
-  for (int cls = 0; cls < 5 && n_work; ++cls) {
+  // LDS classes: 512 / 640 / 1024 entries for boards whose Ids and Scores fit
+  // 32 bits, then 512 / 640 / 1024 / 2048 entries of 64-bit values, then HBM
+  // boards (lb_launch_apply)
+  for (int cls = 0; cls < 8 && n_work; ++cls) {
     DevBuf* ovf = (list == T.ovf_a.as<uint32_t>()) ? &T.ovf_b : &T.ovf_a;
     a.key_list = list;
     a.ovf_list = ovf->as<uint32_t>();
-    if (cls == 4) {  // HBM boards: entries + a 2x hash per board
+    if (cls == 7) {  // HBM boards: entries + a 2x hash per board
       uint64_t slots = 0;
       CCRDT_TRY(hbm_regions(e, list, n_work, ops->key_ptr,
                             e->fresh ? nullptr : (const uint32_t*)a.meta_in + 1, 4, 1, &slots));

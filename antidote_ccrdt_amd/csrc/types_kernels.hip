@@ -3,6 +3,8 @@
 #include "common.hpp"
 #include "types_kernels.hpp"
 
+#include <type_traits>
+
 namespace ccrdt {
 
 // ===================================================================== average
@@ -361,20 +363,22 @@ __device__ __forceinline__ bool lb_cmp(int64_t i1, int64_t s1, int64_t i2, int64
   return s1 > s2 || (s1 == s2 && i1 > i2);  // cmp/2 (:289-294)
 }
 
-template <int E, int H>
+// ET = int32_t for NARROW boards (every Id and Score of the board fits 32
+// bits): 9 B per entry instead of 17, about twice the boards per CU.
+template <int E, int H, typename ET>
 struct LbLds {
-  int64_t eid[E];
-  int64_t esc[E];
+  ET eid[E];
+  ET esc[E];
   uint8_t est[E];
   uint16_t hslot[H];  // entry + 1, 0 = empty (E <= 2048 fits 16 bits); H >= 1.6 E
 };
 
 // The board's storage: LDS (classes 0/1) or an HBM scratch region (class 2,
 // boards beyond 2048 entries); E is a power of two, the hash has 2E slots.
-template <typename HS>
+template <typename HS, typename ET = int64_t>
 struct LbView {
-  int64_t* eid;
-  int64_t* esc;
+  ET* eid;
+  ET* esc;
   uint8_t* est;
   HS* hslot;
   uint32_t hmask;  // 2E - 1
@@ -639,19 +643,31 @@ __device__ __forceinline__ void lb_board(const LbArgs& a, uint32_t k, const LbMe
   }
 }
 
-template <int E, int H>
+__device__ __forceinline__ bool lb_fits32(int64_t x) { return x == (int64_t)(int32_t)x; }
+
+template <int E, int H, bool NARROW>
 __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
-  __shared__ LbLds<E, H> S;
+  using ET = typename std::conditional<NARROW, int32_t, int64_t>::type;
+  __shared__ LbLds<E, H, ET> S;
   const uint64_t w = blockIdx.x;
   const uint32_t k = a.key_list ? a.key_list[w] : (uint32_t)w;
   LbMeta om{0, 0, 0, 0xFFFFFFFFu};
   if (!a.fresh) om = a.meta_in[k];
-  if ((uint64_t)om.n + (a.key_ptr[k + 1] - a.key_ptr[k]) > (uint64_t)E) {
+  const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
+  bool ovf = (uint64_t)om.n + (op1 - op0) > (uint64_t)E;
+  if (NARROW && !ovf) {  // every Id and Score of the board, old entries included
+    bool wide = false;
+    for (uint64_t i = op0 + lane_id(); i < op1; i += 64) wide |= !lb_fits32(a.id[i]) || !lb_fits32(a.score[i]);
+    for (uint32_t j = lane_id(); j < om.n; j += 64)
+      wide |= !lb_fits32(a.id_in[om.off + j]) || !lb_fits32(a.score_in[om.off + j]);
+    ovf = ballot(wide) != 0;
+  }
+  if (ovf) {
     if (lane_id() == 0) a.ovf_list[atomicAdd(&a.status[0], 1u)] = k;
     return;
   }
   __shared__ uint16_t OL[LB_OL];
-  lb_board(a, k, om, LbView<uint16_t>{S.eid, S.esc, S.est, S.hslot, H - 1, OL, a.k <= LB_OL && om.nobs <= LB_OL});
+  lb_board(a, k, om, LbView<uint16_t, ET>{S.eid, S.esc, S.est, S.hslot, H - 1, OL, a.k <= LB_OL && om.nobs <= LB_OL});
 }
 
 // Boards beyond the LDS classes: the same replay over an HBM scratch region
@@ -703,16 +719,24 @@ __global__ __launch_bounds__(64) void lb_downstream_kernel(LbDownArgs a) {
 
 int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
   if (n_work == 0) return CCRDT_OK;
-  // LDS per board: 17 B per entry + 2 B per hash slot + the Observed list
-  // (11.3 / 13.4 / 21.5 / 43 KB: 14 / 11 / 7 / 3 boards per CU)
+  // LDS per board: 17 B per entry (9 B NARROW) + 2 B per hash slot + the
+  // Observed list.  NARROW 7.1 / 8.3 / 13.5 KB (22 / 19 / 11 boards per CU),
+  // then 11.3 / 13.4 / 21.5 / 43 KB (14 / 11 / 7 / 3 boards per CU).
+  const dim3 g((unsigned)n_work), b(64);
   if (cls == 0)
-    hipLaunchKernelGGL((lb_apply_kernel<512, 1024>), dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<512, 1024, true>), g, b, 0, st, a);
   else if (cls == 1)
-    hipLaunchKernelGGL((lb_apply_kernel<640, 1024>), dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<640, 1024, true>), g, b, 0, st, a);
   else if (cls == 2)
-    hipLaunchKernelGGL((lb_apply_kernel<1024, 2048>), dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<1024, 2048, true>), g, b, 0, st, a);
   else if (cls == 3)
-    hipLaunchKernelGGL((lb_apply_kernel<2048, 4096>), dim3((unsigned)n_work), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((lb_apply_kernel<512, 1024, false>), g, b, 0, st, a);
+  else if (cls == 4)
+    hipLaunchKernelGGL((lb_apply_kernel<640, 1024, false>), g, b, 0, st, a);
+  else if (cls == 5)
+    hipLaunchKernelGGL((lb_apply_kernel<1024, 2048, false>), g, b, 0, st, a);
+  else if (cls == 6)
+    hipLaunchKernelGGL((lb_apply_kernel<2048, 4096, false>), g, b, 0, st, a);
   else
     hipLaunchKernelGGL(lb_apply_hbm_kernel, dim3((unsigned)n_work), dim3(64), 0, st, a);
   CCRDT_HIP(hipGetLastError());

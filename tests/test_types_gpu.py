@@ -48,7 +48,8 @@ def _lb_stream(rng, n, nk, n_players, smax, ban_frac):
 
 @pytest.mark.parametrize("cfg", [(20000, 40, 300, 10**6, 0.01, 100), (20000, 50, 30, 10, 0.05, 5),
                                  (8000, 8, 1500, 1000, 0.02, 100), (3000, 30, 8, 4, 0.2, 1),
-                                 (12000, 4, 1500, 10**4, 0.02, 300)])  # K > 256: full-scan Min path
+                                 (12000, 4, 1500, 10**4, 0.02, 300),  # K > 256: full-scan Min path
+                                 (20000, 40, 300, 2**40, 0.01, 100)])  # 64-bit scores: wide LDS classes
 def test_leaderboard_random(gpu, cfg):
     n, nk, npl, smax, bf, K = cfg
     rng = np.random.default_rng(n + nk)
@@ -270,6 +271,25 @@ def test_topk_hbm_class(gpu):
             assert np.array_equal(a, b)
         pid = rng.integers(0, 12000, n)
         sc = rng.integers(0, 10**6, n)
+
+
+def test_leaderboard_mixed_width(gpu):
+    """Boards whose Ids/Scores fit 32 bits run the NARROW classes, the others
+    (one wide value, in the batch or in the carried state) the 64-bit ones."""
+    rng = np.random.default_rng(7)
+    n, nk = 30000, 60
+    e, o = LeaderboardEngine(nk, 50), orc.LbOracle(nk, 50)
+    for it in range(3):
+        kp, kind, pid, sc = _lb_stream(rng, n, nk, 400, 10**5, 0.02)
+        wide = rng.choice(n, 8, replace=False)
+        if it == 0:
+            sc[wide] = 2**35 + rng.integers(0, 1000, 8)
+            pid[wide[:3]] = -(2**33)
+        xe, xo = e.apply(kp, kind, pid, sc), o.apply(kp, kind, pid, sc)
+        assert np.array_equal(xe["kind"], xo["kind"])
+        m = xo["kind"] == 0
+        assert np.array_equal(xe["id"][m], xo["id"][m]) and np.array_equal(xe["score"][m], xo["score"][m])
+        assert not e.export().diff(o.export())
 
 
 def test_leaderboard_hbm_class(gpu):
