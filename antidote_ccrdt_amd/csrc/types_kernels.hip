@@ -855,11 +855,11 @@ __device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len
   return e;
 }
 
-// Token starts of the staged tile, compacted into an LDS list (offsets from
-// the tile start), so the per-token work runs on full waves instead of one
-// lockstep pass per byte position.  Returns the number of tokens.
-__device__ __forceinline__ uint32_t wc_starts(const WcTileView& v, uint64_t len, uint64_t tile,
-                                              uint16_t* list) {
+// Token starts of the staged tile as per-lane bitmasks (a lane owns
+// WC_TILE/64 consecutive positions) with each lane's exclusive offset in the
+// tile's token order.  Returns the lane's mask; tot = tokens in the tile.
+__device__ __forceinline__ uint64_t wc_start_mask(const WcTileView& v, uint64_t len, uint64_t tile, uint32_t& o,
+                                                  uint32_t& tot) {
   const int lane = lane_id();
   const uint64_t s0 = tile + (uint64_t)lane * (WC_TILE / 64);
   uint64_t m = 0;
@@ -869,15 +869,30 @@ __device__ __forceinline__ uint32_t wc_starts(const WcTileView& v, uint64_t len,
     const bool st = s <= len && (s == 0 || wc_sep(v.at(s - 1)));
     m |= (uint64_t)st << i;
   }
-  uint32_t tot;
-  uint32_t o = wave_excl_scan_u32((uint32_t)__builtin_popcountll(m), tot);
-  while (m) {
+  o = wave_excl_scan_u32((uint32_t)__builtin_popcountll(m), tot);
+  return m;
+}
+
+// Tokens [base, base + WC_LIST) of the tile compacted into an LDS list
+// (offsets from the tile start), so the per-token work runs on full waves
+// instead of one lockstep pass per byte position.  A tile of more than
+// WC_LIST tokens takes several rounds; the list stays small (2 KB) so more
+// waves fit per CU.  Returns the number of tokens in the list.
+constexpr uint32_t WC_LIST = 1024;
+__device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot, uint32_t base, uint16_t* list) {
+  const int lane = lane_id();
+  __syncthreads();  // the previous round's list is no longer read
+  while (m && o < base) {
+    m &= m - 1;
+    ++o;
+  }
+  while (m && o < base + WC_LIST) {
     const int i = __builtin_ctzll(m);
     m &= m - 1;
-    list[o++] = (uint16_t)(lane * (WC_TILE / 64) + i);
+    list[o++ - base] = (uint16_t)(lane * (WC_TILE / 64) + i);
   }
   __syncthreads();
-  return tot;
+  return tot - base < WC_LIST ? tot - base : WC_LIST;
 }
 
 __device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
@@ -945,7 +960,7 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   __shared__ uint32_t llen[WC_LDS];
   __shared__ uint64_t lpos[WC_LDS];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
-  __shared__ uint16_t tlist[WC_TILE];
+  __shared__ uint16_t tlist[WC_LIST];
   const int lane = lane_id();
   // a wave takes up to WC_TPW consecutive tiles of ONE document and keeps its
   // LDS table across them (the Zipf head costs one global atomic per word
@@ -962,7 +977,10 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     __syncthreads();  // the previous tile's staged bytes are no longer read
     const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
-    const uint32_t ntk = wc_starts(v, len, tile, tlist);
+    uint32_t mo, tot;
+    const uint64_t mm = wc_start_mask(v, len, tile, mo, tot);
+    for (uint32_t base = 0; base < tot; base += WC_LIST) {
+    const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
     for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
       const uint64_t s = tile + tlist[k];
       uint64_t fnv;
@@ -995,6 +1013,7 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
         if (g != ~0ull) atomicAdd(&a.t_cnt[g], 1ull);
       }
     }
+    }
   }
   __syncthreads();
   for (int i = lane; i < WC_LDS; i += 64) {
@@ -1011,7 +1030,7 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
 // Exactness: every token must equal its word's representative byte-for-byte.
 __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
-  __shared__ uint16_t tlist[WC_TILE];
+  __shared__ uint16_t tlist[WC_LIST];
   const int lane = lane_id();
   uint64_t d, tile;
   wc_tile(a, a.tile0 + blockIdx.x, d, tile);
@@ -1020,7 +1039,10 @@ __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
   for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
   __syncthreads();
   const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
-  const uint32_t ntk = wc_starts(v, len, tile, tlist);
+  uint32_t mo, tot;
+  const uint64_t mm = wc_start_mask(v, len, tile, mo, tot);
+  for (uint32_t base = 0; base < tot; base += WC_LIST) {
+  const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
   for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
     const uint64_t s = tile + tlist[k];
     uint64_t fnv;
@@ -1055,6 +1077,7 @@ __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
       for (int j = 0; j < 8; ++j) eq = eq && (j0 + j >= tl || r[j] == v.at(s + j0 + j));
     }
     if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+  }
   }
   }
 }
