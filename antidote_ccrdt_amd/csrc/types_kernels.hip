@@ -876,9 +876,9 @@ __device__ __forceinline__ uint64_t wc_start_mask(const WcTileView& v, uint64_t 
 // Tokens [base, base + WC_LIST) of the tile compacted into an LDS list
 // (offsets from the tile start), so the per-token work runs on full waves
 // instead of one lockstep pass per byte position.  A tile of more than
-// WC_LIST tokens takes several rounds; the list stays small (2 KB) so more
+// WC_LIST tokens takes several rounds; the list stays small (1 KB) so more
 // waves fit per CU.  Returns the number of tokens in the list.
-constexpr uint32_t WC_LIST = 1024;
+constexpr uint32_t WC_LIST = 512;
 __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot, uint32_t base, uint16_t* list) {
   const int lane = lane_id();
   __syncthreads();  // the previous round's list is no longer read
@@ -957,8 +957,7 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
   __shared__ unsigned long long lh[WC_LDS];
   __shared__ uint32_t lc[WC_LDS];
-  __shared__ uint32_t llen[WC_LDS];
-  __shared__ uint64_t lpos[WC_LDS];
+  __shared__ uint64_t lpos[WC_LDS];  // representative: position << 16 | length
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
   __shared__ uint16_t tlist[WC_LIST];
   const int lane = lane_id();
@@ -990,11 +989,11 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
       // per-tile LDS table
       uint32_t sl = (uint32_t)(h >> 17) & (WC_LDS - 1);
       int where = -1;  // 0: counted in LDS, 1: global
-      for (int p = 0; p < WC_PROBE; ++p) {
+      // (tokens of 64 KiB or more go straight to the global table)
+      for (int p = 0; p < (tl < 0xFFFFu ? WC_PROBE : 0); ++p) {
         const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
         if (prev == 0ull) {
-          llen[sl] = tl;
-          lpos[sl] = b0 + s;
+          lpos[sl] = (b0 + s) << 16 | tl;
           where = 0;
           if (!a.wdc) atomicAdd(&lc[sl], 1u);
           else lc[sl] = 1u;
@@ -1022,7 +1021,7 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
     // worddocumentcount: other tiles of the document may hold the word too;
     // the (document, word) dedupe table admits one of them
     if (a.wdc && !wc_doc_first(a, h, d)) continue;
-    const uint64_t g = wc_global_insert(a, h, key, llen[i], lpos[i]);
+    const uint64_t g = wc_global_insert(a, h, key, (uint32_t)(lpos[i] & 0xFFFFu), lpos[i] >> 16);
     if (g != ~0ull) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
   }
 }
