@@ -231,8 +231,8 @@ def test_wordcount_tile_edges(gpu, wdc):
     d3 = b"x" * (T - 1) + b" "          # exactly one tile, ends in a separator
     d4 = b"y" * T                       # exactly one tile, no separator
     d5 = b" ".join([b"ab", b"cd"] * 4000) + b"  "
-    d6 = b" " * (2 * T + 5)             # 4096 empty tokens per tile: 4 list rounds of 1024
-    d7 = b"a\n" * 5000                  # 2048 tokens per tile: 2 rounds
+    d6 = b" " * (2 * T + 5)             # 4096 empty tokens per tile: 8 list rounds of 512
+    d7 = b"a\n" * 5000                  # 2048 tokens per tile: 4 rounds
     d8 = b"z" * 70000 + b" " + b"z" * 70000 + b" z"  # tokens of >= 64 KiB bypass the LDS table
     docs = [[bytes(d1), d2, d3, d6], [d4, d5, b"", b" ", d7, d8]]
     E = WordDocumentCountEngine if wdc else WordcountEngine
