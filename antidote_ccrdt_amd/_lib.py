@@ -147,7 +147,7 @@ SIGNATURES = {
     "ccrdt_splitmix64": (U64, [U64]),
     "ccrdt_gen_trmv_count": (I64, [I64, U64, INT]),
     "ccrdt_gen_corpus": (INT, [I64, I64, I64, U64, INT, P, P]),
-    "ccrdt_gen_trmv": (INT, [I64, I64, INT, I64, I64, INT, INT, INT, INT, U64,
+    "ccrdt_gen_trmv": (INT, [I64, I64, INT, I64, I64, INT, INT, INT, INT, U64, I64,
                              P, P, P, P, P, P, P]),
 }
 

@@ -38,6 +38,9 @@ uint64_t ccrdt_splitmix64(uint64_t x) { return splitmix64(x); }
 // After grouping by key (stable), with probability swap_pm/1000 an op is
 // swapped with its successor inside the key (out-of-order delivery).
 // rmv ops carry ts = row index into rmv_vc (rows in CSR order).
+// Every DC clock starts at clock0 (0 for a fresh stream): batch b of a long
+// stream passes clock0 >= the clocks the earlier batches reached (e.g.
+// b * n_ops), so timestamps keep rising across batches (steady state).
 int64_t ccrdt_gen_trmv_count(int64_t n_ops, uint64_t seed, int rmv_pm) {
   int64_t n = 0;
   for (int64_t p = 0; p < n_ops; ++p) n += (int64_t)(h(seed, p, 1) % 1000) < rmv_pm;
@@ -46,10 +49,10 @@ int64_t ccrdt_gen_trmv_count(int64_t n_ops, uint64_t seed, int rmv_pm) {
 
 int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, int64_t score_max,
                    int rmv_pm, int lag_max, int dup_pm, int swap_pm, uint64_t seed,
-                   uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score, uint8_t* dc,
-                   int64_t* ts, int64_t* rmv_vc) {
+                   int64_t clock0, uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score,
+                   uint8_t* dc, int64_t* ts, int64_t* rmv_vc) {
   if (n_ops < 0 || n_keys <= 0 || n_dc < 1 || n_dc > 8 || n_players < 1 || score_max < 1 ||
-      lag_max < 1)
+      lag_max < 1 || clock0 < 0)
     return CCRDT_EINVAL;
   std::vector<uint32_t> key(n_ops);
   std::vector<uint64_t> cnt(n_keys + 1, 0);
@@ -60,7 +63,7 @@ int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, i
   for (int64_t k = 0; k < n_keys; ++k) cnt[k + 1] += cnt[k];
   memcpy(key_ptr, cnt.data(), (n_keys + 1) * 8);
   std::vector<uint64_t> fill(cnt.begin(), cnt.end() - 1);
-  std::vector<int64_t> clock(n_dc, 0);
+  std::vector<int64_t> clock(n_dc, clock0);
   std::vector<int64_t> recent(n_keys * 4, 0);   // last 4 added ids per key
   std::vector<uint32_t> nrecent(n_keys, 0);
   std::vector<int64_t> last_sc(n_keys, 0), last_ts(n_keys, 0);

@@ -324,14 +324,18 @@ class TopkRmvEngine(_Engine):
 
 def gen_trmv(n_ops: int, n_keys: int, n_dc: int = 8, n_players: int = 256,
              score_max: int = 10**6, rmv_pm: int = 100, lag_max: int = 64, dup_pm: int = 0,
-             swap_pm: int = 0, seed: int = 0xCC0DE + 2) -> TrmvBatch:
-    """Seeded synthetic topk_rmv stream, CSR by key (include/ccrdt_gen.h)."""
+             swap_pm: int = 0, seed: int = 0xCC0DE + 2, clock0: int = 0) -> TrmvBatch:
+    """Seeded synthetic topk_rmv stream, CSR by key (include/ccrdt_gen.h).
+
+    ``clock0`` is every DC clock's start: batch ``i`` of a long stream uses
+    ``clock0 = i * n_ops`` (and its own seed) so timestamps keep rising across
+    batches applied to the same resident state."""
     n_rmv = int(lib.ccrdt_gen_trmv_count(n_ops, seed, rmv_pm))
     b = TrmvBatch(np.empty(n_keys + 1, np.uint64), np.empty(n_ops, np.uint8),
                   np.empty(n_ops, np.int64), np.empty(n_ops, np.int64), np.empty(n_ops, np.uint8),
                   np.empty(n_ops, np.int64), np.empty((n_rmv, n_dc), np.int64))
     check(lib.ccrdt_gen_trmv(n_ops, n_keys, n_dc, n_players, score_max, rmv_pm, lag_max, dup_pm,
-                             swap_pm, seed, ptr(b.key_ptr), ptr(b.kind), ptr(b.id), ptr(b.score),
+                             swap_pm, seed, clock0, ptr(b.key_ptr), ptr(b.kind), ptr(b.id), ptr(b.score),
                              ptr(b.dc), ptr(b.ts), ptr(b.rmv_vc)), "gen_trmv")
     return b
 

@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--n-dc", type=int, default=8)
     ap.add_argument("--cpu-sample-keys", type=int, default=1 << 18,
                     help="keys of the batch the CPU baseline replays (0 = skip)")
+    ap.add_argument("--steady-batches", type=int, default=4,
+                    help="steady-state leg: batches 2..n+1 of the same stream applied onto the "
+                         "resident keys after batch 1 (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "trmv_pmc.json"))
     ap.add_argument("--dist-backend", default=None,
                     help="N > 1: nccl (RCCL, default on GPUs) or gloo (host-staged; tests)")
@@ -220,6 +223,43 @@ def main():
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
+    # Steady state (reported beside the headline, never as `value`): the
+    # same keys keep their state and receive the next batches of the stream
+    # (clocks keep rising), so Observed is full, P > K, adds evict and rmvs
+    # promote.  Timed per batch: one apply_device on resident state.
+    steady = None
+    if args.steady_batches > 0:
+        eng.reset()
+        eng.apply_device(db)
+        eng.sync()
+        rows = []
+        for i in range(1, args.steady_batches + 1):
+            bi = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6,
+                          rmv_pm=100, lag_max=64, seed=seed + 7919 * i, clock0=i * args.n_ops)
+            dbi = DeviceTrmvBatch(bi)
+            del bi
+            eng.sync()
+            barrier()
+            ts0 = time.perf_counter()
+            eng.apply_device(dbi)
+            eng.sync()
+            ms = (time.perf_counter() - ts0) * 1e3
+            dbi.close()
+            rows.append({"batch": i + 1, "ms": round(ms, 3),
+                         "ops_per_s": args.n_ops / (ms * 1e-3),
+                         "apply_chain_ms": round(eng.last_kernel_ms(), 3),
+                         "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in
+                                                    (0, 1, 2, 4, 8, 16, 1000)},
+                         "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in
+                                               (0, 1, 2, 4, 8, 16, 1000)},
+                         "state_after": dict(zip(("observed", "masked", "removal_rows"),
+                                                 eng.sizes()))})
+        mean_ms = sum(r["ms"] for r in rows) / len(rows)
+        steady = {"what": "batches 2..n of the bench stream onto the resident keys (no reset), "
+                          "one apply_device each, wall time around it",
+                  "ops_per_s_mean": args.n_ops / (mean_ms * 1e-3), "ms_mean": mean_ms,
+                  "batches": rows}
+
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_sample_keys > 0:  # reported at N=1 only
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -295,6 +335,7 @@ def main():
                                 "achieved_GBs": alg_bytes / (chain_ms * 1e-3) / 1e9},
                 "extra_effects": n_extra,
                 "cpu_baseline_threads": cpu_mt,
+                "steady_state": steady,
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),

@@ -14,11 +14,13 @@ uint64_t ccrdt_splitmix64(uint64_t x);
 int64_t ccrdt_gen_trmv_count(int64_t n_ops, uint64_t seed, int rmv_pm);
 
 /* topk_rmv effect stream, CSR by key (see gen.cpp for the distribution).
+ * Every DC clock starts at clock0 (0 = a fresh stream; a later batch of the
+ * same long stream passes a clock0 above every earlier timestamp).
  * Outputs: key_ptr[n_keys+1], kind/id/score/dc/ts[n_ops],
  * rmv_vc[ccrdt_gen_trmv_count(...) * n_dc]. */
 int ccrdt_gen_trmv(int64_t n_ops, int64_t n_keys, int n_dc, int64_t n_players, int64_t score_max,
                    int rmv_pm, int lag_max, int dup_pm, int swap_pm, uint64_t seed,
-                   uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score, uint8_t* dc,
+                   int64_t clock0, uint64_t* key_ptr, uint8_t* kind, int64_t* id, int64_t* score, uint8_t* dc,
                    int64_t* ts, int64_t* rmv_vc);
 
 /* Synthetic Zipf text corpus (wordcount / worddocumentcount):

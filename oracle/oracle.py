@@ -111,6 +111,25 @@ class TrmvOracle:
         return out
 
 
+def trmv_mismatches(eng_state, eng_extra, orc_state: dict, orc_extra: dict | None) -> list[str]:
+    """Bit-exact comparison of an engine apply with the oracle's: the
+    canonical state images (every field) and every extra effect's payload
+    ({add, {Id, Score, {Dc, Ts}}} fields for promotions, {rmv, {Id, Vc}} for
+    dominated adds).  Returns the names of the differing fields."""
+    bad = [f for f in TRMV_FIELDS
+           if not np.array_equal(getattr(eng_state, f), orc_state[f])]
+    if eng_extra is not None and orc_extra is not None:
+        ok = orc_extra["kind"]
+        if not np.array_equal(eng_extra.kind, ok):
+            bad.append("extra.kind")
+        else:
+            add, rmv = ok == 0, ok == 2
+            for f, m in (("id", ok != 255), ("score", add), ("dc", add), ("ts", add), ("vc", rmv)):
+                if not np.array_equal(getattr(eng_extra, f)[m], orc_extra[f][m]):
+                    bad.append(f"extra.{f}")
+    return bad
+
+
 # ----------------------------------------------------------- other types
 def _setup_types(l):
     P, I64, INT = C.c_void_p, C.c_int64, C.c_int
