@@ -24,10 +24,9 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
-int trmv_launch_apply(const TrmvApplyArgs& a, int slots, uint64_t n_work, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
-int trmv_launch_fast(const TrmvApplyArgs& a, int tier, uint64_t n_work, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
+int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st);
 int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
                            hipStream_t st);
@@ -35,12 +34,13 @@ int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, con
                             const int64_t* ex_vc, uint64_t n_keys, int n_dc, int64_t* rows,
                             int64_t cap, uint32_t* count, hipStream_t st);
 
-static constexpr int TRMV_SLOT_CLASSES[] = {2, 4, 8, 16};
-static constexpr uint32_t TRMV_MAX_CAP = 64u * 16u;      // players / pool per key
-static constexpr uint32_t TRMV_MAX_ROWS = 8u * 2u * 16u;  // removal rows per key
-static constexpr int TRMV_STATUS_WORDS = 32;  // [0,14) scan + main tiers, [16,26) side chain
+// Tiers of the apply chain: 0 = trmv_wave (tier 0), 1 / 2 = trmv_steady with
+// up to 256 / 1024 players per key (tier S).
+static constexpr int TRMV_N_TIERS = 3;
+static constexpr uint32_t TRMV_MAX_PLAYERS = 1024u;  // players per key (tier S, last class)
+static constexpr int TRMV_STATUS_WORDS = 32;  // [0,8) scan + main tiers, [16,22) side chain
 static constexpr int TRMV_SIDE = 16;
-static constexpr uint32_t TRMV_LATER_GRID = 2048;  // workgroups of the tiers after the first
+static constexpr uint32_t TRMV_LATER_GRID = 4096;  // keys the grids of the later tiers cover
 
 }  // namespace ccrdt
 
@@ -56,6 +56,7 @@ TrmvSide ccrdt_engine::trmv_side(int s) const {
   t.m_ts = b.m_ts.as<int64_t>();
   t.m_dc = b.m_dc.as<uint8_t>();
   t.pl_slab = b.pl_slab.as<uint32_t>();
+  t.pl_gb = b.pl_gb.as<uint16_t>();
   t.r_vc = b.r_vc.as<int64_t>();
   t.vc = b.vc.as<int64_t>();
   return t;
@@ -70,6 +71,7 @@ void ccrdt_engine::release_all() {
     b.m_ts.release();
     b.m_dc.release();
     b.pl_slab.release();
+    b.pl_gb.release();
     b.r_vc.release();
     b.vc.release();
   }
@@ -325,6 +327,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     CCRDT_TRY(b.pl_id.ensure(tot[0] * 8));
     CCRDT_TRY(b.pl_info.ensure(tot[0] * 4));
     CCRDT_TRY(b.pl_slab.ensure(tot[0] * 4));
+    CCRDT_TRY(b.pl_gb.ensure(tot[0] * 2));
     CCRDT_TRY(b.m_score.ensure(tot[1] * 8));
     CCRDT_TRY(b.m_ts.ensure(tot[1] * 8));
     CCRDT_TRY(b.m_dc.ensure(tot[1]));
@@ -346,22 +349,21 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
-  // 2) per-player-parallel tiers over every key, then the sequential kernel
-  //    (escalating register classes) for the keys each tier hands on.  Every
-  //    later tier reads its list length from the device, so the whole chain is
-  //    queued without a host round trip; one sync at the end reads the status.
-  // CCRDT_TRMV_FIRST_TIER (tuning knob, default 0): 1 skips the all-LDS tier,
-  // 2 sends every key to the sequential kernel.
-  static const int first_tier = [] {
+  // 2) tier 0 over every key, then tier S (256, then 1024 players per key) for
+  //    the keys each tier hands on.  Every later tier reads its list length
+  //    from the device, so the whole chain is queued without a host round
+  //    trip; one sync at the end reads the status.
+  // CCRDT_TRMV_FIRST_TIER (tuning knob): -1 = tier 0 for fresh batches and
+  // tier S for batches onto resident state (default), 0 = always tier 0 first,
+  // 1 = always tier S.
+  static const int first_env = [] {
     const char* v = getenv("CCRDT_TRMV_FIRST_TIER");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : -1;
   }();
-  constexpr int N_TIERS = 2 + (int)(sizeof(TRMV_SLOT_CLASSES) / sizeof(int));
+  const int first_tier = first_env >= 0 ? std::min(first_env, 1) : (E.fresh ? 0 : 1);
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
-  constexpr int N_CLS = (int)(sizeof(TRMV_SLOT_CLASSES) / sizeof(int));
   // Side chain (stream2, after the scan): keys with more ops than tier 0
-  // takes go straight to the sequential kernel's classes, concurrently with
-  // tier 0, which skips them.
+  // takes go straight to tier S, concurrently with tier 0, which skips them.
   const bool side = first_tier == 0 && nk;
   if (side) {
     CCRDT_HIP(hipEventRecord(E.ev_scan, E.stream));
@@ -375,12 +377,12 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     b.status = status + TRMV_SIDE;
     CCRDT_TRY(trmv_launch_classify(b, E.stream2));
     CCRDT_HIP(hipEventRecord(E.evb[1], E.stream2));
-    for (int i = 0; i < N_CLS; ++i) {
+    for (int i = 0; i < 2; ++i) {
       b.key_list = E.tier_ovf_b[i].as<uint32_t>();
       b.n_list_dev = status + TRMV_SIDE + 2 * i;
       b.ovf_list = E.tier_ovf_b[i + 1].as<uint32_t>();
       b.status = status + TRMV_SIDE + 2 + 2 * i;
-      CCRDT_TRY(trmv_launch_apply(b, TRMV_SLOT_CLASSES[i], later_grid, E.stream2));
+      CCRDT_TRY(trmv_launch_steady(b, i, later_grid, E.stream2));
       CCRDT_HIP(hipEventRecord(E.evb[i + 2], E.stream2));
     }
     CCRDT_HIP(hipEventRecord(E.ev_side, E.stream2));
@@ -390,7 +392,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   const uint32_t* n_dev = nullptr;
   int ev = 0;
   CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-  for (int t = first_tier; t < N_TIERS && nk; ++t) {
+  for (int t = first_tier; t < TRMV_N_TIERS && nk; ++t) {
     DevBuf* ovf = &E.tier_ovf[t];
     a.key_list = work ? work->as<uint32_t>() : nullptr;
     a.n_list = work ? 0u : (uint32_t)nk;
@@ -399,8 +401,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     a.status = status + 2 + 2 * t;
     const uint64_t grid = work ? later_grid : nk;
     if (t == 0) CCRDT_TRY(trmv_launch_wave(a, grid, E.stream));
-    else if (t == 1) CCRDT_TRY(trmv_launch_fast(a, 1, grid, E.stream));
-    else CCRDT_TRY(trmv_launch_apply(a, TRMV_SLOT_CLASSES[t - 2], grid, E.stream));
+    else CCRDT_TRY(trmv_launch_steady(a, t - 1, grid, E.stream));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     work = ovf;
     n_dev = a.status;
@@ -413,14 +414,14 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
                            E.stream));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
-  if (hs[1] & TRMV_ERR_SEG) {
+  uint32_t err = 0;
+  for (int t = first_tier; t < TRMV_N_TIERS; ++t) err |= hs[3 + 2 * t];
+  if (side)
+    for (int i = 0; i < 2; ++i) err |= hs[TRMV_SIDE + 3 + 2 * i];
+  if ((hs[1] | err) & TRMV_ERR_SEG) {
     set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
     return CCRDT_ENOMEM;
   }
-  uint32_t err = 0;
-  for (int t = first_tier; t < N_TIERS; ++t) err |= hs[3 + 2 * t];
-  if (side)
-    for (int i = 0; i < N_CLS; ++i) err |= hs[TRMV_SIDE + 3 + 2 * i];
   if (err) {
     std::string m = "trmv_apply: invalid op in batch:";
     if (err & TRMV_ERR_KIND) m += " kind>3";
@@ -433,34 +434,33 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
                ? CCRDT_ERANGE
                : CCRDT_EINVAL;
   }
-  if (nk && (hs[2 + 2 * (N_TIERS - 1)] || (side && hs[TRMV_SIDE + 2 * N_CLS]))) {
-    set_error("trmv_apply: a key exceeds the per-key capacity (1024 Ids or Masked elements, "
-              "256 Removals entries)");
-    return CCRDT_ENOMEM;
-  }
   E.trmv_overflow_keys.clear();
   E.trmv_tier_ms.clear();
   E.trmv_first_tier = first_tier;
-  float kernel_ms = 0.f;
-  for (int t = first_tier, i = 1; t < N_TIERS && nk; ++t, ++i) {
-    const int key = t < 2 ? t : TRMV_SLOT_CLASSES[t - 2];
+  for (int t = first_tier, i = 1; t < TRMV_N_TIERS && nk; ++t, ++i) {
     float ms = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[i - 1], E.evt[i]));
-    E.trmv_tier_ms[key] = ms;
-    E.trmv_overflow_keys[key] = hs[2 + 2 * t];
+    E.trmv_tier_ms[t] = ms;
+    E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
-  if (side) {  // side chain: 1000 = keys sent to it, 1000 + class = its hand-ons / times
+  if (side) {  // side chain: 1000 = keys sent to it, 1001 / 1002 = its tier S classes
     E.trmv_overflow_keys[1000] = hs[TRMV_SIDE];
-    for (int i = 0; i < N_CLS; ++i) {
+    for (int i = 0; i < 2; ++i) {
       float ms = 0.f;
       CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[i + 1], E.evb[i + 2]));
-      E.trmv_tier_ms[1000 + TRMV_SLOT_CLASSES[i]] = ms;
-      E.trmv_overflow_keys[1000 + TRMV_SLOT_CLASSES[i]] = hs[TRMV_SIDE + 2 + 2 * i];
+      E.trmv_tier_ms[1001 + i] = ms;
+      E.trmv_overflow_keys[1001 + i] = hs[TRMV_SIDE + 2 + 2 * i];
     }
     float ms = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[0], E.evb[1]));
     E.trmv_tier_ms[1000] = ms;
   }
+  if (nk && (hs[2 + 2 * (TRMV_N_TIERS - 1)] || (side && hs[TRMV_SIDE + 4]))) {
+    set_error("trmv_apply: a key would hold more than 1024 players (Ids with a Masked or "
+              "Removals entry); ccrdt_engine_handed_on(e, 2) / (e, 1002) lists them");
+    return CCRDT_ENOMEM;
+  }
+  float kernel_ms = 0.f;
   if (nk && ev > 1) CCRDT_HIP(hipEventElapsedTime(&kernel_ms, E.evt[0], E.evt[ev - 1]));
   CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
                            E.stream));
@@ -596,6 +596,7 @@ struct HostTrmv {
   std::vector<KeyMeta> meta;
   std::vector<int64_t> pl_id, m_score, m_ts, r_vc, vc;
   std::vector<uint32_t> pl_info, pl_slab;
+  std::vector<uint16_t> pl_gb;
   std::vector<uint8_t> m_dc;
 };
 
@@ -675,9 +676,9 @@ int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* 
 
 int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, int64_t* n) {
   if (!e || !n || cap < 0) return CCRDT_EINVAL;
-  static constexpr int tiers[] = {0, 1, 2, 4, 8, 16, 1000, 1002, 1004, 1008, 1016};
+  static constexpr int tiers[] = {0, 1, 2, 1000, 1001, 1002};
   int ti = -1;
-  for (int i = 0; i < 11; ++i)
+  for (int i = 0; i < 6; ++i)
     if (tiers[i] == t) ti = i;
   auto it = e->trmv_overflow_keys.find(t);
   if (ti < 0 || e->type != CCRDT_TOPK_RMV || it == e->trmv_overflow_keys.end()) {
@@ -687,7 +688,7 @@ int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, 
   *n = it->second;
   const int64_t m = std::min<int64_t>(cap, *n);
   if (m > 0 && keys) {
-    const DevBuf& src = ti < 6 ? e->tier_ovf[ti] : e->tier_ovf_b[ti - 6];
+    const DevBuf& src = ti < 3 ? e->tier_ovf[ti] : e->tier_ovf_b[ti - 3];
     CCRDT_HIP(hipStreamSynchronize(e->stream));
     CCRDT_HIP(hipMemcpy(keys, src.p, (size_t)m * 4, hipMemcpyDeviceToHost));
   }
@@ -813,8 +814,8 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     std::sort(ids.begin(), ids.end());
     ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
     const uint64_t nmk = in->m_ptr[k + 1] - in->m_ptr[k], nrk = in->r_ptr[k + 1] - in->r_ptr[k];
-    if (ids.size() > TRMV_MAX_CAP || nmk > TRMV_MAX_CAP || nrk > TRMV_MAX_ROWS) {
-      set_error("trmv_import: key exceeds per-key capacity");
+    if (ids.size() > TRMV_MAX_PLAYERS || nmk > TRMV_SEG_MAX || nrk >= NONE16) {
+      set_error("trmv_import: key exceeds per-key capacity (1024 players, 65535 Masked elements)");
       return CCRDT_ENOMEM;
     }
     auto pidx = [&](int64_t id) -> uint32_t {
@@ -830,9 +831,15 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
       per[pidx(in->m_id[i])].push_back({in->m_score[i], in->m_dc[i], in->m_ts[i]});
     }
     std::vector<uint32_t> info(ids.size(), NONE32), slab(ids.size(), 0);
+    std::vector<uint16_t> gb(ids.size(), 0);
     uint32_t off = 0;
     for (size_t q = 0; q < ids.size(); ++q) {
       slab[q] = off | ((uint32_t)per[q].size() << 16);
+      for (size_t j = 1; j < per[q].size(); ++j) {  // gb_sets:largest: (Score, DcId, Ts)
+        const E3& x = per[q][j];
+        const E3& y = per[q][gb[q]];
+        if (std::tie(x.score, x.dc, x.ts) > std::tie(y.score, y.dc, y.ts)) gb[q] = (uint16_t)j;
+      }
       for (const E3& x : per[q]) {
         h.m_score.push_back(x.score);
         h.m_dc.push_back(x.dc);
@@ -899,6 +906,7 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
       h.pl_id.push_back(ids[q]);
       h.pl_info.push_back(info[q]);
       h.pl_slab.push_back(slab[q]);
+      h.pl_gb.push_back(gb[q]);
     }
     m.np = (uint32_t)ids.size();
     m.nm = (uint32_t)nmk;
@@ -912,6 +920,7 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   CCRDT_TRY(b.pl_id.ensure(h.pl_id.size() * 8));
   CCRDT_TRY(b.pl_info.ensure(h.pl_info.size() * 4));
   CCRDT_TRY(b.pl_slab.ensure(h.pl_slab.size() * 4));
+  CCRDT_TRY(b.pl_gb.ensure(h.pl_gb.size() * 2));
   CCRDT_TRY(b.m_score.ensure(h.m_score.size() * 8));
   CCRDT_TRY(b.m_ts.ensure(h.m_ts.size() * 8));
   CCRDT_TRY(b.m_dc.ensure(h.m_dc.size()));
@@ -925,6 +934,7 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     CCRDT_HIP(hipMemcpy(b.pl_id.p, h.pl_id.data(), h.pl_id.size() * 8, hipMemcpyHostToDevice));
     CCRDT_HIP(hipMemcpy(b.pl_info.p, h.pl_info.data(), h.pl_info.size() * 4, hipMemcpyHostToDevice));
     CCRDT_HIP(hipMemcpy(b.pl_slab.p, h.pl_slab.data(), h.pl_slab.size() * 4, hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(b.pl_gb.p, h.pl_gb.data(), h.pl_gb.size() * 2, hipMemcpyHostToDevice));
   }
   if (!h.m_score.empty()) {
     CCRDT_HIP(hipMemcpy(b.m_score.p, h.m_score.data(), h.m_score.size() * 8, hipMemcpyHostToDevice));

@@ -10,7 +10,7 @@ namespace ccrdt {
 
 // One ping-pong side of GPU-resident topk_rmv state (trmv_kernels.hpp).
 struct TrmvBufs {
-  DevBuf meta, pl_id, pl_info, pl_slab, m_score, m_ts, m_dc, r_vc, vc;
+  DevBuf meta, pl_id, pl_info, pl_slab, pl_gb, m_score, m_ts, m_dc, r_vc, vc;
 };
 
 // Per-type resident state of the other CCRDTs (types_kernels.hip); [2] =
@@ -81,8 +81,8 @@ struct ccrdt_engine {
   ccrdt::TrmvBufs trmv[2];
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status;
-  ccrdt::DevBuf tier_ovf[6];    // keys each topk_rmv tier handed on (last batch)
-  ccrdt::DevBuf tier_ovf_b[5];  // side chain: big keys, then each class's hand-ons
+  ccrdt::DevBuf tier_ovf[3];    // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf tier_ovf_b[3];  // side chain: big keys, then each tier S class's hand-ons
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held

@@ -95,6 +95,7 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
     CCRDT_TRY(copy_buf(d.pl_id, s.pl_id, stream));
     CCRDT_TRY(copy_buf(d.pl_info, s.pl_info, stream));
     CCRDT_TRY(copy_buf(d.pl_slab, s.pl_slab, stream));
+    CCRDT_TRY(copy_buf(d.pl_gb, s.pl_gb, stream));
     CCRDT_TRY(copy_buf(d.m_score, s.m_score, stream));
     CCRDT_TRY(copy_buf(d.m_ts, s.m_ts, stream));
     CCRDT_TRY(copy_buf(d.m_dc, s.m_dc, stream));

@@ -11,6 +11,10 @@
 //                         row (high 16): Removals row, 0xFFFF = none
 //            pl_slab[u32] Masked slab of the player inside the key's pool
 //                         segment: offset (low 16) | element count (high 16)
+//            pl_gb[u16]   gb_sets:largest(Masked[Id]) as an index into the
+//                         slab (term order (Score, DcId, Ts) inside one Id;
+//                         the promotion candidate of rmv/3, :279,291); 0 when
+//                         the slab is empty
 //   pool     m_score[i64], m_ts[i64], m_dc[u8]   the Masked elements, one
 //                         slab per player (slabs may leave holes)
 //   rows     r_vc[n_dc x i64]   Removals[Id] (0 = DC absent)
@@ -25,8 +29,6 @@ namespace ccrdt {
 
 constexpr uint32_t NONE16 = 0xFFFFu;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
-constexpr uint32_t PD_INOBS = 1u << 31;  // in-register flags (sequential kernel)
-constexpr uint32_t PD_ALIVE = 1u << 30;
 constexpr int TRMV_DPAD = 8;             // lanes per removal row (n_dc <= 8)
 constexpr uint32_t TRMV_SEG_MAX = 0xFFFFu;  // pool elements addressable per key
 
@@ -46,6 +48,7 @@ struct TrmvSide {
   int64_t* pl_id;
   uint32_t* pl_info;
   uint32_t* pl_slab;
+  uint16_t* pl_gb;
   int64_t* m_score;
   int64_t* m_ts;
   uint8_t* m_dc;

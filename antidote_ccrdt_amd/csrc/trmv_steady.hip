@@ -1,0 +1,930 @@
+// trmv_steady.hip — tier S of the topk_rmv apply: any key, fresh or resident,
+// any number of ops, Masked slabs of any size inside the key's segment, and
+// Observed full with more players than K (evictions, promotions).  One
+// wavefront per key.  Tier 0 (trmv_wave.hip) takes the keys whose history
+// decomposes per player; everything else ends here.
+//
+// Why the sequential part is small.  The reference state machine
+// (src/antidote_ccrdt_topk_rmv.erl:231-334) keeps this invariant after every
+// op (proof in DESIGN.md §4.1):
+//   * Obs[Id] has the largest Score in Masked[Id] (Q2: Obs[Id] ∈ Masked[Id]);
+//   * if |Observed| = K, every Id outside Observed ranks below Min by
+//     (max Score of Masked[Id], Id); if |Observed| < K, every Id with Masked
+//     elements is in Observed.
+// So Observed is the top K players by (max Score, Id), and only three things
+// depend on the order of ops across players: which element of a player is
+// Obs[Id] when Scores tie inside Masked[Id] (cmp/2 keeps the first arrival,
+// :389-395; a promotion takes gb_sets:largest, :291), Min, and the extra
+// effects.  Everything per player — Removals[Id] merges, the rmv filters of
+// Masked[Id], dominated adds (:234) and set semantics (:240-246) — is decided
+// per player, off the sequential path:
+//   K1  old players -> LDS (Id hash, old slab, Obs[Id] and gb_sets:largest
+//       elements gathered from the pool);
+//   K2  every op's player (new Ids numbered in claim order), ops per player,
+//       new slab offsets (old count + ops: the key's new segment), new
+//       Removals rows;
+//   K3  old Masked slabs and Removals rows -> the new side, position-parallel
+//       (coalesced), except the slabs of players with a rmv in the batch;
+//   K4  per chunk of <= 64 ops (<= 16 rmvs): ops sorted by player (wave radix
+//       sort); players without a rmv append their non-dominated adds
+//       op-parallel; players with a rmv (or a possibly duplicated element) are
+//       replayed by one lane each over their own slab and Removals row
+//       (Masked filter, merge_vc, dominance, set semantics, the largest
+//       survivor after each rmv); then one uniform pass over the chunk's ops
+//       in stream order does recompute_observed/5 and the Observed half of
+//       rmv/3 (impact, promotion, Min) with per-player LDS state;
+//   K5  Obs/largest positions of replayed players, player records, Vc, meta.
+#include <algorithm>
+
+#include "common.hpp"
+#include "trmv_kernels.hpp"
+
+namespace ccrdt {
+
+namespace {
+
+constexpr int S_CH = 64;    // ops per chunk
+constexpr int S_CHR = 16;   // rmvs per chunk (rows of the clock table)
+constexpr uint32_t S_NONE = 0xFFFFFFFFu;
+constexpr uint32_t S_CLAIM = 0x80000000u;
+// opd[p] = flags (8) | Obs[Id] dc (8) | Obs[Id] slab position (16)
+constexpr uint32_t F_OBS = 1u;    // Id in Observed
+constexpr uint32_t F_HASM = 2u;   // Masked[Id] is not empty
+constexpr uint32_t F_RMV = 4u;    // a rmv of Id in this batch: slab and row replayed by one lane
+constexpr uint32_t F_MAT = 8u;    // (F_RMV) old slab already copied to the new region
+constexpr uint32_t F_ROWV = 16u;  // the player's Removals row holds an entry
+constexpr uint32_t F_WALK = 32u;  // slab compacted by a replay: positions restated at the end
+constexpr uint32_t R_DOM = 1u;    // cres: dominated add (:234-237)
+
+enum : int { S_DONE = 0, S_NEXT = 1, S_REJECT = 2 };
+
+template <int N>
+struct Log2 {
+  static constexpr int v = 1 + Log2<N / 2>::v;
+};
+template <>
+struct Log2<1> {
+  static constexpr int v = 0;
+};
+
+template <int PCAP>
+struct alignas(16) SLds {
+  static constexpr int HS = 2 * PCAP;
+  uint32_t hs[HS];                       // Id hash: player | S_CLAIM|lane | S_NONE
+  int64_t pid[PCAP + 1];                 // player Ids
+  int64_t osc[PCAP + 1], ots[PCAP + 1];  // Obs[Id]: Score, Ts
+  int64_t gsc[PCAP + 1], gts[PCAP + 1];  // gb_sets:largest(Masked[Id]): Score, Ts
+  uint32_t opd[PCAP + 1];                // flags | Obs dc << 8 | Obs position << 16
+  uint32_t gpd[PCAP + 1];                // largest: dc << 8 | position << 16
+  uint32_t oslab[PCAP + 1];              // old slab: offset | count << 16
+  uint32_t orow[PCAP + 1];               // old Obs index | Removals row << 16 (new side)
+  uint32_t nslab[PCAP + 1];              // new slab: offset | current count << 16
+  uint32_t nops[PCAP + 1];               // ops of the player in the batch
+  // the current chunk (stream order unless noted)
+  int64_t csc[S_CH + 1], cts[S_CH + 1];
+  uint32_t ckd[S_CH + 1];                // kind | dc << 2 | dup candidate << 5 | player << 8
+  uint32_t cres[S_CH + 1];               // add: R_DOM | slab position << 16; rmv: its rank
+  uint32_t crow[S_CHR + 1];              // rmv_vc row of the chunk's rmvs
+  int64_t vtab[S_CHR][TRMV_DPAD];        // their clocks
+  int64_t rgsc[S_CHR], rgts[S_CHR];      // Masked[Id]'s largest survivor after each rmv
+  uint32_t rgd[S_CHR];                   // non-empty | dc << 8 | position << 16
+  uint8_t csrt[S_CH];                    // sorted (player, stream) order -> stream index
+  uint16_t cwp[S_CH];                    // replayed players of the chunk
+  uint8_t cws[S_CH], cwe[S_CH];          // and their sorted ranges
+  uint32_t mark[S_CH];                   // K3: player (+1) whose slab starts at a position
+  int64_t claim[S_CH];                   // K2: Ids being claimed
+  unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
+  uint32_t nex;
+};
+
+template <int PCAP>
+__device__ __forceinline__ uint32_t shash(int64_t id) {
+  constexpr int B = Log2<2 * PCAP>::v;
+  return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> (64 - B));
+}
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int64_t ufl64(int64_t v) {
+  const uint32_t lo = ufl((uint32_t)v), hi = ufl((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Forward permute: lane i's v goes to lane dst (ds_permute).
+__device__ __forceinline__ uint32_t perm32(uint32_t v, uint32_t dst) {
+  return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)v);
+}
+
+// Inclusive max-scan over the 64 lanes (DPP; identity 0).
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+  uint32_t o;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  v = o > v ? o : v;
+  return v;
+}
+
+// Stable sort of the wave by key bits [6, 6 + BITS) of kv (payload: low 6
+// bits); one ballot split per bit.
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_radix_sort(uint32_t kv) {
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const bool bit = (kv >> (6 + b)) & 1u;
+    const uint64_t ones = ballot(bit);
+    const uint32_t nz = 64u - (uint32_t)__builtin_popcountll(ones);
+    const uint32_t dst = bit ? nz + mbcnt(ones) : mbcnt(~ones);
+    kv = perm32(kv, dst);
+  }
+  return kv;
+}
+
+typedef int64_t Row8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int64_t pick8(const Row8& v, uint32_t d) {
+  int64_t r = v[0];
+#pragma unroll
+  for (int k = 1; k < TRMV_DPAD; ++k) r = d == (uint32_t)k ? v[k] : r;
+  return r;
+}
+
+// gb_sets term order of two elements of one Id: (Score, DcId, Ts).
+__device__ __forceinline__ bool gb_gt(int64_t s1, uint32_t d1, int64_t t1, int64_t s2, uint32_t d2,
+                                      int64_t t2) {
+  return s1 > s2 || (s1 == s2 && (d1 > d2 || (d1 == d2 && t1 > t2)));
+}
+
+template <int PCAP>
+__device__ __forceinline__ void s_emit(const TrmvApplyArgs& a, SLds<PCAP>& L, uint64_t op0, uint64_t op,
+                                       uint8_t kind, int64_t id, int64_t sc, uint32_t dc, int64_t ts,
+                                       const Row8* vc) {
+  const uint32_t pos = atomicAdd(&L.nex, 1u);
+  TrmvExtraRec r;
+  r.op = (uint32_t)op;
+  r.kind = kind;
+  r.dc = (uint8_t)dc;
+  r.pad = 0;
+  r.id = id;
+  r.score = sc;
+  r.ts = ts;
+  a.ex[op0 + pos] = r;
+  if (vc)
+    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = pick8(*vc, (uint32_t)d);
+}
+
+// Player of each lane's Id (v lanes); new Ids are claimed and numbered
+// np, np+1, ... in lane order.  Returns false if the key outgrows PCAP.
+template <int PCAP>
+__device__ __forceinline__ bool s_resolve(SLds<PCAP>& L, int64_t id, bool v, uint32_t& np, uint32_t& p) {
+  constexpr int HS = SLds<PCAP>::HS;
+  const int lane = lane_id();
+  L.claim[lane] = id;
+  wave_lds_sync();
+  uint32_t h = shash<PCAP>(id);
+  bool resolved = !v, claimed = false;
+  int follow = -1;
+  p = 0;
+  while (ballot(!resolved)) {
+    if (!resolved) {
+      const uint32_t s = L.hs[h];
+      if (s == S_NONE) {
+        if (atomicCAS(&L.hs[h], S_NONE, S_CLAIM | (uint32_t)lane) == S_NONE) {
+          claimed = true;
+          resolved = true;
+        }  // lost the race: read the slot again
+      } else if (s & S_CLAIM) {
+        const int c = (int)(s & 63u);
+        if (L.claim[c] == id) {
+          follow = c;
+          resolved = true;
+        } else {
+          h = (h + 1) & (HS - 1);
+        }
+      } else if (L.pid[s] == id) {
+        p = s;
+        resolved = true;
+      } else {
+        h = (h + 1) & (HS - 1);
+      }
+    }
+  }
+  wave_lds_sync();
+  const uint64_t cm = ballot(claimed);
+  const uint32_t nn = np + (uint32_t)__builtin_popcountll(cm);
+  if (nn > (uint32_t)PCAP) return false;
+  if (claimed) {
+    p = np + mbcnt(cm);
+    L.pid[p] = id;
+    L.hs[h] = p;
+    L.oslab[p] = 0u;
+    L.orow[p] = S_NONE;
+    L.nops[p] = 0u;
+    L.opd[p] = NONE16 << 16;
+    L.gpd[p] = 0u;
+    L.osc[p] = L.ots[p] = L.gsc[p] = L.gts[p] = 0;
+  }
+  const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
+  if (follow >= 0) p = fp;
+  np = nn;
+  wave_lds_sync();
+  return true;
+}
+
+template <int PCAP>
+__device__ __forceinline__ uint32_t s_lookup(const SLds<PCAP>& L, int64_t id, bool v) {
+  constexpr int HS = SLds<PCAP>::HS;
+  uint32_t h = shash<PCAP>(id), p = (uint32_t)PCAP;
+  if (v) {
+    for (;;) {
+      const uint32_t s = L.hs[h];
+      if (s == S_NONE) break;  // cannot happen: K2 resolved every Id
+      if (L.pid[s] == id) {
+        p = s;
+        break;
+      }
+      h = (h + 1) & (HS - 1);
+    }
+  }
+  return p;
+}
+
+struct SMin {
+  uint32_t p;  // player of Min, S_NONE = {nil, nil, nil}
+  int64_t sc, id, ts;
+};
+
+// min_observed/1 (:398-406): term-order smallest Observed value; Ids are
+// distinct, so (Score, Id) decides.
+template <int PCAP>
+__device__ __forceinline__ void s_min(const SLds<PCAP>& L, uint32_t np, SMin& m) {
+  const int lane = lane_id();
+  uint32_t bp = S_NONE;
+  int64_t bs = INT64_MAX, bi = INT64_MAX;
+  for (uint32_t b = 0; b < np; b += 64) {
+    const uint32_t p = b + lane;
+    const uint32_t q = p < np ? p : (uint32_t)PCAP;
+    const bool ok = p < np && (L.opd[q] & F_OBS);
+    const int64_t sc = L.osc[q], id = L.pid[q];
+    if (ok && (bp == S_NONE || sc < bs || (sc == bs && id < bi))) {
+      bp = p;
+      bs = sc;
+      bi = id;
+    }
+  }
+  const bool has = bp != S_NONE;
+  if (!ballot(has)) {
+    m.p = S_NONE;
+    return;
+  }
+  const int64_t ms = wave_min_i64_dpp(has ? bs : INT64_MAX);
+  const int64_t mi = wave_min_i64_dpp(has && bs == ms ? bi : INT64_MAX);
+  const uint64_t hit = ballot(has && bs == ms && bi == mi);
+  m.p = rl32(bp, (int)__builtin_ctzll(hit));
+  m.sc = ms;
+  m.id = mi;
+  m.ts = ufl64(L.ots[m.p]);
+}
+
+// Promotion candidate of rmv/3 (:276-281, :291): the Id outside Observed
+// whose largest Masked element is the term-order largest, i.e. the largest
+// (max Score, Id); S_NONE if no Id outside Observed has Masked elements.
+template <int PCAP>
+__device__ __forceinline__ uint32_t s_promote(const SLds<PCAP>& L, uint32_t np) {
+  const int lane = lane_id();
+  uint32_t bp = S_NONE;
+  int64_t bs = INT64_MIN, bi = INT64_MIN;
+  for (uint32_t b = 0; b < np; b += 64) {
+    const uint32_t p = b + lane;
+    const uint32_t q = p < np ? p : (uint32_t)PCAP;
+    const uint32_t f = L.opd[q];
+    const bool ok = p < np && !(f & F_OBS) && (f & F_HASM);
+    const int64_t sc = L.gsc[q], id = L.pid[q];
+    if (ok && (bp == S_NONE || sc > bs || (sc == bs && id > bi))) {
+      bp = p;
+      bs = sc;
+      bi = id;
+    }
+  }
+  const bool has = bp != S_NONE;
+  if (!ballot(has)) return S_NONE;
+  const int64_t ms = wave_max_i64_dpp(has ? bs : INT64_MIN);
+  const int64_t mi = wave_max_i64_dpp(has && bs == ms ? bi : INT64_MIN);
+  const uint64_t hit = ballot(has && bs == ms && bi == mi);
+  return rl32(bp, (int)__builtin_ctzll(hit));
+}
+
+// One key.  Writes nothing to the new side before its last early return
+// that hands the key on (S_NEXT).
+template <int PCAP>
+__device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>& L) {
+  constexpr int HS = SLds<PCAP>::HS;
+  const int lane = lane_id();
+  const int D = a.n_dc;
+  const uint64_t op0 = a.key_ptr[key];
+  const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
+  const KeyMeta nm = a.new_s.meta[key];
+  KeyMeta om;
+  if (a.fresh) {
+    om.p_off = om.m_off = om.r_off = 0;
+    om.np = om.nm = om.nr = om.nobs = 0;
+    om.minq = NONE32;
+  } else {
+    om = a.old_s.meta[key];
+  }
+  if (om.np > (uint32_t)PCAP) return S_NEXT;
+
+  for (int i = lane; i < HS; i += 64) L.hs[i] = S_NONE;
+  if (lane <= TRMV_DPAD)
+    L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+  if (lane == 0) L.nex = 0u;
+  // sinks (PCAP) read by lanes without a player
+  if (lane == 0) {
+    L.opd[PCAP] = 0u;
+    L.osc[PCAP] = L.gsc[PCAP] = L.pid[PCAP] = 0;
+    L.ots[PCAP] = 0;
+  }
+  wave_lds_sync();
+
+  // ---- K1. old players
+  uint32_t span = 0;
+  for (uint32_t b = 0; b < om.np; b += 64) {
+    const uint32_t p = b + lane;
+    if (p < om.np) {
+      const uint64_t pp = (uint64_t)om.p_off + p;
+      const int64_t id = a.old_s.pl_id[pp];
+      const uint32_t info = a.old_s.pl_info[pp], slab = a.old_s.pl_slab[pp];
+      const uint32_t gb = a.old_s.pl_gb[pp];
+      const uint32_t off = slab & 0xFFFFu, cnt = slab >> 16, ob = info & 0xFFFFu;
+      const uint64_t g0 = (uint64_t)om.m_off + off;
+      int64_t os = 0, ot = 0, gs = 0, gt = 0;
+      uint32_t od = 0, gd = 0;
+      if (ob != NONE16) {
+        os = a.old_s.m_score[g0 + ob];
+        ot = a.old_s.m_ts[g0 + ob];
+        od = a.old_s.m_dc[g0 + ob];
+      }
+      if (cnt) {
+        gs = a.old_s.m_score[g0 + gb];
+        gt = a.old_s.m_ts[g0 + gb];
+        gd = a.old_s.m_dc[g0 + gb];
+      }
+      L.pid[p] = id;
+      L.oslab[p] = slab;
+      L.orow[p] = info;
+      L.nops[p] = 0u;
+      L.osc[p] = os;
+      L.ots[p] = ot;
+      L.gsc[p] = gs;
+      L.gts[p] = gt;
+      L.opd[p] = (ob != NONE16 ? F_OBS : 0u) | (cnt ? F_HASM : 0u) |
+                 ((info >> 16) != NONE16 ? F_ROWV : 0u) | (od << 8) | (ob << 16);
+      L.gpd[p] = (gd << 8) | (gb << 16);
+      span = off + cnt > span ? off + cnt : span;
+      uint32_t h = shash<PCAP>(id);
+      while (atomicCAS(&L.hs[h], S_NONE, p) != S_NONE) h = (h + 1) & (HS - 1);
+    }
+  }
+  span = wave_max_u32_dpp(span);
+  wave_lds_sync();
+
+  // ---- K2. the player of every op, ops per player, players with a rmv
+  uint32_t np = om.np;
+  for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
+    const uint32_t l = c0 + lane;
+    const bool v = l < nops;
+    const int64_t id = v ? a.id[op0 + l] : 0;
+    const uint32_t kind = v ? (uint32_t)a.kind[op0 + l] : 0u;
+    uint32_t p;
+    if (!s_resolve<PCAP>(L, id, v, np, p)) return S_NEXT;
+    if (v) {
+      atomicAdd(&L.nops[p], 1u);
+      if (kind == 2 || kind == 3) atomicOr(&L.opd[p], F_RMV);
+    }
+  }
+  wave_lds_sync();
+  // new Removals rows, new slab offsets (old count + ops: the new segment)
+  uint32_t nr = om.nr, mtot = 0;
+  for (uint32_t b = 0; b < np; b += 64) {
+    const uint32_t p = b + lane;
+    const bool act = p < np;
+    const uint32_t q = act ? p : (uint32_t)PCAP;
+    const uint32_t info = L.orow[q], f = L.opd[q];
+    const bool newrow = act && (f & F_RMV) && (info >> 16) == NONE16;
+    const uint64_t m = ballot(newrow);
+    if (newrow) L.orow[p] = (info & 0xFFFFu) | ((nr + mbcnt(m)) << 16);
+    nr += (uint32_t)__builtin_popcountll(m);
+    const uint32_t ocnt = act ? (L.oslab[q] >> 16) : 0u;
+    const uint32_t cap = act ? ocnt + L.nops[q] : 0u;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_scan_dpp(cap, tot);
+    if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
+    mtot += tot;
+  }
+  if (nr >= NONE16 || mtot > TRMV_SEG_MAX) {
+    if (lane == 0) atomicOr(&a.status[1], TRMV_ERR_SEG);
+    return S_REJECT;
+  }
+  wave_lds_sync();
+
+  // ---- K3. old slabs (except replayed players') and old Removals rows
+  if (!a.fresh && span) {
+    int32_t prev = -1;  // owner of the position before the window
+    for (uint32_t q0 = 0; q0 < span; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      const uint64_t src = (uint64_t)om.m_off + q;
+      int64_t sc = 0, ts = 0;
+      uint32_t dc = 0;
+      if (q < span) {
+        sc = a.old_s.m_score[src];
+        ts = a.old_s.m_ts[src];
+        dc = a.old_s.m_dc[src];
+      }
+      L.mark[lane] = 0u;
+      wave_lds_sync();
+      for (uint32_t j0 = (uint32_t)(prev + 1);; j0 += 64) {  // slabs starting in the window
+        const uint32_t j = j0 + lane;
+        const uint32_t off = j < om.np ? (L.oslab[j] & 0xFFFFu) : S_NONE;
+        if (off >= q0 && off < q0 + 64) atomicMax(&L.mark[off - q0], j + 1);
+        const uint32_t last = rl32(off, 63);
+        if (!(j0 + 64 < om.np && last < q0 + 64)) break;
+      }
+      wave_lds_sync();
+      const uint32_t own = wave_incl_max_dpp(L.mark[lane]);
+      const int32_t o = own ? (int32_t)own - 1 : prev;
+      prev = (int32_t)rl32((uint32_t)o, 63);
+      if (q < span && o >= 0) {
+        const uint32_t sl = L.oslab[o];
+        const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
+        if (q < off + cnt && !(L.opd[o] & F_RMV)) {
+          const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
+          a.new_s.m_score[dst] = sc;
+          a.new_s.m_ts[dst] = ts;
+          a.new_s.m_dc[dst] = (uint8_t)dc;
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
+    const uint32_t r = r0 + (lane >> 3), d = lane & 7;
+    if (r < om.nr && (int)d < D)
+      a.new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
+  }
+  // the replays read rows written here: retire the stores first
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+  // ---- K4. chunks of the key's ops
+  SMin mn;
+  mn.p = om.minq;
+  mn.sc = mn.id = mn.ts = 0;
+  if (mn.p != NONE32) {
+    mn.sc = ufl64(L.osc[mn.p]);
+    mn.id = ufl64(L.pid[mn.p]);
+    mn.ts = ufl64(L.ots[mn.p]);
+  }
+  uint32_t nobs = om.nobs;
+  const uint32_t K = a.k;
+  for (uint32_t c0 = 0; c0 < nops;) {
+    uint32_t n = nops - c0 < (uint32_t)S_CH ? nops - c0 : (uint32_t)S_CH;
+    bool v = (uint32_t)lane < n;
+    const uint64_t gi = op0 + c0 + lane;
+    const uint32_t kind = v ? (uint32_t)a.kind[gi] : 0u;
+    const int64_t id = v ? a.id[gi] : 0;
+    const int64_t sc = v ? a.score[gi] : 0;
+    const int64_t ts = v ? a.ts[gi] : 0;
+    const uint32_t dc = v ? (uint32_t)a.dc[gi] : 0u;
+    bool isr = v && (kind == 2 || kind == 3);
+    uint64_t rm = ballot(isr);
+    if (__builtin_popcountll(rm) > S_CHR) {  // cut before the chunk's 17th rmv
+      uint64_t m = rm;
+      for (int k = 0; k < S_CHR; ++k) m &= m - 1;
+      n = (uint32_t)__builtin_ctzll(m);
+      v = (uint32_t)lane < n;
+      isr = isr && v;
+      rm = ballot(isr);
+    }
+    const bool add = v && kind < 2;
+    uint32_t err = 0;
+    err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
+    err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
+    err |= (add && ts < 1) ? TRMV_ERR_TS : 0u;
+    err |= (isr && (ts < 0 || ts >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
+    if (ballot(err != 0)) {
+      if (err) atomicOr(&a.status[1], err);
+      return S_REJECT;
+    }
+    const uint32_t p = s_lookup<PCAP>(L, id, v);
+    // the rmvs' clocks (8 lanes per row)
+    const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
+    if (isr) L.crow[rk] = (uint32_t)ts;
+    wave_lds_sync();
+    for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
+      const uint32_t r = r0 + (lane >> 3), d = lane & 7;
+      if (r < nrm) {
+        const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.crow[r] * D + d] : 0;
+        err |= x < 0 ? TRMV_ERR_VC : 0u;
+        L.vtab[r][d] = x;
+      }
+    }
+    if (ballot(err != 0)) {
+      if (err) atomicOr(&a.status[1], err);
+      return S_REJECT;
+    }
+    // Elements that may already be in Masked[Id] (gb_sets:add_element, :240-246):
+    // every element of dc in the key has Ts <= Vc[dc], so an add whose Ts is
+    // above the key's Vc[dc] before it is new.  Exact when the chunk's adds of
+    // each dc have rising Ts (then the previous one holds the maximum);
+    // otherwise every add of that dc after the first fall is a candidate.
+    bool dupc;
+    {
+      const int64_t vcs = (int64_t)L.vc[add ? dc : (uint32_t)TRMV_DPAD];
+      const uint32_t kv = wave_radix_sort<4>(((add ? dc : 8u) << 6) | (uint32_t)lane);
+      const uint32_t src = kv & 63u, sdc = kv >> 6;
+      const int64_t sts = shfl64(ts, (int)src);
+      const uint32_t lkv = shfl32(kv, lane ? lane - 1 : 0);
+      const int64_t lts = shfl64(sts, lane ? lane - 1 : 0);
+      const bool fall = lane > 0 && sdc < 8u && (lkv >> 6) == sdc && lts >= sts;
+      const uint64_t fm = ballot(fall);
+      // a fall taints the rest of its dc run (sorted lanes, stream order inside)
+      bool taint = false;
+      if (fm) {
+        const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        const uint64_t f = fm & below;
+        const uint32_t hi = f ? 63u - (uint32_t)__builtin_clzll(f) : (uint32_t)lane;
+        const uint32_t fkv = shfl32(kv, (int)hi);
+        taint = f != 0 && (fkv >> 6) == sdc;
+      }
+      const bool taint_src = perm32(taint ? 1u : 0u, src) != 0;  // back to stream lanes
+      dupc = add && (ts <= vcs || taint_src);
+    }
+    wave_lds_sync();
+    if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
+    L.csc[lane] = sc;
+    L.cts[lane] = ts;
+    L.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)PCAP << 8);
+    L.cres[lane] = isr ? rk : 0u;
+    wave_lds_sync();
+
+    // ---- ops in (player, stream) order
+    const uint32_t kvs = wave_radix_sort<Log2<PCAP>::v + 1>(((v ? p : (uint32_t)PCAP) << 6) | (uint32_t)lane);
+    const uint32_t sp = kvs >> 6, so = kvs & 63u;
+    const bool sv = sp < (uint32_t)PCAP;
+    const uint32_t lkvs = shfl32(kvs, lane ? lane - 1 : 0);
+    const bool start = sv && (lane == 0 || (lkvs >> 6) != sp);
+    L.csrt[lane] = (uint8_t)so;
+    const uint64_t ss = ballot(start);
+    const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const uint64_t sb = ss & incl;
+    const uint32_t slo = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
+    const uint64_t above = ss & ~incl;
+    const uint32_t shi = above ? (uint32_t)__builtin_ctzll(above) : n;
+    const uint64_t segm = (shi >= 64 ? ~0ull : ((1ull << shi) - 1)) & ~((1ull << slo) - 1);
+    const uint32_t skd = L.ckd[so];
+    const int64_t ssc = L.csc[so], sts = L.cts[so];
+    const uint32_t sdc = (skd >> 2) & 7u;
+    const uint32_t pf = L.opd[sv ? sp : (uint32_t)PCAP];
+    const uint64_t dm = ballot(sv && ((skd >> 5) & 1u));
+    const bool walk = sv && ((pf & F_RMV) || (dm & segm));
+    // players without a rmv: append their non-dominated adds (op-parallel);
+    // their Removals row is the old one for the whole batch
+    bool dom = false;
+    uint32_t orw = NONE16;
+    if (sv && !walk && (pf & F_ROWV)) {
+      orw = L.orow[sp] >> 16;
+      dom = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + sdc] >= sts;
+    }
+    const bool app = sv && !walk && !dom;
+    const uint64_t nd = ballot(app);
+    if (app) {
+      const uint32_t ns = L.nslab[sp];
+      const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << lane) - 1));
+      const uint64_t dst = (uint64_t)nm.m_off + (ns & 0xFFFFu) + pos;
+      a.new_s.m_score[dst] = ssc;
+      a.new_s.m_ts[dst] = sts;
+      a.new_s.m_dc[dst] = (uint8_t)sdc;
+      L.cres[so] = pos << 16;
+    }
+    if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
+      Row8 rv = (Row8)(0);
+      for (int d = 0; d < D; ++d) rv[d] = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + d];
+      L.cres[so] = R_DOM;
+      s_emit<PCAP>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
+    }
+    wave_lds_sync();
+    if (sv && !walk && lane + 1 == (int)shi) {
+      const uint32_t ns = L.nslab[sp];
+      L.nslab[sp] = ns + ((uint32_t)__builtin_popcountll(nd & segm) << 16);
+    }
+    // players with a rmv, or a possibly duplicated element: one lane each
+    const uint64_t wm = ballot(start && walk);
+    if (start && walk) {
+      const uint32_t k = mbcnt(wm);
+      L.cwp[k] = (uint16_t)sp;
+      L.cws[k] = (uint8_t)lane;
+      L.cwe[k] = (uint8_t)shi;
+    }
+    wave_lds_sync();
+    if ((uint32_t)lane < (uint32_t)__builtin_popcountll(wm)) {
+      const uint32_t wp = L.cwp[lane], ws = L.cws[lane], we = L.cwe[lane];
+      uint32_t f = L.opd[wp];
+      const uint32_t ns = L.nslab[wp];
+      const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
+      uint32_t cnt = ns >> 16;
+      const uint32_t row = L.orow[wp] >> 16;
+      if ((f & F_RMV) && !(f & F_MAT)) {  // its old slab, copied by itself
+        const uint32_t os = L.oslab[wp];
+        const uint64_t g0 = (uint64_t)om.m_off + (os & 0xFFFFu);
+        for (uint32_t j = 0; j < (os >> 16); ++j) {
+          a.new_s.m_score[base + j] = a.old_s.m_score[g0 + j];
+          a.new_s.m_ts[base + j] = a.old_s.m_ts[g0 + j];
+          a.new_s.m_dc[base + j] = a.old_s.m_dc[g0 + j];
+        }
+        f |= F_MAT;
+      }
+      bool has_row = (f & F_ROWV) != 0;
+      Row8 R = (Row8)(0);
+      const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
+      if (has_row)
+        for (int d = 0; d < D; ++d) R[d] = a.new_s.r_vc[rbase + d];
+      const int64_t wid = L.pid[wp];
+      bool moved = false;
+      for (uint32_t x = ws; x < we; ++x) {
+        const uint32_t o = L.csrt[x];
+        const uint32_t kd = L.ckd[o];
+        const int64_t esc = L.csc[o], ets = L.cts[o];
+        const uint32_t edc = (kd >> 2) & 7u;
+        if ((kd & 3u) < 2) {  // add/4
+          if (has_row && pick8(R, edc) >= ets) {  // dominated (:234-237)
+            L.cres[o] = R_DOM;
+            s_emit<PCAP>(a, L, op0, op0 + c0 + o, CCRDT_TRMV_RMV, wid, 0, 0, 0, &R);
+            continue;
+          }
+          uint32_t pos = S_NONE;
+          if ((kd >> 5) & 1u)  // set semantics: the element may be there
+            for (uint32_t j = 0; j < cnt; ++j)
+              if (a.new_s.m_ts[base + j] == ets && a.new_s.m_dc[base + j] == edc &&
+                  a.new_s.m_score[base + j] == esc) {
+                pos = j;
+                break;
+              }
+          if (pos == S_NONE) {
+            pos = cnt++;
+            a.new_s.m_score[base + pos] = esc;
+            a.new_s.m_ts[base + pos] = ets;
+            a.new_s.m_dc[base + pos] = (uint8_t)edc;
+          }
+          L.cres[o] = pos << 16;
+        } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
+          const uint32_t r = L.cres[o];
+          Row8 V;
+#pragma unroll
+          for (int d = 0; d < TRMV_DPAD; ++d) V[d] = L.vtab[r][d];
+#pragma unroll
+          for (int d = 0; d < TRMV_DPAD; ++d) R[d] = has_row ? (V[d] > R[d] ? V[d] : R[d]) : V[d];
+          has_row = true;
+          uint32_t w = 0, bpos = 0, bdc = 0;
+          int64_t bsc = 0, bts = 0;
+          for (uint32_t j = 0; j < cnt; ++j) {
+            const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
+            const uint32_t d2 = a.new_s.m_dc[base + j];
+            if (t2 > pick8(V, d2)) {
+              if (w != j) {
+                a.new_s.m_score[base + w] = s2;
+                a.new_s.m_ts[base + w] = t2;
+                a.new_s.m_dc[base + w] = (uint8_t)d2;
+              }
+              if (w == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
+                bsc = s2;
+                bdc = d2;
+                bts = t2;
+                bpos = w;
+              }
+              ++w;
+            }
+          }
+          moved |= w != cnt;
+          cnt = w;
+          L.rgsc[r] = bsc;
+          L.rgts[r] = bts;
+          L.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
+        }
+      }
+      L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
+      if (has_row) {
+        for (int d = 0; d < D; ++d) a.new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
+        f |= F_ROWV;
+      }
+      if (moved) f |= F_WALK;
+      L.opd[wp] = f;
+    }
+    wave_lds_sync();
+    // the next chunk's replays read this chunk's stores
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+    // ---- the Observed half, one op at a time in stream order
+    // (recompute_observed/5 :301-334; rmv/3 :267-298)
+    const uint32_t kdr = L.ckd[lane], crr = L.cres[lane];
+    const int64_t scr = L.csc[lane], tsr = L.cts[lane];
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kd = rl32(kdr, (int)j), cr = rl32(crr, (int)j);
+      const uint32_t q = kd >> 8;
+      if ((kd & 3u) < 2) {
+        if (cr & R_DOM) continue;
+        const int64_t s = rl64(scr, (int)j), t = rl64(tsr, (int)j);
+        const uint32_t edc = (kd >> 2) & 7u, pos = cr >> 16;
+        uint32_t f = ufl(L.opd[q]);
+        // gb_sets:largest(Masked[Id]) after the insert
+        const int64_t gs = ufl64(L.gsc[q]), gt = ufl64(L.gts[q]);
+        const uint32_t gd = (ufl(L.gpd[q]) >> 8) & 0xFFu;
+        if (!(f & F_HASM) || gb_gt(s, edc, t, gs, gd, gt)) {
+          if (lane == 0) {
+            L.gsc[q] = s;
+            L.gts[q] = t;
+            L.gpd[q] = (edc << 8) | (pos << 16);
+          }
+        }
+        f |= F_HASM;
+        const uint32_t fobs = (f & 0xFFu) | F_OBS | (edc << 8) | (pos << 16);
+        bool need_min = false;
+        if (f & F_OBS) {  // Id in Observed (:303-315)
+          const int64_t os = ufl64(L.osc[q]), ot = ufl64(L.ots[q]);
+          if (s > os || (s == os && t > ot)) {
+            if (lane == 0) {
+              L.osc[q] = s;
+              L.ots[q] = t;
+            }
+            f = fobs;
+            need_min = q == mn.p;  // Old =:= Min
+          }
+        } else if (nobs < K) {  // (:317-324)
+          if (lane == 0) {
+            L.osc[q] = s;
+            L.ots[q] = t;
+          }
+          f = fobs;
+          ++nobs;
+          const int64_t qid = ufl64(L.pid[q]);
+          if (mn.p == S_NONE || mn.sc > s || (mn.sc == s && (mn.id > qid || (mn.id == qid && mn.ts > t)))) {
+            mn.p = q;
+            mn.sc = s;
+            mn.id = qid;
+            mn.ts = t;
+          }
+        } else {  // full: evict Min if cmp(Elem, Min) (:325-331)
+          const int64_t qid = ufl64(L.pid[q]);
+          if (s > mn.sc || (s == mn.sc && (qid > mn.id || (qid == mn.id && t > mn.ts)))) {
+            if (lane == 0) {
+              L.opd[mn.p] = L.opd[mn.p] & ~F_OBS;
+              L.osc[q] = s;
+              L.ots[q] = t;
+            }
+            f = fobs;
+            need_min = true;
+          }
+        }
+        if (lane == 0) L.opd[q] = f;
+        wave_lds_sync();
+        if (need_min) s_min<PCAP>(L, np, mn);
+      } else {  // rmv/3
+        const uint32_t r = cr;
+        const uint32_t g = ufl(L.rgd[r]);
+        uint32_t f = ufl(L.opd[q]);
+        const bool nonempty = g & 1u;
+        if (lane == 0 && nonempty) {
+          L.gsc[q] = L.rgsc[r];
+          L.gts[q] = L.rgts[r];
+          L.gpd[q] = g & 0xFFFFFF00u;
+        }
+        f = nonempty ? (f | F_HASM) : (f & ~F_HASM);
+        bool impacts = false;
+        if (f & F_OBS) {  // VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
+          const uint32_t odc = (f >> 8) & 0xFFu;
+          impacts = ufl64(L.vtab[r][odc]) >= ufl64(L.ots[q]);
+        }
+        if (!impacts) {
+          if (lane == 0) L.opd[q] = f;
+          wave_lds_sync();
+          continue;
+        }
+        f &= ~F_OBS;
+        --nobs;
+        if (lane == 0) L.opd[q] = f;
+        wave_lds_sync();
+        const uint32_t w = s_promote<PCAP>(L, np);
+        if (w == S_NONE) {  // (:283-289)
+          if (q == mn.p) s_min<PCAP>(L, np, mn);
+        } else {  // promote the largest (:290-295)
+          const int64_t gs = ufl64(L.gsc[w]), gt = ufl64(L.gts[w]), wid = ufl64(L.pid[w]);
+          const uint32_t gd = ufl(L.gpd[w]);
+          if (lane == 0) {
+            L.osc[w] = gs;
+            L.ots[w] = gt;
+            L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
+          }
+          ++nobs;
+          wave_lds_sync();
+          s_min<PCAP>(L, np, mn);
+          if (lane == 0)
+            s_emit<PCAP>(a, L, op0, op0 + c0 + j, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt,
+                         nullptr);
+        }
+      }
+    }
+    wave_lds_sync();
+    c0 += n;
+  }
+
+  // ---- K5. positions of compacted slabs; player records; Vc; meta
+  uint32_t mcount = 0;
+  for (uint32_t b = 0; b < np; b += 64) {
+    const uint32_t p = b + lane;
+    if (p < np) {
+      uint32_t f = L.opd[p], g = L.gpd[p];
+      const uint32_t ns = L.nslab[p], cnt = ns >> 16;
+      if ((f & F_WALK) && cnt) {
+        const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
+        const int64_t os = L.osc[p], ot = L.ots[p];
+        const uint32_t od = (f >> 8) & 0xFFu;
+        uint32_t opos = NONE16, bpos = 0, bdc = 0;
+        int64_t bsc = 0, bts = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
+          const uint32_t d2 = a.new_s.m_dc[base + j];
+          if (s2 == os && t2 == ot && d2 == od) opos = j;
+          if (j == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
+            bsc = s2;
+            bdc = d2;
+            bts = t2;
+            bpos = j;
+          }
+        }
+        if (f & F_OBS) f = (f & 0xFFFFu) | (opos << 16);
+        g = (bdc << 8) | (bpos << 16);
+      }
+      const uint64_t pp = (uint64_t)nm.p_off + p;
+      a.new_s.pl_id[pp] = L.pid[p];
+      a.new_s.pl_slab[pp] = ns;
+      a.new_s.pl_info[pp] = ((f & F_OBS) ? (f >> 16) : NONE16) | (L.orow[p] & 0xFFFF0000u);
+      a.new_s.pl_gb[pp] = (uint16_t)(cnt ? (g >> 16) : 0u);
+      mcount += cnt;
+    }
+  }
+  uint32_t mtotal;
+  (void)wave_excl_scan_dpp(mcount, mtotal);
+  if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+  if (lane == 0) {
+    KeyMeta out = nm;
+    out.np = np;
+    out.nm = mtotal;
+    out.nr = nr;
+    out.nobs = nobs;
+    out.minq = mn.p;
+    a.new_s.meta[key] = out;
+    a.ex_cnt[key] = L.nex;
+  }
+  return S_DONE;
+}
+
+}  // namespace
+
+template <int PCAP, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a) {
+  __shared__ SLds<PCAP> lds[WAVES];
+  const uint32_t wv = ufl(threadIdx.x >> 6);
+  SLds<PCAP>& L = lds[wv];
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x * WAVES + wv; w < n; w += gridDim.x * WAVES) {
+    const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
+    const int r = trmv_steady_key<PCAP>(a, key, L);
+    if (r == S_NEXT && lane_id() == 0) {
+      const uint32_t pos = atomicAdd(&a.status[0], 1u);
+      a.ovf_list[pos] = key;
+    }
+    wave_lds_sync();
+  }
+}
+
+// cls 0: up to 256 players per key, two keys per workgroup; cls 1: up to 1024
+// players.  grid_keys bounds the work list (its length may live on the device).
+int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st) {
+  if (grid_keys == 0) return CCRDT_OK;
+  if (cls == 0) {
+    const uint64_t blocks = std::min<uint64_t>((grid_keys + 1) / 2, 16384);
+    hipLaunchKernelGGL((trmv_steady_kernel<256, 2>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+  } else {
+    const uint64_t blocks = std::min<uint64_t>(grid_keys, 4096);
+    hipLaunchKernelGGL((trmv_steady_kernel<1024, 1>), dim3((unsigned)blocks), dim3(64), 0, st, a);
+  }
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+}  // namespace ccrdt

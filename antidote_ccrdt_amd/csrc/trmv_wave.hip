@@ -108,6 +108,8 @@ struct alignas(16) WaveLds {
   uint8_t fin[NS_ * (W_ECAP + 8)];       // final pool: element of every output position
   uint8_t pstart[W_PCAP + 8];            // first position of each player's ops
   uint8_t pobs[W_PCAP + 8];              // Obs[Id] of each player (element), NONE8 = none
+  uint8_t pgb[W_PCAP + 8];               // gb_sets:largest(Masked[Id]) (element; slab-relative
+                                         // + slab start for replayed players)
   uint8_t pflag[W_PCAP + 8];             // 1 = player replayed op by op
   uint8_t pcntf[W_PCAP + 8];             // replayed player: final |Masked[Id]|
   uint8_t pmoff[NS_ * (W_PCAP + 8)];     // replayed player: its working slab in `slab`
@@ -568,7 +570,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     // ---- 5a. players without rmv or old state, op-parallel: each add
     // decides whether it is its player's Obs[Id] and whether its Ts rises
     // over every earlier add's
-    bool simple[2], beaten[2] = {false, false}, risk[2] = {false, false};
+    bool simple[2], beaten[2] = {false, false}, gbeaten[2] = {false, false}, risk[2] = {false, false};
     uint32_t me[2], cl[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -583,16 +585,19 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const bool valid = x < cl[s] && x != me[s];
         const uint32_t pos = x < cl[s] ? xst[s] + x : (uint32_t)ESINK;
         const int64_t sx = L.esc[pos], tx = L.ets[pos];
+        const uint32_t dx = (L.ekd[pos] >> 2) & 7u;
         const int64_t sm = xsc[s], tm = xts[s];
         const bool before = x < me[s];
         risk[s] |= valid && before && tx >= tm;
         beaten[s] |= valid && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
+        gbeaten[s] |= valid && (sx > sm || (sx == sm && (dx > xdc[s] || (dx == xdc[s] && tx > tm))));
       }
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (risk[s]) L.pflag[xp[s]] = 1;
       if (simple[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
+      if (simple[s] && !gbeaten[s]) L.pgb[xp[s]] = (uint8_t)xq[s];
     }
     wave_lds_sync();
   } else {
@@ -610,7 +615,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bool single = xv[s] && xc[s] == 1;
-        if (single && xa[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
+        if (single && xa[s]) {
+          L.pobs[xp[s]] = (uint8_t)xq[s];
+          L.pgb[xp[s]] = (uint8_t)xq[s];
+        }
         if (single && xr[s]) {
           L.prow[xp[s]] = (uint8_t)xsc[s];
           L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
@@ -637,7 +645,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t adc = ya ? ((kd >> 2) & 7u) : 0u;
       const uint32_t st = L.pstart[p], c = act ? pcnt_of(L, p) : 0u;
       const uint32_t me = q - st;
-      bool fb = false, beaten = false, risk = false, seen = false, first = true;
+      bool fb = false, beaten = false, gbeaten = false, risk = false, seen = false, first = true;
+      const uint32_t mdc = (kd >> 2) & 7u;
       const uint32_t maxc = wave_max_u32_dpp(c);
       // software-pipelined: position x+1 is read while position x's clock
       // entry (its address depends on x's element) is in flight
@@ -646,6 +655,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
         const int64_t sx = sxn, tx = txn;
+        const uint32_t dx = (kxn >> 2) & 7u;
         const bool valid = x < c && x != me;
         const bool isr = valid && (kxn & 2u) != 0;
         const bool before = x < me;
@@ -662,12 +672,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         first &= !(isr && before);
         risk = risk && !isr;
         beaten = beaten && !isr;
+        gbeaten = gbeaten && !isr;
         const bool both = ya && valid && !isr;
         risk |= both && before && tx >= tm;
         beaten |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
+        // gb_sets term order inside one Id: (Score, DcId, Ts); the last
+        // segment's Ts rise strictly (else the player is replayed), so no ties
+        gbeaten |= both && (sx > sm || (sx == sm && (dx > mdc || (dx == mdc && tx > tm))));
       }
       if (act && (fb || risk)) L.pflag[p] = 1;
       if (ya && !seen && !beaten) L.pobs[p] = (uint8_t)q;
+      if (ya && !seen && !gbeaten) L.pgb[p] = (uint8_t)q;
       if (yr && first) L.prow[p] = (uint8_t)sm;  // a rmv's "score" is its clock row
       if (yr && !seen) L.plr[p] = (uint8_t)(q + 1);
       if (act) mrg[k] = (uint8_t)(yr && !first);
@@ -853,16 +868,26 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (FRESH) {
       // the player's slab at [pstart, pstart + cnt); its record is written
       // with every other player's below
-      uint32_t opos = NONE16;
+      uint32_t opos = NONE16, gj = 0, gdc = 0;
+      int64_t gsc = 0, gts = 0;
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t e2 = L.slab[moff + j];
-        (a.new_s.m_score + nmeta.m_off)[st + j] = L.esc[e2];
-        (a.new_s.m_ts + nmeta.m_off)[st + j] = L.ets[e2];
-        (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)((L.ekd[e2] >> 2) & 7u);
+        const int64_t s2 = L.esc[e2], t2 = L.ets[e2];
+        const uint32_t d2 = (L.ekd[e2] >> 2) & 7u;
+        (a.new_s.m_score + nmeta.m_off)[st + j] = s2;
+        (a.new_s.m_ts + nmeta.m_off)[st + j] = t2;
+        (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)d2;
         opos = e2 == o ? j : opos;
+        if (j == 0 || s2 > gsc || (s2 == gsc && (d2 > gdc || (d2 == gdc && t2 > gts)))) {
+          gj = j;
+          gsc = s2;
+          gdc = d2;
+          gts = t2;
+        }
       }
       if (act) {
         L.pobs[p] = (uint8_t)(o == NONE8 ? NONE8 : st + opos);
+        L.pgb[p] = (uint8_t)(st + gj);
         L.pcntf[p] = (uint8_t)cnt;
         L.prow[p] = (uint8_t)prow;
       }
@@ -905,6 +930,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       if (act) {
         (a.new_s.pl_id + nmeta.p_off)[p] = id;
         (a.new_s.pl_slab + nmeta.p_off)[p] = off | (cnt << 16);
+        (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)(cnt ? (uint32_t)L.pgb[pp] - off : 0u);
         (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : o - off) |
                                              ((prow != NONE8 ? rix : NONE16) << 16);
       }
@@ -916,7 +942,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     wave_lds_sync();
   } else {
   {
-    uint32_t cnt[2], st[2], moff[2], goff[2], prow[2], opos[2];
+    uint32_t cnt[2], st[2], moff[2], goff[2], prow[2], opos[2], gbj[2], gbd[2];
+    int64_t gbs[2], gbt[2];
     bool act[2], cx[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -934,6 +961,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       goff[s] = fbase + wave_excl_scan_dpp(cnt[s], ftot);
       fbase += ftot;
       opos[s] = (act[s] && !cx[s]) ? po[s] - st[s] : NONE16;
+      gbj[s] = (act[s] && !cx[s]) ? (uint32_t)L.pgb[pp] - st[s] : 0u;
+      gbd[s] = 0u;
+      gbs[s] = gbt[s] = 0;
     }
     // final pool order: replayed players' slabs, simple players' op runs
     const uint32_t maxcnt = wave_max_u32_dpp(cnt[0] > cnt[1] ? cnt[0] : cnt[1]);
@@ -944,6 +974,16 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const uint32_t e = cx[s] ? (uint32_t)L.slab[in ? moff[s] + j : 0u] : st[s] + j;
         if (in) L.fin[goff[s] + j] = (uint8_t)e;
         opos[s] = (cx[s] && in && e == po[s]) ? j : opos[s];
+        if (cx[s] && in) {  // gb_sets:largest of a replayed player's slab
+          const int64_t s2 = L.esc[e], t2 = L.ets[e];
+          const uint32_t d2 = (L.ekd[e] >> 2) & 7u;
+          if (j == 0 || s2 > gbs[s] || (s2 == gbs[s] && (d2 > gbd[s] || (d2 == gbd[s] && t2 > gbt[s])))) {
+            gbj[s] = j;
+            gbs[s] = s2;
+            gbd[s] = d2;
+            gbt[s] = t2;
+          }
+        }
       }
     }
 #pragma unroll
@@ -959,6 +999,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         (a.new_s.pl_info + nmeta.p_off)[p] = (po[s] == NONE8 ? NONE16 : opos[s]) |
                                              ((prow[s] != NONE8 ? rix : NONE16) << 16);
         (a.new_s.pl_slab + nmeta.p_off)[p] = goff[s] | (cnt[s] << 16);
+        (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)(cnt[s] ? gbj[s] : 0u);
       }
       nobs += (uint32_t)__builtin_popcountll(ballot(act[s] && po[s] != NONE8));
     }

@@ -219,7 +219,9 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    tiers = (0, 1, 2, 4, 8, 16, 1000, 1002, 1004, 1008, 1016)  # 1000+: side chain (big keys)
+    # 0 = tier 0, 1 / 2 = tier S (256 / 1024 players); 1000 = side chain
+    # (keys with > 128 ops), 1001 / 1002 = its tier S classes
+    tiers = (0, 1, 2, 1000, 1001, 1002)
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
@@ -248,10 +250,8 @@ def main():
             rows.append({"batch": i + 1, "ms": round(ms, 3),
                          "ops_per_s": args.n_ops / (ms * 1e-3),
                          "apply_chain_ms": round(eng.last_kernel_ms(), 3),
-                         "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in
-                                                    (0, 1, 2, 4, 8, 16, 1000)},
-                         "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in
-                                               (0, 1, 2, 4, 8, 16, 1000)},
+                         "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in tiers},
+                         "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers},
                          "state_after": dict(zip(("observed", "masked", "removal_rows"),
                                                  eng.sizes()))})
         mean_ms = sum(r["ms"] for r in rows) / len(rows)
