@@ -27,7 +27,6 @@ int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st)
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
-int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st);
 int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
                            hipStream_t st);
 int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
@@ -38,8 +37,7 @@ int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, con
 // up to 256 / 1024 players per key (tier S).
 static constexpr int TRMV_N_TIERS = 3;
 static constexpr uint32_t TRMV_MAX_PLAYERS = 1024u;  // players per key (tier S, last class)
-static constexpr int TRMV_STATUS_WORDS = 32;  // [0,8) scan + main tiers, [16,22) side chain
-static constexpr int TRMV_SIDE = 16;
+static constexpr int TRMV_STATUS_WORDS = 8;  // [0,2) scan, [2+2t, 4+2t) tier t
 static constexpr uint32_t TRMV_LATER_GRID = 4096;  // keys the grids of the later tiers cover
 
 }  // namespace ccrdt
@@ -76,7 +74,6 @@ void ccrdt_engine::release_all() {
     b.vc.release();
   }
   for (DevBuf& d : tier_ovf) d.release();
-  for (DevBuf& d : tier_ovf_b) d.release();
   for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -188,7 +185,6 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->evk0) (void)hipEventDestroy(e->evk0);
   if (e->evk1) (void)hipEventDestroy(e->evk1);
-  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   e->destroy_tier_events();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -345,7 +341,6 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
   for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
-  for (DevBuf& d : E.tier_ovf_b) CCRDT_TRY(d.ensure(nk * 4));
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
@@ -353,6 +348,8 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   //    the keys each tier hands on.  Every later tier reads its list length
   //    from the device, so the whole chain is queued without a host round
   //    trip; one sync at the end reads the status.
+  // Keys with more ops than tier 0 takes are handed on by it like the others
+  // (tier S runs them after it, ~0.1 ms for a bench batch).
   // CCRDT_TRMV_FIRST_TIER (tuning knob): -1 = tier 0 for fresh batches and
   // tier S for batches onto resident state (default), 0 = always tier 0 first,
   // 1 = always tier S.
@@ -362,32 +359,6 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   }();
   const int first_tier = first_env >= 0 ? std::min(first_env, 1) : (E.fresh ? 0 : 1);
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
-  // Side chain (stream2, after the scan): keys with more ops than tier 0
-  // takes go straight to tier S, concurrently with tier 0, which skips them.
-  const bool side = first_tier == 0 && nk;
-  if (side) {
-    CCRDT_HIP(hipEventRecord(E.ev_scan, E.stream));
-    CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.ev_scan, 0));
-    TrmvApplyArgs b = a;
-    CCRDT_HIP(hipEventRecord(E.evb[0], E.stream2));
-    b.key_list = nullptr;
-    b.n_list = (uint32_t)nk;
-    b.n_list_dev = nullptr;
-    b.ovf_list = E.tier_ovf_b[0].as<uint32_t>();
-    b.status = status + TRMV_SIDE;
-    CCRDT_TRY(trmv_launch_classify(b, E.stream2));
-    CCRDT_HIP(hipEventRecord(E.evb[1], E.stream2));
-    for (int i = 0; i < 2; ++i) {
-      b.key_list = E.tier_ovf_b[i].as<uint32_t>();
-      b.n_list_dev = status + TRMV_SIDE + 2 * i;
-      b.ovf_list = E.tier_ovf_b[i + 1].as<uint32_t>();
-      b.status = status + TRMV_SIDE + 2 + 2 * i;
-      CCRDT_TRY(trmv_launch_steady(b, i, later_grid, E.stream2));
-      CCRDT_HIP(hipEventRecord(E.evb[i + 2], E.stream2));
-    }
-    CCRDT_HIP(hipEventRecord(E.ev_side, E.stream2));
-  }
-  a.skip_big = side ? 1 : 0;
   DevBuf* work = nullptr;
   const uint32_t* n_dev = nullptr;
   int ev = 0;
@@ -406,18 +377,12 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     work = ovf;
     n_dev = a.status;
   }
-  if (side) {
-    CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_side, 0));
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-  }
   CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost,
                            E.stream));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
   uint32_t err = 0;
   for (int t = first_tier; t < TRMV_N_TIERS; ++t) err |= hs[3 + 2 * t];
-  if (side)
-    for (int i = 0; i < 2; ++i) err |= hs[TRMV_SIDE + 3 + 2 * i];
   if ((hs[1] | err) & TRMV_ERR_SEG) {
     set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
     return CCRDT_ENOMEM;
@@ -443,21 +408,9 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     E.trmv_tier_ms[t] = ms;
     E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
-  if (side) {  // side chain: 1000 = keys sent to it, 1001 / 1002 = its tier S classes
-    E.trmv_overflow_keys[1000] = hs[TRMV_SIDE];
-    for (int i = 0; i < 2; ++i) {
-      float ms = 0.f;
-      CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[i + 1], E.evb[i + 2]));
-      E.trmv_tier_ms[1001 + i] = ms;
-      E.trmv_overflow_keys[1001 + i] = hs[TRMV_SIDE + 2 + 2 * i];
-    }
-    float ms = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&ms, E.evb[0], E.evb[1]));
-    E.trmv_tier_ms[1000] = ms;
-  }
-  if (nk && (hs[2 + 2 * (TRMV_N_TIERS - 1)] || (side && hs[TRMV_SIDE + 4]))) {
+  if (nk && hs[2 + 2 * (TRMV_N_TIERS - 1)]) {
     set_error("trmv_apply: a key would hold more than 1024 players (Ids with a Masked or "
-              "Removals entry); ccrdt_engine_handed_on(e, 2) / (e, 1002) lists them");
+              "Removals entry); ccrdt_engine_handed_on(e, 2) lists them");
     return CCRDT_ENOMEM;
   }
   float kernel_ms = 0.f;
@@ -676,10 +629,7 @@ int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* 
 
 int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, int64_t* n) {
   if (!e || !n || cap < 0) return CCRDT_EINVAL;
-  static constexpr int tiers[] = {0, 1, 2, 1000, 1001, 1002};
-  int ti = -1;
-  for (int i = 0; i < 6; ++i)
-    if (tiers[i] == t) ti = i;
+  const int ti = t >= 0 && t < TRMV_N_TIERS ? t : -1;
   auto it = e->trmv_overflow_keys.find(t);
   if (ti < 0 || e->type != CCRDT_TOPK_RMV || it == e->trmv_overflow_keys.end()) {
     *n = 0;
@@ -688,7 +638,7 @@ int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, 
   *n = it->second;
   const int64_t m = std::min<int64_t>(cap, *n);
   if (m > 0 && keys) {
-    const DevBuf& src = ti < 3 ? e->tier_ovf[ti] : e->tier_ovf_b[ti - 3];
+    const DevBuf& src = e->tier_ovf[ti];
     CCRDT_HIP(hipStreamSynchronize(e->stream));
     CCRDT_HIP(hipMemcpy(keys, src.p, (size_t)m * 4, hipMemcpyDeviceToHost));
   }

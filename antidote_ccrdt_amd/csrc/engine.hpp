@@ -47,31 +47,14 @@ struct ccrdt_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the main apply kernel
   hipEvent_t evt[8] = {};                      // topk_rmv tier boundaries
-  // topk_rmv side chain: keys too large for tier 0 run the sequential kernel
-  // on a second stream, concurrently with tier 0
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_scan = nullptr, ev_side = nullptr, evb[6] = {};
   bool create_tier_events() {
     for (hipEvent_t& v : evt)
       if (hipEventCreate(&v) != hipSuccess) return false;
-    for (hipEvent_t& v : evb)
-      if (hipEventCreate(&v) != hipSuccess) return false;
-    // the side chain gets the highest stream priority: tier 0 fills every
-    // CU, and without it the side chain's later classes would only start
-    // once tier 0 has drained
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-    return hipEventCreate(&ev_scan) == hipSuccess && hipEventCreate(&ev_side) == hipSuccess &&
-           hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, hi) == hipSuccess;
+    return true;
   }
   void destroy_tier_events() {
     for (hipEvent_t& v : evt)
       if (v) (void)hipEventDestroy(v);
-    for (hipEvent_t& v : evb)
-      if (v) (void)hipEventDestroy(v);
-    if (ev_scan) (void)hipEventDestroy(ev_scan);
-    if (ev_side) (void)hipEventDestroy(ev_side);
-    if (stream2) (void)hipStreamDestroy(stream2);
   }
   float last_kernel_ms = 0.f;
   void* h_status = nullptr;  // pinned, 256 bytes
@@ -82,7 +65,6 @@ struct ccrdt_engine {
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status;
   ccrdt::DevBuf tier_ovf[3];    // keys each topk_rmv tier handed on (last batch)
-  ccrdt::DevBuf tier_ovf_b[3];  // side chain: big keys, then each tier S class's hand-ons
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held

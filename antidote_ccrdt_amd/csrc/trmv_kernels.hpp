@@ -13,8 +13,9 @@
 //                         segment: offset (low 16) | element count (high 16)
 //            pl_gb[u16]   gb_sets:largest(Masked[Id]) as an index into the
 //                         slab (term order (Score, DcId, Ts) inside one Id;
-//                         the promotion candidate of rmv/3, :279,291); 0 when
-//                         the slab is empty
+//                         the promotion candidate of rmv/3, :279,291); only
+//                         meaningful for slabs of 2+ elements (readers take 0
+//                         otherwise, whatever is stored)
 //   pool     m_score[i64], m_ts[i64], m_dc[u8]   the Masked elements, one
 //                         slab per player (slabs may leave holes)
 //   rows     r_vc[n_dc x i64]   Removals[Id] (0 = DC absent)
@@ -96,7 +97,6 @@ struct TrmvApplyArgs {
                                // (the previous tier's overflow count)
   uint32_t* ovf_list;
   uint32_t* status;  // [0] overflow count, [1] error flags
-  int32_t skip_big;  // tier 0: keys with more ops than it takes run on the side chain
 };
 
 enum : uint32_t {

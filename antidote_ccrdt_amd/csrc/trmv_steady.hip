@@ -39,6 +39,28 @@
 #include "common.hpp"
 #include "trmv_kernels.hpp"
 
+// Diagnostic build only (-DTRMV_PROF): per-phase s_memtime stamps summed over
+// a sample of keys; read with ccrdt_debug_steady_prof().
+#ifdef TRMV_PROF
+__device__ unsigned long long g_steady_prof[16];
+#define SPROF_STAMP(v)                                                        \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#define SPROF(i)                                                                              \
+  do {                                                                                        \
+    unsigned long long _t;                                                                    \
+    SPROF_STAMP(_t);                                                                          \
+    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_steady_prof[i], _t - prof_t);      \
+    prof_t = _t;                                                                              \
+  } while (0)
+#else
+#define SPROF_STAMP(v) (void)0
+#define SPROF(i) (void)0
+#endif
+
 namespace ccrdt {
 
 namespace {
@@ -79,20 +101,29 @@ struct alignas(16) SLds {
   uint32_t oslab[PCAP + 1];              // old slab: offset | count << 16
   uint32_t orow[PCAP + 1];               // old Obs index | Removals row << 16 (new side)
   uint32_t nslab[PCAP + 1];              // new slab: offset | current count << 16
-  uint32_t nops[PCAP + 1];               // ops of the player in the batch
-  // the current chunk (stream order unless noted)
-  int64_t csc[S_CH + 1], cts[S_CH + 1];
-  uint32_t ckd[S_CH + 1];                // kind | dc << 2 | dup candidate << 5 | player << 8
-  uint32_t cres[S_CH + 1];               // add: R_DOM | slab position << 16; rmv: its rank
-  uint32_t crow[S_CHR + 1];              // rmv_vc row of the chunk's rmvs
-  int64_t vtab[S_CHR][TRMV_DPAD];        // their clocks
-  int64_t rgsc[S_CHR], rgts[S_CHR];      // Masked[Id]'s largest survivor after each rmv
-  uint32_t rgd[S_CHR];                   // non-empty | dc << 8 | position << 16
-  uint8_t csrt[S_CH];                    // sorted (player, stream) order -> stream index
-  uint16_t cwp[S_CH];                    // replayed players of the chunk
-  uint8_t cws[S_CH], cwe[S_CH];          // and their sorted ranges
-  uint32_t mark[S_CH];                   // K3: player (+1) whose slab starts at a position
-  int64_t claim[S_CH];                   // K2: Ids being claimed
+  struct Chunk {                         // the current chunk (stream order unless noted)
+    int64_t csc[S_CH + 1], cts[S_CH + 1];
+    uint32_t ckd[S_CH + 1];              // kind | dc << 2 | dup candidate << 5 | player << 8
+    uint32_t cres[S_CH + 1];             // add: R_DOM | slab position << 16; rmv: its rank
+    uint32_t crow[S_CHR + 1];            // rmv_vc row of the chunk's rmvs
+    int64_t vtab[S_CHR][TRMV_DPAD];      // their clocks
+    int64_t rgsc[S_CHR], rgts[S_CHR];    // Masked[Id]'s largest survivor after each rmv
+    uint32_t rgd[S_CHR];                 // non-empty | dc << 8 | position << 16
+    uint8_t csrt[S_CH];                  // sorted (player, stream) order -> stream index
+    uint16_t cwp[S_CH];                  // replayed players of the chunk
+    uint8_t cws[S_CH], cwe[S_CH];        // and their sorted ranges
+    uint32_t mark[S_CH];                 // K3: player (+1) whose slab starts at a position
+  };
+  struct Build {                         // old Observed, before it is sorted into registers
+    int64_t bsc[128], bid[128];
+    uint32_t bp[128];
+  };
+  union {
+    uint32_t nops[PCAP + 1];             // K2: ops of each player in the batch
+    Chunk c;
+    Build b;
+  } u;
+  int64_t claim[S_CH];                   // K2: Ids being claimed (beside nops)
   unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
   uint32_t nex;
 };
@@ -226,7 +257,7 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP>& L, int64_t id, bool v, uin
     L.hs[h] = p;
     L.oslab[p] = 0u;
     L.orow[p] = S_NONE;
-    L.nops[p] = 0u;
+    L.u.nops[p] = 0u;
     L.opd[p] = NONE16 << 16;
     L.gpd[p] = 0u;
     L.osc[p] = L.ots[p] = L.gsc[p] = L.gts[p] = 0;
@@ -321,13 +352,106 @@ __device__ __forceinline__ uint32_t s_promote(const SLds<PCAP>& L, uint32_t np) 
   return rl32(bp, (int)__builtin_ctzll(hit));
 }
 
+// Observed as a register table (K <= 128): entry i in lane i % 64 of slot
+// i / 64, in no particular order, with Min (min_observed/1, :398-406: the
+// smallest (Score, Id); Ids are distinct) tracked beside it.  Adds change one
+// entry with two selects; only an eviction, or an Obs[Id] change of the Min
+// player, re-reduces Min (DPP).  Obs[Id]'s Ts / dc / slab position live in
+// LDS (ots, opd), written on every change.
+struct ObsTab {
+  int64_t sc[2], id[2];  // Obs[Id] score, Id
+  uint32_t p[2];         // player
+  uint32_t n;            // |Observed|
+  uint32_t mi;           // entry of Min (S_NONE: {nil, nil, nil})
+  int64_t msc, mid;      // Min's score and Id
+};
+
+__device__ __forceinline__ uint32_t ot_find(const ObsTab& o, uint32_t q) {
+  const int lane = lane_id();
+  const uint64_t m0 = ballot((uint32_t)lane < o.n && o.p[0] == q);
+  const uint64_t m1 = ballot((uint32_t)(64 + lane) < o.n && o.p[1] == q);
+  return m0 ? (uint32_t)__builtin_ctzll(m0) : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : S_NONE);
+}
+__device__ __forceinline__ int64_t ot_get64(const int64_t f[2], uint32_t i) {
+  const int64_t a = rl64(f[0], (int)(i & 63u)), b = rl64(f[1], (int)(i & 63u));
+  return i < 64 ? a : b;
+}
+__device__ __forceinline__ uint32_t ot_get32(const uint32_t f[2], uint32_t i) {
+  const uint32_t a = rl32(f[0], (int)(i & 63u)), b = rl32(f[1], (int)(i & 63u));
+  return i < 64 ? a : b;
+}
+__device__ __forceinline__ void ot_set(ObsTab& o, uint32_t i, int64_t s, int64_t id, uint32_t p) {
+  const int lane = lane_id();
+  const bool h0 = i < 64 && (uint32_t)lane == i, h1 = i >= 64 && (uint32_t)(64 + lane) == i;
+  o.sc[0] = h0 ? s : o.sc[0];
+  o.sc[1] = h1 ? s : o.sc[1];
+  o.id[0] = h0 ? id : o.id[0];
+  o.id[1] = h1 ? id : o.id[1];
+  o.p[0] = h0 ? p : o.p[0];
+  o.p[1] = h1 ? p : o.p[1];
+}
+// Min := min_observed(Observed)
+__device__ __forceinline__ void ot_min(ObsTab& o) {
+  const int lane = lane_id();
+  const bool v0 = (uint32_t)lane < o.n, v1 = (uint32_t)(64 + lane) < o.n;
+  if (o.n == 0) {
+    o.mi = S_NONE;
+    return;
+  }
+  const bool t1 = v1 && (!v0 || o.sc[1] < o.sc[0] || (o.sc[1] == o.sc[0] && o.id[1] < o.id[0]));
+  const int64_t s = t1 ? o.sc[1] : (v0 ? o.sc[0] : INT64_MAX);
+  const int64_t id = t1 ? o.id[1] : (v0 ? o.id[0] : INT64_MAX);
+  const uint32_t ix = t1 ? 64u + (uint32_t)lane : (uint32_t)lane;
+  const bool v = v0 || v1;
+  const int64_t ms = wave_min_i64_dpp(v ? s : INT64_MAX);
+  uint64_t m = ballot(v && s == ms);
+  if (__builtin_popcountll(m) > 1) {  // Score tie: the smaller Id
+    const int64_t mid = wave_min_i64_dpp(v && s == ms ? id : INT64_MAX);
+    m = ballot(v && s == ms && id == mid);
+  }
+  const int l = (int)__builtin_ctzll(m);
+  o.mi = rl32(ix, l);
+  o.msc = ms;
+  o.mid = rl64(id, l);
+}
+
+// Deferred maintenance of each player's gb_sets:largest(Masked[Id]) (LDS
+// gsc/gts/gpd): for the ops [lo, hi) of the chunk, the last op of each player
+// in the range writes the running largest of the player's non-dominated adds
+// since its last rmv (rok/rsc/rts/rd, computed in the sorted view; a rmv
+// resets it, and the rmv itself sets the player's largest from its replay).
+// One writer per player, so no two lanes race.  Called before a promotion
+// reads the players' largest elements, and at the end of a chunk.
+template <int PCAP>
+__device__ __forceinline__ void s_catch_up(SLds<PCAP>& L, uint32_t lo, uint32_t hi, uint32_t kd, uint32_t nxt,
+                                           bool rok, int64_t rsc, int64_t rts, uint32_t rd) {
+  const uint32_t l = (uint32_t)lane_id();
+  if (l >= lo && l < hi && nxt >= hi && rok) {
+    const uint32_t p = kd >> 8, rdc = rd & 0xFFu;
+    const uint32_t f = L.opd[p];
+    const int64_t gs = L.gsc[p], gt = L.gts[p];
+    const uint32_t gd = (L.gpd[p] >> 8) & 0xFFu;
+    if (!(f & F_HASM) || gb_gt(rsc, rdc, rts, gs, gd, gt)) {
+      L.gsc[p] = rsc;
+      L.gts[p] = rts;
+      L.gpd[p] = (rdc << 8) | ((rd >> 8) << 16);
+      atomicOr(&L.opd[p], F_HASM);
+    }
+  }
+  wave_lds_sync();
+}
+
 // One key.  Writes nothing to the new side before its last early return
 // that hands the key on (S_NEXT).
-template <int PCAP>
+template <int PCAP, bool RANKED>
 __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>& L) {
   constexpr int HS = SLds<PCAP>::HS;
   const int lane = lane_id();
   const int D = a.n_dc;
+#ifdef TRMV_PROF
+  unsigned long long prof_t;
+  SPROF_STAMP(prof_t);
+#endif
   const uint64_t op0 = a.key_ptr[key];
   const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
   const KeyMeta nm = a.new_s.meta[key];
@@ -361,7 +485,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       const uint64_t pp = (uint64_t)om.p_off + p;
       const int64_t id = a.old_s.pl_id[pp];
       const uint32_t info = a.old_s.pl_info[pp], slab = a.old_s.pl_slab[pp];
-      const uint32_t gb = a.old_s.pl_gb[pp];
+      const uint32_t gb = (slab >> 16) > 1 ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
       const uint32_t off = slab & 0xFFFFu, cnt = slab >> 16, ob = info & 0xFFFFu;
       const uint64_t g0 = (uint64_t)om.m_off + off;
       int64_t os = 0, ot = 0, gs = 0, gt = 0;
@@ -379,7 +503,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       L.pid[p] = id;
       L.oslab[p] = slab;
       L.orow[p] = info;
-      L.nops[p] = 0u;
+      L.u.nops[p] = 0u;
       L.osc[p] = os;
       L.ots[p] = ot;
       L.gsc[p] = gs;
@@ -394,6 +518,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
   }
   span = wave_max_u32_dpp(span);
   wave_lds_sync();
+  SPROF(0);
 
   // ---- K2. the player of every op, ops per player, players with a rmv
   uint32_t np = om.np;
@@ -405,7 +530,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     uint32_t p;
     if (!s_resolve<PCAP>(L, id, v, np, p)) return S_NEXT;
     if (v) {
-      atomicAdd(&L.nops[p], 1u);
+      atomicAdd(&L.u.nops[p], 1u);
       if (kind == 2 || kind == 3) atomicOr(&L.opd[p], F_RMV);
     }
   }
@@ -422,7 +547,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     if (newrow) L.orow[p] = (info & 0xFFFFu) | ((nr + mbcnt(m)) << 16);
     nr += (uint32_t)__builtin_popcountll(m);
     const uint32_t ocnt = act ? (L.oslab[q] >> 16) : 0u;
-    const uint32_t cap = act ? ocnt + L.nops[q] : 0u;
+    const uint32_t cap = act ? ocnt + L.u.nops[q] : 0u;
     uint32_t tot;
     const uint32_t ex = wave_excl_scan_dpp(cap, tot);
     if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
@@ -433,6 +558,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     return S_REJECT;
   }
   wave_lds_sync();
+  SPROF(1);
 
   // ---- K3. old slabs (except replayed players') and old Removals rows
   if (!a.fresh && span) {
@@ -447,17 +573,17 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         ts = a.old_s.m_ts[src];
         dc = a.old_s.m_dc[src];
       }
-      L.mark[lane] = 0u;
+      L.u.c.mark[lane] = 0u;
       wave_lds_sync();
       for (uint32_t j0 = (uint32_t)(prev + 1);; j0 += 64) {  // slabs starting in the window
         const uint32_t j = j0 + lane;
         const uint32_t off = j < om.np ? (L.oslab[j] & 0xFFFFu) : S_NONE;
-        if (off >= q0 && off < q0 + 64) atomicMax(&L.mark[off - q0], j + 1);
+        if (off >= q0 && off < q0 + 64) atomicMax(&L.u.c.mark[off - q0], j + 1);
         const uint32_t last = rl32(off, 63);
         if (!(j0 + 64 < om.np && last < q0 + 64)) break;
       }
       wave_lds_sync();
-      const uint32_t own = wave_incl_max_dpp(L.mark[lane]);
+      const uint32_t own = wave_incl_max_dpp(L.u.c.mark[lane]);
       const int32_t o = own ? (int32_t)own - 1 : prev;
       prev = (int32_t)rl32((uint32_t)o, 63);
       if (q < span && o >= 0) {
@@ -480,18 +606,49 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
   }
   // the replays read rows written here: retire the stores first
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  SPROF(2);
 
   // ---- K4. chunks of the key's ops
-  SMin mn;
-  mn.p = om.minq;
-  mn.sc = mn.id = mn.ts = 0;
-  if (mn.p != NONE32) {
-    mn.sc = ufl64(L.osc[mn.p]);
-    mn.id = ufl64(L.pid[mn.p]);
-    mn.ts = ufl64(L.ots[mn.p]);
-  }
-  uint32_t nobs = om.nobs;
   const uint32_t K = a.k;
+  SMin mn;  // !RANKED: Min and |Observed|
+  uint32_t nobs = om.nobs;
+  ObsTab ob;  // RANKED: Observed in registers
+  if (!RANKED) {
+    mn.p = om.minq;
+    mn.sc = mn.id = mn.ts = 0;
+    if (mn.p != NONE32) {
+      mn.sc = ufl64(L.osc[mn.p]);
+      mn.id = ufl64(L.pid[mn.p]);
+      mn.ts = ufl64(L.ots[mn.p]);
+    }
+  } else {
+    // the old Observed -> LDS list -> registers
+    uint32_t c = 0;
+    for (uint32_t b = 0; b < om.np; b += 64) {
+      const uint32_t p = b + lane;
+      const bool ok = p < om.np && (L.opd[p] & F_OBS);
+      const uint64_t m = ballot(ok);
+      if (ok) {
+        const uint32_t k = c + mbcnt(m);
+        L.u.b.bsc[k] = L.osc[p];
+        L.u.b.bid[k] = L.pid[p];
+        L.u.b.bp[k] = p;
+      }
+      c += (uint32_t)__builtin_popcountll(m);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t k = (uint32_t)(t * 64 + lane);
+      const bool ok = k < c;
+      ob.sc[t] = ok ? L.u.b.bsc[k] : INT64_MAX;
+      ob.id[t] = ok ? L.u.b.bid[k] : INT64_MAX;
+      ob.p[t] = ok ? L.u.b.bp[k] : (uint32_t)PCAP;
+    }
+    ob.n = c;
+    ot_min(ob);
+    wave_lds_sync();
+  }
   for (uint32_t c0 = 0; c0 < nops;) {
     uint32_t n = nops - c0 < (uint32_t)S_CH ? nops - c0 : (uint32_t)S_CH;
     bool v = (uint32_t)lane < n;
@@ -524,20 +681,21 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     const uint32_t p = s_lookup<PCAP>(L, id, v);
     // the rmvs' clocks (8 lanes per row)
     const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
-    if (isr) L.crow[rk] = (uint32_t)ts;
+    if (isr) L.u.c.crow[rk] = (uint32_t)ts;
     wave_lds_sync();
     for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7;
       if (r < nrm) {
-        const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.crow[r] * D + d] : 0;
+        const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
         err |= x < 0 ? TRMV_ERR_VC : 0u;
-        L.vtab[r][d] = x;
+        L.u.c.vtab[r][d] = x;
       }
     }
     if (ballot(err != 0)) {
       if (err) atomicOr(&a.status[1], err);
       return S_REJECT;
     }
+    SPROF(3);
     // Elements that may already be in Masked[Id] (gb_sets:add_element, :240-246):
     // every element of dc in the key has Ts <= Vc[dc], so an add whose Ts is
     // above the key's Vc[dc] before it is new.  Exact when the chunk's adds of
@@ -567,19 +725,20 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     }
     wave_lds_sync();
     if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
-    L.csc[lane] = sc;
-    L.cts[lane] = ts;
-    L.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)PCAP << 8);
-    L.cres[lane] = isr ? rk : 0u;
+    L.u.c.csc[lane] = sc;
+    L.u.c.cts[lane] = ts;
+    L.u.c.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)PCAP << 8);
+    L.u.c.cres[lane] = isr ? rk : 0u;
     wave_lds_sync();
 
+    SPROF(4);
     // ---- ops in (player, stream) order
     const uint32_t kvs = wave_radix_sort<Log2<PCAP>::v + 1>(((v ? p : (uint32_t)PCAP) << 6) | (uint32_t)lane);
     const uint32_t sp = kvs >> 6, so = kvs & 63u;
     const bool sv = sp < (uint32_t)PCAP;
     const uint32_t lkvs = shfl32(kvs, lane ? lane - 1 : 0);
     const bool start = sv && (lane == 0 || (lkvs >> 6) != sp);
-    L.csrt[lane] = (uint8_t)so;
+    L.u.c.csrt[lane] = (uint8_t)so;
     const uint64_t ss = ballot(start);
     const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1);
     const uint64_t sb = ss & incl;
@@ -587,8 +746,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     const uint64_t above = ss & ~incl;
     const uint32_t shi = above ? (uint32_t)__builtin_ctzll(above) : n;
     const uint64_t segm = (shi >= 64 ? ~0ull : ((1ull << shi) - 1)) & ~((1ull << slo) - 1);
-    const uint32_t skd = L.ckd[so];
-    const int64_t ssc = L.csc[so], sts = L.cts[so];
+    const uint32_t skd = L.u.c.ckd[so];
+    const int64_t ssc = L.u.c.csc[so], sts = L.u.c.cts[so];
     const uint32_t sdc = (skd >> 2) & 7u;
     const uint32_t pf = L.opd[sv ? sp : (uint32_t)PCAP];
     const uint64_t dm = ballot(sv && ((skd >> 5) & 1u));
@@ -610,12 +769,12 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       a.new_s.m_score[dst] = ssc;
       a.new_s.m_ts[dst] = sts;
       a.new_s.m_dc[dst] = (uint8_t)sdc;
-      L.cres[so] = pos << 16;
+      L.u.c.cres[so] = pos << 16;
     }
     if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
       Row8 rv = (Row8)(0);
       for (int d = 0; d < D; ++d) rv[d] = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + d];
-      L.cres[so] = R_DOM;
+      L.u.c.cres[so] = R_DOM;
       s_emit<PCAP>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
     }
     wave_lds_sync();
@@ -623,17 +782,18 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       const uint32_t ns = L.nslab[sp];
       L.nslab[sp] = ns + ((uint32_t)__builtin_popcountll(nd & segm) << 16);
     }
+    SPROF(5);
     // players with a rmv, or a possibly duplicated element: one lane each
     const uint64_t wm = ballot(start && walk);
     if (start && walk) {
       const uint32_t k = mbcnt(wm);
-      L.cwp[k] = (uint16_t)sp;
-      L.cws[k] = (uint8_t)lane;
-      L.cwe[k] = (uint8_t)shi;
+      L.u.c.cwp[k] = (uint16_t)sp;
+      L.u.c.cws[k] = (uint8_t)lane;
+      L.u.c.cwe[k] = (uint8_t)shi;
     }
     wave_lds_sync();
     if ((uint32_t)lane < (uint32_t)__builtin_popcountll(wm)) {
-      const uint32_t wp = L.cwp[lane], ws = L.cws[lane], we = L.cwe[lane];
+      const uint32_t wp = L.u.c.cwp[lane], ws = L.u.c.cws[lane], we = L.u.c.cwe[lane];
       uint32_t f = L.opd[wp];
       const uint32_t ns = L.nslab[wp];
       const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
@@ -657,13 +817,13 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       const int64_t wid = L.pid[wp];
       bool moved = false;
       for (uint32_t x = ws; x < we; ++x) {
-        const uint32_t o = L.csrt[x];
-        const uint32_t kd = L.ckd[o];
-        const int64_t esc = L.csc[o], ets = L.cts[o];
+        const uint32_t o = L.u.c.csrt[x];
+        const uint32_t kd = L.u.c.ckd[o];
+        const int64_t esc = L.u.c.csc[o], ets = L.u.c.cts[o];
         const uint32_t edc = (kd >> 2) & 7u;
         if ((kd & 3u) < 2) {  // add/4
           if (has_row && pick8(R, edc) >= ets) {  // dominated (:234-237)
-            L.cres[o] = R_DOM;
+            L.u.c.cres[o] = R_DOM;
             s_emit<PCAP>(a, L, op0, op0 + c0 + o, CCRDT_TRMV_RMV, wid, 0, 0, 0, &R);
             continue;
           }
@@ -681,12 +841,12 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
             a.new_s.m_ts[base + pos] = ets;
             a.new_s.m_dc[base + pos] = (uint8_t)edc;
           }
-          L.cres[o] = pos << 16;
+          L.u.c.cres[o] = pos << 16;
         } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
-          const uint32_t r = L.cres[o];
+          const uint32_t r = L.u.c.cres[o];
           Row8 V;
 #pragma unroll
-          for (int d = 0; d < TRMV_DPAD; ++d) V[d] = L.vtab[r][d];
+          for (int d = 0; d < TRMV_DPAD; ++d) V[d] = L.u.c.vtab[r][d];
 #pragma unroll
           for (int d = 0; d < TRMV_DPAD; ++d) R[d] = has_row ? (V[d] > R[d] ? V[d] : R[d]) : V[d];
           has_row = true;
@@ -712,9 +872,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           }
           moved |= w != cnt;
           cnt = w;
-          L.rgsc[r] = bsc;
-          L.rgts[r] = bts;
-          L.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
+          L.u.c.rgsc[r] = bsc;
+          L.u.c.rgts[r] = bts;
+          L.u.c.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
         }
       }
       L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
@@ -728,121 +888,262 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     wave_lds_sync();
     // the next chunk's replays read this chunk's stores
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    SPROF(6);
 
-    // ---- the Observed half, one op at a time in stream order
-    // (recompute_observed/5 :301-334; rmv/3 :267-298)
-    const uint32_t kdr = L.ckd[lane], crr = L.cres[lane];
-    const int64_t scr = L.csc[lane], tsr = L.cts[lane];
-    for (uint32_t j = 0; j < n; ++j) {
-      const uint32_t kd = rl32(kdr, (int)j), cr = rl32(crr, (int)j);
-      const uint32_t q = kd >> 8;
-      if ((kd & 3u) < 2) {
-        if (cr & R_DOM) continue;
-        const int64_t s = rl64(scr, (int)j), t = rl64(tsr, (int)j);
-        const uint32_t edc = (kd >> 2) & 7u, pos = cr >> 16;
-        uint32_t f = ufl(L.opd[q]);
-        // gb_sets:largest(Masked[Id]) after the insert
-        const int64_t gs = ufl64(L.gsc[q]), gt = ufl64(L.gts[q]);
-        const uint32_t gd = (ufl(L.gpd[q]) >> 8) & 0xFFu;
-        if (!(f & F_HASM) || gb_gt(s, edc, t, gs, gd, gt)) {
-          if (lane == 0) {
-            L.gsc[q] = s;
-            L.gts[q] = t;
-            L.gpd[q] = (edc << 8) | (pos << 16);
+    // ---- the running largest element of each player's adds since its last
+    // rmv (sorted view, segmented max-scan), for the deferred catch-up
+    bool rok;
+    int64_t rsc, rts;
+    uint32_t rd, nxt;
+    {
+      const uint32_t scres = L.u.c.cres[so];
+      const bool srmv = sv && (skd & 3u) >= 2;
+      bool ok = sv && !srmv && !(scres & R_DOM);
+      int64_t vs = ssc, vt = sts;
+      uint32_t vd = sdc | ((scres >> 16) << 8);
+      bool hf = start || srmv;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int src = lane >= d ? lane - d : lane;
+        const bool yok = shfl32(ok ? 1u : 0u, src) != 0;
+        const int64_t ys = shfl64(vs, src), yt = shfl64(vt, src);
+        const uint32_t yd = shfl32(vd, src);
+        const bool yhf = shfl32(hf ? 1u : 0u, src) != 0;
+        if (lane >= d && !hf) {
+          if (yok && (!ok || gb_gt(ys, yd & 0xFFu, yt, vs, vd & 0xFFu, vt))) {
+            vs = ys;
+            vt = yt;
+            vd = yd;
+            ok = true;
           }
+          hf = yhf;
         }
-        f |= F_HASM;
-        const uint32_t fobs = (f & 0xFFu) | F_OBS | (edc << 8) | (pos << 16);
-        bool need_min = false;
-        if (f & F_OBS) {  // Id in Observed (:303-315)
-          const int64_t os = ufl64(L.osc[q]), ot = ufl64(L.ots[q]);
-          if (s > os || (s == os && t > ot)) {
-            if (lane == 0) {
-              L.osc[q] = s;
-              L.ots[q] = t;
-            }
-            f = fobs;
-            need_min = q == mn.p;  // Old =:= Min
-          }
-        } else if (nobs < K) {  // (:317-324)
-          if (lane == 0) {
-            L.osc[q] = s;
-            L.ots[q] = t;
-          }
-          f = fobs;
-          ++nobs;
-          const int64_t qid = ufl64(L.pid[q]);
-          if (mn.p == S_NONE || mn.sc > s || (mn.sc == s && (mn.id > qid || (mn.id == qid && mn.ts > t)))) {
-            mn.p = q;
-            mn.sc = s;
-            mn.id = qid;
-            mn.ts = t;
-          }
-        } else {  // full: evict Min if cmp(Elem, Min) (:325-331)
-          const int64_t qid = ufl64(L.pid[q]);
-          if (s > mn.sc || (s == mn.sc && (qid > mn.id || (qid == mn.id && t > mn.ts)))) {
-            if (lane == 0) {
-              L.opd[mn.p] = L.opd[mn.p] & ~F_OBS;
-              L.osc[q] = s;
-              L.ots[q] = t;
-            }
-            f = fobs;
-            need_min = true;
-          }
-        }
-        if (lane == 0) L.opd[q] = f;
-        wave_lds_sync();
-        if (need_min) s_min<PCAP>(L, np, mn);
-      } else {  // rmv/3
-        const uint32_t r = cr;
-        const uint32_t g = ufl(L.rgd[r]);
-        uint32_t f = ufl(L.opd[q]);
-        const bool nonempty = g & 1u;
-        if (lane == 0 && nonempty) {
-          L.gsc[q] = L.rgsc[r];
-          L.gts[q] = L.rgts[r];
-          L.gpd[q] = g & 0xFFFFFF00u;
-        }
-        f = nonempty ? (f | F_HASM) : (f & ~F_HASM);
-        bool impacts = false;
-        if (f & F_OBS) {  // VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
-          const uint32_t odc = (f >> 8) & 0xFFu;
-          impacts = ufl64(L.vtab[r][odc]) >= ufl64(L.ots[q]);
-        }
-        if (!impacts) {
-          if (lane == 0) L.opd[q] = f;
+      }
+      // stream index of the player's next op in the chunk (0xFF: none)
+      const uint32_t nso = shfl32(so, lane < 63 ? lane + 1 : lane);
+      const uint64_t nb = lane < 63 ? (1ull << (lane + 1)) : 0ull;
+      const bool has_next = lane < 63 && (uint32_t)(lane + 1) < n && !(ss & nb);
+      const uint32_t nx = has_next ? nso : 0xFFu;
+      // back to stream order (so is a permutation of the lanes)
+      rok = perm32(ok ? 1u : 0u, so) != 0;
+      rsc = (int64_t)(((uint64_t)perm32((uint32_t)((uint64_t)vs >> 32), so) << 32) | perm32((uint32_t)vs, so));
+      rts = (int64_t)(((uint64_t)perm32((uint32_t)((uint64_t)vt >> 32), so) << 32) | perm32((uint32_t)vt, so));
+      rd = perm32(vd, so);
+      nxt = perm32(nx, so);
+    }
+
+    // ---- the Observed half, in stream order (recompute_observed/5 :301-334;
+    // rmv/3 :267-298).  Per run of adds between two rmvs, a lane-parallel
+    // filter drops the adds that cannot change Observed given the state at
+    // the run's start (inside a run Min and every Obs[Id] only rise, so an add
+    // below them stays below them); the others run one by one.
+    const uint32_t kdr = L.u.c.ckd[lane], crr = L.u.c.cres[lane];
+    const int64_t scr = L.u.c.csc[lane], tsr = L.u.c.cts[lane];
+    const uint32_t rl = (uint32_t)lane < (uint32_t)S_CHR ? (uint32_t)lane : 0u;
+    const int64_t rgs = L.u.c.rgsc[rl], rgt = L.u.c.rgts[rl];
+    const uint32_t rgdv = L.u.c.rgd[rl];
+    const int64_t vt0 = L.u.c.vtab[lane >> 3][lane & 7], vt1 = L.u.c.vtab[8 + (lane >> 3)][lane & 7];
+    const bool ladd = (uint32_t)lane < n && (kdr & 3u) < 2 && !(crr & R_DOM);
+    uint32_t last = 0;
+    for (uint32_t j = 0; j < n;) {
+      const uint64_t nr = j < 64 ? rm & (~0ull << j) : 0ull;
+      const uint32_t hi = nr ? (uint32_t)__builtin_ctzll(nr) : n;
+      if (hi > j) {
+        const bool inr = ladd && (uint32_t)lane >= j && (uint32_t)lane < hi;
+        bool rel = inr;
+        if (RANKED) {
           wave_lds_sync();
-          continue;
+          const uint32_t pq = inr ? (kdr >> 8) : (uint32_t)PCAP;
+          const uint32_t f = L.opd[pq];
+          const int64_t os = L.osc[pq], ot = L.ots[pq];
+          rel = inr && ((f & F_OBS) ? (scr > os || (scr == os && tsr > ot))
+                                    : (ob.n < K || scr > ob.msc || (scr == ob.msc && id > ob.mid)));
         }
-        f &= ~F_OBS;
-        --nobs;
-        if (lane == 0) L.opd[q] = f;
-        wave_lds_sync();
-        const uint32_t w = s_promote<PCAP>(L, np);
-        if (w == S_NONE) {  // (:283-289)
-          if (q == mn.p) s_min<PCAP>(L, np, mn);
-        } else {  // promote the largest (:290-295)
-          const int64_t gs = ufl64(L.gsc[w]), gt = ufl64(L.gts[w]), wid = ufl64(L.pid[w]);
-          const uint32_t gd = ufl(L.gpd[w]);
-          if (lane == 0) {
-            L.osc[w] = gs;
-            L.ots[w] = gt;
-            L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
+        uint64_t relm = ballot(rel);
+        while (relm) {
+          const uint32_t x = (uint32_t)__builtin_ctzll(relm);
+          relm &= relm - 1;
+          const uint32_t kd = rl32(kdr, (int)x), cr = rl32(crr, (int)x);
+          const uint32_t q = kd >> 8;
+          const int64_t s = rl64(scr, (int)x), t = rl64(tsr, (int)x), qid = rl64(id, (int)x);
+          const uint32_t edc = (kd >> 2) & 7u, pos = cr >> 16;
+          const uint32_t obits = (edc << 8) | (pos << 16);
+          if (RANKED) {
+            const uint32_t ix = ot_find(ob, q);
+            if (ix != S_NONE) {  // Id in Observed (:303-315)
+              const int64_t os = ot_get64(ob.sc, ix);
+              bool better = s > os;
+              if (!better && s == os) better = t > ufl64(L.ots[q]);
+              if (better) {
+                ot_set(ob, ix, s, qid, q);
+                if (lane == 0) {
+                  L.osc[q] = s;
+                  L.ots[q] = t;
+                  L.opd[q] = (L.opd[q] & 0xFFu) | obits;
+                }
+                if (ix == ob.mi) ot_min(ob);  // Old =:= Min
+              }
+            } else if (ob.n < K) {  // (:317-324)
+              ot_set(ob, ob.n, s, qid, q);
+              if (lane == 0) {
+                L.osc[q] = s;
+                L.ots[q] = t;
+                L.opd[q] = (L.opd[q] & 0xFFu) | F_OBS | obits;
+              }
+              if (ob.mi == S_NONE || s < ob.msc || (s == ob.msc && qid < ob.mid)) {
+                ob.mi = ob.n;
+                ob.msc = s;
+                ob.mid = qid;
+              }
+              ++ob.n;
+            } else if (s > ob.msc || (s == ob.msc && qid > ob.mid)) {  // evict Min (:325-331)
+              const uint32_t ev = ot_get32(ob.p, ob.mi);
+              ot_set(ob, ob.mi, s, qid, q);
+              if (lane == 0) {
+                atomicAnd(&L.opd[ev], ~F_OBS);
+                L.osc[q] = s;
+                L.ots[q] = t;
+                L.opd[q] = (L.opd[q] & 0xFFu) | F_OBS | obits;
+              }
+              ot_min(ob);
+            }
+          } else {
+            uint32_t f = ufl(L.opd[q]);
+            const uint32_t fobs = (f & 0xFFu) | F_OBS | obits;
+            bool need_min = false;
+            if (f & F_OBS) {  // Id in Observed (:303-315)
+              const int64_t os = ufl64(L.osc[q]), ot = ufl64(L.ots[q]);
+              if (s > os || (s == os && t > ot)) {
+                if (lane == 0) {
+                  L.osc[q] = s;
+                  L.ots[q] = t;
+                }
+                f = fobs;
+                need_min = q == mn.p;  // Old =:= Min
+              }
+            } else if (nobs < K) {  // (:317-324)
+              if (lane == 0) {
+                L.osc[q] = s;
+                L.ots[q] = t;
+              }
+              f = fobs;
+              ++nobs;
+              if (mn.p == S_NONE || mn.sc > s || (mn.sc == s && (mn.id > qid || (mn.id == qid && mn.ts > t)))) {
+                mn.p = q;
+                mn.sc = s;
+                mn.id = qid;
+                mn.ts = t;
+              }
+            } else {  // full: evict Min if cmp(Elem, Min) (:325-331)
+              if (s > mn.sc || (s == mn.sc && (qid > mn.id || (qid == mn.id && t > mn.ts)))) {
+                if (lane == 0) {
+                  atomicAnd(&L.opd[mn.p], ~F_OBS);
+                  L.osc[q] = s;
+                  L.ots[q] = t;
+                }
+                f = fobs;
+                need_min = true;
+              }
+            }
+            if (lane == 0) L.opd[q] = (L.opd[q] & F_HASM) | (f & ~F_HASM);
+            wave_lds_sync();
+            if (need_min) s_min<PCAP>(L, np, mn);
           }
+        }
+      }
+      if (hi >= n) break;
+      // ---- the rmv at hi
+      const uint32_t jr = hi;
+      j = hi + 1;
+      const uint32_t kd = rl32(kdr, (int)jr), r = rl32(crr, (int)jr);
+      const uint32_t q = kd >> 8;
+      const uint32_t g = rl32(rgdv, (int)r);
+      const int64_t gsv = rl64(rgs, (int)r), gtv = rl64(rgt, (int)r);
+      if (lane == 0) {  // Masked[Id] after the filter (:255-266): its largest
+        if (g & 1u) {
+          L.gsc[q] = gsv;
+          L.gts[q] = gtv;
+          L.gpd[q] = g & 0xFFFFFF00u;
+          atomicOr(&L.opd[q], F_HASM);
+        } else {
+          atomicAnd(&L.opd[q], ~F_HASM);
+        }
+      }
+      wave_lds_sync();
+      // impacts Observed?  VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
+      uint32_t ix = S_NONE;
+      {
+        const uint32_t f = ufl(L.opd[q]);
+        if (RANKED) ix = ot_find(ob, q);
+        else ix = (f & F_OBS) ? 0u : S_NONE;
+        if (ix == S_NONE) continue;
+        const uint32_t odc = (f >> 8) & 7u;
+        const int64_t ot = ufl64(L.ots[q]);
+        const int vl = (int)(((r & 7u) << 3) | odc);
+        const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
+        if ((r < 8 ? va : vb) < ot) continue;
+      }
+      bool was_min;
+      if (RANKED) {  // drop the entry (the last one takes its place)
+        const uint32_t lst = ob.n - 1;
+        was_min = ix == ob.mi;
+        if (ix != lst) {
+          ot_set(ob, ix, ot_get64(ob.sc, lst), ot_get64(ob.id, lst), ot_get32(ob.p, lst));
+          if (ob.mi == lst) ob.mi = ix;
+        }
+        --ob.n;
+      } else {
+        was_min = q == mn.p;
+        --nobs;
+      }
+      if (lane == 0) atomicAnd(&L.opd[q], ~F_OBS);
+      s_catch_up<PCAP>(L, last, jr + 1, kdr, nxt, rok, rsc, rts, rd);
+      last = jr + 1;
+      const uint32_t w = s_promote<PCAP>(L, np);
+      if (w == S_NONE) {  // (:283-289)
+        if (was_min) {
+          if (RANKED) ot_min(ob);
+          else s_min<PCAP>(L, np, mn);
+        }
+      } else {  // promote the largest (:290-295)
+        const int64_t gs = ufl64(L.gsc[w]), gt = ufl64(L.gts[w]), wid = ufl64(L.pid[w]);
+        const uint32_t gd = ufl(L.gpd[w]);
+        if (lane == 0) {
+          L.osc[w] = gs;
+          L.ots[w] = gt;
+          L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
+        }
+        if (RANKED) {
+          ot_set(ob, ob.n, gs, wid, w);
+          ++ob.n;
+          if (was_min) {
+            ot_min(ob);
+          } else if (gs < ob.msc || (gs == ob.msc && wid < ob.mid)) {
+            ob.mi = ob.n - 1;
+            ob.msc = gs;
+            ob.mid = wid;
+          }
+        } else {
           ++nobs;
           wave_lds_sync();
           s_min<PCAP>(L, np, mn);
-          if (lane == 0)
-            s_emit<PCAP>(a, L, op0, op0 + c0 + j, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt,
-                         nullptr);
         }
+        if (lane == 0)
+          s_emit<PCAP>(a, L, op0, op0 + c0 + jr, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt, nullptr);
       }
+      wave_lds_sync();
     }
+    s_catch_up<PCAP>(L, last, n, kdr, nxt, rok, rsc, rts, rd);
     wave_lds_sync();
     c0 += n;
+    SPROF(7);
   }
 
   // ---- K5. positions of compacted slabs; player records; Vc; meta
+  if (RANKED) {
+    nobs = ob.n;
+    mn.p = ob.mi == S_NONE ? S_NONE : ot_get32(ob.p, ob.mi);
+  }
   uint32_t mcount = 0;
   for (uint32_t b = 0; b < np; b += 64) {
     const uint32_t p = b + lane;
@@ -890,12 +1191,13 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     a.new_s.meta[key] = out;
     a.ex_cnt[key] = L.nex;
   }
+  SPROF(8);
   return S_DONE;
 }
 
 }  // namespace
 
-template <int PCAP, int WAVES>
+template <int PCAP, int WAVES, bool RANKED>
 __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a) {
   __shared__ SLds<PCAP> lds[WAVES];
   const uint32_t wv = ufl(threadIdx.x >> 6);
@@ -903,7 +1205,7 @@ __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x * WAVES + wv; w < n; w += gridDim.x * WAVES) {
     const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
-    const int r = trmv_steady_key<PCAP>(a, key, L);
+    const int r = trmv_steady_key<PCAP, RANKED>(a, key, L);
     if (r == S_NEXT && lane_id() == 0) {
       const uint32_t pos = atomicAdd(&a.status[0], 1u);
       a.ovf_list[pos] = key;
@@ -916,15 +1218,34 @@ __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a
 // players.  grid_keys bounds the work list (its length may live on the device).
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
+  // Observed in registers when K <= 128 (ObsTab), else in LDS
+  const bool ranked = a.k <= 128;
   if (cls == 0) {
     const uint64_t blocks = std::min<uint64_t>((grid_keys + 1) / 2, 16384);
-    hipLaunchKernelGGL((trmv_steady_kernel<256, 2>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    if (ranked)
+      hipLaunchKernelGGL((trmv_steady_kernel<256, 2, true>), dim3((unsigned)blocks), dim3(128), 0, st, a);
+    else
+      hipLaunchKernelGGL((trmv_steady_kernel<256, 2, false>), dim3((unsigned)blocks), dim3(128), 0, st, a);
   } else {
     const uint64_t blocks = std::min<uint64_t>(grid_keys, 4096);
-    hipLaunchKernelGGL((trmv_steady_kernel<1024, 1>), dim3((unsigned)blocks), dim3(64), 0, st, a);
+    if (ranked)
+      hipLaunchKernelGGL((trmv_steady_kernel<1024, 1, true>), dim3((unsigned)blocks), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((trmv_steady_kernel<1024, 1, false>), dim3((unsigned)blocks), dim3(64), 0, st, a);
   }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
 
 }  // namespace ccrdt
+
+#ifdef TRMV_PROF
+extern "C" int ccrdt_debug_steady_prof(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_steady_prof), 16 * 8) != hipSuccess) return 4;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_steady_prof), z, sizeof(z)) != hipSuccess) return 4;
+  }
+  return 0;
+}
+#endif

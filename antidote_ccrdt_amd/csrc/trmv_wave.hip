@@ -256,7 +256,7 @@ __device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, W& L, Key
 
 // Outcome of one key.  Only W_DONE has already issued the loads of the wave's
 // next key; the rare other paths leave that to the caller.
-enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2, W_SIDE = 3 };
+enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
 
 template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
@@ -280,7 +280,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     om = a.old_s.meta[key];
   }
   const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
-  if (nops > (uint32_t)W_ECAP && a.skip_big) return W_SIDE;  // the side chain has it
   if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
       om.nr > (uint32_t)W_RCAP)
     return W_NEXT_TIER;
@@ -615,10 +614,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bool single = xv[s] && xc[s] == 1;
-        if (single && xa[s]) {
-          L.pobs[xp[s]] = (uint8_t)xq[s];
-          L.pgb[xp[s]] = (uint8_t)xq[s];
-        }
+        if (single && xa[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
         if (single && xr[s]) {
           L.prow[xp[s]] = (uint8_t)xsc[s];
           L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
@@ -645,8 +641,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t adc = ya ? ((kd >> 2) & 7u) : 0u;
       const uint32_t st = L.pstart[p], c = act ? pcnt_of(L, p) : 0u;
       const uint32_t me = q - st;
-      bool fb = false, beaten = false, gbeaten = false, risk = false, seen = false, first = true;
-      const uint32_t mdc = (kd >> 2) & 7u;
+      bool fb = false, beaten = false, risk = false, seen = false, first = true;
       const uint32_t maxc = wave_max_u32_dpp(c);
       // software-pipelined: position x+1 is read while position x's clock
       // entry (its address depends on x's element) is in flight
@@ -655,7 +650,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
         const int64_t sx = sxn, tx = txn;
-        const uint32_t dx = (kxn >> 2) & 7u;
         const bool valid = x < c && x != me;
         const bool isr = valid && (kxn & 2u) != 0;
         const bool before = x < me;
@@ -672,17 +666,12 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         first &= !(isr && before);
         risk = risk && !isr;
         beaten = beaten && !isr;
-        gbeaten = gbeaten && !isr;
         const bool both = ya && valid && !isr;
         risk |= both && before && tx >= tm;
         beaten |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
-        // gb_sets term order inside one Id: (Score, DcId, Ts); the last
-        // segment's Ts rise strictly (else the player is replayed), so no ties
-        gbeaten |= both && (sx > sm || (sx == sm && (dx > mdc || (dx == mdc && tx > tm))));
       }
       if (act && (fb || risk)) L.pflag[p] = 1;
       if (ya && !seen && !beaten) L.pobs[p] = (uint8_t)q;
-      if (ya && !seen && !gbeaten) L.pgb[p] = (uint8_t)q;
       if (yr && first) L.prow[p] = (uint8_t)sm;  // a rmv's "score" is its clock row
       if (yr && !seen) L.plr[p] = (uint8_t)(q + 1);
       if (act) mrg[k] = (uint8_t)(yr && !first);
@@ -868,8 +857,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (FRESH) {
       // the player's slab at [pstart, pstart + cnt); its record is written
       // with every other player's below
-      uint32_t opos = NONE16, gj = 0, gdc = 0;
-      int64_t gsc = 0, gts = 0;
+      uint32_t opos = NONE16, gj = 0;
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t e2 = L.slab[moff + j];
         const int64_t s2 = L.esc[e2], t2 = L.ets[e2];
@@ -878,12 +866,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         (a.new_s.m_ts + nmeta.m_off)[st + j] = t2;
         (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)d2;
         opos = e2 == o ? j : opos;
-        if (j == 0 || s2 > gsc || (s2 == gsc && (d2 > gdc || (d2 == gdc && t2 > gts)))) {
-          gj = j;
-          gsc = s2;
-          gdc = d2;
-          gts = t2;
-        }
+        // gb_sets:largest so far (re-read from LDS: no registers held across)
+        const uint32_t eb = L.slab[moff + gj];
+        const int64_t bs = L.esc[eb], bt = L.ets[eb];
+        const uint32_t bd = (L.ekd[eb] >> 2) & 7u;
+        if (s2 > bs || (s2 == bs && (d2 > bd || (d2 == bd && t2 > bt)))) gj = j;
       }
       if (act) {
         L.pobs[p] = (uint8_t)(o == NONE8 ? NONE8 : st + opos);
@@ -927,10 +914,19 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
       const int64_t id = (int64_t)L.htab[L.pslot[pp]];
+      // gb_sets:largest of a decided player's slab (its last segment, strictly
+      // rising Ts, so no two elements tie): term order (Score, DcId, Ts)
+      uint32_t gb = replayed ? (uint32_t)L.pgb[pp] - off : 0u;
+      if (!replayed && cnt > 1)
+        for (uint32_t j = 1; j < cnt; ++j) {
+          const int64_t s2 = L.esc[off + j], t2 = L.ets[off + j], bs = L.esc[off + gb], bt = L.ets[off + gb];
+          const uint32_t d2 = (L.ekd[off + j] >> 2) & 7u, bd = (L.ekd[off + gb] >> 2) & 7u;
+          if (s2 > bs || (s2 == bs && (d2 > bd || (d2 == bd && t2 > bt)))) gb = j;
+        }
       if (act) {
         (a.new_s.pl_id + nmeta.p_off)[p] = id;
         (a.new_s.pl_slab + nmeta.p_off)[p] = off | (cnt << 16);
-        (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)(cnt ? (uint32_t)L.pgb[pp] - off : 0u);
+        if (cnt > 1) (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)gb;  // readers take 0 for cnt <= 1
         (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : o - off) |
                                              ((prow != NONE8 ? rix : NONE16) << 16);
       }
@@ -1104,26 +1100,6 @@ __global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_k
       cur = nxt;
     }
   }
-}
-
-// The side chain's work list: every key with more ops than tier 0 takes.
-__global__ __launch_bounds__(256) void trmv_classify_kernel(TrmvApplyArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool big = k < (uint64_t)a.n_keys && a.key_ptr[k + 1] - a.key_ptr[k] > (uint64_t)W_ECAP;
-  const uint64_t m = ballot(big);
-  if (m) {
-    uint32_t base = 0;
-    if (lane_id() == (int)__builtin_ctzll(m)) base = atomicAdd(&a.status[0], (uint32_t)__builtin_popcountll(m));
-    base = rl32(base, (int)__builtin_ctzll(m));
-    if (big) a.ovf_list[base + mbcnt(m)] = (uint32_t)k;
-  }
-}
-
-int trmv_launch_classify(const TrmvApplyArgs& a, hipStream_t st) {
-  if (a.n_keys == 0) return CCRDT_OK;
-  hipLaunchKernelGGL(trmv_classify_kernel, dim3((unsigned)((a.n_keys + 255) / 256)), dim3(256), 0, st, a);
-  CCRDT_HIP(hipGetLastError());
-  return CCRDT_OK;
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)

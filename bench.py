@@ -219,9 +219,8 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    # 0 = tier 0, 1 / 2 = tier S (256 / 1024 players); 1000 = side chain
-    # (keys with > 128 ops), 1001 / 1002 = its tier S classes
-    tiers = (0, 1, 2, 1000, 1001, 1002)
+    # 0 = tier 0, 1 / 2 = tier S (up to 256 / 1024 players per key)
+    tiers = (0, 1, 2)
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 

@@ -73,3 +73,22 @@ def test_steady_state_stream(gpu, n_keys, batches):
     # the stream really is in steady state: Observed full, P > K, promotions
     nobs = np.diff(st.obs_ptr.astype(np.int64))
     assert (nobs == K).mean() > 0.9
+
+
+def test_one_key_grows_past_5000_masked(gpu):
+    """A single key accumulates more than 5,000 Masked elements (and 300
+    players, K=100) over several batches, the reference's unbounded Masked
+    (src/antidote_ccrdt_topk_rmv.erl:240-246): bit-exact after every batch,
+    with no per-key capacity error."""
+    nk, D, K, n = 1, 8, 100, 1600
+    eng = TopkRmvEngine(nk, K, D)
+    o = orc.TrmvOracle(nk, K, D)
+    for i in range(5):
+        b = gen_trmv(n, nk, D, n_players=300, score_max=10**6, rmv_pm=20, lag_max=3000,
+                     dup_pm=10, swap_pm=5, seed=4242 + i, clock0=i * n)
+        xe = eng.apply(b)
+        xo = o.apply(b, 1, want_extra=True)
+        bad = orc.trmv_mismatches(eng.export(), xe, o.export(), xo)
+        assert not bad, f"batch {i}: fields differ from the oracle: {bad}"
+    m = np.diff(eng.export().m_ptr.astype(np.int64))
+    assert m.max() > 5000
