@@ -4,10 +4,14 @@
 One step = one pass of the hot path (antidote_ccrdt_topk_rmv update/2 for
 every effect of the batch, src/antidote_ccrdt_topk_rmv.erl:140-148) over one
 batch of synthetic input: 100M effect ops (90% add / 10% rmv, 8-DC vector
-clocks) CSR-grouped over 2^20 keys, applied to fresh keys (new(100)), with the
-ops already resident in HBM.  Each rank owns its own 2^20-key shard (keys are
-independent CRDT objects; no data-path collective), so per-GPU work is fixed
-and scaling is weak.
+clocks) CSR-grouped over 2^20 keys (BASELINE configs[2]), applied to fresh
+keys (new(100)), with the ops already resident in HBM.  With N ranks the same
+global keyspace is hash-sharded, owner(key) = splitmix64(key) mod N
+(antidote_ccrdt_amd/cluster.py): every rank generates the global stream, keeps
+its keys' ops (stream order kept), and a step is its apply plus the batch's
+two exchange steps (extras all-gather, replica-Vc max all-reduce).  Total work
+is fixed, so scaling is strong.  --weak gives every rank its own 2^20-key /
+100M-op stream instead (per-GPU work fixed, weak scaling).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -42,6 +46,9 @@ def parse():
                     help="steady-state leg: batches 2..n+1 of the same stream applied onto the "
                          "resident keys after batch 1 (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "trmv_pmc.json"))
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: every rank its own 2^20-key stream (weak scaling) instead of a "
+                         "shard of the global keyspace")
     ap.add_argument("--dist-backend", default=None,
                     help="N > 1: nccl (RCCL, default on GPUs) or gloo (host-staged; tests)")
     return ap.parse_args()
@@ -150,13 +157,20 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    seed = 0xCC0DE + 2 + 1_000_003 * rank
+    sharded = world > 1 and not args.weak
+    seed = 0xCC0DE + 2 + (0 if sharded else 1_000_003 * rank)
     t_gen = time.perf_counter()
     b = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6, rmv_pm=100,
                  lag_max=64, seed=seed)
+    n_local_keys = args.n_keys
+    if sharded:  # this rank's shard of the global keyspace (cluster.py)
+        from antidote_ccrdt_amd.cluster import owned_keys, route
+        my_keys = owned_keys(args.n_keys, world, rank)
+        b = route(b, my_keys).batch
+        n_local_keys = int(my_keys.shape[0])
     t_gen = time.perf_counter() - t_gen
     db = DeviceTrmvBatch(b)
-    eng = TopkRmvEngine(args.n_keys, args.k, args.n_dc, device=device)
+    eng = TopkRmvEngine(n_local_keys, args.k, args.n_dc, device=device)
     xchg = Exchange(eng, args.n_dc, world, backend, device, dist) if world > 1 else None
 
     def step():
@@ -183,7 +197,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1000.0 / args.steps
-    value = world * args.n_ops * args.steps / dt
+    value = (1 if sharded else world) * args.n_ops * args.steps / dt
 
     # Dominant kernel: tier 0 of the apply chain (trmv_wave_kernel), which
     # completes every key except the few it hands on.  Its algorithmic bytes
@@ -203,7 +217,7 @@ def main():
                        ks["nr"].astype(np.int64) * (8 + 8 * D) + 8 * D + 16)
     key_bytes = key_op_bytes + key_state_bytes
     handed = eng.handed_on(0)
-    tier0 = np.ones(args.n_keys, bool)
+    tier0 = np.ones(n_local_keys, bool)
     tier0[handed] = False
     alg_bytes = int(key_bytes.sum()) + 32 * n_extra          # whole batch
     alg_bytes_t0 = int(key_bytes[tier0].sum()) + 32 * n_extra  # extras: 46 per 100M ops, all counted here
@@ -215,7 +229,7 @@ def main():
         try:
             with open(args.pmc) as f:
                 pm = json.load(f)
-            if pm.get("n_ops") == args.n_ops and pm.get("n_keys") == args.n_keys:
+            if world == 1 and pm.get("n_ops") == args.n_ops and pm.get("n_keys") == args.n_keys:
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -237,6 +251,8 @@ def main():
         for i in range(1, args.steady_batches + 1):
             bi = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6,
                           rmv_pm=100, lag_max=64, seed=seed + 7919 * i, clock0=i * args.n_ops)
+            if sharded:
+                bi = route(bi, my_keys).batch
             dbi = DeviceTrmvBatch(bi)
             del bi
             eng.sync()
@@ -246,17 +262,19 @@ def main():
             eng.sync()
             ms = (time.perf_counter() - ts0) * 1e3
             dbi.close()
+            n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
             rows.append({"batch": i + 1, "ms": round(ms, 3),
-                         "ops_per_s": args.n_ops / (ms * 1e-3),
+                         "ops_per_s": n_step / (ms * 1e-3),
                          "apply_chain_ms": round(eng.last_kernel_ms(), 3),
                          "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in tiers},
                          "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers},
                          "state_after": dict(zip(("observed", "masked", "removal_rows"),
                                                  eng.sizes()))})
         mean_ms = sum(r["ms"] for r in rows) / len(rows)
+        n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
         steady = {"what": "batches 2..n of the bench stream onto the resident keys (no reset), "
-                          "one apply_device each, wall time around it",
-                  "ops_per_s_mean": args.n_ops / (mean_ms * 1e-3), "ms_mean": mean_ms,
+                          "one apply_device each, wall time around it (this rank)",
+                  "ops_per_s_mean": n_step / (mean_ms * 1e-3), "ms_mean": mean_ms,
                   "batches": rows}
 
     cpu = cpu_mt = None
@@ -301,7 +319,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
@@ -309,11 +327,17 @@ def main():
                 "workload": f"antidote_ccrdt_topk_rmv update/2, K={args.k}, {args.n_dc}-DC "
                             f"vector clocks, {args.n_ops} effect ops (90% add / 10% rmv, 256 "
                             f"players/key, score U[1,1e6], rmv lag U[0,64)) CSR-grouped over "
-                            f"{args.n_keys} fresh keys per GPU, ops resident in HBM",
-                "n_ops_per_gpu": args.n_ops, "n_keys_per_gpu": args.n_keys, "K": args.k,
+                            f"{args.n_keys} fresh keys"
+                            + (", one global keyspace hash-sharded over the GPUs" if sharded else
+                               " per GPU") + ", ops resident in HBM",
+                "n_ops_total": args.n_ops * (1 if sharded else world),
+                "n_keys_total": args.n_keys * (1 if sharded else world),
+                "n_keys_rank0": n_local_keys, "n_ops_rank0": int(b.n_ops), "K": args.k,
                 "n_dc": args.n_dc,
-                "parallelism": f"key-sharded x{world}" + (f", {backend} exchange per step" if world > 1 else ""),
-                "seed": "0xCC0DE+2 (+1000003*rank)",
+                "parallelism": (f"key-sharded x{world} (splitmix64(key) mod {world})" if sharded else
+                                f"independent shards x{world}")
+                               + (f", {backend} exchange per step" if world > 1 else ""),
+                "seed": "0xCC0DE+2" + ("" if (sharded or world == 1) else " (+1000003*rank)"),
             },
             "roofline": {
                 "bound": "hbm",
