@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # -DTRMV_PROF build of tools/prof_phases.py); the default is the in-tree one.
 LIB_PATH = os.environ.get("CCRDT_LIB") or os.path.join(_HERE, "lib", "libccrdt.so")
 
-OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS = range(6)
+OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS, EKEYCAP = range(7)
 AVERAGE, TOPK, TOPK_RMV, LEADERBOARD, WORDCOUNT, WORDDOCUMENTCOUNT = range(6)
 TRMV_ADD, TRMV_ADD_R, TRMV_RMV, TRMV_RMV_R = range(4)
 NOOP = 255
@@ -34,8 +34,17 @@ class CcrdtError(RuntimeError):
         self.code = code
 
 
+class KeyCapacityError(CcrdtError):
+    """CCRDT_EKEYCAP: the topk_rmv batch committed for every key except
+    `keys` (over the per-key capacity; they keep their previous state and
+    their ops go to the host path).  `extra` holds the batch's extra effects
+    when they were asked for."""
+    keys = None
+    extra = None
+
+
 _ERRNAMES = {EINVAL: "EINVAL", ERANGE: "ERANGE", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE",
-             ENOSYS: "ENOSYS"}
+             ENOSYS: "ENOSYS", EKEYCAP: "EKEYCAP"}
 
 
 class TrmvOps(C.Structure):
@@ -110,10 +119,13 @@ SIGNATURES = {
     "ccrdt_trmv_extra_count": (INT, [P, C.POINTER(I64)]),
     "ccrdt_trmv_fetch_extra": (INT, [P, C.POINTER(TrmvExtra)]),
     "ccrdt_trmv_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
+    "ccrdt_trmv_range_sizes": (INT, [P, I64, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_trmv_key_sizes": (INT, [P, P, P, P, P]),
     "ccrdt_trmv_replica_vc_device": (INT, [P, P]),
     "ccrdt_trmv_extras_device": (INT, [P, P, I64, P]),
     "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
+    "ccrdt_trmv_export_range": (INT, [P, I64, I64, C.POINTER(TrmvState)]),
+    "ccrdt_trmv_import_range": (INT, [P, I64, I64, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),
     # average
@@ -143,6 +155,8 @@ SIGNATURES = {
     "ccrdt_wc_apply_device": (INT, [P, C.POINTER(WcDocs)]),
     "ccrdt_wc_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_wc_export": (INT, [P, P, P, P, P]),
+    "ccrdt_wc_merge": (INT, [P, I64, P, P, P, P]),
+    "ccrdt_wc_import": (INT, [P, I64, P, P, P, P]),
     # ccrdt_gen.h
     "ccrdt_splitmix64": (U64, [U64]),
     "ccrdt_gen_trmv_count": (I64, [I64, U64, INT]),
@@ -171,7 +185,7 @@ lib = _load()
 def check(rc: int, where: str) -> None:
     if rc != OK:
         msg = lib.ccrdt_last_error().decode(errors="replace")
-        raise CcrdtError(rc, where, msg)
+        raise (KeyCapacityError if rc == EKEYCAP else CcrdtError)(rc, where, msg)
 
 
 def ptr(a) -> int | None:

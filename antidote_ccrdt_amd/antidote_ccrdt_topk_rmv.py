@@ -66,7 +66,10 @@ def new(size: int = 100) -> TopkRmv:
 
 
 def value(state: TopkRmv):
-    """value/1 (topk_rmv.erl:91-95): [{Id, Score}] (canonical order: by Id)."""
+    """value/1 (topk_rmv.erl:91-95): [{Id, Score}] sorted by Id.  The
+    reference builds the list with maps:fold, so its order is the map's
+    iteration order (an implementation detail of the BEAM, Q7): compare
+    value/1 results as sets."""
     return [(i, sc) for i, sc, _, _ in state._export()["obs"]]
 
 
@@ -144,7 +147,20 @@ def equal(a: TopkRmv, b: TopkRmv) -> bool:
 
 
 def _atom(dc):
+    """A registry DcId as its Erlang term: str -> atom, recursively inside
+    tuples (antidote DcIds are {Node, {Mega, Sec, Micro}})."""
+    if isinstance(dc, tuple):
+        return tuple(_atom(x) for x in dc)
     return etf.Atom(dc) if isinstance(dc, str) and not isinstance(dc, etf.Atom) else dc
+
+
+def _dc_rank(d) -> int:
+    """Registry rank of a decoded DcId term (an atom, or any term such as a
+    {Node, {Mega, Sec, Micro}} tuple); an unregistered one is an EtfError."""
+    try:
+        return terms.DC_REGISTRY.rank(d)
+    except KeyError as e:
+        raise etf.EtfError(str(e)) from None
 
 
 def to_binary(state: TopkRmv) -> bytes:
@@ -170,7 +186,7 @@ def from_binary(b: bytes):
     obs, masked, rem, vc, mn, size = t
     if not (_is_int(size) and size > 0):
         raise etf.EtfError("topkrmv() Size must be a positive integer")
-    rank = lambda d: terms.DC_REGISTRY.rank(str(d))
+    rank = _dc_rank
     nd = terms.DC_REGISTRY.capacity
     el = lambda e: (int(e[1]), int(e[0]), rank(e[2][0]), int(e[2][1]))  # (id, score, dc, ts)
     o = sorted(el(e) for e in obs.values())

@@ -439,27 +439,27 @@ class _WordcountModule:
 
     @classmethod
     def _with(cls, m: dict) -> Wordcount:
-        """A fresh object holding the map m (replayed as documents: a word
-        joined by single spaces is exactly its own tokens)."""
+        """A fresh object holding the map m, imported as (word, count) pairs
+        (ccrdt_wc_import; no text is replayed)."""
         st = cls.new()
         if m:
             words = sorted(m)
-            if cls.WDC:  # document c holds every word with count > c
-                docs = [b" ".join(w for w in words if m[w] > c) for c in range(max(m.values()))]
-            else:
-                docs = [b" ".join(w for w in words for _ in range(m[w]))]
-            st.engine.apply_docs([docs])
+            off = np.zeros(len(words) + 1, np.uint64)
+            off[1:] = np.cumsum([len(w) for w in words])
+            kp = np.array([0, len(words)], np.uint64)
+            st.engine.import_state(kp, off, b"".join(words), np.array([m[w] for w in words], np.int64))
         return st
 
     @classmethod
     def update(cls, effect, st: Wordcount):
         """update/2 (:57-58): add/2 splits on <<"\\n">> and <<" ">> only, empty
         tokens counted (Q13); worddocumentcount counts each distinct token of
-        the file once."""
+        the file once.  Functional: the new state is a device copy of the old
+        one with the file applied."""
         tag, f = effect
         if tag != "add" or not isinstance(f, (bytes, bytearray)):
             raise FunctionClause("update/2")
-        new = cls._with(st.to_term())
+        new = Wordcount(st.engine.clone())
         new.engine.apply_docs([[bytes(f)]])
         return ("ok", new)
 

@@ -24,6 +24,7 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
+int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
@@ -89,6 +90,7 @@ const char* ccrdt_strerror(int code) {
     case CCRDT_EINVAL: return "invalid argument or operation";
     case CCRDT_ERANGE: return "integer outside engine range";
     case CCRDT_ENOMEM: return "out of device memory or per-key capacity";
+    case CCRDT_EKEYCAP: return "keys over the per-key capacity were left out of the batch";
     case CCRDT_EDEVICE: return "HIP device error";
     case CCRDT_ENOSYS: return "operation not supported for this CCRDT type";
     default: return "unknown error";
@@ -383,10 +385,6 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   const uint32_t* hs = (const uint32_t*)E.h_status;
   uint32_t err = 0;
   for (int t = first_tier; t < TRMV_N_TIERS; ++t) err |= hs[3 + 2 * t];
-  if ((hs[1] | err) & TRMV_ERR_SEG) {
-    set_error("trmv_apply: a key's Masked segment would exceed 65535 elements");
-    return CCRDT_ENOMEM;
-  }
   if (err) {
     std::string m = "trmv_apply: invalid op in batch:";
     if (err & TRMV_ERR_KIND) m += " kind>3";
@@ -408,10 +406,14 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     E.trmv_tier_ms[t] = ms;
     E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
-  if (nk && hs[2 + 2 * (TRMV_N_TIERS - 1)]) {
-    set_error("trmv_apply: a key would hold more than 1024 players (Ids with a Masked or "
-              "Removals entry); ccrdt_engine_handed_on(e, 2) lists them");
-    return CCRDT_ENOMEM;
+  // Keys over the per-key capacity (the last tier's hand-ons) keep their old
+  // state; every other key commits.
+  const uint32_t n_over = nk ? hs[2 + 2 * (TRMV_N_TIERS - 1)] : 0u;
+  if (n_over) {
+    a.key_list = E.tier_ovf[TRMV_N_TIERS - 1].as<uint32_t>();
+    a.n_list = 0;
+    a.n_list_dev = status + 2 + 2 * (TRMV_N_TIERS - 1);
+    CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>(n_over, TRMV_LATER_GRID), E.stream));
   }
   float kernel_ms = 0.f;
   if (nk && ev > 1) CCRDT_HIP(hipEventElapsedTime(&kernel_ms, E.evt[0], E.evt[ev - 1]));
@@ -422,6 +424,13 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   E.fresh = false;
   E.last_n_ops = n_ops;
   E.last_kernel_ms = kernel_ms;
+  if (n_over) {
+    set_error("trmv_apply: " + std::to_string(n_over) +
+              " key(s) would exceed the per-key capacity (1024 players, 65535 Masked "
+              "elements, 65534 Removals rows): they keep their previous state, the other "
+              "keys committed; ccrdt_engine_handed_on(e, 2) lists them");
+    return CCRDT_EKEYCAP;
+  }
   return CCRDT_OK;
 }
 
@@ -537,9 +546,14 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   d.ts = E.st_ts.as<int64_t>();
   d.rmv_vc = nr ? E.st_rvc.as<int64_t>() : nullptr;
   d.n_rmv_rows = (int64_t)nr;
-  CCRDT_TRY(ccrdt_trmv_apply_device(e, &d));
-  if (extra) CCRDT_TRY(ccrdt_trmv_fetch_extra(e, extra));
-  return CCRDT_OK;
+  const int rc = ccrdt_trmv_apply_device(e, &d);
+  if (rc != CCRDT_OK && rc != CCRDT_EKEYCAP) return rc;
+  if (extra) {  // EKEYCAP: the batch committed; its extras are fetched too
+    const std::string msg = g_last_error;
+    CCRDT_TRY(ccrdt_trmv_fetch_extra(e, extra));
+    if (rc != CCRDT_OK) set_error(msg);
+  }
+  return rc;
 }
 
 // ---- state image conversion
@@ -553,59 +567,71 @@ struct HostTrmv {
   std::vector<uint8_t> m_dc;
 };
 
-int download_trmv(Engine& E, HostTrmv& h) {
-  const uint64_t nk = (uint64_t)E.n_keys;
+// Keys [k0, k1) of the resident state -> host, offsets rebased to the range
+// (segments of consecutive keys are consecutive: the capacity scan and the
+// import lay them out in key order).
+int download_trmv(Engine& E, HostTrmv& h, uint64_t k0, uint64_t k1) {
+  const uint64_t n = k1 - k0;
   const int D = E.n_dc;
-  h.meta.assign(nk, KeyMeta{0, 0, 0, 0, 0, 0, 0, NONE32});
-  h.vc.assign(nk * D, 0);
-  if (E.fresh || !nk) return CCRDT_OK;
+  h.meta.assign(n, KeyMeta{0, 0, 0, 0, 0, 0, 0, NONE32});
+  h.vc.assign(n * D, 0);
+  h.pl_id.clear();
+  h.pl_info.clear();
+  h.pl_slab.clear();
+  h.m_score.clear();
+  h.m_ts.clear();
+  h.m_dc.clear();
+  h.r_vc.clear();
+  if (E.fresh || !n) return CCRDT_OK;
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const TrmvBufs& b = E.trmv[E.cur];
-  CCRDT_HIP(hipMemcpy(h.meta.data(), b.meta.p, nk * sizeof(KeyMeta), hipMemcpyDeviceToHost));
-  CCRDT_HIP(hipMemcpy(h.vc.data(), b.vc.p, nk * D * 8, hipMemcpyDeviceToHost));
-  const uint64_t np = std::min({b.pl_id.bytes / 8, b.pl_info.bytes / 4, b.pl_slab.bytes / 4});
-  const uint64_t nm = std::min({b.m_dc.bytes, b.m_score.bytes / 8, b.m_ts.bytes / 8});
-  const uint64_t nr = b.r_vc.bytes / (8 * D);
+  CCRDT_HIP(hipMemcpy(h.meta.data(), b.meta.as<KeyMeta>() + k0, n * sizeof(KeyMeta), hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(h.vc.data(), b.vc.as<int64_t>() + k0 * D, n * D * 8, hipMemcpyDeviceToHost));
+  const uint64_t p0 = h.meta[0].p_off, r0 = h.meta[0].r_off, m0 = h.meta[0].m_off;
+  uint64_t p1 = p0, r1 = r0;
+  for (const KeyMeta& m : h.meta) {
+    p1 = std::max<uint64_t>(p1, (uint64_t)m.p_off + m.np);
+    r1 = std::max<uint64_t>(r1, (uint64_t)m.r_off + m.nr);
+  }
+  const uint64_t np = p1 - p0, nr = r1 - r0;
   h.pl_id.resize(np);
   h.pl_info.resize(np);
   h.pl_slab.resize(np);
+  if (np) {
+    CCRDT_HIP(hipMemcpy(h.pl_id.data(), b.pl_id.as<int64_t>() + p0, np * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.pl_info.data(), b.pl_info.as<uint32_t>() + p0, np * 4, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.pl_slab.data(), b.pl_slab.as<uint32_t>() + p0, np * 4, hipMemcpyDeviceToHost));
+  }
+  uint64_t m1 = m0;
+  for (const KeyMeta& m : h.meta)
+    for (uint32_t p = 0; p < m.np; ++p) {
+      const uint32_t sl = h.pl_slab[m.p_off - p0 + p];
+      m1 = std::max<uint64_t>(m1, (uint64_t)m.m_off + (sl & 0xFFFFu) + (sl >> 16));
+    }
+  const uint64_t nm = m1 - m0;
   h.m_score.resize(nm);
   h.m_ts.resize(nm);
   h.m_dc.resize(nm);
   h.r_vc.resize(nr * D);
-  if (np) {
-    CCRDT_HIP(hipMemcpy(h.pl_id.data(), b.pl_id.p, np * 8, hipMemcpyDeviceToHost));
-    CCRDT_HIP(hipMemcpy(h.pl_info.data(), b.pl_info.p, np * 4, hipMemcpyDeviceToHost));
-    CCRDT_HIP(hipMemcpy(h.pl_slab.data(), b.pl_slab.p, np * 4, hipMemcpyDeviceToHost));
-  }
   if (nm) {
-    CCRDT_HIP(hipMemcpy(h.m_score.data(), b.m_score.p, nm * 8, hipMemcpyDeviceToHost));
-    CCRDT_HIP(hipMemcpy(h.m_ts.data(), b.m_ts.p, nm * 8, hipMemcpyDeviceToHost));
-    CCRDT_HIP(hipMemcpy(h.m_dc.data(), b.m_dc.p, nm, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_score.data(), b.m_score.as<int64_t>() + m0, nm * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_ts.data(), b.m_ts.as<int64_t>() + m0, nm * 8, hipMemcpyDeviceToHost));
+    CCRDT_HIP(hipMemcpy(h.m_dc.data(), b.m_dc.as<uint8_t>() + m0, nm, hipMemcpyDeviceToHost));
   }
-  if (nr) CCRDT_HIP(hipMemcpy(h.r_vc.data(), b.r_vc.p, nr * D * 8, hipMemcpyDeviceToHost));
+  if (nr)
+    CCRDT_HIP(hipMemcpy(h.r_vc.data(), b.r_vc.as<int64_t>() + r0 * D, nr * D * 8, hipMemcpyDeviceToHost));
+  for (KeyMeta& m : h.meta) {
+    m.p_off -= (uint32_t)p0;
+    m.m_off -= (uint32_t)m0;
+    m.r_off -= (uint32_t)r0;
+  }
   return CCRDT_OK;
 }
 }  // namespace
 
 int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows) {
   CCRDT_TRY(check_trmv(e));
-  int64_t o = 0, m = 0, r = 0;
-  if (!e->fresh && e->n_keys) {
-    std::vector<KeyMeta> meta(e->n_keys);
-    CCRDT_HIP(hipStreamSynchronize(e->stream));
-    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.p, meta.size() * sizeof(KeyMeta),
-                        hipMemcpyDeviceToHost));
-    for (const KeyMeta& k : meta) {
-      o += k.nobs;
-      m += k.nm;
-      r += k.nr;
-    }
-  }
-  if (n_obs) *n_obs = o;
-  if (n_masked) *n_masked = m;
-  if (n_rows) *n_rows = r;
-  return CCRDT_OK;
+  return ccrdt_trmv_range_sizes(e, 0, e->n_keys, n_obs, n_masked, n_rows);
 }
 
 int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* nr, uint32_t* nobs) {
@@ -647,10 +673,43 @@ int ccrdt_engine_handed_on(ccrdt_engine* e, int t, uint32_t* keys, int64_t cap, 
 
 int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out) {
   CCRDT_TRY(check_trmv(e));
-  if (!out) return CCRDT_EINVAL;
+  return ccrdt_trmv_export_range(e, 0, e->n_keys, out);
+}
+
+int ccrdt_trmv_range_sizes(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_obs, int64_t* n_masked,
+                           int64_t* n_rows) {
+  CCRDT_TRY(check_trmv(e));
+  if (k0 < 0 || k1 < k0 || k1 > e->n_keys) {
+    set_error("trmv_range_sizes: bad key range");
+    return CCRDT_EINVAL;
+  }
+  int64_t o = 0, m = 0, r = 0;
+  if (!e->fresh && k1 > k0) {
+    std::vector<KeyMeta> meta(k1 - k0);
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.as<KeyMeta>() + k0, meta.size() * sizeof(KeyMeta),
+                        hipMemcpyDeviceToHost));
+    for (const KeyMeta& k : meta) {
+      o += k.nobs;
+      m += k.nm;
+      r += k.nr;
+    }
+  }
+  if (n_obs) *n_obs = o;
+  if (n_masked) *n_masked = m;
+  if (n_rows) *n_rows = r;
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, ccrdt_trmv_state* out) {
+  CCRDT_TRY(check_trmv(e));
+  if (!out || k0 < 0 || k1 < k0 || k1 > e->n_keys) {
+    set_error("trmv_export_range: bad arguments");
+    return CCRDT_EINVAL;
+  }
   HostTrmv h;
-  CCRDT_TRY(download_trmv(*e, h));
-  const uint64_t nk = (uint64_t)e->n_keys;
+  CCRDT_TRY(download_trmv(*e, h, (uint64_t)k0, (uint64_t)k1));
+  const uint64_t nk = (uint64_t)(k1 - k0);
   const int D = e->n_dc;
   uint64_t po = 0, pm = 0, pr = 0;
   if (out->obs_ptr) out->obs_ptr[0] = 0;
@@ -898,6 +957,102 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   E.trmv_tot[E.cur][2] = h.r_vc.size() / D;
   E.fresh = false;
   return CCRDT_OK;
+}
+
+int ccrdt_trmv_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const ccrdt_trmv_state* in) {
+  CCRDT_TRY(check_trmv(e));
+  if (!in || !in->vc || !in->obs_ptr || !in->m_ptr || !in->r_ptr || !in->min_valid || k0 < 0 || k1 < k0 ||
+      k1 > e->n_keys) {
+    set_error("trmv_import_range: bad arguments");
+    return CCRDT_EINVAL;
+  }
+  // the whole image with keys [k0, k1) replaced, imported at once (the
+  // import validates and lays out every key); O(n_keys) host work
+  const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)(k1 - k0);
+  const int D = e->n_dc;
+  int64_t no = 0, nm = 0, nr = 0;
+  CCRDT_TRY(ccrdt_trmv_state_sizes(e, &no, &nm, &nr));
+  struct Img {
+    std::vector<int64_t> vc, obs_id, obs_score, obs_ts, m_id, m_score, m_ts, r_id, r_vc, min_id, min_score,
+        min_ts;
+    std::vector<uint64_t> obs_ptr, m_ptr, r_ptr;
+    std::vector<uint8_t> obs_dc, m_dc, min_valid, min_dc;
+    ccrdt_trmv_state view() {
+      return ccrdt_trmv_state{vc.data(), obs_ptr.data(), obs_id.data(), obs_score.data(), obs_ts.data(),
+                              obs_dc.data(), m_ptr.data(), m_id.data(), m_score.data(), m_ts.data(),
+                              m_dc.data(), r_ptr.data(), r_id.data(), r_vc.data(), min_valid.data(),
+                              min_id.data(), min_score.data(), min_ts.data(), min_dc.data()};
+    }
+    void size(uint64_t k, uint64_t o, uint64_t m, uint64_t r, int d) {
+      vc.resize(k * d);
+      obs_ptr.resize(k + 1);
+      m_ptr.resize(k + 1);
+      r_ptr.resize(k + 1);
+      obs_id.resize(o), obs_score.resize(o), obs_ts.resize(o), obs_dc.resize(o);
+      m_id.resize(m), m_score.resize(m), m_ts.resize(m), m_dc.resize(m);
+      r_id.resize(r), r_vc.resize(r * d);
+      min_valid.resize(k), min_id.resize(k), min_score.resize(k), min_ts.resize(k), min_dc.resize(k);
+    }
+  } cur, out;
+  cur.size(nk, (uint64_t)no, (uint64_t)nm, (uint64_t)nr, D);
+  ccrdt_trmv_state cv = cur.view();
+  CCRDT_TRY(ccrdt_trmv_export(e, &cv));
+  const uint64_t io = in->obs_ptr[n], im = in->m_ptr[n], ir = in->r_ptr[n];
+  const uint64_t ro = cur.obs_ptr[k1] - cur.obs_ptr[k0], rm = cur.m_ptr[k1] - cur.m_ptr[k0],
+                 rr = cur.r_ptr[k1] - cur.r_ptr[k0];
+  out.size(nk, no - ro + io, nm - rm + im, nr - rr + ir, D);
+  uint64_t po = 0, pm = 0, pr = 0;
+  out.obs_ptr[0] = out.m_ptr[0] = out.r_ptr[0] = 0;
+  for (uint64_t k = 0; k < nk; ++k) {
+    const bool mine = k >= (uint64_t)k0 && k < (uint64_t)k1;
+    const uint64_t j = mine ? k - k0 : k;
+    auto take = [&](const uint64_t* sp, const int64_t* id, const int64_t* sc, const int64_t* ts,
+                    const uint8_t* dc, std::vector<int64_t>& oid, std::vector<int64_t>& osc,
+                    std::vector<int64_t>& ots, std::vector<uint8_t>& odc, uint64_t& p) {
+      for (uint64_t i = sp[j]; i < sp[j + 1]; ++i, ++p) {
+        oid[p] = id[i];
+        osc[p] = sc[i];
+        ots[p] = ts[i];
+        odc[p] = dc[i];
+      }
+    };
+    if (mine) {
+      take(in->obs_ptr, in->obs_id, in->obs_score, in->obs_ts, in->obs_dc, out.obs_id, out.obs_score,
+           out.obs_ts, out.obs_dc, po);
+      take(in->m_ptr, in->m_id, in->m_score, in->m_ts, in->m_dc, out.m_id, out.m_score, out.m_ts, out.m_dc,
+           pm);
+      for (uint64_t i = in->r_ptr[j]; i < in->r_ptr[j + 1]; ++i, ++pr) {
+        out.r_id[pr] = in->r_id[i];
+        for (int d = 0; d < D; ++d) out.r_vc[pr * D + d] = in->r_vc[i * D + d];
+      }
+      for (int d = 0; d < D; ++d) out.vc[k * D + d] = in->vc[j * D + d];
+      out.min_valid[k] = in->min_valid[j];
+      out.min_id[k] = in->min_id ? in->min_id[j] : 0;
+      out.min_score[k] = in->min_score ? in->min_score[j] : 0;
+      out.min_ts[k] = in->min_ts ? in->min_ts[j] : 0;
+      out.min_dc[k] = in->min_dc ? in->min_dc[j] : 0;
+    } else {
+      take(cur.obs_ptr.data(), cur.obs_id.data(), cur.obs_score.data(), cur.obs_ts.data(), cur.obs_dc.data(),
+           out.obs_id, out.obs_score, out.obs_ts, out.obs_dc, po);
+      take(cur.m_ptr.data(), cur.m_id.data(), cur.m_score.data(), cur.m_ts.data(), cur.m_dc.data(), out.m_id,
+           out.m_score, out.m_ts, out.m_dc, pm);
+      for (uint64_t i = cur.r_ptr[k]; i < cur.r_ptr[k + 1]; ++i, ++pr) {
+        out.r_id[pr] = cur.r_id[i];
+        for (int d = 0; d < D; ++d) out.r_vc[pr * D + d] = cur.r_vc[i * D + d];
+      }
+      for (int d = 0; d < D; ++d) out.vc[k * D + d] = cur.vc[k * D + d];
+      out.min_valid[k] = cur.min_valid[k];
+      out.min_id[k] = cur.min_id[k];
+      out.min_score[k] = cur.min_score[k];
+      out.min_ts[k] = cur.min_ts[k];
+      out.min_dc[k] = cur.min_dc[k];
+    }
+    out.obs_ptr[k + 1] = po;
+    out.m_ptr[k + 1] = pm;
+    out.r_ptr[k + 1] = pr;
+  }
+  const ccrdt_trmv_state ov = out.view();
+  return ccrdt_trmv_import(e, &ov);
 }
 
 int ccrdt_trmv_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,

@@ -31,6 +31,8 @@ int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs,
 int wc_launch_insert(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st);
+int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
+                    int verify, hipStream_t st);
 int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
                      const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st);
 }  // namespace ccrdt
@@ -959,7 +961,10 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     uint64_t d0 = 0;
     while (d0 < nd) {
       uint64_t d1 = d0, tk = 0;
-      while (d1 < nd && (d1 == d0 || !a.wdc || tk + ntok[d1] <= (1ull << 28))) tk += ntok[d1++];
+      // (worddocumentcount dedupe entries hold the launch-local document
+      // index in 24 bits: at most 2^23 documents per launch)
+      while (d1 < nd && (d1 == d0 || !a.wdc || (tk + ntok[d1] <= (1ull << 28) && d1 - d0 < (1ull << 23))))
+        tk += ntok[d1++];
       a.n_docs = (int64_t)(d1 - d0);
       a.doc_key = T.stage[0].as<uint64_t>() + d0;
       a.doc_off = docs->doc_off + d0;
@@ -1027,6 +1032,110 @@ int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   ccrdt_wc_docs d{docs->n_docs, T.kp.as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[3].as<uint8_t>(),
                   docs->n_bytes};
   return ccrdt_wc_apply_device(e, &d);
+}
+
+static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr,
+                          const uint64_t* word_off, const uint8_t* bytes, const int64_t* count,
+                          bool replace) {
+  if (n_words < 0 || !key_ptr || !word_off || (n_words && !count)) {
+    set_error("wc_merge: null arrays");
+    return CCRDT_EINVAL;
+  }
+  const uint64_t nk = (uint64_t)e->n_keys, nw = (uint64_t)n_words;
+  CCRDT_TRY(check_csr(key_ptr, nk, nw));
+  if (word_off[0] != 0) {
+    set_error("wc_merge: word_off must start at 0");
+    return CCRDT_EINVAL;
+  }
+  for (uint64_t i = 0; i < nw; ++i) {
+    if (word_off[i + 1] < word_off[i] || word_off[i + 1] - word_off[i] > 0xFFFFFFFFull) {
+      set_error("wc_merge: word_off not monotone");
+      return CCRDT_EINVAL;
+    }
+    if (count[i] < 1) {  // a map entry counts at least one token (wordcount.erl:57-58)
+      set_error("wc_merge: counts must be >= 1");
+      return CCRDT_EINVAL;
+    }
+  }
+  const uint64_t nb = word_off[nw];
+  if (nb && !bytes) {
+    set_error("wc_merge: null bytes");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.status.ensure(64));
+  CCRDT_TRY(T.arena_top.ensure(16));
+  // replace: the maps := the words (ccrdt_wc_import); the old state stays
+  // intact until the new table has been verified.
+  const bool start_empty = e->fresh || replace;
+  // words -> device: keys, offsets, bytes, counts
+  CCRDT_TRY(h2d(T.kp, key_ptr, (nk + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[2], word_off, (nw + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(T.stage[3], bytes, nb, e->stream));
+  CCRDT_TRY(T.stage[3].ensure(8));
+  CCRDT_TRY(h2d(T.stage[1], count, nw * 8, e->stream));
+  CCRDT_TRY(T.stage[0].ensure(nw * 8 + 8));
+  CCRDT_TRY(wc_launch_doc_key(T.kp.as<uint64_t>(), nk, nw, T.stage[0].as<uint64_t>(), e->stream));
+  std::vector<uint64_t> top{0, 0};
+  if (!e->fresh) CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
+  const uint64_t words_old = start_empty ? 0 : top[1], arena_used = top[0];
+  if (arena_used + nb > T.arena_cap) {
+    DevBuf grown;
+    const uint64_t cap = std::max<uint64_t>(2 * (arena_used + nb), 4096);
+    CCRDT_TRY(grown.ensure(cap));
+    if (arena_used)
+      CCRDT_HIP(hipMemcpyAsync(grown.p, T.arena.p, arena_used, hipMemcpyDeviceToDevice, e->stream));
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    T.arena.release();
+    T.arena = grown;
+    grown.p = nullptr;
+    T.arena_cap = cap;
+  }
+  const int in = T.tcur, out = 1 - T.tcur;
+  const uint64_t slots = pow2_at_least(2 * (words_old + nw));
+  CCRDT_TRY(wc_alloc_table(e, out, slots));
+  WcArgs a = wc_table_args(e, out);
+  if (!start_empty && T.t_slots[in])
+    CCRDT_TRY(wc_launch_rehash(T.t_hash[in].as<uint64_t>(), T.t_key[in].as<uint32_t>(),
+                               T.t_len[in].as<uint32_t>(), T.t_arena[in].as<uint64_t>(),
+                               T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+  CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+  a.bytes = T.stage[3].as<uint8_t>();
+  a.n_bytes = nb;
+  const uint64_t* wk = T.stage[0].as<uint64_t>();
+  const uint64_t* wo = T.stage[2].as<uint64_t>();
+  const int64_t* wc = T.stage[1].as<int64_t>();
+  CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 0, e->stream));
+  CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 1, e->stream));
+  uint32_t st[2];
+  CCRDT_TRY(read_status(e, st));
+  if (st[0] || st[1]) {
+    set_error(st[1] & 1   ? "wc_merge: 64-bit word hash collision between distinct words"
+              : st[1] & 4 ? "wc_merge: a count would leave int64"
+                          : "wc_merge: word table overflow");
+    return st[1] & 5 ? CCRDT_ERANGE : CCRDT_ENOMEM;
+  }
+  // persist appends the new words' bytes at arena_top[0] and counts words in
+  // arena_top[1]; a replaced state starts both from zero
+  CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + (start_empty ? 0 : 1), 0, start_empty ? 16 : 8,
+                           e->stream));
+  CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  T.tcur = out;
+  e->fresh = false;
+  return CCRDT_OK;
+}
+
+int ccrdt_wc_merge(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                   const uint8_t* bytes, const int64_t* count) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  return wc_merge_words(e, n_words, key_ptr, word_off, bytes, count, false);
+}
+
+int ccrdt_wc_import(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                    const uint8_t* bytes, const int64_t* count) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  return wc_merge_words(e, n_words, key_ptr, word_off, bytes, count, true);
 }
 
 int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes) {

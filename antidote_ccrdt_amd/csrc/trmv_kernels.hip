@@ -33,7 +33,9 @@ __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint
     c[1] = m.nm + nops;
     c[2] = m.nr + nops;
   }
-  if (c[1] > TRMV_SEG_MAX) atomicOr(&a.status[1], TRMV_ERR_SEG);  // u16 slab offsets
+  // No per-key limit here: a segment is address space only.  The tiers check
+  // the key's real layout against the u16 slab offsets (TRMV_SEG_MAX) and hand
+  // on a key that does not fit.
 }
 
 __device__ __forceinline__ void block_scan3(uint64_t v[3], uint64_t total[3]) {
@@ -182,7 +184,81 @@ __global__ __launch_bounds__(64) void trmv_downstream_kernel(TrmvDownArgs a) {
   if (lane == 0) a.out_kind[r] = kind;
 }
 
+// --------------------------------------------------- over-capacity keys
+// The keys the last tier handed on (over the per-key capacity) keep their
+// previous state: one wave per listed key copies it from the old side into
+// the segments the scan laid out on the new side (which hold old counts +
+// ops, so the old state fits), closing the holes between Masked slabs, and
+// clears the key's extras.  A fresh engine's previous state is empty.
+__global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
+  const uint32_t n = *a.n_list_dev;
+  const int lane = lane_id();
+  const int D = a.n_dc;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t key = a.key_list[w];
+    KeyMeta nm = a.new_s.meta[key];
+    if (lane == 0) a.ex_cnt[key] = 0u;
+    if (a.fresh) {
+      if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = 0;
+      if (lane == 0) {
+        nm.np = nm.nm = nm.nr = nm.nobs = 0;
+        nm.minq = NONE32;
+        a.new_s.meta[key] = nm;
+      }
+      continue;
+    }
+    const KeyMeta om = a.old_s.meta[key];
+    const TrmvSide& o = a.old_s;
+    const TrmvSide& d = a.new_s;
+    uint32_t base = 0;
+    for (uint32_t p0 = 0; p0 < om.np; p0 += 64) {
+      const uint32_t p = p0 + lane;
+      const bool v = p < om.np;
+      const uint32_t slab = v ? o.pl_slab[om.p_off + p] : 0u;
+      const uint32_t cnt = slab >> 16;
+      uint32_t tot;
+      const uint32_t off = base + wave_excl_scan_u32(cnt, tot);
+      if (v) {
+        d.pl_id[nm.p_off + p] = o.pl_id[om.p_off + p];
+        d.pl_info[nm.p_off + p] = o.pl_info[om.p_off + p];
+        d.pl_gb[nm.p_off + p] = o.pl_gb[om.p_off + p];
+        d.pl_slab[nm.p_off + p] = off | (cnt << 16);
+      }
+      for (int j = 0; j < 64; ++j) {  // each player's elements, lanes over elements
+        const uint32_t c = shfl32(cnt, j);
+        const uint32_t so = shfl32(slab & 0xFFFFu, j);
+        const uint32_t to = shfl32(off, j);
+        for (uint32_t e = lane; e < c; e += 64) {
+          const uint64_t src = (uint64_t)om.m_off + so + e, dst = (uint64_t)nm.m_off + to + e;
+          d.m_score[dst] = o.m_score[src];
+          d.m_ts[dst] = o.m_ts[src];
+          d.m_dc[dst] = o.m_dc[src];
+        }
+      }
+      base += tot;
+    }
+    for (uint32_t i = lane; i < om.nr * (uint32_t)D; i += 64)
+      d.r_vc[(uint64_t)nm.r_off * D + i] = o.r_vc[(uint64_t)om.r_off * D + i];
+    if (lane < D) d.vc[(uint64_t)key * D + lane] = o.vc[(uint64_t)key * D + lane];
+    if (lane == 0) {
+      nm.np = om.np;
+      nm.nm = om.nm;
+      nm.nr = om.nr;
+      nm.nobs = om.nobs;
+      nm.minq = om.minq;
+      d.meta[key] = nm;
+    }
+  }
+}
+
 // ------------------------------------------------------------- launchers
+int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st) {
+  if (grid == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_keep_kernel, dim3(grid), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st) {
   const uint64_t nb = ((uint64_t)a.n_keys + SCAN_TILE - 1) / SCAN_TILE;
   if (nb == 0) return CCRDT_OK;

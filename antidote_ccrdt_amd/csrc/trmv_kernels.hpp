@@ -105,7 +105,6 @@ enum : uint32_t {
   TRMV_ERR_TS = 4u,
   TRMV_ERR_ROW = 8u,
   TRMV_ERR_VC = 16u,
-  TRMV_ERR_SEG = 32u,  // a key's pool segment would exceed TRMV_SEG_MAX
 };
 
 struct TrmvDownArgs {

@@ -553,10 +553,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
     mtot += tot;
   }
-  if (nr >= NONE16 || mtot > TRMV_SEG_MAX) {
-    if (lane == 0) atomicOr(&a.status[1], TRMV_ERR_SEG);
-    return S_REJECT;
-  }
+  if (nr >= NONE16 || mtot > TRMV_SEG_MAX) return S_NEXT;  // over the per-key capacity
   wave_lds_sync();
   SPROF(1);
 

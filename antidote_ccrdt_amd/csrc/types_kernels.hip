@@ -921,10 +921,13 @@ __device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h
   return ~0ull;
 }
 
-__device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t h, uint64_t doc) {
-  // worddocumentcount: first occurrence of (doc, word) in the global dedupe table
-  const uint64_t dh = wc_mix(h, doc + 1, 0x5151);
-  uint64_t sl = dh & a.d_mask;
+__device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64_t doc) {
+  // worddocumentcount: first occurrence of (doc, word) in the global dedupe
+  // table.  The entry is the exact pair -- (launch-local document + 1) << 40 |
+  // the word's table slot g (one slot per distinct word) -- so no two pairs
+  // share an entry; the hash only picks where to probe.
+  const uint64_t dh = ((doc + 1) << 40) | g;
+  uint64_t sl = wc_mix(dh, 0x5151, 0) & a.d_mask;
   for (uint64_t probe = 0; probe <= a.d_mask; ++probe) {
     const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], 0ull, (unsigned long long)dh);
     if (prev == 0ull) return true;
@@ -1011,9 +1014,8 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
         sl = (sl + 1) & (WC_LDS - 1);
       }
       if (where < 0) {  // LDS table full: global path
-        if (a.wdc && !wc_doc_first(a, h, d)) continue;
         const uint64_t g = wc_global_insert(a, h, key, tl, b0 + s);
-        if (g != ~0ull) atomicAdd(&a.t_cnt[g], 1ull);
+        if (g != ~0ull && (!a.wdc || wc_doc_first(a, g, d))) atomicAdd(&a.t_cnt[g], 1ull);
       }
     }
     }
@@ -1024,9 +1026,8 @@ __global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
     if (h == 0ull) continue;
     // worddocumentcount: other tiles of the document may hold the word too;
     // the (document, word) dedupe table admits one of them
-    if (a.wdc && !wc_doc_first(a, h, d)) continue;
     const uint64_t g = wc_global_insert(a, h, key, (uint32_t)(lpos[i] & 0xFFFFu), lpos[i] >> 16);
-    if (g != ~0ull) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
+    if (g != ~0ull && (!a.wdc || wc_doc_first(a, g, d))) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
   }
 }
 
@@ -1158,6 +1159,50 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st) {
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st) {
   const uint64_t n = a.t_mask + 1;
   hipLaunchKernelGGL(wc_persist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, arena, top);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// Merge (word, count) pairs into the table (ccrdt_wc_merge: the map union
+// with counts added, e.g. from_binary/1 or a shard's histogram): one thread
+// per word, the word's hash as the tokenizer computes it; pass 2 (verify)
+// byte-compares every word with its slot's representative.
+__global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt,
+                                uint64_t n, int verify) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = woff[i], e = woff[i + 1];
+  const uint32_t len = (uint32_t)(e - s), key = (uint32_t)wkey[i];
+  uint64_t f = 0xCBF29CE484222325ull;
+  for (uint64_t j = s; j < e; ++j) f = (f ^ a.bytes[j]) * 0x100000001B3ull;
+  const uint64_t h = wc_mix(f, key, len);
+  if (!verify) {
+    const uint64_t g = wc_global_insert(a, h, key, len, s);
+    if (g != ~0ull) {
+      const unsigned long long c = (unsigned long long)cnt[i];
+      const unsigned long long o = atomicAdd(&a.t_cnt[g], c);
+      if (o + c > 0x7FFFFFFFFFFFFFFFull) atomicOr(&a.status[1], 4u);  // leaves int64
+    }
+    return;
+  }
+  uint64_t sl = h & a.t_mask;
+  for (uint64_t probe = 0; probe <= a.t_mask && a.t_hash[sl] != h && a.t_hash[sl] != 0ull; ++probe)
+    sl = (sl + 1) & a.t_mask;
+  if (a.t_hash[sl] != h) {
+    atomicOr(&a.status[1], 2u);
+    return;
+  }
+  const uint8_t* rep = a.t_arena[sl] != ~0ull ? a.arena + a.t_arena[sl] : a.bytes + a.t_pos[sl];
+  bool eq = a.t_key[sl] == key && a.t_len[sl] == len;
+  for (uint32_t j = 0; eq && j < len; ++j) eq = rep[j] == a.bytes[s + j];
+  if (!eq) atomicOr(&a.status[1], 1u);
+}
+
+int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
+                    int verify, hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, wkey, woff, cnt,
+                     n, verify);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

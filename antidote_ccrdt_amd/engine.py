@@ -108,6 +108,23 @@ class TrmvState:
         return [f.name for f in fields(self)
                 if not np.array_equal(getattr(self, f.name), getattr(other, f.name))]
 
+    def slice(self, k0: int, k1: int) -> "TrmvState":
+        """The image of keys [k0, k1) alone (offsets rebased), as
+        ccrdt_trmv_export_range lays it out."""
+        def seg(ptr_name, names):
+            p = getattr(self, ptr_name).astype(np.int64)
+            a, b = int(p[k0]), int(p[k1])
+            out = {ptr_name: (p[k0:k1 + 1] - a).astype(np.uint64)}
+            out.update({n: getattr(self, n)[a:b].copy() for n in names})
+            return out
+        d = {"vc": self.vc[k0:k1].copy()}
+        d.update(seg("obs_ptr", ("obs_id", "obs_score", "obs_dc", "obs_ts")))
+        d.update(seg("m_ptr", ("m_id", "m_score", "m_dc", "m_ts")))
+        d.update(seg("r_ptr", ("r_id", "r_vc")))
+        for n in ("min_valid", "min_id", "min_score", "min_dc", "min_ts"):
+            d[n] = getattr(self, n)[k0:k1].copy()
+        return TrmvState(**d)
+
     def key_state(self, k: int) -> dict:
         """One key as plain Python (for debugging and the behaviour mirror)."""
         o0, o1 = int(self.obs_ptr[k]), int(self.obs_ptr[k + 1])
@@ -254,18 +271,27 @@ class TopkRmvEngine(_Engine):
         if b.rmv_vc.ndim != 2 or (b.rmv_vc.shape[0] and b.rmv_vc.shape[1] != self.n_dc):
             raise ValueError("rmv_vc must be [n_rmv, n_dc]")
         ops = self._ops(b)
-        if not want_extra:
-            check(lib.ccrdt_trmv_apply(self.h, C.byref(ops), None), "trmv_apply")
-            return None
-        n = b.n_ops
-        x = TrmvExtra(np.empty(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64),
-                      np.zeros(n, np.uint8), np.zeros(n, np.int64), np.zeros((n, self.n_dc), np.int64))
-        cx = _lib.TrmvExtra(ptr(x.kind), ptr(x.id), ptr(x.score), ptr(x.dc), ptr(x.ts), ptr(x.vc))
-        check(lib.ccrdt_trmv_apply(self.h, C.byref(ops), C.byref(cx)), "trmv_apply")
+        x = cx = None
+        if want_extra:
+            n = b.n_ops
+            x = TrmvExtra(np.empty(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64),
+                          np.zeros(n, np.uint8), np.zeros(n, np.int64),
+                          np.zeros((n, self.n_dc), np.int64))
+            cx = C.byref(_lib.TrmvExtra(ptr(x.kind), ptr(x.id), ptr(x.score), ptr(x.dc), ptr(x.ts),
+                                        ptr(x.vc)))
+        self._checked(lib.ccrdt_trmv_apply(self.h, C.byref(ops), cx), "trmv_apply", x)
         return x
 
     def apply_device(self, db: DeviceTrmvBatch) -> None:
-        check(lib.ccrdt_trmv_apply_device(self.h, C.byref(db.c)), "trmv_apply_device")
+        self._checked(lib.ccrdt_trmv_apply_device(self.h, C.byref(db.c)), "trmv_apply_device")
+
+    def _checked(self, rc: int, where: str, extra=None) -> None:
+        """check(), with the over-capacity keys attached to KeyCapacityError."""
+        try:
+            check(rc, where)
+        except _lib.KeyCapacityError as err:
+            err.keys, err.extra = self.handed_on(2), extra
+            raise
 
     def extra_count(self) -> int:
         n = C.c_int64()
@@ -305,6 +331,27 @@ class TopkRmvEngine(_Engine):
         """from_binary/1 analogue (topk_rmv.erl:161-163)."""
         cs = st.as_c()
         check(lib.ccrdt_trmv_import(self.h, C.byref(cs)), "trmv_import")
+
+    def export_range(self, k0: int, k1: int) -> TrmvState:
+        """Canonical image of keys [k0, k1) only (downloads just their segments)."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        check(lib.ccrdt_trmv_range_sizes(self.h, k0, k1, C.byref(a), C.byref(b), C.byref(c)),
+              "range_sizes")
+        st = TrmvState.empty(k1 - k0, self.n_dc, a.value, b.value, c.value)
+        cs = st.as_c()
+        check(lib.ccrdt_trmv_export_range(self.h, k0, k1, C.byref(cs)), "trmv_export_range")
+        return st
+
+    def import_range(self, k0: int, k1: int, st: TrmvState) -> None:
+        """Keys [k0, k1) take the image `st` (laid out for k1 - k0 keys)."""
+        cs = st.as_c()
+        check(lib.ccrdt_trmv_import_range(self.h, k0, k1, C.byref(cs)), "trmv_import_range")
+
+    def value(self, key: int) -> list[tuple[int, int]]:
+        """value/1 of one key (topk_rmv.erl:91-95): [(Id, Score)] of Observed,
+        sorted by Id (the reference's list order is map-iteration order, Q7)."""
+        st = self.export_range(key, key + 1)
+        return [(int(i), int(s)) for i, s in zip(st.obs_id, st.obs_score)]
 
     def downstream(self, key, op, id, score, dc, ts):
         """downstream/2 probes (topk_rmv.erl:102-124).  op 0 add, 1 rmv.

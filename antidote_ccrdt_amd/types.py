@@ -236,6 +236,23 @@ class WordcountEngine(_Engine):
         check(lib.ccrdt_wc_export(self.h, ptr(kp), ptr(wo), ptr(wb), ptr(cnt)), "wc_export")
         return kp, wo, wb[:nb], cnt
 
+    def _words(self, fn, key_ptr, word_off, word_bytes, count, where):
+        kp, wo = _c(key_ptr, np.uint64), _c(word_off, np.uint64)
+        wb = (np.frombuffer(word_bytes, np.uint8) if isinstance(word_bytes, (bytes, bytearray))
+              else _c(word_bytes, np.uint8))
+        cnt = _c(count, np.int64)
+        check(fn(self.h, int(cnt.shape[0]), ptr(kp), ptr(wo), ptr(wb) if wb.shape[0] else None,
+                 ptr(cnt)), where)
+
+    def merge(self, key_ptr, word_off, word_bytes, count) -> None:
+        """Add word -> count pairs (the layout of export()) into the maps: the
+        merge step of a key-sharded histogram (ccrdt_wc_merge)."""
+        self._words(lib.ccrdt_wc_merge, key_ptr, word_off, word_bytes, count, "wc_merge")
+
+    def import_state(self, key_ptr, word_off, word_bytes, count) -> None:
+        """from_binary/1 analogue: the maps := the given words and counts."""
+        self._words(lib.ccrdt_wc_import, key_ptr, word_off, word_bytes, count, "wc_import")
+
     def value(self, k: int = 0) -> dict[bytes, int]:
         """value/1 of key k: the map word -> count."""
         kp, wo, wb, cnt = self.export()

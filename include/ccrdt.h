@@ -42,6 +42,12 @@ extern "C" {
 #define CCRDT_ENOMEM 3  /* device or per-key capacity exhausted */
 #define CCRDT_EDEVICE 4 /* HIP / RCCL failure */
 #define CCRDT_ENOSYS 5  /* operation not supported for this type */
+#define CCRDT_EKEYCAP 6 /* topk_rmv: the batch COMMITTED except for the keys
+                           that would exceed the per-key capacity (1024
+                           players, 65535 Masked elements, 65534 Removals
+                           rows); those keep their previous state, produce no
+                           extras, and are listed by ccrdt_engine_handed_on(e,
+                           2).  Their ops go to the host (Erlang) path. */
 
 /* Registry: antidote_ccrdt:?CCRDTS (src/antidote_ccrdt.erl:28-35). */
 #define CCRDT_AVERAGE 0
@@ -200,11 +206,21 @@ typedef struct {
 
 /* Totals for sizing a ccrdt_trmv_state. */
 int ccrdt_trmv_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows);
+/* The same for keys [k0, k1) only. */
+int ccrdt_trmv_range_sizes(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_obs, int64_t* n_masked,
+                           int64_t* n_rows);
 /* Per-key counts of the resident state (players, Masked elements, Removals
  * rows, |Observed|); any output may be NULL.  For bench.py's byte accounting. */
 int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* nr, uint32_t* nobs);
 /* to_binary/1 analogue (topk_rmv.erl:156-158): canonical image of every key. */
 int ccrdt_trmv_export(ccrdt_engine* e, ccrdt_trmv_state* out);
+/* The canonical image of keys [k0, k1) only (value/1, to_binary/1 of a few
+ * keys): downloads just their segments.  `out` is laid out as for an engine of
+ * k1 - k0 keys (ptr arrays [k1-k0+1], vc / min arrays [k1-k0]). */
+int ccrdt_trmv_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, ccrdt_trmv_state* out);
+/* from_binary/1 of keys [k0, k1): those keys take the given image (laid out
+ * as for an engine of k1 - k0 keys); the other keys keep their state. */
+int ccrdt_trmv_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const ccrdt_trmv_state* in);
 /* from_binary/1 analogue (topk_rmv.erl:161-163).  Arrays as in export
  * (sorting not required); invariants of the reference are checked. */
 int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in);
@@ -326,6 +342,19 @@ int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes);
  * over word_bytes. */
 int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint8_t* word_bytes,
                     int64_t* count);
+/* Merge word -> count pairs into the resident maps (host arrays, CSR by key:
+ * key_ptr[n_keys+1] over words, word_off[n_words+1] over bytes): count is
+ * added to the word's entry, created if absent.  The map union with summed
+ * counts -- how a key-sharded histogram is merged after the all-to-all by word
+ * owner; every word is byte-compared with its table entry
+ * (ERANGE on a 64-bit hash collision). */
+int ccrdt_wc_merge(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                   const uint8_t* bytes, const int64_t* count);
+/* from_binary/1 analogue (wordcount.erl:59-63, worddocumentcount.erl:59-63):
+ * every key's map := the given words and counts (the layout of
+ * ccrdt_wc_export), without replaying any text. */
+int ccrdt_wc_import(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                    const uint8_t* bytes, const int64_t* count);
 
 #ifdef __cplusplus
 }

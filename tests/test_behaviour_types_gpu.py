@@ -126,6 +126,18 @@ def test_wordcount_empty_tokens_roundtrip(gpu):
         assert W.from_binary(W.to_binary(st))[1].to_term() == want
 
 
+def test_wordcount_from_binary_large_counts(gpu):
+    """from_binary/1 of maps whose counts no text replay could reach: the map
+    is imported as (word, count) pairs (ccrdt_wc_import)."""
+    for W in (bh.wordcount, bh.worddocumentcount):
+        m = {b"x": 10**8, b"": 2**40, b"long" * 1000: 3}
+        st = W.from_binary(etf.term_to_binary(m))[1]
+        assert W.value(st) == m
+        st2 = W.update(("add", b"x y"), st)[1]
+        assert W.value(st2) == {**m, b"x": 10**8 + 1, b"y": 1}
+        assert W.value(st) == m  # update/2 is functional
+
+
 def test_topk_rmv_etf_roundtrip(gpu, monkeypatch):
     names = ("dc1", "dc2", "dc3")
     monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry(names))
@@ -144,3 +156,22 @@ def test_topk_rmv_etf_roundtrip(gpu, monkeypatch):
     empty = trmv.new(5)
     assert etf.binary_to_term(trmv.to_binary(empty))[4] == (etf.Atom("nil"),) * 3
     assert trmv.from_binary(trmv.to_binary(empty))[1].to_term() == empty.to_term()
+
+
+def test_topk_rmv_tuple_dcids(gpu, monkeypatch):
+    """antidote DcIds are {Node, {Mega, Sec, Micro}} tuples: to_binary writes
+    them as such (atoms inside), from_binary looks the decoded term up in the
+    registry, and a DcId the registry lacks is an EtfError."""
+    d1, d2 = ("n1@h", (1, 2, 3)), ("n2@h", (1, 2, 4))
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry((d1, d2)))
+    t = trmv.new(3)
+    for e in [("add", (1, 10, (d2, 5))), ("add", (2, 9, (d1, 4))), ("rmv", (2, {d1: 4}))]:
+        t = trmv.update(e, t)[1]
+    b = trmv.to_binary(t)
+    vc = etf.binary_to_term(b)[3]
+    assert set(vc) == {d1, d2} and all(isinstance(k[0], etf.Atom) for k in vc)
+    ok, t2 = trmv.from_binary(b)
+    assert ok == "ok" and t2.to_term() == t.to_term()
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry((d1,)))
+    with pytest.raises(etf.EtfError):
+        trmv.from_binary(b)
