@@ -155,6 +155,7 @@ SIGNATURES = {
     "ccrdt_wc_apply_device": (INT, [P, C.POINTER(WcDocs)]),
     "ccrdt_wc_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_wc_export": (INT, [P, P, P, P, P]),
+    "ccrdt_wc_owner": (INT, [I64, I64, P, P, P, INT, P]),
     "ccrdt_wc_merge": (INT, [P, I64, P, P, P, P]),
     "ccrdt_wc_import": (INT, [P, I64, P, P, P, P]),
     # ccrdt_gen.h

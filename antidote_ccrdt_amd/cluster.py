@@ -184,3 +184,319 @@ class ShardedTopkRmv:
 
     def export(self):
         return self.engine.export()
+
+
+def all_reduce_sum(v: int) -> int:
+    import torch
+    dist = _dist()
+    if dist is None:
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=_device_for(dist))
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+# ------------------------------------------------------- replication mode
+# Each rank is one DC replica holding the whole keyspace (SURVEY §8(e),
+# BASELINE configs[3]).  A step: every rank applies the effects it originates
+# (update/2 at the origin, src/antidote_ccrdt_leaderboard.erl:128-134,
+# src/antidote_ccrdt_topk_rmv.erl:140-148) and keeps the extra effects that
+# returns (:282-284; topk_rmv :236,294) as effects it originates too; the
+# effect rows of all ranks are all-gathered, and every rank applies the
+# effects of the OTHER origins in canonical order -- by key, then origin
+# rank, then the origin's sequence number.  Applying remote effects can
+# return extras again; they go out in the next round, until a round gathers
+# nothing.  Rows are int64: origin, seq, key, then the effect's fields.
+
+@dataclass
+class _TrmvCodec:
+    """topk_rmv effects as rows: origin, seq, key, kind, id, score, dc, ts, vc[n_dc]."""
+    n_keys: int
+    n_dc: int
+    COLS = 8
+
+    def rows_of_batch(self, b: TrmvBatch) -> np.ndarray:
+        kp = np.asarray(b.key_ptr, np.int64)
+        n = b.n_ops
+        r = np.zeros((n, self.COLS + self.n_dc), np.int64)
+        r[:, 2] = np.repeat(np.arange(self.n_keys, dtype=np.int64), np.diff(kp))
+        r[:, 3], r[:, 4], r[:, 5], r[:, 6] = b.kind, b.id, b.score, b.dc
+        rm = np.asarray(b.kind) >= 2
+        r[~rm, 7] = np.asarray(b.ts)[~rm]
+        if rm.any():
+            r[rm, self.COLS:] = np.asarray(b.rmv_vc)[np.asarray(b.ts)[rm]]
+        return r
+
+    def batch_of_rows(self, r: np.ndarray) -> TrmvBatch:
+        kp = np.zeros(self.n_keys + 1, np.uint64)
+        kp[1:] = np.cumsum(np.bincount(r[:, 2], minlength=self.n_keys))
+        kind = r[:, 3].astype(np.uint8)
+        rm = kind >= 2
+        ts = r[:, 7].copy()
+        ts[rm] = np.arange(int(rm.sum()), dtype=np.int64)
+        vc = np.ascontiguousarray(r[rm, self.COLS:], dtype=np.int64).reshape(-1, self.n_dc)
+        return TrmvBatch(kp, kind, r[:, 4].copy(), r[:, 5].copy(), r[:, 6].astype(np.uint8), ts, vc)
+
+    def apply(self, engine, r: np.ndarray) -> np.ndarray:
+        """Apply rows (already in canonical order); the extras as rows
+        (origin/seq left for the caller)."""
+        b = self.batch_of_rows(r)
+        x = engine.apply(b, want_extra=True)
+        if isinstance(x, dict):
+            x = TrmvExtra(**x)
+        sel = np.nonzero(x.kind != 255)[0]
+        out = np.zeros((sel.shape[0], self.COLS + self.n_dc), np.int64)
+        out[:, 2] = r[sel, 2]
+        out[:, 3] = x.kind[sel]  # CCRDT_TRMV_ADD (0) or CCRDT_TRMV_RMV (2): effects as they are
+        out[:, 4], out[:, 5], out[:, 6] = x.id[sel], x.score[sel], x.dc[sel]
+        out[:, 7] = np.where(x.kind[sel] == 0, x.ts[sel], 0)
+        out[:, self.COLS:] = np.where((x.kind[sel] == 2)[:, None], x.vc[sel], 0)
+        return out
+
+
+@dataclass
+class _LbCodec:
+    """leaderboard effects as rows: origin, seq, key, kind, id, score."""
+    n_keys: int
+    COLS = 6
+
+    def rows_of_batch(self, b) -> np.ndarray:
+        kp, kind, id_, score = b
+        kp = np.asarray(kp, np.int64)
+        r = np.zeros((int(kp[-1]), self.COLS), np.int64)
+        r[:, 2] = np.repeat(np.arange(self.n_keys, dtype=np.int64), np.diff(kp))
+        r[:, 3], r[:, 4], r[:, 5] = kind, id_, score
+        return r
+
+    def apply(self, engine, r: np.ndarray) -> np.ndarray:
+        kp = np.zeros(self.n_keys + 1, np.uint64)
+        kp[1:] = np.cumsum(np.bincount(r[:, 2], minlength=self.n_keys))
+        x = engine.apply(kp, r[:, 3].astype(np.uint8), r[:, 4].copy(), r[:, 5].copy())
+        sel = np.nonzero(np.asarray(x["kind"]) != 255)[0]
+        out = np.zeros((sel.shape[0], self.COLS), np.int64)
+        out[:, 2] = r[sel, 2]
+        out[:, 3] = np.asarray(x["kind"])[sel]  # 0: {add, {Id, Score}} (leaderboard.erl:282-284)
+        out[:, 4], out[:, 5] = np.asarray(x["id"])[sel], np.asarray(x["score"])[sel]
+        return out
+
+
+def canonical(rows: np.ndarray) -> np.ndarray:
+    """Rows sorted by (key, origin, seq)."""
+    return rows[np.lexsort((rows[:, 1], rows[:, 0], rows[:, 2]))] if rows.shape[0] else rows
+
+
+class _Replica:
+    def __init__(self, codec, engine, rank, world):
+        self.codec, self.engine, self.rank, self.world = codec, engine, rank, world
+        self.seq = 0
+
+    def _stamp(self, r: np.ndarray) -> np.ndarray:
+        r[:, 0] = self.rank
+        r[:, 1] = self.seq + np.arange(r.shape[0], dtype=np.int64)
+        self.seq += r.shape[0]
+        return r
+
+    def originate(self, batch) -> np.ndarray:
+        """Apply this replica's own effects (CSR batch over all keys, stream
+        order per key); returns them plus the extras they produced, as the
+        rows this replica sends."""
+        own = self._stamp(self.codec.rows_of_batch(batch))
+        ex = self.codec.apply(self.engine, own) if own.shape[0] else own[:0]
+        return np.concatenate([own, self._stamp(ex)])
+
+    def deliver(self, gathered: np.ndarray) -> np.ndarray:
+        """Apply every other origin's rows in canonical order; returns the
+        extras that produced, stamped as this replica's effects."""
+        r = canonical(gathered[gathered[:, 0] != self.rank])
+        if not r.shape[0]:
+            return r
+        return self._stamp(self.codec.apply(self.engine, r))
+
+    def step(self, batch, max_rounds: int = 64) -> int:
+        """One replication step over torch.distributed (all_gather_rows);
+        returns the number of delivery rounds."""
+        out = self.originate(batch)
+        for rounds in range(max_rounds):
+            allr = all_gather_rows(out)
+            if not allr.shape[0]:
+                return rounds
+            out = self.deliver(allr)
+        raise RuntimeError("replication did not quiesce")
+
+    def export(self):
+        return self.engine.export()
+
+
+class ReplicatedTopkRmv(_Replica):
+    """This rank's DC replica of an n_keys topk_rmv keyspace."""
+
+    def __init__(self, n_keys: int, k: int = 100, n_dc: int = 8, rank: int | None = None,
+                 world: int | None = None, engine=None, device: int = 0):
+        dist = _dist()
+        rank = rank if rank is not None else (dist.get_rank() if dist else 0)
+        world = world if world is not None else (dist.get_world_size() if dist else 1)
+        if engine is None:
+            from .engine import TopkRmvEngine
+            engine = TopkRmvEngine(n_keys, k, n_dc, device=device)
+        super().__init__(_TrmvCodec(n_keys, n_dc), engine, rank, world)
+
+
+class ReplicatedLeaderboard(_Replica):
+    """This rank's DC replica of n_keys leaderboards."""
+
+    def __init__(self, n_keys: int, k: int = 100, rank: int | None = None,
+                 world: int | None = None, engine=None, device: int = 0):
+        dist = _dist()
+        rank = rank if rank is not None else (dist.get_rank() if dist else 0)
+        world = world if world is not None else (dist.get_world_size() if dist else 1)
+        if engine is None:
+            from .types import LeaderboardEngine
+            engine = LeaderboardEngine(n_keys, k, device=device)
+        super().__init__(_LbCodec(n_keys), engine, rank, world)
+
+
+def replicate_local(replicas, batches, max_rounds: int = 64) -> int:
+    """The replication step of `replicas` (one process, e.g. several engines
+    on one GPU), exchanging rows by concatenation instead of all_gather."""
+    outs = [r.originate(b) for r, b in zip(replicas, batches)]
+    for rounds in range(max_rounds):
+        allr = np.concatenate(outs)
+        if not allr.shape[0]:
+            return rounds
+        outs = [r.deliver(allr) for r in replicas]
+    raise RuntimeError("replication did not quiesce")
+
+
+# ------------------------------------------- key-sharded word histogram
+def word_owner(kp, wo, wb, world: int) -> np.ndarray:
+    """Owner rank of every word of an export()-layout word list
+    (ccrdt_wc_owner: a function of (key, bytes) alone)."""
+    from . import _lib
+    kp, wo = np.ascontiguousarray(kp, np.uint64), np.ascontiguousarray(wo, np.uint64)
+    wb = np.ascontiguousarray(np.frombuffer(wb, np.uint8) if isinstance(wb, (bytes, bytearray)) else wb,
+                              np.uint8)
+    n = int(kp[-1])
+    out = np.zeros(n, np.int32)
+    _lib.check(_lib.lib.ccrdt_wc_owner(kp.shape[0] - 1, n, _lib.ptr(kp), _lib.ptr(wo),
+                                       _lib.ptr(wb) if wb.shape[0] else None, world, _lib.ptr(out)),
+               "wc_owner")
+    return out
+
+
+def _gather_bytes(wb: np.ndarray, starts: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """Concatenation of the byte ranges [starts[i], starts[i] + lens[i])."""
+    tot = int(lens.sum())
+    if not tot:
+        return np.zeros(0, np.uint8)
+    dst0 = np.zeros(lens.shape[0], np.int64)
+    np.cumsum(lens[:-1], out=dst0[1:])
+    idx = np.arange(tot, dtype=np.int64) + np.repeat(starts - dst0, lens)
+    return wb[idx]
+
+
+def all_to_all_v(send: np.ndarray, splits: list[int]) -> tuple[np.ndarray, list[int]]:
+    """Variable all-to-all of a 1-D array (RCCL all_to_all_single on the GPU
+    node, gloo on the host): rank r receives the slice `splits[r]` of every
+    rank's `send`, concatenated in rank order.  Returns (received, sizes)."""
+    import torch
+    dist = _dist()
+    if dist is None:
+        return send, splits
+    dev = _device_for(dist)
+    world = dist.get_world_size()
+    sz = torch.tensor(splits, dtype=torch.int64, device=dev)
+    rsz = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rsz, sz)
+    rsplits = [int(v) for v in rsz.cpu()]
+    t = torch.from_numpy(np.ascontiguousarray(send)).to(dev)
+    out = torch.empty(sum(rsplits), dtype=t.dtype, device=dev)
+    dist.all_to_all_single(out, t, rsplits, list(splits))
+    return out.cpu().numpy(), rsplits
+
+
+class ShardedWordcount:
+    """wordcount / worddocumentcount over the GPUs of a node (SURVEY §8(e),
+    BASELINE configs[4]): every rank tokenises and histograms its own share of
+    the documents (src/antidote_ccrdt_wordcount.erl:76-85,
+    src/antidote_ccrdt_worddocumentcount.erl:76-86), then each word goes to its
+    owner rank, word_owner(key, bytes), by one variable all-to-all, and the
+    owner adds it into its maps (ccrdt_wc_merge).  Rank r ends up holding the
+    words it owns of every key; the union over the ranks is the map of all
+    the documents.  A document lives on one rank, so worddocumentcount's
+    per-document counts add across ranks too."""
+
+    def __init__(self, n_keys: int = 1, wdc: bool = False, rank: int | None = None,
+                 world: int | None = None, local_factory=None, owned=None, device: int = 0):
+        dist = _dist()
+        self.rank = rank if rank is not None else (dist.get_rank() if dist else 0)
+        self.world = world if world is not None else (dist.get_world_size() if dist else 1)
+        self.n_keys = n_keys
+        from .types import WordcountEngine, WordDocumentCountEngine
+        E = WordDocumentCountEngine if wdc else WordcountEngine
+        self.local_factory = local_factory or (lambda: E(n_keys, device=device))
+        self.owned = owned if owned is not None else E(n_keys, device=device)
+        self.local = self.local_factory()
+
+    def apply(self, key_ptr, doc_off, data) -> None:
+        """Histogram this rank's documents (CSR by key, as ccrdt_wc_apply)."""
+        self.local.apply(key_ptr, doc_off, data)
+
+    def partition(self):
+        """The local histogram cut by owner: (send_meta [n, 3] = key, length,
+        count in destination order, send_bytes, per-rank word counts)."""
+        kp, wo, wb, cnt = self.local.export()
+        kp, wo = np.asarray(kp, np.int64), np.asarray(wo, np.int64)
+        n = int(kp[-1])
+        own = word_owner(kp, wo, wb, self.world) if n else np.zeros(0, np.int32)
+        perm = np.argsort(own, kind="stable")
+        keys = np.repeat(np.arange(self.n_keys, dtype=np.int64), np.diff(kp))
+        lens = np.diff(wo)
+        meta = np.stack([keys[perm], lens[perm], np.asarray(cnt, np.int64)[perm]], axis=1)
+        data = _gather_bytes(np.asarray(wb, np.uint8), wo[:-1][perm], lens[perm])
+        per_rank = np.bincount(own, minlength=self.world)
+        return meta, data, per_rank, lens[perm]
+
+    def exchange(self, a2a=all_to_all_v) -> None:
+        """Send every local word to its owner and merge what arrives; the
+        local histogram starts over."""
+        meta, data, per_rank, lens = self.partition()
+        bsplit = [int(lens[o0:o1].sum()) for o0, o1 in
+                  zip(np.r_[0, np.cumsum(per_rank)[:-1]], np.cumsum(per_rank))]
+        rmeta, _ = a2a(meta.reshape(-1), [int(c) * 3 for c in per_rank])
+        rdata, _ = a2a(data, bsplit)
+        self.merge_received(rmeta.reshape(-1, 3), rdata)
+        self.local = self.local_factory()
+
+    def merge_received(self, meta: np.ndarray, data: np.ndarray) -> None:
+        if not meta.shape[0]:
+            return
+        lens = meta[:, 1]
+        starts = np.zeros(lens.shape[0], np.int64)
+        np.cumsum(lens[:-1], out=starts[1:])
+        order = np.argsort(meta[:, 0], kind="stable")  # CSR by key
+        kp = np.zeros(self.n_keys + 1, np.uint64)
+        kp[1:] = np.cumsum(np.bincount(meta[:, 0], minlength=self.n_keys))
+        wo = np.zeros(meta.shape[0] + 1, np.uint64)
+        wo[1:] = np.cumsum(lens[order])
+        self.owned.merge(kp, wo, _gather_bytes(np.asarray(data, np.uint8), starts[order], lens[order]),
+                         meta[order, 2])
+
+    def export(self):
+        return self.owned.export()
+
+
+def exchange_local(shards: list[ShardedWordcount]) -> None:
+    """ShardedWordcount.exchange for several shards held by one process (the
+    all-to-all done by slicing)."""
+    parts = [s.partition() for s in shards]
+    for dst, s in enumerate(shards):
+        metas, datas = [], []
+        for meta, data, per_rank, lens in parts:
+            w0 = int(per_rank[:dst].sum())
+            w1 = w0 + int(per_rank[dst])
+            b0 = int(lens[:w0].sum())
+            metas.append(meta[w0:w1])
+            datas.append(data[b0:b0 + int(lens[w0:w1].sum())])
+        s.merge_received(np.concatenate(metas), np.concatenate(datas))
+    for s in shards:
+        s.local = s.local_factory()

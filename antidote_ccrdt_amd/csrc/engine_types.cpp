@@ -1126,6 +1126,37 @@ static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_
   return CCRDT_OK;
 }
 
+static uint64_t owner_mix(uint64_t z) {  // splitmix64 (cluster.splitmix64)
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+int ccrdt_wc_owner(int64_t n_keys, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                   const uint8_t* bytes, int world, int32_t* owner) {
+  if (n_keys < 0 || n_words < 0 || world < 1 || !key_ptr || (n_words && (!word_off || !owner))) {
+    set_error("wc_owner: bad arguments");
+    return CCRDT_EINVAL;
+  }
+  if (key_ptr[0] != 0 || key_ptr[n_keys] != (uint64_t)n_words) {
+    set_error("wc_owner: key_ptr must run from 0 to n_words");
+    return CCRDT_EINVAL;
+  }
+  for (int64_t k = 0; k < n_keys; ++k) {
+    if (key_ptr[k + 1] < key_ptr[k]) {
+      set_error("wc_owner: key_ptr not monotone");
+      return CCRDT_EINVAL;
+    }
+    for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i) {
+      uint64_t f = 0xCBF29CE484222325ull;
+      for (uint64_t j = word_off[i]; j < word_off[i + 1]; ++j) f = (f ^ bytes[j]) * 0x100000001B3ull;
+      owner[i] = (int32_t)(owner_mix(f ^ ((uint64_t)k * 0x9E3779B97F4A7C15ull)) % (uint64_t)world);
+    }
+  }
+  return CCRDT_OK;
+}
+
 int ccrdt_wc_merge(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
                    const uint8_t* bytes, const int64_t* count) {
   CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));

@@ -342,6 +342,14 @@ int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes);
  * over word_bytes. */
 int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint8_t* word_bytes,
                     int64_t* count);
+/* Owner rank of every word of a CSR word list (the layout of ccrdt_wc_export):
+ * splitmix64(FNV-1a64(bytes) ^ key * 0x9E3779B97F4A7C15) mod world.  The
+ * key-sharded word histogram of the multi-GPU wordcount sends
+ * each word to this rank, which merges it (ccrdt_wc_merge).  Host-only; no
+ * engine needed. */
+int ccrdt_wc_owner(int64_t n_keys, int64_t n_words, const uint64_t* key_ptr, const uint64_t* word_off,
+                   const uint8_t* bytes, int world, int32_t* owner);
+
 /* Merge word -> count pairs into the resident maps (host arrays, CSR by key:
  * key_ptr[n_keys+1] over words, word_off[n_words+1] over bytes): count is
  * added to the word's entry, created if absent.  The map union with summed
