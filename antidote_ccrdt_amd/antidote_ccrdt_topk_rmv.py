@@ -33,6 +33,11 @@ class TopkRmv:
     def __init__(self, size: int, engine: TopkRmvEngine):
         self.size = size
         self.engine = engine
+        terms.DC_REGISTRY.watch(self)
+
+    def rerank(self, perm) -> None:
+        """A DC joined ahead of existing ones (terms.DcRegistry)."""
+        self.engine.permute_dcs(perm)
 
     def _export(self) -> dict:
         return self.engine.export().key_state(0)

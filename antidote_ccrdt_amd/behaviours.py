@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import etf
+from . import etf, terms
 from ._lib import NOOP
 from .antidote_ccrdt_topk_rmv import FunctionClause
 from .types import (AverageEngine, LbState, LeaderboardEngine, TopkEngine, WordcountEngine,
@@ -152,19 +152,30 @@ class average:
 
 # ======================================================================== topk
 class Topk:
-    """topk() = {#{Id => Score}, Size} (topk.erl:52), one key in HBM."""
+    """topk() = {#{Id => Score}, Size} (topk.erl:52), one key in HBM.  Ids
+    are any Erlang terms, held on the GPU as term-order codes (`ids`,
+    terms.TermInterner, shared by the states one update chain produces)."""
 
-    def __init__(self, eng: TopkEngine, size: int):
-        self.engine, self.size = eng, size
+    def __init__(self, eng: TopkEngine, size: int, ids: terms.TermInterner):
+        self.engine, self.size, self.ids = eng, size, ids
+        ids.watch(self)
+
+    def recode(self, mapping: dict) -> None:
+        """The interner re-spaced its codes: re-code this state's Ids."""
+        p, i, s = self.engine.export()
+        if i.shape[0]:
+            self.engine.import_state(p, np.array([mapping[int(c)] for c in i], np.int64), s)
 
     def to_term(self):
         p, i, s = self.engine.export()
-        return ({int(a): int(b) for a, b in zip(i, s)}, self.size)
+        return ({self.ids.term(a): int(b) for a, b in zip(i, s)}, self.size)
 
 
 class topk:
-    """antidote_ccrdt_topk (src/antidote_ccrdt_topk.erl).  Ids are int64
-    (other Erlang terms need the host interning of SURVEY Q17)."""
+    """antidote_ccrdt_topk (src/antidote_ccrdt_topk.erl).  Ids may be any
+    Erlang term (binaries in the reference's tests, :179-204): they are
+    interned into int64 codes that keep Erlang term order, so the GPU's
+    value/1 order is the reference's."""
 
     @staticmethod
     def new(*args) -> Topk:
@@ -175,24 +186,25 @@ class topk:
             size = args[0]
             if not (_is_int(size) and size > 0):
                 raise FunctionClause("new/1")
-            return Topk(TopkEngine(1, size), size)
+            return Topk(TopkEngine(1, size), size, terms.TermInterner())
         if len(args) == 2:
             m, size = args
             if not (_is_int(size) and size > 0 and isinstance(m, dict)):
                 return topk.new()
-            st = Topk(TopkEngine(1, size), size)
+            st = Topk(TopkEngine(1, size), size, terms.TermInterner())
             if m:
-                ids = sorted(m)
-                st.engine.import_state(_kp1(len(ids)), np.array(ids, np.int64),
-                                       np.array([m[i] for i in ids], np.int64))
+                codes = sorted((st.ids.code(i), m[i]) for i in m)
+                st.engine.import_state(_kp1(len(codes)), np.array([c for c, _ in codes], np.int64),
+                                       np.array([v for _, v in codes], np.int64))
             return st
         raise FunctionClause("new")
 
     @staticmethod
     def value(st: Topk):
-        """value/1 (:81-83): every entry, Score desc then Id desc (GPU sort)."""
+        """value/1 (:81-83): every entry, Score desc then Id desc (GPU sort of
+        the term-order codes)."""
         p, i, s = st.engine.value()
-        return [(int(a), int(b)) for a, b in zip(i, s)]
+        return [(st.ids.term(a), int(b)) for a, b in zip(i, s)]
 
     @staticmethod
     def downstream(op, st: Topk):
@@ -204,7 +216,8 @@ class topk:
 
     @staticmethod
     def update(effect, st: Topk):
-        """update/2 (:100-104): maps:put (last writer wins) / maps:merge."""
+        """update/2 (:100-104): maps:put (last writer wins) / maps:merge.
+        Functional: the new state is a device copy of the old one."""
         tag, p = effect
         if tag == "add" and isinstance(p, tuple) and len(p) == 2 and _is_int(p[1]):
             ids, scores = [p[0]], [p[1]]
@@ -212,11 +225,10 @@ class topk:
             ids, scores = list(p), [p[i] for i in p]
         else:
             raise FunctionClause("update/2")
-        if not all(_is_int(i) for i in ids):
-            raise ValueError("topk: non-integer Ids need host-side interning (SURVEY Q17)")
-        new = topk.new(st.to_term()[0], st.size)
+        codes = [st.ids.code(i) for i in ids]  # may re-code st (and its chain) first
+        new = Topk(st.engine.clone(), st.size, st.ids)
         if ids:
-            new.engine.apply(_kp1(len(ids)), ids, scores)
+            new.engine.apply(_kp1(len(ids)), codes, scores)
         return ("ok", new)
 
     @staticmethod

@@ -62,6 +62,33 @@ static int d2h(std::vector<T>& v, const DevBuf& d, uint64_t n, hipStream_t st) {
   return CCRDT_OK;
 }
 
+template <class T>
+static int d2h_at(std::vector<T>& v, const DevBuf& d, uint64_t at, uint64_t n, hipStream_t st) {
+  v.resize(n);
+  if (n) {
+    CCRDT_HIP(hipMemcpyAsync(v.data(), (const T*)d.p + at, n * sizeof(T), hipMemcpyDeviceToHost, st));
+    CCRDT_HIP(hipStreamSynchronize(st));
+  }
+  return CCRDT_OK;
+}
+
+// CSR splice: keys [k0, k1) of (fp, fv...) replaced by the range image (ip, iv...).
+template <class T>
+static void splice_csr(const std::vector<uint64_t>& fp, const std::vector<T>& fv, const uint64_t* ip,
+                       const T* iv, uint64_t k0, uint64_t k1, std::vector<uint64_t>& op, std::vector<T>& ov,
+                       size_t width = 1) {
+  const uint64_t nk = fp.size() - 1;
+  op.assign(nk + 1, 0);
+  ov.clear();
+  for (uint64_t k = 0; k < nk; ++k) {
+    if (k >= k0 && k < k1)
+      ov.insert(ov.end(), iv + ip[k - k0] * width, iv + ip[k - k0 + 1] * width);
+    else
+      ov.insert(ov.end(), fv.begin() + fp[k] * width, fv.begin() + fp[k + 1] * width);
+    op[k + 1] = ov.size() / width;
+  }
+}
+
 int ccrdt_engine::init_type() {
   fresh = true;
   return CCRDT_OK;
@@ -402,19 +429,36 @@ struct TopkHost {
   std::vector<uint32_t> cnt;
   std::vector<int64_t> id, score;
 };
-int topk_download(ccrdt_engine* e, TopkHost& h) {
-  const uint64_t nk = (uint64_t)e->n_keys;
+// Keys [k0, k1) only (offsets rebased to the downloaded slice).
+int topk_download(ccrdt_engine* e, TopkHost& h, uint64_t k0, uint64_t k1) {
+  const uint64_t nk = k1 - k0;
   h.cnt.assign(nk, 0);
   h.off.assign(nk + 1, 0);
   if (e->fresh || !nk) return CCRDT_OK;
   TypeBufs& T = e->tb;
   const int c = T.tcur;
-  CCRDT_TRY(d2h(h.off, T.tk_off[c], nk + 1, e->stream));
-  CCRDT_TRY(d2h(h.cnt, T.tk_cnt[c], nk, e->stream));
-  const uint64_t n = std::min(T.tk_id[c].bytes, T.tk_score[c].bytes) / 8;
-  CCRDT_TRY(d2h(h.id, T.tk_id[c], n, e->stream));
-  CCRDT_TRY(d2h(h.score, T.tk_score[c], n, e->stream));
+  CCRDT_TRY(d2h_at(h.off, T.tk_off[c], k0, nk + 1, e->stream));
+  CCRDT_TRY(d2h_at(h.cnt, T.tk_cnt[c], k0, nk, e->stream));
+  const uint64_t b = h.off[0], n = h.off[nk] - b;
+  for (uint64_t& o : h.off) o -= b;
+  CCRDT_TRY(d2h_at(h.id, T.tk_id[c], b, n, e->stream));
+  CCRDT_TRY(d2h_at(h.score, T.tk_score[c], b, n, e->stream));
   return CCRDT_OK;
+}
+void topk_export_host(const TopkHost& h, uint64_t nk, uint64_t* ptr, int64_t* id, int64_t* score) {
+  std::vector<std::pair<int64_t, int64_t>> v;
+  uint64_t p = 0;
+  ptr[0] = 0;
+  for (uint64_t k = 0; k < nk; ++k) {
+    v.clear();
+    for (uint32_t j = 0; j < h.cnt[k]; ++j) v.push_back({h.id[h.off[k] + j], h.score[h.off[k] + j]});
+    std::sort(v.begin(), v.end());
+    for (auto& [i, s] : v) {
+      id[p] = i;
+      score[p++] = s;
+    }
+    ptr[k + 1] = p;
+  }
 }
 }  // namespace
 
@@ -432,24 +476,55 @@ int ccrdt_topk_size(ccrdt_engine* e, int64_t* n_entries) {
 }
 
 int ccrdt_topk_export(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score) {
-  CCRDT_TRY(check_type(e, CCRDT_TOPK));
-  TopkHost h;
-  CCRDT_TRY(topk_download(e, h));
-  const uint64_t nk = (uint64_t)e->n_keys;
-  std::vector<std::pair<int64_t, int64_t>> v;
-  uint64_t p = 0;
-  ptr[0] = 0;
-  for (uint64_t k = 0; k < nk; ++k) {
-    v.clear();
-    for (uint32_t j = 0; j < h.cnt[k]; ++j) v.push_back({h.id[h.off[k] + j], h.score[h.off[k] + j]});
-    std::sort(v.begin(), v.end());
-    for (auto& [i, s] : v) {
-      id[p] = i;
-      score[p++] = s;
-    }
-    ptr[k + 1] = p;
+  return ccrdt_topk_export_range(e, 0, e ? e->n_keys : 0, ptr, id, score);
+}
+
+static int key_range(ccrdt_engine* e, int64_t k0, int64_t k1, const char* where) {
+  if (k0 < 0 || k1 < k0 || k1 > e->n_keys) {
+    set_error(std::string(where) + ": key range outside [0, n_keys]");
+    return CCRDT_EINVAL;
   }
   return CCRDT_OK;
+}
+
+int ccrdt_topk_range_size(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_entries) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  CCRDT_TRY(key_range(e, k0, k1, "topk_range_size"));
+  int64_t s = 0;
+  if (!e->fresh && k1 > k0) {
+    std::vector<uint32_t> cnt;
+    CCRDT_TRY(d2h_at(cnt, e->tb.tk_cnt[e->tb.tcur], (uint64_t)k0, (uint64_t)(k1 - k0), e->stream));
+    for (uint32_t c : cnt) s += c;
+  }
+  *n_entries = s;
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, uint64_t* ptr, int64_t* id,
+                            int64_t* score) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  CCRDT_TRY(key_range(e, k0, k1, "topk_export_range"));
+  TopkHost h;
+  CCRDT_TRY(topk_download(e, h, (uint64_t)k0, (uint64_t)k1));
+  topk_export_host(h, (uint64_t)(k1 - k0), ptr, id, score);
+  return CCRDT_OK;
+}
+
+int ccrdt_topk_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const uint64_t* ptr, const int64_t* id,
+                            const int64_t* score) {
+  CCRDT_TRY(check_type(e, CCRDT_TOPK));
+  CCRDT_TRY(key_range(e, k0, k1, "topk_import_range"));
+  const uint64_t nk = (uint64_t)e->n_keys;
+  int64_t n = 0;
+  CCRDT_TRY(ccrdt_topk_size(e, &n));
+  std::vector<uint64_t> fp(nk + 1), op, op2;
+  std::vector<int64_t> fi((size_t)n + 1), fs((size_t)n + 1), oi, os;
+  CCRDT_TRY(ccrdt_topk_export(e, fp.data(), fi.data(), fs.data()));
+  splice_csr(fp, fi, ptr, id, (uint64_t)k0, (uint64_t)k1, op, oi);
+  splice_csr(fp, fs, ptr, score, (uint64_t)k0, (uint64_t)k1, op2, os);
+  oi.push_back(0);
+  os.push_back(0);
+  return ccrdt_topk_import(e, op.data(), oi.data(), os.data());
 }
 
 int ccrdt_topk_import(ccrdt_engine* e, const uint64_t* ptr, const int64_t* id, const int64_t* score) {
@@ -684,25 +759,33 @@ struct LbHost {
   std::vector<int64_t> id, score;
   std::vector<uint8_t> st;
 };
-int lb_download(ccrdt_engine* e, LbHost& h) {
-  const uint64_t nk = (uint64_t)e->n_keys;
+// Keys [k0, k1) only (board offsets rebased to the downloaded slice).
+int lb_download(ccrdt_engine* e, LbHost& h, uint64_t k0, uint64_t k1) {
+  const uint64_t nk = k1 - k0;
   h.meta.assign(nk, LbMeta{0, 0, 0, 0xFFFFFFFFu});
   if (e->fresh || !nk) return CCRDT_OK;
   TypeBufs& T = e->tb;
   const int c = T.tcur;
-  CCRDT_TRY(d2h(h.meta, T.lb_meta[c], nk, e->stream));
-  const uint64_t n = std::min({T.lb_id[c].bytes / 8, T.lb_score[c].bytes / 8, T.lb_st[c].bytes});
-  CCRDT_TRY(d2h(h.id, T.lb_id[c], n, e->stream));
-  CCRDT_TRY(d2h(h.score, T.lb_score[c], n, e->stream));
-  CCRDT_TRY(d2h(h.st, T.lb_st[c], n, e->stream));
+  CCRDT_TRY(d2h_at(h.meta, T.lb_meta[c], k0, nk, e->stream));
+  uint64_t b = ~0ull, t = 0;
+  for (const LbMeta& m : h.meta) {
+    b = std::min<uint64_t>(b, m.off);
+    t = std::max<uint64_t>(t, (uint64_t)m.off + m.n);
+  }
+  if (t <= b) b = t = 0;
+  for (LbMeta& m : h.meta) m.off = (uint32_t)(m.off - b);
+  CCRDT_TRY(d2h_at(h.id, T.lb_id[c], b, t - b, e->stream));
+  CCRDT_TRY(d2h_at(h.score, T.lb_score[c], b, t - b, e->stream));
+  CCRDT_TRY(d2h_at(h.st, T.lb_st[c], b, t - b, e->stream));
   return CCRDT_OK;
 }
+
 }  // namespace
 
 int ccrdt_lb_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans) {
   CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
   LbHost h;
-  CCRDT_TRY(lb_download(e, h));
+  CCRDT_TRY(lb_download(e, h, 0, (uint64_t)e->n_keys));
   int64_t o = 0, m = 0, b = 0;
   for (const LbMeta& mt : h.meta)
     for (uint32_t j = 0; j < mt.n; ++j) {
@@ -718,10 +801,35 @@ int ccrdt_lb_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int
 }
 
 int ccrdt_lb_export(ccrdt_engine* e, ccrdt_lb_state* out) {
+  return ccrdt_lb_export_range(e, 0, e ? e->n_keys : 0, out);
+}
+
+int ccrdt_lb_range_sizes(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_obs, int64_t* n_masked,
+                         int64_t* n_bans) {
   CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  CCRDT_TRY(key_range(e, k0, k1, "lb_range_sizes"));
   LbHost h;
-  CCRDT_TRY(lb_download(e, h));
-  const uint64_t nk = (uint64_t)e->n_keys;
+  CCRDT_TRY(lb_download(e, h, (uint64_t)k0, (uint64_t)k1));
+  int64_t o = 0, m = 0, b = 0;
+  for (const LbMeta& mt : h.meta)
+    for (uint32_t j = 0; j < mt.n; ++j) {
+      const uint8_t s = h.st[mt.off + j];
+      o += s == LB_OBS;
+      m += s == LB_MASKED;
+      b += s == LB_BANNED;
+    }
+  *n_obs = o;
+  *n_masked = m;
+  *n_bans = b;
+  return CCRDT_OK;
+}
+
+int ccrdt_lb_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, ccrdt_lb_state* out) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  CCRDT_TRY(key_range(e, k0, k1, "lb_export_range"));
+  LbHost h;
+  CCRDT_TRY(lb_download(e, h, (uint64_t)k0, (uint64_t)k1));
+  const uint64_t nk = (uint64_t)(k1 - k0);
   uint64_t po = 0, pm = 0, pb = 0;
   out->obs_ptr[0] = out->m_ptr[0] = out->b_ptr[0] = 0;
   std::vector<std::pair<int64_t, int64_t>> o, m;
@@ -813,6 +921,42 @@ int ccrdt_lb_import(ccrdt_engine* e, const ccrdt_lb_state* in) {
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   e->fresh = false;
   return CCRDT_OK;
+}
+
+int ccrdt_lb_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const ccrdt_lb_state* in) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  CCRDT_TRY(key_range(e, k0, k1, "lb_import_range"));
+  if (!in) return CCRDT_EINVAL;
+  const uint64_t nk = (uint64_t)e->n_keys, a = (uint64_t)k0, b = (uint64_t)k1;
+  int64_t no = 0, nm = 0, nb = 0;
+  CCRDT_TRY(ccrdt_lb_state_sizes(e, &no, &nm, &nb));
+  std::vector<uint64_t> op(nk + 1), mp(nk + 1), bp(nk + 1);
+  std::vector<int64_t> oi(no + 1), os(no + 1), mi(nm + 1), ms(nm + 1), bi(nb + 1), mid(nk), msc(nk);
+  std::vector<uint8_t> mv(nk);
+  ccrdt_lb_state f{op.data(), oi.data(), os.data(), mp.data(), mi.data(), ms.data(), bp.data(),
+                   bi.data(), mv.data(), mid.data(), msc.data()};
+  CCRDT_TRY(ccrdt_lb_export(e, &f));
+  oi.resize(no);
+  os.resize(no);
+  mi.resize(nm);
+  ms.resize(nm);
+  bi.resize(nb);
+  std::vector<uint64_t> op2, mp2, bp2, tmp;
+  std::vector<int64_t> oi2, os2, mi2, ms2, bi2;
+  splice_csr(op, oi, in->obs_ptr, in->obs_id, a, b, op2, oi2);
+  splice_csr(op, os, in->obs_ptr, in->obs_score, a, b, tmp, os2);
+  splice_csr(mp, mi, in->m_ptr, in->m_id, a, b, mp2, mi2);
+  splice_csr(mp, ms, in->m_ptr, in->m_score, a, b, tmp, ms2);
+  splice_csr(bp, bi, in->b_ptr, in->b_id, a, b, bp2, bi2);
+  for (uint64_t k = a; k < b; ++k) {
+    mv[k] = in->min_valid[k - a];
+    mid[k] = in->min_id[k - a];
+    msc[k] = in->min_score[k - a];
+  }
+  for (auto* v : {&oi2, &os2, &mi2, &ms2, &bi2}) v->push_back(0);
+  ccrdt_lb_state g{op2.data(), oi2.data(), os2.data(), mp2.data(), mi2.data(), ms2.data(), bp2.data(),
+                   bi2.data(), mv.data(), mid.data(), msc.data()};
+  return ccrdt_lb_import(e, &g);
 }
 
 int ccrdt_lb_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,

@@ -56,9 +56,14 @@ __device__ unsigned long long g_steady_prof[16];
     if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_steady_prof[i], _t - prof_t);      \
     prof_t = _t;                                                                              \
   } while (0)
+#define SCOUNT(i, v)                                                             \
+  do {                                                                           \
+    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_steady_prof[i], (unsigned long long)(v)); \
+  } while (0)
 #else
 #define SPROF_STAMP(v) (void)0
 #define SPROF(i) (void)0
+#define SCOUNT(i, v) (void)0
 #endif
 
 namespace ccrdt {
@@ -124,6 +129,8 @@ struct alignas(16) SLds {
     Build b;
   } u;
   int64_t claim[S_CH];                   // K2: Ids being claimed (beside nops)
+  int64_t tsc[128], tid[128];            // Observed merge: entries at their new rank
+  uint32_t tp[128];
   unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
   uint32_t nex;
 };
@@ -352,17 +359,16 @@ __device__ __forceinline__ uint32_t s_promote(const SLds<PCAP>& L, uint32_t np) 
   return rl32(bp, (int)__builtin_ctzll(hit));
 }
 
-// Observed as a register table (K <= 128): entry i in lane i % 64 of slot
-// i / 64, in no particular order, with Min (min_observed/1, :398-406: the
-// smallest (Score, Id); Ids are distinct) tracked beside it.  Adds change one
-// entry with two selects; only an eviction, or an Obs[Id] change of the Min
-// player, re-reduces Min (DPP).  Obs[Id]'s Ts / dc / slab position live in
-// LDS (ots, opd), written on every change.
+// Observed as a register table (K <= 128), kept sorted ascending by
+// (Score, Id) -- min_observed/1's order (:398-406; Ids are distinct, so
+// (Score, Id) decides): entry r in lane r % 64 of slot r / 64, entries >= n
+// hold the sentinel (INT64_MAX, INT64_MAX, PCAP).  Min is entry 0.  Obs[Id]'s
+// Ts / dc / slab position live in LDS (ots, opd), written on every change.
 struct ObsTab {
   int64_t sc[2], id[2];  // Obs[Id] score, Id
   uint32_t p[2];         // player
   uint32_t n;            // |Observed|
-  uint32_t mi;           // entry of Min (S_NONE: {nil, nil, nil})
+  uint32_t mi;           // entry of Min: 0, or S_NONE ({nil, nil, nil}) when empty
   int64_t msc, mid;      // Min's score and Id
 };
 
@@ -372,47 +378,96 @@ __device__ __forceinline__ uint32_t ot_find(const ObsTab& o, uint32_t q) {
   const uint64_t m1 = ballot((uint32_t)(64 + lane) < o.n && o.p[1] == q);
   return m0 ? (uint32_t)__builtin_ctzll(m0) : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : S_NONE);
 }
-__device__ __forceinline__ int64_t ot_get64(const int64_t f[2], uint32_t i) {
-  const int64_t a = rl64(f[0], (int)(i & 63u)), b = rl64(f[1], (int)(i & 63u));
-  return i < 64 ? a : b;
-}
 __device__ __forceinline__ uint32_t ot_get32(const uint32_t f[2], uint32_t i) {
   const uint32_t a = rl32(f[0], (int)(i & 63u)), b = rl32(f[1], (int)(i & 63u));
   return i < 64 ? a : b;
 }
-__device__ __forceinline__ void ot_set(ObsTab& o, uint32_t i, int64_t s, int64_t id, uint32_t p) {
-  const int lane = lane_id();
-  const bool h0 = i < 64 && (uint32_t)lane == i, h1 = i >= 64 && (uint32_t)(64 + lane) == i;
-  o.sc[0] = h0 ? s : o.sc[0];
-  o.sc[1] = h1 ? s : o.sc[1];
-  o.id[0] = h0 ? id : o.id[0];
-  o.id[1] = h1 ? id : o.id[1];
-  o.p[0] = h0 ? p : o.p[0];
-  o.p[1] = h1 ? p : o.p[1];
+__device__ __forceinline__ bool key_lt(int64_t s1, int64_t i1, int64_t s2, int64_t i2) {
+  return s1 < s2 || (s1 == s2 && i1 < i2);
 }
-// Min := min_observed(Observed)
-__device__ __forceinline__ void ot_min(ObsTab& o) {
+__device__ __forceinline__ void ot_set_min(ObsTab& o) {
+  o.mi = o.n ? 0u : S_NONE;
+  o.msc = rl64(o.sc[0], 0);
+  o.mid = rl64(o.id[0], 0);
+}
+
+// One merge step of Observed: drop the entries whose rank the `del` lanes
+// hold in dr, add the `ins` lanes' (is, iid, ip) entries, and keep the K
+// largest by (Score, Id).  For an add run this is exact: Observed at the end
+// of a run of adds is the top K players by (max Score, Id) (invariant in the
+// header), so the order of the run's adds across players does not matter;
+// within a player the caller applies its adds one merge step each.  Players
+// of evicted old entries lose F_OBS here; returns each `ins` lane's new rank,
+// -1 if evicted (and -1 on the other lanes).
+template <int PCAP>
+__device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP>& L, uint32_t K, bool del, uint32_t dr,
+                                            bool ins, int64_t is, int64_t iid, uint32_t ip) {
   const int lane = lane_id();
-  const bool v0 = (uint32_t)lane < o.n, v1 = (uint32_t)(64 + lane) < o.n;
-  if (o.n == 0) {
-    o.mi = S_NONE;
-    return;
+  bool d0 = false, d1 = false;
+  uint64_t dm = ballot(del);
+  const uint32_t nd = (uint32_t)__builtin_popcountll(dm);
+  while (dm) {
+    const int x = (int)__builtin_ctzll(dm);
+    dm &= dm - 1;
+    const uint32_t r = rl32(dr, x);
+    d0 |= r == (uint32_t)lane;
+    d1 |= r == (uint32_t)(64 + lane);
   }
-  const bool t1 = v1 && (!v0 || o.sc[1] < o.sc[0] || (o.sc[1] == o.sc[0] && o.id[1] < o.id[0]));
-  const int64_t s = t1 ? o.sc[1] : (v0 ? o.sc[0] : INT64_MAX);
-  const int64_t id = t1 ? o.id[1] : (v0 ? o.id[0] : INT64_MAX);
-  const uint32_t ix = t1 ? 64u + (uint32_t)lane : (uint32_t)lane;
-  const bool v = v0 || v1;
-  const int64_t ms = wave_min_i64_dpp(v ? s : INT64_MAX);
-  uint64_t m = ballot(v && s == ms);
-  if (__builtin_popcountll(m) > 1) {  // Score tie: the smaller Id
-    const int64_t mid = wave_min_i64_dpp(v && s == ms ? id : INT64_MAX);
-    m = ballot(v && s == ms && id == mid);
+  const bool v0 = (uint32_t)lane < o.n && !d0, v1 = (uint32_t)(64 + lane) < o.n && !d1;
+  uint64_t im = ballot(ins);
+  const uint32_t ni = (uint32_t)__builtin_popcountll(im);
+  uint32_t li0 = 0, li1 = 0, ri = 0, lo = 0;
+  while (im) {
+    const int x = (int)__builtin_ctzll(im);
+    im &= im - 1;
+    const int64_t xs = rl64(is, x), xi = rl64(iid, x);
+    li0 += key_lt(xs, xi, o.sc[0], o.id[0]) ? 1u : 0u;
+    li1 += key_lt(xs, xi, o.sc[1], o.id[1]) ? 1u : 0u;
+    ri += (ins && key_lt(xs, xi, is, iid)) ? 1u : 0u;
+    const uint32_t c = (uint32_t)__builtin_popcountll(ballot(v0 && key_lt(o.sc[0], o.id[0], xs, xi))) +
+                       (uint32_t)__builtin_popcountll(ballot(v1 && key_lt(o.sc[1], o.id[1], xs, xi)));
+    lo = lane == x ? c : lo;
   }
-  const int l = (int)__builtin_ctzll(m);
-  o.mi = rl32(ix, l);
-  o.msc = ms;
-  o.mid = rl64(id, l);
+  const uint64_t dm0 = ballot(d0), dm1 = ballot(d1);
+  const uint32_t db0 = mbcnt(dm0), db1 = (uint32_t)__builtin_popcountll(dm0) + mbcnt(dm1);
+  const uint32_t tot = o.n - nd + ni;
+  const int32_t m = tot > K ? (int32_t)(tot - K) : 0;
+  const int32_t pos0 = (int32_t)((uint32_t)lane - db0 + li0) - m;
+  const int32_t pos1 = (int32_t)((uint32_t)(64 + lane) - db1 + li1) - m;
+  const int32_t posi = (int32_t)(ri + lo) - m;
+  if (v0 && pos0 >= 0) {
+    L.tsc[pos0] = o.sc[0];
+    L.tid[pos0] = o.id[0];
+    L.tp[pos0] = o.p[0];
+  }
+  if (v1 && pos1 >= 0) {
+    L.tsc[pos1] = o.sc[1];
+    L.tid[pos1] = o.id[1];
+    L.tp[pos1] = o.p[1];
+  }
+  if (ins && posi >= 0) {
+    L.tsc[posi] = is;
+    L.tid[posi] = iid;
+    L.tp[posi] = ip;
+  }
+  if (v0 && pos0 < 0) atomicAnd(&L.opd[o.p[0]], ~F_OBS);  // evicted (:325-331)
+  if (v1 && pos1 < 0) atomicAnd(&L.opd[o.p[1]], ~F_OBS);
+  wave_lds_sync();
+  o.n = tot - (uint32_t)m;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t k = (uint32_t)(t * 64 + lane);
+    const bool ok = k < o.n;
+    const uint32_t kk = ok ? k : 0u;
+    const int64_t sv = L.tsc[kk], iv = L.tid[kk];
+    const uint32_t pv = L.tp[kk];
+    o.sc[t] = ok ? sv : INT64_MAX;
+    o.id[t] = ok ? iv : INT64_MAX;
+    o.p[t] = ok ? pv : (uint32_t)PCAP;
+  }
+  wave_lds_sync();
+  ot_set_min(o);
+  return ins ? posi : -1;
 }
 
 // Deferred maintenance of each player's gb_sets:largest(Masked[Id]) (LDS
@@ -634,16 +689,43 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       c += (uint32_t)__builtin_popcountll(m);
     }
     wave_lds_sync();
+    // sorted by (Score, Id): each entry's rank is the number of entries
+    // below it (broadcast LDS reads, independent across j)
+    int64_t es[2], ei[2];
+    uint32_t ep[2], rk[2] = {0u, 0u};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t k = (uint32_t)(t * 64 + lane);
+      const uint32_t kk = k < c ? k : 0u;
+      es[t] = L.u.b.bsc[kk];
+      ei[t] = L.u.b.bid[kk];
+      ep[t] = L.u.b.bp[kk];
+    }
+    for (uint32_t j = 0; j < c; ++j) {
+      const int64_t js = L.u.b.bsc[j], ji = L.u.b.bid[j];
+      rk[0] += key_lt(js, ji, es[0], ei[0]) ? 1u : 0u;
+      rk[1] += key_lt(js, ji, es[1], ei[1]) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if ((uint32_t)(t * 64 + lane) < c) {
+        L.tsc[rk[t]] = es[t];
+        L.tid[rk[t]] = ei[t];
+        L.tp[rk[t]] = ep[t];
+      }
+    }
+    wave_lds_sync();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t k = (uint32_t)(t * 64 + lane);
       const bool ok = k < c;
-      ob.sc[t] = ok ? L.u.b.bsc[k] : INT64_MAX;
-      ob.id[t] = ok ? L.u.b.bid[k] : INT64_MAX;
-      ob.p[t] = ok ? L.u.b.bp[k] : (uint32_t)PCAP;
+      const uint32_t kk = ok ? k : 0u;
+      ob.sc[t] = ok ? L.tsc[kk] : INT64_MAX;
+      ob.id[t] = ok ? L.tid[kk] : INT64_MAX;
+      ob.p[t] = ok ? L.tp[kk] : (uint32_t)PCAP;
     }
     ob.n = c;
-    ot_min(ob);
+    ot_set_min(ob);
     wave_lds_sync();
   }
   for (uint32_t c0 = 0; c0 < nops;) {
@@ -957,7 +1039,49 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
                                     : (ob.n < K || scr > ob.msc || (scr == ob.msc && id > ob.mid)));
         }
         uint64_t relm = ballot(rel);
-        while (relm) {
+        SCOUNT(13, __builtin_popcountll(relm));
+        SCOUNT(14, 1);
+        if (RANKED) {
+          // The run's relevant adds in merge steps: step g takes the g-th
+          // add of each player (so a player's adds keep their stream order);
+          // usually one step per run.
+          const uint32_t q = kdr >> 8;
+          while (relm) {
+            bool later = false;  // an earlier remaining add of the same player
+            for (uint64_t t = relm; t; t &= t - 1) {
+              const int x = (int)__builtin_ctzll(t);
+              later |= lane > x && q == (rl32(kdr, x) >> 8);
+            }
+            const bool mine = ((relm >> lane) & 1ull) && !later;
+            relm &= ~ballot(mine);
+            wave_lds_sync();
+            const uint32_t qq = mine ? q : (uint32_t)PCAP;
+            const uint32_t f = L.opd[qq];
+            const int64_t os = L.osc[qq], ot = L.ots[qq];
+            // Id in Observed: a better element replaces Obs[Id] (:303-315);
+            // else it competes for a place (:317-331)
+            const bool up = mine && (f & F_OBS) && (scr > os || (scr == os && tsr > ot));
+            const bool en = mine && !(f & F_OBS);
+            uint32_t dr = 0;
+            for (uint64_t t = ballot(up); t; t &= t - 1) {
+              const int x = (int)__builtin_ctzll(t);
+              const uint32_t r = ot_find(ob, rl32(kdr, x) >> 8);
+              dr = lane == x ? r : dr;
+            }
+            SCOUNT(15, 1);
+            const int32_t pos = ot_merge<PCAP>(ob, L, K, up, dr, up || en, scr, id, q);
+            const uint32_t obits = (((kdr >> 2) & 7u) << 8) | ((crr >> 16) << 16);
+            if ((up || en) && pos >= 0) {
+              L.osc[q] = scr;
+              L.ots[q] = tsr;
+              L.opd[q] = (f & 0xFFu) | F_OBS | obits;
+            } else if (up) {
+              atomicAnd(&L.opd[q], ~F_OBS);
+            }
+            wave_lds_sync();
+          }
+        }
+        while (!RANKED && relm) {
           const uint32_t x = (uint32_t)__builtin_ctzll(relm);
           relm &= relm - 1;
           const uint32_t kd = rl32(kdr, (int)x), cr = rl32(crr, (int)x);
@@ -965,46 +1089,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           const int64_t s = rl64(scr, (int)x), t = rl64(tsr, (int)x), qid = rl64(id, (int)x);
           const uint32_t edc = (kd >> 2) & 7u, pos = cr >> 16;
           const uint32_t obits = (edc << 8) | (pos << 16);
-          if (RANKED) {
-            const uint32_t ix = ot_find(ob, q);
-            if (ix != S_NONE) {  // Id in Observed (:303-315)
-              const int64_t os = ot_get64(ob.sc, ix);
-              bool better = s > os;
-              if (!better && s == os) better = t > ufl64(L.ots[q]);
-              if (better) {
-                ot_set(ob, ix, s, qid, q);
-                if (lane == 0) {
-                  L.osc[q] = s;
-                  L.ots[q] = t;
-                  L.opd[q] = (L.opd[q] & 0xFFu) | obits;
-                }
-                if (ix == ob.mi) ot_min(ob);  // Old =:= Min
-              }
-            } else if (ob.n < K) {  // (:317-324)
-              ot_set(ob, ob.n, s, qid, q);
-              if (lane == 0) {
-                L.osc[q] = s;
-                L.ots[q] = t;
-                L.opd[q] = (L.opd[q] & 0xFFu) | F_OBS | obits;
-              }
-              if (ob.mi == S_NONE || s < ob.msc || (s == ob.msc && qid < ob.mid)) {
-                ob.mi = ob.n;
-                ob.msc = s;
-                ob.mid = qid;
-              }
-              ++ob.n;
-            } else if (s > ob.msc || (s == ob.msc && qid > ob.mid)) {  // evict Min (:325-331)
-              const uint32_t ev = ot_get32(ob.p, ob.mi);
-              ot_set(ob, ob.mi, s, qid, q);
-              if (lane == 0) {
-                atomicAnd(&L.opd[ev], ~F_OBS);
-                L.osc[q] = s;
-                L.ots[q] = t;
-                L.opd[q] = (L.opd[q] & 0xFFu) | F_OBS | obits;
-              }
-              ot_min(ob);
-            }
-          } else {
+          {
             uint32_t f = ufl(L.opd[q]);
             const uint32_t fobs = (f & 0xFFu) | F_OBS | obits;
             bool need_min = false;
@@ -1048,6 +1133,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           }
         }
       }
+      SPROF(9);
       if (hi >= n) break;
       // ---- the rmv at hi
       const uint32_t jr = hi;
@@ -1067,6 +1153,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         }
       }
       wave_lds_sync();
+      SPROF(10);
       // impacts Observed?  VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
       uint32_t ix = S_NONE;
       {
@@ -1080,28 +1167,19 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
         if ((r < 8 ? va : vb) < ot) continue;
       }
-      bool was_min;
-      if (RANKED) {  // drop the entry (the last one takes its place)
-        const uint32_t lst = ob.n - 1;
-        was_min = ix == ob.mi;
-        if (ix != lst) {
-          ot_set(ob, ix, ot_get64(ob.sc, lst), ot_get64(ob.id, lst), ot_get32(ob.p, lst));
-          if (ob.mi == lst) ob.mi = ix;
-        }
-        --ob.n;
-      } else {
+      bool was_min = false;
+      if (!RANKED) {
         was_min = q == mn.p;
         --nobs;
       }
       if (lane == 0) atomicAnd(&L.opd[q], ~F_OBS);
       s_catch_up<PCAP>(L, last, jr + 1, kdr, nxt, rok, rsc, rts, rd);
       last = jr + 1;
+      SPROF(11);
       const uint32_t w = s_promote<PCAP>(L, np);
-      if (w == S_NONE) {  // (:283-289)
-        if (was_min) {
-          if (RANKED) ot_min(ob);
-          else s_min<PCAP>(L, np, mn);
-        }
+      if (w == S_NONE) {  // (:283-289): Obs[Id] dropped, Min of the rest
+        if (RANKED) (void)ot_merge<PCAP>(ob, L, K, lane == 0, ix, false, 0, 0, 0u);
+        else if (was_min) s_min<PCAP>(L, np, mn);
       } else {  // promote the largest (:290-295)
         const int64_t gs = ufl64(L.gsc[w]), gt = ufl64(L.gts[w]), wid = ufl64(L.pid[w]);
         const uint32_t gd = ufl(L.gpd[w]);
@@ -1110,16 +1188,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           L.ots[w] = gt;
           L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
         }
-        if (RANKED) {
-          ot_set(ob, ob.n, gs, wid, w);
-          ++ob.n;
-          if (was_min) {
-            ot_min(ob);
-          } else if (gs < ob.msc || (gs == ob.msc && wid < ob.mid)) {
-            ob.mi = ob.n - 1;
-            ob.msc = gs;
-            ob.mid = wid;
-          }
+        if (RANKED) {  // Obs[Id] dropped and the promoted entry placed in one step
+          wave_lds_sync();
+          (void)ot_merge<PCAP>(ob, L, K, lane == 0, ix, lane == 0, gs, wid, w);
         } else {
           ++nobs;
           wave_lds_sync();
@@ -1129,6 +1200,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           s_emit<PCAP>(a, L, op0, op0 + c0 + jr, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt, nullptr);
       }
       wave_lds_sync();
+      SPROF(12);
     }
     s_catch_up<PCAP>(L, last, n, kdr, nxt, rok, rsc, rts, rd);
     wave_lds_sync();

@@ -347,6 +347,29 @@ class TopkRmvEngine(_Engine):
         cs = st.as_c()
         check(lib.ccrdt_trmv_import_range(self.h, k0, k1, C.byref(cs)), "trmv_import_range")
 
+    def permute_dcs(self, perm) -> None:
+        """Re-rank the DCs of every resident key: DC rank r becomes perm[r]
+        (a DC joined that sorts before existing ones, terms.DcRegistry).
+        Clocks move to their new columns and elements keep their DcId; the
+        import re-derives everything that depends on DC order
+        (gb_sets:largest inside Masked[Id])."""
+        perm = np.asarray(perm, np.int64)
+        st = self.export()
+        # ranks beyond perm (no DC registered yet: all-zero columns) take the
+        # new ranks perm leaves free, in order
+        free = [r for r in range(self.n_dc) if r not in set(perm.tolist())]
+        full = np.array(perm.tolist() + free[:self.n_dc - perm.shape[0]], np.int64)
+        if sorted(full.tolist()) != list(range(self.n_dc)):
+            raise ValueError("perm must be a permutation of the DC ranks")
+        for f in ("vc", "r_vc"):
+            a = getattr(st, f)
+            b = np.zeros_like(a)
+            b[:, full] = a
+            setattr(st, f, b)
+        lut = full.astype(np.uint8)
+        st.obs_dc, st.m_dc, st.min_dc = lut[st.obs_dc], lut[st.m_dc], lut[st.min_dc]
+        self.import_state(st)
+
     def value(self, key: int) -> list[tuple[int, int]]:
         """value/1 of one key (topk_rmv.erl:91-95): [(Id, Score)] of Observed,
         sorted by Id (the reference's list order is map-iteration order, Q7)."""

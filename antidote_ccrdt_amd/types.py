@@ -99,6 +99,19 @@ class TopkEngine(_Engine):
         p, i, s = _c(p, np.uint64), _c(i, np.int64), _c(s, np.int64)
         check(lib.ccrdt_topk_import(self.h, ptr(p), ptr(i), ptr(s)), "topk_import")
 
+    def export_range(self, k0: int, k1: int):
+        """The maps of keys [k0, k1) only (ptr, id, score), sorted by Id."""
+        n = C.c_int64()
+        check(lib.ccrdt_topk_range_size(self.h, k0, k1, C.byref(n)), "topk_range_size")
+        p = np.zeros(max(k1 - k0, 0) + 1, np.uint64)
+        i, s = np.zeros(n.value, np.int64), np.zeros(n.value, np.int64)
+        check(lib.ccrdt_topk_export_range(self.h, k0, k1, ptr(p), ptr(i), ptr(s)), "topk_export_range")
+        return p, i, s
+
+    def import_range(self, k0: int, k1: int, p, i, s) -> None:
+        p, i, s = _c(p, np.uint64), _c(i, np.int64), _c(s, np.int64)
+        check(lib.ccrdt_topk_import_range(self.h, k0, k1, ptr(p), ptr(i), ptr(s)), "topk_import_range")
+
     def downstream(self, score):
         s = _c(score, np.int64)
         out = np.zeros(s.shape[0], np.uint8)
@@ -184,6 +197,27 @@ class LeaderboardEngine(_Engine):
     def import_state(self, st: LbState) -> None:
         cs = st.as_c()
         check(lib.ccrdt_lb_import(self.h, C.byref(cs)), "lb_import")
+
+    @staticmethod
+    def _empty(nk: int, no: int, nm: int, nb: int) -> LbState:
+        z = np.zeros
+        return LbState(z(nk + 1, np.uint64), z(no, np.int64), z(no, np.int64), z(nk + 1, np.uint64),
+                       z(nm, np.int64), z(nm, np.int64), z(nk + 1, np.uint64), z(nb, np.int64),
+                       z(nk, np.uint8), z(nk, np.int64), z(nk, np.int64))
+
+    def export_range(self, k0: int, k1: int) -> LbState:
+        """Boards [k0, k1) only (laid out for k1 - k0 boards)."""
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        check(lib.ccrdt_lb_range_sizes(self.h, k0, k1, C.byref(a), C.byref(b), C.byref(c)),
+              "lb_range_sizes")
+        st = self._empty(max(k1 - k0, 0), a.value, b.value, c.value)
+        cs = st.as_c()
+        check(lib.ccrdt_lb_export_range(self.h, k0, k1, C.byref(cs)), "lb_export_range")
+        return st
+
+    def import_range(self, k0: int, k1: int, st: LbState) -> None:
+        cs = st.as_c()
+        check(lib.ccrdt_lb_import_range(self.h, k0, k1, C.byref(cs)), "lb_import_range")
 
     def downstream(self, key, op, id, score):
         key = _c(key, np.uint64)

@@ -120,6 +120,19 @@ class Exchange:
         self.replica_vc = vc
 
 
+def cpu_share() -> int:
+    """CPUs this process may use: the cgroup v2 quota (cpu.max) when set,
+    else the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -300,13 +313,15 @@ def main():
         del o
         # the same sample with keys partitioned over the box's CPU share
         # (single-threaded AND all cores); reported in detail
-        nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        nt = cpu_share()
         o = orc.TrmvOracle(m, args.k, args.n_dc)
         tc = time.perf_counter()
         o.apply(sb, nt, want_extra=True)
         tc = time.perf_counter() - tc
         cpu_mt = {"value": n_s / tc, "unit": "ops/s", "cores": nt, "kind": "port",
-                  "sample": f"same sample, keys partitioned statically over {nt} std::threads"}
+                  "sample": f"same sample, keys partitioned statically over {nt} std::threads "
+                            f"(every CPU this process may use: cgroup quota / affinity), "
+                            f"per-thread node pools"}
         del o
 
     if rank == 0:

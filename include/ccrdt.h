@@ -272,6 +272,14 @@ int ccrdt_topk_size(ccrdt_engine* e, int64_t* n_entries);
 /* The map of every key, sorted by Id: ptr[n_keys+1], id/score[n_entries]. */
 int ccrdt_topk_export(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score);
 int ccrdt_topk_import(ccrdt_engine* e, const uint64_t* ptr, const int64_t* id, const int64_t* score);
+/* Keys [k0, k1) only (value/1, to_binary/from_binary of single objects
+ * without a whole-engine round trip): entry count, the image laid out for
+ * k1 - k0 keys (ptr[k1 - k0 + 1]), and its import over those keys. */
+int ccrdt_topk_range_size(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_entries);
+int ccrdt_topk_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, uint64_t* ptr, int64_t* id,
+                            int64_t* score);
+int ccrdt_topk_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const uint64_t* ptr,
+                            const int64_t* id, const int64_t* score);
 /* value/1 (:81-83): every key's entries sorted by Score desc, Id desc (GPU
  * segmented sort). */
 int ccrdt_topk_value(ccrdt_engine* e, uint64_t* ptr, int64_t* id, int64_t* score);
@@ -318,6 +326,11 @@ typedef struct {
 int ccrdt_lb_state_sizes(ccrdt_engine* e, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans);
 int ccrdt_lb_export(ccrdt_engine* e, ccrdt_lb_state* out);
 int ccrdt_lb_import(ccrdt_engine* e, const ccrdt_lb_state* in);
+/* Boards [k0, k1) only; the image is laid out for k1 - k0 boards. */
+int ccrdt_lb_range_sizes(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_obs, int64_t* n_masked,
+                         int64_t* n_bans);
+int ccrdt_lb_export_range(ccrdt_engine* e, int64_t k0, int64_t k1, ccrdt_lb_state* out);
+int ccrdt_lb_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const ccrdt_lb_state* in);
 /* downstream/2 (:93-116): op 0 = {add, {Id, Score}}, 1 = {ban, Id};
  * out_kind CCRDT_LB_ADD / _ADD_R / _BAN / CCRDT_NOOP. */
 int ccrdt_lb_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const uint8_t* op,

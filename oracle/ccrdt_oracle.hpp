@@ -52,7 +52,84 @@ struct RElem {
     return score == o.score && id == o.id && dc == o.dc && ts == o.ts;
   }
 };
-using Vc = std::map<int, i64>;
+// Node pools for the topk_rmv containers.  bench.py's threaded CPU baseline
+// partitions keys over threads; with the default allocator every thread's
+// map/set nodes go through glibc malloc.  A thread whose tl_pool is set
+// (oracle_capi.cpp sets one per worker, owned by the oracle instance) takes
+// nodes from its own chunks and recycles them on its own free lists; other
+// threads use the heap.  A 16-byte header records the source.
+struct NodePool {
+  static constexpr size_t CHUNK = size_t(1) << 20;
+  std::vector<char*> chunks;
+  char* cur = nullptr;
+  size_t left = 0;
+  void* freel[16] = {};  // by 16-byte size class, blocks of <= 256 bytes
+  NodePool() = default;
+  NodePool(const NodePool&) = delete;
+  NodePool& operator=(const NodePool&) = delete;
+  ~NodePool() {
+    for (char* c : chunks) ::operator delete(c);
+  }
+  void* get(size_t n) {
+    const size_t cls = n / 16 - 1;
+    if (freel[cls]) {
+      void* p = freel[cls];
+      freel[cls] = *(void**)p;
+      return p;
+    }
+    if (left < n) {
+      cur = (char*)::operator new(CHUNK);
+      chunks.push_back(cur);
+      left = CHUNK;
+    }
+    void* p = cur;
+    cur += n;
+    left -= n;
+    return p;
+  }
+  void put(void* p, size_t n) {
+    const size_t cls = n / 16 - 1;
+    *(void**)p = freel[cls];
+    freel[cls] = p;
+  }
+};
+inline thread_local NodePool* tl_pool = nullptr;
+
+template <class T>
+struct PoolAlloc {
+  using value_type = T;
+  PoolAlloc() = default;
+  template <class U>
+  PoolAlloc(const PoolAlloc<U>&) {}
+  T* allocate(size_t n) {
+    const size_t bytes = (n * sizeof(T) + 16 + 15) & ~size_t(15);
+    char* p;
+    if (tl_pool && bytes <= 256) {
+      p = (char*)tl_pool->get(bytes);
+      *(uint64_t*)p = bytes;
+    } else {
+      p = (char*)::operator new(bytes);
+      *(uint64_t*)p = 0;
+    }
+    return (T*)(p + 16);
+  }
+  void deallocate(T* t, size_t) {
+    char* p = (char*)t - 16;
+    const uint64_t h = *(uint64_t*)p;
+    if (!h) ::operator delete(p);
+    else if (tl_pool) tl_pool->put(p, h);  // else: freed with its pool
+  }
+  template <class U>
+  bool operator==(const PoolAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PoolAlloc<U>&) const { return false; }
+};
+template <class K, class V>
+using PMap = std::map<K, V, std::less<K>, PoolAlloc<std::pair<const K, V>>>;
+template <class T>
+using PSet = std::set<T, std::less<T>, PoolAlloc<T>>;
+
+using Vc = PMap<int, i64>;
 
 // cmp/2 (topk_rmv.erl:389-395): strict > on (Score, Id, Ts); DcId ignored.
 // nil is std::nullopt: cmp(nil,_) = false, cmp(_,nil) = true.
@@ -102,9 +179,9 @@ struct RExtra {
 
 // topkrmv() state (topk_rmv.erl:67-74).
 struct TopkRmv {
-  std::map<i64, RElem> obs;              // Observed
-  std::map<i64, std::set<RElem>> masked; // Masked
-  std::map<i64, Vc> removals;            // Removals
+  PMap<i64, RElem> obs;                  // Observed
+  PMap<i64, PSet<RElem>> masked;         // Masked
+  PMap<i64, Vc> removals;                // Removals
   Vc vc;                                 // replica Vc
   std::optional<RElem> min;              // Min ({nil,nil,nil} = nullopt)
   i64 size;                              // Size
@@ -113,7 +190,7 @@ struct TopkRmv {
   explicit TopkRmv(i64 k = 100) : size(k) {}
 
   // min_observed/1 (topk_rmv.erl:398-406): term-order smallest Obs value.
-  std::optional<RElem> min_observed(const std::map<i64, RElem>& o) const {
+  std::optional<RElem> min_observed(const PMap<i64, RElem>& o) const {
     if (o.empty()) return std::nullopt;
     RElem best = o.begin()->second;
     for (const auto& [k, e] : o)
@@ -175,7 +252,7 @@ struct TopkRmv {
     // filter masked (:255-266)
     auto mit = masked.find(id);
     if (mit != masked.end()) {
-      std::set<RElem> keep;
+      PSet<RElem> keep;
       for (const auto& e : mit->second)
         if (e.ts > vc_get(vc_rmv, e.dc)) keep.insert(e);
       if (keep.empty()) masked.erase(mit);

@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -14,6 +15,8 @@ using namespace ccrdt_oracle;
 
 namespace {
 struct TrmvSet {
+  std::vector<std::unique_ptr<NodePool>> pools;  // one per worker thread (declared first:
+                                                 // destroyed after the keys' nodes)
   std::vector<TopkRmv> keys;
   int D;
 };
@@ -27,18 +30,31 @@ struct AvgSet {
   std::vector<Average> keys;
 };
 
+// Static partition of the keys over n_threads std::threads.  With `pools`,
+// worker t allocates its containers' nodes from (*pools)[t] (NodePool); a key
+// stays with the same worker for the same n_threads.
 template <class F>
-void parallel_keys(int64_t n_keys, int n_threads, F f) {
-  if (n_threads <= 1 || n_keys < 2) {
-    f(0, n_keys);
+void parallel_keys(int64_t n_keys, int n_threads, F f,
+                   std::vector<std::unique_ptr<NodePool>>* pools = nullptr) {
+  const int nt = (n_threads <= 1 || n_keys < 2) ? 1 : n_threads;
+  if (pools)
+    while ((int)pools->size() < nt) pools->push_back(std::make_unique<NodePool>());
+  auto run = [&](int t, int64_t b, int64_t e) {
+    NodePool* prev = tl_pool;
+    tl_pool = pools ? (*pools)[t].get() : nullptr;
+    f(b, e);
+    tl_pool = prev;
+  };
+  if (nt == 1) {
+    run(0, 0, n_keys);
     return;
   }
   std::vector<std::thread> th;
-  const int64_t chunk = (n_keys + n_threads - 1) / n_threads;
-  for (int t = 0; t < n_threads; ++t) {
+  const int64_t chunk = (n_keys + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
     const int64_t b = t * chunk, e = std::min<int64_t>(n_keys, b + chunk);
     if (b >= e) break;
-    th.emplace_back([=] { f(b, e); });
+    th.emplace_back([=, &run] { run(t, b, e); });
   }
   for (auto& x : th) x.join();
 }
@@ -90,7 +106,7 @@ int orc_trmv_apply(void* h, const uint64_t* key_ptr, const uint8_t* kind, const 
         }
       }
     }
-  });
+  }, &s->pools);
   return 0;
 }
 

@@ -175,3 +175,65 @@ def test_topk_rmv_tuple_dcids(gpu, monkeypatch):
     monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry((d1,)))
     with pytest.raises(etf.EtfError):
         trmv.from_binary(b)
+
+
+def test_topk_binary_ids(gpu):
+    """The reference's topk EUnit tests verbatim, binary Ids included
+    (src/antidote_ccrdt_topk.erl:178-193): Ids are interned in term order, so
+    value/1's Id tie-break is Erlang's."""
+    T = bh.topk
+    top = T.new({b"foo": 102, b"bar": 101}, 100)
+    assert T.value(top) == [(b"foo", 102), (b"bar", 101)]
+    assert T.downstream(("add", (b"baz", 1)), top) == ("ok", "noop")
+    assert T.downstream(("add", (b"baz", 500)), top) == ("ok", ("add", (b"baz", 500)))
+    t = T.new(100)
+    t = T.update(("add", (b"foo", 101)), t)[1]
+    t = T.update(("add", (b"bar", 102)), t)[1]
+    assert T.value(t) == [(b"bar", 102), (b"foo", 101)]
+    # equal scores: Id desc in term order (numbers < atoms < tuples < binaries)
+    t = T.update(("add_map", {b"a": 7, b"b": 7, 3: 7, etf.Atom("z"): 7, (1, 2): 7}), t)[1]
+    assert T.value(t)[2:] == [(b"b", 7), (b"a", 7), ((1, 2), 7), (etf.Atom("z"), 7), (3, 7)]
+    ok, t2 = T.from_binary(T.to_binary(t))
+    assert ok == "ok" and T.equal(t, t2) and T.value(t2) == T.value(t)
+    # many Ids arriving in descending order: the interner re-spaces its codes
+    # and re-codes the live states of the chain
+    s0 = T.new(10)
+    s = s0
+    for i in range(300):
+        s = T.update(("add", (b"k%05d" % (300 - i), i)), s)[1]
+    v = T.value(s)
+    assert [x[1] for x in v] == sorted(range(300), reverse=True)
+    assert T.value(T.update(("add_map", {b"k00001": 299}), s)[1])[0:2] == [(b"k00001", 299), (b"k00002", 298)]
+
+
+def test_topk_rmv_dc_joins_before_existing(gpu, monkeypatch):
+    """A DC that sorts before the registered ones gets rank 0: the resident
+    states are re-ranked (TopkRmvEngine.permute_dcs) and behave exactly like
+    states built with the full registry from the start (Q1: ranks keep
+    Erlang term order, which cmp/gb_sets ties depend on)."""
+    ops1 = [("add", (1, 10, ("dc_b", 5))), ("add", (1, 10, ("dc_c", 5))), ("add", (2, 9, ("dc_c", 3))),
+            ("rmv", (2, {"dc_c": 3})), ("add", (3, 10, ("dc_b", 6)))]
+    ops2 = [("add", (1, 10, ("dc_a", 5))), ("add", (4, 11, ("dc_a", 9))), ("rmv", (1, {"dc_b": 5}))]
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry(("dc_b", "dc_c")))
+    t = trmv.new(2)
+    for e in ops1:
+        t = trmv.update(e, t)[1]
+    terms.DC_REGISTRY.register("dc_a")
+    assert terms.DC_REGISTRY.rank("dc_a") == 0 and terms.DC_REGISTRY.rank("dc_c") == 2
+    xs = []
+    for e in ops2:
+        r = trmv.update(e, t)
+        t = r[1]
+        xs.append(r[2] if len(r) == 3 else None)
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry(("dc_a", "dc_b", "dc_c")))
+    u = trmv.new(2)
+    ys = []
+    for e in ops1:
+        u = trmv.update(e, u)[1]
+    for e in ops2:
+        r = trmv.update(e, u)
+        u = r[1]
+        ys.append(r[2] if len(r) == 3 else None)
+    assert xs == ys
+    monkeypatch.setattr(terms, "DC_REGISTRY", terms.DcRegistry(("dc_a", "dc_b", "dc_c")))
+    assert t.to_term() == u.to_term()

@@ -220,3 +220,40 @@ def test_wc_merge_equals_text(gpu):
     o = orc.WcOracle(1, False)
     o.apply_docs([docs])
     assert e.value() == o.value()
+
+
+def test_topk_lb_ranges(gpu):
+    """topk and leaderboard key-range export / import: the range image is the
+    slice of the full one, and range imports assemble an equal engine."""
+    from antidote_ccrdt_amd.types import LeaderboardEngine, TopkEngine, _csr
+    rng = np.random.default_rng(9)
+    nk, n = 3000, 200000
+    keys = rng.integers(0, nk, n)
+    order, kp = _csr(keys, nk)
+    e = TopkEngine(nk, 100)
+    e.apply(kp, rng.integers(0, 500, n)[order], rng.integers(0, 10**6, n)[order])
+    p, i, s = e.export()
+    for k0, k1 in ((0, 1), (10, 900), (2999, 3000), (0, nk), (5, 5)):
+        rp, ri, rs = e.export_range(k0, k1)
+        a, b = int(p[k0]), int(p[k1])
+        assert np.array_equal(rp, (p[k0:k1 + 1] - p[k0]).astype(np.uint64))
+        assert np.array_equal(ri, i[a:b]) and np.array_equal(rs, s[a:b])
+    e2 = TopkEngine(nk, 100)
+    for k0, k1 in ((1000, nk), (0, 1000)):
+        e2.import_range(k0, k1, *e.export_range(k0, k1))
+    assert all(np.array_equal(x, y) for x, y in zip(e2.export(), e.export()))
+    assert all(np.array_equal(x, y) for x, y in zip(e2.value(), e.value()))
+
+    lb = LeaderboardEngine(nk, 20)
+    kind = np.where(rng.random(n) < 0.03, 2, rng.integers(0, 2, n)).astype(np.uint8)
+    lb.apply(kp, kind[order], rng.integers(0, 300, n)[order], rng.integers(0, 10**5, n)[order],
+             want_extra=False)
+    full = lb.export()
+    for k0, k1 in ((0, 1), (17, 2000), (2999, 3000)):
+        part = lb.export_range(k0, k1)
+        for k in (k0, k1 - 1):
+            assert part.key_state(k - k0) == full.key_state(k)
+    lb2 = LeaderboardEngine(nk, 20)
+    for k0, k1 in ((0, 1500), (1500, nk)):
+        lb2.import_range(k0, k1, lb.export_range(k0, k1))
+    assert not lb2.export().diff(full)

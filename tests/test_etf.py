@@ -144,3 +144,25 @@ def test_wordcount_host_callbacks():
         assert W.can_compact(("add", b"a"), ("add", b"b"))
         assert W.compact_ops(("add", b"a"), ("add", b"b")) == ("noop", "noop")  # Q12
         assert not W.require_state_downstream(None)
+
+
+def test_term_interner_order_and_respace():
+    from antidote_ccrdt_amd.terms import TermInterner, term_key
+    t = TermInterner()
+    seen = []
+
+    class Holder:
+        def recode(self, m):
+            seen.append(len(m))
+    h = Holder()
+    t.watch(h)
+    xs = [b"foo", b"bar", 5, -3, b"a" * 10, "atom", (1, 2), b"", 7, True, 1]
+    for x in xs:
+        t.code(x)
+    assert sorted(xs, key=t.code) == sorted(xs, key=term_key)
+    assert t.code(True) != t.code(1)
+    for i in range(400):  # always just above the smallest binary: gaps run out
+        t.code(b"\x00" + b"\x01" * i)
+    assert seen, "codes were re-spaced"
+    assert sorted(t._term.values(), key=t.code) == sorted(t._term.values(), key=term_key)
+    assert all(t.term(t.code(x)) == x for x in xs)
