@@ -297,8 +297,9 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   uint32_t* status = E.status.as<uint32_t>();
   CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
   a.status = status;
-  // 1) capacities -> segment offsets of the new state
-  CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
+  // 1) capacities -> segment offsets of the new state (a fresh batch's
+  //    offsets are the keys' op offsets: trmv_new_meta, no scan)
+  if (!E.fresh) CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
   // Sizes of the new side.  Its totals are sum(old counts + ops per key) <=
   // (old side's totals) + n_ops, known on the host without waiting for the
   // scan; only when that bound outgrows the buffers does the host read the
@@ -310,7 +311,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     return b.pl_id.bytes >= tot[0] * 8 && b.m_score.bytes >= tot[1] * 8 &&
            b.r_vc.bytes >= tot[2] * 8 * D && b.vc.bytes >= nk * 8 * D;
   };
-  if (nk && !fits(ob)) {
+  if (nk && !E.fresh && !fits(ob)) {  // (fresh: tot is exact)
     CCRDT_HIP(hipMemcpyAsync(E.h_status, E.partials.as<uint64_t>() + nb * 3, 3 * sizeof(uint64_t),
                              hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
   const int D = a.n_dc;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t key = a.key_list[w];
-    KeyMeta nm = a.new_s.meta[key];
+    KeyMeta nm = trmv_new_meta(a, key);
     if (lane == 0) a.ex_cnt[key] = 0u;
     if (a.fresh) {
       if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = 0;

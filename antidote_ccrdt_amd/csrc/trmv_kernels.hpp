@@ -99,6 +99,21 @@ struct TrmvApplyArgs {
   uint32_t* status;  // [0] overflow count, [1] error flags
 };
 
+// New-side metadata of key k before its tier writes it.  A fresh batch's
+// segments hold exactly the key's ops (capacity = ops for players, pool and
+// rows), so their offsets are the key's op offset and the capacity scan is
+// skipped; otherwise the scan laid them out in new_s.meta.
+__device__ __forceinline__ KeyMeta trmv_new_meta(const TrmvApplyArgs& a, uint64_t k) {
+  if (a.fresh) {
+    KeyMeta m;
+    m.p_off = m.m_off = m.r_off = (uint32_t)a.key_ptr[k];
+    m.np = m.nm = m.nr = m.nobs = 0;
+    m.minq = NONE32;
+    return m;
+  }
+  return a.new_s.meta[k];
+}
+
 enum : uint32_t {
   TRMV_ERR_KIND = 1u,
   TRMV_ERR_DC = 2u,

@@ -509,7 +509,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
 #endif
   const uint64_t op0 = a.key_ptr[key];
   const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
-  const KeyMeta nm = a.new_s.meta[key];
+  const KeyMeta nm = trmv_new_meta(a, key);
   KeyMeta om;
   if (a.fresh) {
     om.p_off = om.m_off = om.r_off = 0;

@@ -183,7 +183,12 @@ __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t
     const uint32_t m = 8 * i + (lane >> 3);
     const uint32_t jm = m < n ? m : 0u;
     const uint32_t km = a.key_list ? a.key_list[c0 + jm] : c0 + jm;
-    h.meta[i] = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
+    if (a.fresh) {  // trmv_new_meta: offsets = the key's op offset, counts 0, Min nil
+      const uint32_t d = lane & 7;
+      h.meta[i] = d < 3 ? (uint32_t)a.key_ptr[km] : (d == 7 ? NONE32 : 0u);
+    } else {
+      h.meta[i] = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
+    }
   }
 }
 
