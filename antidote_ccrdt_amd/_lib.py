@@ -155,6 +155,7 @@ SIGNATURES = {
     "ccrdt_wc_apply_device": (INT, [P, C.POINTER(WcDocs)]),
     "ccrdt_wc_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_wc_export": (INT, [P, P, P, P, P]),
+    "ccrdt_lb_extras_device": (INT, [P, P, I64, P]),
     "ccrdt_topk_range_size": (INT, [P, I64, I64, C.POINTER(I64)]),
     "ccrdt_topk_export_range": (INT, [P, I64, I64, P, P, P]),
     "ccrdt_topk_import_range": (INT, [P, I64, I64, P, P, P]),

@@ -500,3 +500,104 @@ def exchange_local(shards: list[ShardedWordcount]) -> None:
         s.merge_received(np.concatenate(metas), np.concatenate(datas))
     for s in shards:
         s.local = s.local_factory()
+
+
+# ------------------------------------- replication mode, on the device
+class _TorchBatch:
+    """Device tensors handed to an engine's apply_device (pointers only)."""
+
+    def __init__(self, n: int, **cols):
+        self.n, self.cols = n, cols
+
+    def __getitem__(self, k):
+        return self.cols[k].data_ptr()
+
+
+def _lb_rows_device(kp, kind, id_, score, origin: int, seq0: int):
+    """Effect rows [n, 6] = key, origin, seq, kind, id, score of a CSR batch
+    (device tensors), seq = seq0 + position in the batch."""
+    import torch
+    dev = kp.device
+    n = kind.shape[0]
+    nk = kp.shape[0] - 1
+    key = torch.repeat_interleave(torch.arange(nk, device=dev), (kp[1:] - kp[:-1]).long(), output_size=n)
+    r = torch.empty((n, 6), dtype=torch.int64, device=dev)
+    r[:, 0] = key
+    r[:, 1] = origin
+    r[:, 2] = torch.arange(seq0, seq0 + n, device=dev)
+    r[:, 3] = kind.long()
+    r[:, 4] = id_
+    r[:, 5] = score
+    return r
+
+
+def _lb_apply_rows_device(engine, rows):
+    """Apply effect rows in canonical order (key, origin, seq) on the device;
+    returns the extras as rows (origin/seq left to the caller) and the sorted
+    batch size."""
+    import torch
+    nk = engine.n_keys
+    if nk >= (1 << 23):
+        raise ValueError("device replication packs keys into 23 bits")
+    order = torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])
+    r = rows[order]
+    kp = torch.zeros(nk + 1, dtype=torch.int64, device=rows.device)
+    kp[1:] = torch.cumsum(torch.bincount(r[:, 0], minlength=nk), 0)
+    kind = r[:, 3].to(torch.uint8).contiguous()
+    id_, score = r[:, 4].contiguous(), r[:, 5].contiguous()
+    n = int(r.shape[0])
+    torch.cuda.synchronize()
+    engine.apply_device(_TorchBatch(n, key_ptr=kp, kind=kind, id=id_, score=score))
+    ex = torch.empty((max(n, 1), 4), dtype=torch.int64, device=rows.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=rows.device)
+    from . import _lib
+    _lib.check(_lib.lib.ccrdt_lb_extras_device(engine.h, ex.data_ptr(), max(n, 1), cnt.data_ptr()),
+               "lb_extras_device")
+    engine.sync()
+    m = int(cnt.item())
+    out = torch.empty((m, 6), dtype=torch.int64, device=rows.device)
+    if m:
+        e = ex[:m]
+        out[:, 0] = e[:, 0]
+        out[:, 3] = 0  # {add, {Id, Score}}
+        out[:, 4] = e[:, 2]
+        out[:, 5] = e[:, 3]
+        out[:, 2] = e[:, 1]  # op index in the applied batch: stream order of the extras
+    return out
+
+
+def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
+    """ReplicatedLeaderboard's step with every row on the device, for several
+    replicas held by one process (exchange = concatenation).  `batches` are
+    (key_ptr, kind, id, score) device tensors, CSR by key.  Returns the number
+    of delivery rounds."""
+    import torch
+    W = len(engines)
+    seq = [0] * W
+    outs = []
+    # seq: a replica's rows are numbered in the order it sends them; extras
+    # take the counter + their op index in the batch that produced them
+    for o, (e, b) in enumerate(zip(engines, batches)):
+        own = _lb_rows_device(*b, origin=o, seq0=0)
+        seq[o] = int(own.shape[0])
+        ex = _lb_apply_rows_device(e, own)
+        ex[:, 1] = o
+        ex[:, 2] += seq[o]
+        seq[o] += int(own.shape[0])
+        outs.append(torch.cat([own, ex]))
+    for rounds in range(max_rounds):
+        allr = torch.cat(outs)
+        if not allr.shape[0]:
+            return rounds
+        outs = []
+        for r, e in enumerate(engines):
+            mine = allr[allr[:, 1] != r]
+            if not mine.shape[0]:
+                outs.append(mine)
+                continue
+            ex = _lb_apply_rows_device(e, mine)
+            ex[:, 1] = r
+            ex[:, 2] += seq[r]
+            seq[r] += int(mine.shape[0])
+            outs.append(ex)
+    raise RuntimeError("replication did not quiesce")

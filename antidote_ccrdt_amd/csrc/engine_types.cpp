@@ -20,6 +20,8 @@ int topk_launch_apply(const TopkArgs& a, int cls, uint64_t n_work, hipStream_t s
 int topk_launch_value(const TopkValueArgs& a, int cls, uint64_t n_work, hipStream_t st);
 int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st);
 int lb_launch_downstream(const LbDownArgs& a, hipStream_t st);
+int lb_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const LbExtraRec* ex, uint64_t n_keys,
+                          int64_t* rows, int64_t cap, uint32_t* count, hipStream_t st);
 int launch_ovf_need(const uint32_t* list, uint64_t n, const uint64_t* key_ptr, const uint32_t* cnt,
                     uint32_t stride, uint64_t* need, hipStream_t st);
 int launch_caps_scan(const uint64_t* key_ptr, const uint32_t* cnt, uint32_t stride, uint64_t n,
@@ -711,6 +713,15 @@ int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* ops) {
   T.tcur = out;
   e->fresh = false;
   return CCRDT_OK;
+}
+
+int ccrdt_lb_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, uint32_t* d_count) {
+  CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  if (!d_rows || !d_count || cap_rows < 0) return CCRDT_EINVAL;
+  const bool have = e->last_n_ops > 0 && e->tb.ex_cnt.p;
+  return lb_launch_pack_extras(e->tb.kp.as<uint64_t>(), have ? e->tb.ex_cnt.as<uint32_t>() : nullptr,
+                               e->tb.ex.as<LbExtraRec>(), (uint64_t)e->n_keys, d_rows, cap_rows, d_count,
+                               e->stream);
 }
 
 int ccrdt_lb_fetch_extra(ccrdt_engine* e, ccrdt_lb_extra* x) {

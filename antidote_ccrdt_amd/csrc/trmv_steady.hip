@@ -1039,8 +1039,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
                                     : (ob.n < K || scr > ob.msc || (scr == ob.msc && id > ob.mid)));
         }
         uint64_t relm = ballot(rel);
-        SCOUNT(13, __builtin_popcountll(relm));
-        SCOUNT(14, 1);
+        SPROF(13);
         if (RANKED) {
           // The run's relevant adds in merge steps: step g takes the g-th
           // add of each player (so a player's adds keep their stream order);
@@ -1068,8 +1067,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
               const uint32_t r = ot_find(ob, rl32(kdr, x) >> 8);
               dr = lane == x ? r : dr;
             }
-            SCOUNT(15, 1);
+            SPROF(14);
             const int32_t pos = ot_merge<PCAP>(ob, L, K, up, dr, up || en, scr, id, q);
+            SPROF(15);
             const uint32_t obits = (((kdr >> 2) & 7u) << 8) | ((crr >> 16) << 16);
             if ((up || en) && pos >= 0) {
               L.osc[q] = scr;

@@ -742,6 +742,37 @@ int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
+// The last apply's extra effects ({add, {Id, Score}}, leaderboard.erl:282-284)
+// packed into device rows [cap][4] = {key, op, id, score}, in any order
+// (op orders them); *count = how many there were.
+__global__ __launch_bounds__(256) void lb_pack_extras_kernel(const uint64_t* key_ptr, const uint32_t* ex_cnt,
+                                                             const LbExtraRec* ex, uint64_t n_keys,
+                                                             int64_t* rows, int64_t cap, uint32_t* count) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = k < n_keys ? ex_cnt[k] : 0u;
+  if (c == 0) return;
+  const uint32_t pos = atomicAdd(count, c);
+  const uint64_t op0 = key_ptr[k];
+  for (uint32_t j = 0; j < c && (int64_t)pos + j < cap; ++j) {
+    const LbExtraRec e = ex[op0 + j];
+    int64_t* row = rows + ((int64_t)pos + j) * 4;
+    row[0] = (int64_t)k;
+    row[1] = e.op;
+    row[2] = e.id;
+    row[3] = e.score;
+  }
+}
+
+int lb_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const LbExtraRec* ex, uint64_t n_keys,
+                          int64_t* rows, int64_t cap, uint32_t* count, hipStream_t st) {
+  CCRDT_HIP(hipMemsetAsync(count, 0, 4, st));
+  if (n_keys == 0 || !ex_cnt) return CCRDT_OK;
+  hipLaunchKernelGGL(lb_pack_extras_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0, st, key_ptr,
+                     ex_cnt, ex, n_keys, rows, cap, count);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
 int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
   if (a.n == 0) return CCRDT_OK;
   hipLaunchKernelGGL(lb_downstream_kernel, dim3((unsigned)a.n), dim3(64), 0, st, a);

@@ -11,6 +11,8 @@ engine stream):
   wordcount    8 GiB Zipf corpus (8192 docs of 1 MiB, 1M-word vocabulary)  configs[4] / 8 GPUs
   wdc          worddocumentcount on the same corpus
   average      1M adds over 10k keys                                        configs[0]
+  lb_replicated  configs[3] replication mode (replicas on one GPU)
+  wc_sharded     configs[4] per-shard histogram + all-to-all merge (shards on one GPU)
 
 Each line carries a `roofline` object (algorithmic bytes per launch / kernel
 time vs 8 TB/s).  Algorithmic bytes: ops in + final state out, counted from
@@ -241,6 +243,109 @@ def bench_average(args, rng):
     d.close()
 
 
+def bench_lb_replicated(args, rng):
+    """BASELINE configs[3]: 50M leaderboard effect ops over 100k boards
+    replicated across DC replicas (cluster.lb_replicate_device_local: each
+    replica applies its own effects, then every other replica's effects and
+    extras in canonical order, rows sorted on the device).  Here the replicas
+    share one GPU, so the step holds all of their applies back to back."""
+    import torch
+
+    from antidote_ccrdt_amd.cluster import lb_replicate_device_local
+    from antidote_ccrdt_amd.types import LeaderboardEngine
+    W, n, nk = args.replicas, args.lb_ops, 100_000
+    batches = []
+    for o in range(W):
+        m = n // W
+        kp = csr_counts(rng, m, nk)
+        ban = rng.random(m) < 0.01
+        kind = np.where(ban, 2, rng.integers(0, 2, m)).astype(np.uint8)
+        pid = rng.integers(0, 10**4, m, dtype=np.int64)
+        sc = rng.integers(0, 10**6 + 1, m, dtype=np.int64)
+        batches.append(tuple(torch.as_tensor(x).cuda() for x in (kp.astype(np.int64), kind, pid, sc)))
+    engs = [LeaderboardEngine(nk, 100) for _ in range(W)]
+    rounds = []
+
+    def step():
+        for e in engs:
+            e.reset()
+        rounds.append(lb_replicate_device_local(engs, batches))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1000.0 / args.steps
+    st = [e.export() for e in engs]
+    agree = all(np.array_equal(st[0].obs_id, x.obs_id) and np.array_equal(st[0].obs_score, x.obs_score)
+                and np.array_equal(st[0].obs_ptr, x.obs_ptr) for x in st[1:])
+    out = {"workload": "leaderboard_replicated",
+           "config": f"antidote_ccrdt_leaderboard: {n} effect ops over {nk} boards (99% add / 1% ban, "
+                     f"K=100) originated by {W} DC replicas, replicated to all of them with extras "
+                     f"re-broadcast until quiescent; replicas on one GPU, rows sorted on the device",
+           "value": n / (ms * 1e-3), "unit": "ops/s (effect ops replicated to every replica)",
+           "ms_per_step": ms, "higher_is_better": True,
+           "detail": {"replicas": W, "op_applications_per_s": W * n / (ms * 1e-3),
+                      "delivery_rounds": rounds[-1], "replicas_agree_on_value": agree}}
+    print(json.dumps(out), flush=True)
+
+
+def bench_wc_sharded(args, rng):
+    """BASELINE configs[4] at one GPU: the corpus split over shards (here on
+    one GPU), each histogrammed on its own, then every word sent to its owner
+    and merged there (cluster.ShardedWordcount / exchange_local)."""
+    from antidote_ccrdt_amd import _lib
+    from antidote_ccrdt_amd.cluster import ShardedWordcount, exchange_local
+    from antidote_ccrdt_amd.types import DeviceBatch
+    doc = 1 << 20
+    n_docs = int(args.corpus_gib * 1024)
+    if "data" not in CORPUS:
+        b = np.empty(n_docs * doc, np.uint8)
+        off = np.empty(n_docs + 1, np.uint64)
+        _lib.check(_lib.lib.ccrdt_gen_corpus(n_docs, doc, 10**6, 0xCC0DE + 4, 16, _lib.ptr(b),
+                                             _lib.ptr(off)), "gen_corpus")
+        CORPUS["data"] = (b, off)
+    b, off = CORPUS["data"]
+    W = args.replicas
+    per = n_docs // W
+    devs = []
+    for r in range(W):
+        lo, hi = int(off[r * per]), int(off[(r + 1) * per])
+        o = (off[r * per:(r + 1) * per + 1] - off[r * per]).astype(np.uint64)
+        devs.append((DeviceBatch(per, key_ptr=np.array([0, per], np.uint64), doc_off=o, bytes=b[lo:hi]), hi - lo))
+    shards = [ShardedWordcount(1, False, rank=r, world=W) for r in range(W)]
+    t_hist, t_x = [], []
+    for it in range(args.warmup + args.steps):
+        for sh in shards:
+            sh.owned.reset()
+            sh.local.reset()
+        t = time.perf_counter()
+        for sh, (d, nb) in zip(shards, devs):
+            sh.local.apply_device(d, nb)
+        for sh in shards:
+            sh.local.sync()
+        t1 = time.perf_counter()
+        exchange_local(shards)
+        t2 = time.perf_counter()
+        if it >= args.warmup:
+            t_hist.append(t1 - t)
+            t_x.append(t2 - t1)
+    ms_h, ms_x = 1000 * sum(t_hist) / len(t_hist), 1000 * sum(t_x) / len(t_x)
+    words = sum(sh.owned.sizes()[0] for sh in shards)
+    out = {"workload": "wordcount_sharded",
+           "config": f"antidote_ccrdt_wordcount: {b.shape[0] / 2**30:.0f} GiB Zipf(1) corpus split over "
+                     f"{W} shards (here on one GPU), per-shard histogram then the all-to-all merge by "
+                     f"word owner (ccrdt_wc_owner + ccrdt_wc_merge, via host buffers)",
+           "value": b.shape[0] / ((ms_h + ms_x) * 1e-3), "unit": "bytes/s", "ms_per_step": ms_h + ms_x,
+           "higher_is_better": True,
+           "detail": {"shards": W, "histogram_ms": ms_h, "exchange_merge_ms": ms_x, "distinct_words": words}}
+    print(json.dumps(out), flush=True)
+    for d, _ in devs:
+        d.close()
+
+
 CORPUS = {}
 
 
@@ -252,6 +357,8 @@ def main():
     ap.add_argument("--topk-ops", type=int, default=100_000_000)
     ap.add_argument("--lb-ops", type=int, default=50_000_000)
     ap.add_argument("--corpus-gib", type=float, default=8.0)
+    ap.add_argument("--replicas", type=int, default=2,
+                    help="DC replicas / shards of the leaderboard_replicated and wc_sharded legs")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false",
                     help="skip the cpu_baseline legs (oracle timed on a bounded sample)")
     args = ap.parse_args()
@@ -262,7 +369,8 @@ def main():
     for t in args.types.split(","):
         {"topk": bench_topk, "leaderboard": bench_leaderboard, "average": bench_average,
          "wordcount": lambda a, r: bench_wordcount(a, r, False),
-         "wdc": lambda a, r: bench_wordcount(a, r, True)}[t](args, rng)
+         "wdc": lambda a, r: bench_wordcount(a, r, True),
+         "lb_replicated": bench_lb_replicated, "wc_sharded": bench_wc_sharded}[t](args, rng)
 
 
 if __name__ == "__main__":

@@ -311,6 +311,11 @@ typedef struct {
 int ccrdt_lb_apply(ccrdt_engine* e, const ccrdt_lb_ops* ops, ccrdt_lb_extra* extra);
 int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* dev_ops);
 int ccrdt_lb_fetch_extra(ccrdt_engine* e, ccrdt_lb_extra* extra);
+/* The last apply's extra effects packed into device rows d_rows[cap_rows][4]
+ * = {key, op, id, score} ({add, {Id, Score}}, leaderboard.erl:282-284), in
+ * any order (op gives stream order); *d_count (device) = how many there were.
+ * The replication step ships these without a host round trip. */
+int ccrdt_lb_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, uint32_t* d_count);
 /* leaderboard() = {Observed, Masked, Bans, Min, Size} (:62-68), canonical
  * (each list sorted by Id). */
 typedef struct {

@@ -265,3 +265,25 @@ def test_sharded_wordcount_two_engines_gpu(gpu, wdc):
     exp = _wc_expected(2, wdc)
     for r, sh in enumerate(shards):
         assert _flat(sh.export()) == _owned_part(exp, 2, r)
+
+
+@pytest.mark.gpu
+def test_lb_replication_device_matches_host(gpu):
+    """The device-resident replication step (rows, canonical sort, extras all
+    on the GPU) reaches the same replica states as the host protocol on oracle
+    replicas."""
+    import torch
+
+    from antidote_ccrdt_amd.cluster import lb_replicate_device_local
+    from antidote_ccrdt_amd.types import LeaderboardEngine
+    W = 3
+    g = [LeaderboardEngine(NK, K) for _ in range(W)]
+    o = [ReplicatedLeaderboard(NK, K, rank=r, world=W, engine=orc.LbOracle(NK, K)) for r in range(W)]
+    for s in range(STEPS):
+        bs = _lb_batches(W, s)
+        dev = [tuple(torch.as_tensor(np.asarray(x, dt)).cuda() for x, dt in
+                     zip(b, (np.int64, np.uint8, np.int64, np.int64))) for b in bs]
+        lb_replicate_device_local(g, dev)
+        replicate_local(o, bs)
+        for r in range(W):
+            assert not _same(g[r].export(), o[r].export()), (s, r)

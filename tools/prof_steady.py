@@ -16,7 +16,7 @@ NAMES = ["K0/K1 init + old players", "K2 resolve + offsets", "K3 bulk copy",
          "C1 load/validate/lookup/clocks", "C2 dup candidates + staging",
          "C3-5 sort + appends", "C6 replays", "C7 Observed pass (tail)", "K5 records",
          "C7a add runs (+ non-impacting rmvs)", "C7b rmv prologue", "C7c impact + catch-up",
-         "C7d promote / Min"]
+         "C7d promote / Min", "C7a1 prefilter", "C7a2 groups + ranks", "C7a3 ot_merge"]
 n_ops = int(os.environ.get("N_OPS", 100_000_000))
 nk = 1 << 20
 eng = TopkRmvEngine(nk, 100, 8)
@@ -41,8 +41,7 @@ for i in range(int(os.environ.get("BATCHES", 2))):
     if not f:
         continue
     f(buf, 1)
-    tot = sum(buf[j] for j in range(len(NAMES))) or 1  # counters 13-15 are not times
+    tot = sum(buf[j] for j in range(len(NAMES))) or 1
     for j, n in enumerate(NAMES):
         print(f"  {n:34s} {buf[j] / tot * 100:6.1f} %   {buf[j] / (nk / 64):9.0f} cyc/key")
-    for j, n in ((13, "relevant adds"), (14, "add runs"), (15, "merge steps")):
-        print(f"  {n:34s} {buf[j] / (nk / 64):9.2f} per key")
+
