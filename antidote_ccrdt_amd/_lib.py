@@ -156,6 +156,8 @@ SIGNATURES = {
     "ccrdt_wc_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_wc_export": (INT, [P, P, P, P, P]),
     "ccrdt_lb_extras_device": (INT, [P, P, I64, P]),
+    "ccrdt_wc_partition_device": (INT, [P, INT, P, P, I64, I64, P, P]),
+    "ccrdt_wc_merge_device": (INT, [P, I64, P, P, I64]),
     "ccrdt_topk_range_size": (INT, [P, I64, I64, C.POINTER(I64)]),
     "ccrdt_topk_export_range": (INT, [P, I64, I64, P, P, P]),
     "ccrdt_topk_import_range": (INT, [P, I64, I64, P, P, P]),

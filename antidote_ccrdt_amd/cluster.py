@@ -485,6 +485,70 @@ class ShardedWordcount:
         return self.owned.export()
 
 
+def _wc_partition_device(engine, world: int):
+    """(meta [n, 3] int64, bytes uint8, per-owner word counts, per-owner byte
+    counts) of an engine's maps, grouped by owner, all on the device."""
+    import torch
+
+    from . import _lib
+    nw, nb = engine.sizes()
+    meta = torch.empty((max(nw, 1), 3), dtype=torch.int64, device="cuda")
+    data = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+    ow, ob = np.zeros(world, np.int64), np.zeros(world, np.int64)
+    _lib.check(_lib.lib.ccrdt_wc_partition_device(engine.h, world, meta.data_ptr(), data.data_ptr(), nw, nb,
+                                                  _lib.ptr(ow), _lib.ptr(ob)), "wc_partition_device")
+    return meta[:nw], data[:nb], ow, ob
+
+
+def _wc_merge_device(engine, meta, data) -> None:
+    import torch
+
+    from . import _lib
+    torch.cuda.synchronize()
+    _lib.check(_lib.lib.ccrdt_wc_merge_device(engine.h, int(meta.shape[0]), meta.data_ptr() if meta.numel() else None,
+                                              data.data_ptr() if data.numel() else None, int(data.shape[0])),
+               "wc_merge_device")
+
+
+def exchange_device(shard: ShardedWordcount) -> None:
+    """ShardedWordcount.exchange with the words kept on the device: partition
+    by owner on the GPU, one all_to_all_single each for the rows and their
+    bytes (RCCL), merge on the GPU.  The local histogram starts over."""
+    import torch
+    dist = _dist()
+    meta, data, ow, ob = _wc_partition_device(shard.local, shard.world)
+    if dist is not None:
+        world = dist.get_world_size()
+        sz = torch.tensor(np.concatenate([ow, ob]), dtype=torch.int64, device=meta.device)
+        rsz = torch.empty(2 * world, dtype=torch.int64, device=meta.device)
+        dist.all_to_all_single(rsz, sz, [2] * world, [2] * world)
+        r = rsz.view(world, 2).cpu().numpy()
+        rmeta = torch.empty((int(r[:, 0].sum()), 3), dtype=torch.int64, device=meta.device)
+        rdata = torch.empty(int(r[:, 1].sum()), dtype=torch.uint8, device=meta.device)
+        dist.all_to_all_single(rmeta.view(-1), meta.contiguous().view(-1), [int(x) * 3 for x in r[:, 0]],
+                               [int(x) * 3 for x in ow])
+        dist.all_to_all_single(rdata, data.contiguous(), [int(x) for x in r[:, 1]], [int(x) for x in ob])
+        meta, data = rmeta, rdata
+    _wc_merge_device(shard.owned, meta, data)
+    shard.local = shard.local_factory()
+
+
+def exchange_local_device(shards: list[ShardedWordcount]) -> None:
+    """exchange_device for several shards held by one process (the
+    all-to-all done by slicing device tensors)."""
+    import torch
+    parts = [_wc_partition_device(s.local, len(shards)) for s in shards]
+    for dst, s in enumerate(shards):
+        metas, datas = [], []
+        for meta, data, ow, ob in parts:
+            w0, b0 = int(ow[:dst].sum()), int(ob[:dst].sum())
+            metas.append(meta[w0:w0 + int(ow[dst])])
+            datas.append(data[b0:b0 + int(ob[dst])])
+        _wc_merge_device(s.owned, torch.cat(metas), torch.cat(datas))
+    for s in shards:
+        s.local = s.local_factory()
+
+
 def exchange_local(shards: list[ShardedWordcount]) -> None:
     """ShardedWordcount.exchange for several shards held by one process (the
     all-to-all done by slicing)."""

@@ -33,6 +33,11 @@ int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs,
 int wc_launch_insert(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st);
+int wc_launch_owner_count(const WcArgs& a, uint32_t world, uint32_t* owner, unsigned long long* cur, hipStream_t st);
+int wc_launch_owner_scatter(const WcArgs& a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
+                            uint8_t* out, hipStream_t st);
+int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_t* wcnt, uint32_t* wlen,
+                         hipStream_t st);
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
                     int verify, hipStream_t st);
 int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
@@ -1189,6 +1194,9 @@ int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   return ccrdt_wc_apply_device(e, &d);
 }
 
+static int wc_merge_core(ccrdt_engine* e, uint64_t nw, const uint64_t* wk, const uint64_t* wo, const int64_t* wc,
+                         const uint8_t* bytes, uint64_t nb, bool replace);
+
 static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr,
                           const uint64_t* word_off, const uint8_t* bytes, const int64_t* count,
                           bool replace) {
@@ -1218,11 +1226,6 @@ static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_
     return CCRDT_EINVAL;
   }
   TypeBufs& T = e->tb;
-  CCRDT_TRY(T.status.ensure(64));
-  CCRDT_TRY(T.arena_top.ensure(16));
-  // replace: the maps := the words (ccrdt_wc_import); the old state stays
-  // intact until the new table has been verified.
-  const bool start_empty = e->fresh || replace;
   // words -> device: keys, offsets, bytes, counts
   CCRDT_TRY(h2d(T.kp, key_ptr, (nk + 1) * 8, e->stream));
   CCRDT_TRY(h2d(T.stage[2], word_off, (nw + 1) * 8, e->stream));
@@ -1231,6 +1234,20 @@ static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_
   CCRDT_TRY(h2d(T.stage[1], count, nw * 8, e->stream));
   CCRDT_TRY(T.stage[0].ensure(nw * 8 + 8));
   CCRDT_TRY(wc_launch_doc_key(T.kp.as<uint64_t>(), nk, nw, T.stage[0].as<uint64_t>(), e->stream));
+  return wc_merge_core(e, nw, T.stage[0].as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[1].as<int64_t>(),
+                       T.stage[3].as<uint8_t>(), nb, replace);
+}
+
+// The words (device arrays: key, offsets, counts, bytes) added into the maps,
+// or replacing them.
+static int wc_merge_core(ccrdt_engine* e, uint64_t nw, const uint64_t* wk, const uint64_t* wo, const int64_t* wc,
+                         const uint8_t* bytes, uint64_t nb, bool replace) {
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.status.ensure(64));
+  CCRDT_TRY(T.arena_top.ensure(16));
+  // replace: the maps := the words (ccrdt_wc_import); the old state stays
+  // intact until the new table has been verified.
+  const bool start_empty = e->fresh || replace;
   std::vector<uint64_t> top{0, 0};
   if (!e->fresh) CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   const uint64_t words_old = start_empty ? 0 : top[1], arena_used = top[0];
@@ -1255,20 +1272,18 @@ static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_
                                T.t_len[in].as<uint32_t>(), T.t_arena[in].as<uint64_t>(),
                                T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
   CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
-  a.bytes = T.stage[3].as<uint8_t>();
+  a.bytes = bytes;
   a.n_bytes = nb;
-  const uint64_t* wk = T.stage[0].as<uint64_t>();
-  const uint64_t* wo = T.stage[2].as<uint64_t>();
-  const int64_t* wc = T.stage[1].as<int64_t>();
   CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 0, e->stream));
   CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 1, e->stream));
   uint32_t st[2];
   CCRDT_TRY(read_status(e, st));
   if (st[0] || st[1]) {
-    set_error(st[1] & 1   ? "wc_merge: 64-bit word hash collision between distinct words"
+    set_error(st[1] & 8   ? "wc_merge: a count < 1 or a key outside [0, n_keys)"
+              : st[1] & 1 ? "wc_merge: 64-bit word hash collision between distinct words"
               : st[1] & 4 ? "wc_merge: a count would leave int64"
                           : "wc_merge: word table overflow");
-    return st[1] & 5 ? CCRDT_ERANGE : CCRDT_ENOMEM;
+    return st[1] & 8 ? CCRDT_EINVAL : st[1] & 5 ? CCRDT_ERANGE : CCRDT_ENOMEM;
   }
   // persist appends the new words' bytes at arena_top[0] and counts words in
   // arena_top[1]; a replaced state starts both from zero
@@ -1322,6 +1337,69 @@ int ccrdt_wc_import(ccrdt_engine* e, int64_t n_words, const uint64_t* key_ptr, c
                     const uint8_t* bytes, const int64_t* count) {
   CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
   return wc_merge_words(e, n_words, key_ptr, word_off, bytes, count, true);
+}
+
+int ccrdt_wc_partition_device(ccrdt_engine* e, int world, int64_t* d_meta, uint8_t* d_bytes, int64_t cap_words,
+                              int64_t cap_bytes, int64_t* owner_words, int64_t* owner_bytes) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (world < 1 || !owner_words || !owner_bytes || cap_words < 0 || cap_bytes < 0) return CCRDT_EINVAL;
+  for (int o = 0; o < world; ++o) owner_words[o] = owner_bytes[o] = 0;
+  int64_t nw = 0, nb = 0;
+  CCRDT_TRY(ccrdt_wc_sizes(e, &nw, &nb));
+  if (!nw) return CCRDT_OK;
+  if (nw > cap_words || nb > cap_bytes || !d_meta || (nb && !d_bytes)) {
+    set_error("wc_partition_device: output buffers smaller than ccrdt_wc_sizes");
+    return CCRDT_EINVAL;
+  }
+  TypeBufs& T = e->tb;
+  const int c = T.tcur;
+  WcArgs a = wc_table_args(e, c);
+  CCRDT_TRY(T.caps.ensure(T.t_slots[c] * 4));
+  CCRDT_TRY(T.part.ensure((size_t)world * 8));
+  unsigned long long* cur = T.part.as<unsigned long long>();
+  CCRDT_HIP(hipMemsetAsync(cur, 0, (size_t)world * 8, e->stream));
+  CCRDT_TRY(wc_launch_owner_count(a, (uint32_t)world, T.caps.as<uint32_t>(), cur, e->stream));
+  std::vector<uint64_t> cnt;
+  CCRDT_TRY(d2h(cnt, T.part, (uint64_t)world, e->stream));
+  std::vector<uint64_t> base(world);
+  uint64_t w = 0, b = 0;
+  for (int o = 0; o < world; ++o) {
+    owner_words[o] = (int64_t)(cnt[o] >> 40);
+    owner_bytes[o] = (int64_t)(cnt[o] & ((1ull << 40) - 1));
+    base[o] = (w << 40) | b;
+    w += (uint64_t)owner_words[o];
+    b += (uint64_t)owner_bytes[o];
+  }
+  CCRDT_HIP(hipMemcpyAsync(cur, base.data(), (size_t)world * 8, hipMemcpyHostToDevice, e->stream));
+  CCRDT_TRY(wc_launch_owner_scatter(a, T.caps.as<uint32_t>(), cur, d_meta, d_bytes, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  return CCRDT_OK;
+}
+
+int ccrdt_wc_merge_device(ccrdt_engine* e, int64_t n_words, const int64_t* d_meta, const uint8_t* d_bytes,
+                          int64_t n_bytes) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (n_words < 0 || n_bytes < 0 || (n_words && !d_meta) || (n_bytes && !d_bytes)) return CCRDT_EINVAL;
+  const uint64_t nw = (uint64_t)n_words;
+  TypeBufs& T = e->tb;
+  CCRDT_TRY(T.stage[0].ensure(nw * 8 + 8));
+  CCRDT_TRY(T.stage[1].ensure(nw * 8 + 8));
+  CCRDT_TRY(T.stage[2].ensure((nw + 1) * 8));
+  CCRDT_TRY(T.caps.ensure((nw + 1) * 8));
+  CCRDT_TRY(T.part.ensure(((nw + 255) / 256 + 2) * 8));
+  CCRDT_TRY(wc_launch_meta_split(d_meta, nw, T.stage[0].as<uint64_t>(), T.stage[1].as<int64_t>(), nullptr,
+                                 e->stream));
+  // word offsets: exclusive scan of the lengths (the low words of column 1)
+  CCRDT_TRY(launch_caps_scan(nullptr, nw ? (const uint32_t*)d_meta + 2 : nullptr, 6, nw, T.caps.as<uint64_t>(),
+                             T.stage[2].as<uint64_t>(), T.part.as<uint64_t>(), e->stream));
+  std::vector<uint64_t> tot;
+  CCRDT_TRY(d2h_at(tot, T.stage[2], nw, 1, e->stream));
+  if (tot[0] != (uint64_t)n_bytes) {
+    set_error("wc_merge_device: the word lengths do not add up to n_bytes");
+    return CCRDT_EINVAL;
+  }
+  return wc_merge_core(e, nw, T.stage[0].as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[1].as<int64_t>(),
+                       d_bytes, (uint64_t)n_bytes, false);
 }
 
 int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes) {

@@ -1208,6 +1208,10 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
   for (uint64_t j = s; j < e; ++j) f = (f ^ a.bytes[j]) * 0x100000001B3ull;
   const uint64_t h = wc_mix(f, key, len);
   if (!verify) {
+    if (cnt[i] < 1 || key >= (uint64_t)a.n_keys) {  // a map entry counts at least one token
+      atomicOr(&a.status[1], 8u);
+      return;
+    }
     const uint64_t g = wc_global_insert(a, h, key, len, s);
     if (g != ~0ull) {
       const unsigned long long c = (unsigned long long)cnt[i];
@@ -1227,6 +1231,74 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
   bool eq = a.t_key[sl] == key && a.t_len[sl] == len;
   for (uint32_t j = 0; eq && j < len; ++j) eq = rep[j] == a.bytes[s + j];
   if (!eq) atomicOr(&a.status[1], 1u);
+}
+
+// ---- the key-sharded histogram's exchange, on the device (cluster.py):
+// every word of the table goes to the rank ccrdt_wc_owner names, grouped by
+// owner.  One packed 64-bit cursor per owner (words << 40 | bytes) keeps the
+// rows and their bytes in the same order, so a receiver's word offsets are
+// the prefix sum of the lengths.
+__device__ __forceinline__ uint64_t wc_owner_mix(uint64_t z) {  // splitmix64
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t wc_slot_owner(const WcArgs& a, uint64_t sl, uint32_t world) {
+  const uint8_t* w = a.arena + a.t_arena[sl];
+  uint64_t f = 0xCBF29CE484222325ull;
+  for (uint32_t j = 0; j < a.t_len[sl]; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
+  return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)a.t_key[sl] * 0x9E3779B97F4A7C15ull)) % world);
+}
+__global__ void wc_owner_count_kernel(WcArgs a, uint32_t world, uint32_t* owner, unsigned long long* cur) {
+  const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
+  const uint32_t o = wc_slot_owner(a, sl, world);
+  owner[sl] = o;
+  atomicAdd(&cur[o], (1ull << 40) + a.t_len[sl]);
+}
+__global__ void wc_owner_scatter_kernel(WcArgs a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
+                                        uint8_t* out) {
+  const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
+  const uint32_t len = a.t_len[sl];
+  const unsigned long long c = atomicAdd(&cur[owner[sl]], (1ull << 40) + len);
+  const uint64_t w = c >> 40, b = c & ((1ull << 40) - 1);
+  meta[w * 3] = a.t_key[sl];
+  meta[w * 3 + 1] = len;
+  meta[w * 3 + 2] = (int64_t)a.t_cnt[sl];
+  const uint8_t* src = a.arena + a.t_arena[sl];
+  for (uint32_t j = 0; j < len; ++j) out[b + j] = src[j];
+}
+// rows (key, len, count) -> the merge kernel's per-word arrays
+__global__ void wc_meta_split_kernel(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_t* wcnt, uint32_t* wlen) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  wkey[i] = (uint64_t)meta[i * 3];
+  if (wlen) wlen[i] = (uint32_t)meta[i * 3 + 1];
+  wcnt[i] = meta[i * 3 + 2];
+}
+int wc_launch_owner_count(const WcArgs& a, uint32_t world, uint32_t* owner, unsigned long long* cur, hipStream_t st) {
+  const uint64_t n = a.t_mask + 1;
+  hipLaunchKernelGGL(wc_owner_count_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, world, owner, cur);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_owner_scatter(const WcArgs& a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
+                            uint8_t* out, hipStream_t st) {
+  const uint64_t n = a.t_mask + 1;
+  hipLaunchKernelGGL(wc_owner_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, owner, cur,
+                     meta, out);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_t* wcnt, uint32_t* wlen,
+                         hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_meta_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, meta, n, wkey, wcnt,
+                     wlen);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
 }
 
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,

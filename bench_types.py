@@ -297,7 +297,7 @@ def bench_wc_sharded(args, rng):
     one GPU), each histogrammed on its own, then every word sent to its owner
     and merged there (cluster.ShardedWordcount / exchange_local)."""
     from antidote_ccrdt_amd import _lib
-    from antidote_ccrdt_amd.cluster import ShardedWordcount, exchange_local
+    from antidote_ccrdt_amd.cluster import ShardedWordcount, exchange_local_device
     from antidote_ccrdt_amd.types import DeviceBatch
     doc = 1 << 20
     n_docs = int(args.corpus_gib * 1024)
@@ -327,7 +327,7 @@ def bench_wc_sharded(args, rng):
         for sh in shards:
             sh.local.sync()
         t1 = time.perf_counter()
-        exchange_local(shards)
+        exchange_local_device(shards)
         t2 = time.perf_counter()
         if it >= args.warmup:
             t_hist.append(t1 - t)
@@ -337,7 +337,7 @@ def bench_wc_sharded(args, rng):
     out = {"workload": "wordcount_sharded",
            "config": f"antidote_ccrdt_wordcount: {b.shape[0] / 2**30:.0f} GiB Zipf(1) corpus split over "
                      f"{W} shards (here on one GPU), per-shard histogram then the all-to-all merge by "
-                     f"word owner (ccrdt_wc_owner + ccrdt_wc_merge, via host buffers)",
+                     f"word owner (ccrdt_wc_partition_device + ccrdt_wc_merge_device, words kept on the device)",
            "value": b.shape[0] / ((ms_h + ms_x) * 1e-3), "unit": "bytes/s", "ms_per_step": ms_h + ms_x,
            "higher_is_better": True,
            "detail": {"shards": W, "histogram_ms": ms_h, "exchange_merge_ms": ms_x, "distinct_words": words}}

@@ -360,6 +360,18 @@ int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes);
  * over word_bytes. */
 int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint8_t* word_bytes,
                     int64_t* count);
+/* The key-sharded histogram's exchange on the device (cluster.py): every
+ * word of the maps, grouped by owner rank (the ccrdt_wc_owner function),
+ * into device rows d_meta[n_words][3] = {key, length, count} and their bytes
+ * d_bytes in the same order; owner_words / owner_bytes (host, [world]) get
+ * each owner's share.  Buffers sized by ccrdt_wc_sizes. */
+int ccrdt_wc_partition_device(ccrdt_engine* e, int world, int64_t* d_meta, uint8_t* d_bytes, int64_t cap_words,
+                              int64_t cap_bytes, int64_t* owner_words, int64_t* owner_bytes);
+/* ccrdt_wc_merge of device rows {key, length, count} and their bytes (the
+ * layout ccrdt_wc_partition_device writes; words in any order). */
+int ccrdt_wc_merge_device(ccrdt_engine* e, int64_t n_words, const int64_t* d_meta, const uint8_t* d_bytes,
+                          int64_t n_bytes);
+
 /* Owner rank of every word of a CSR word list (the layout of ccrdt_wc_export):
  * splitmix64(FNV-1a64(bytes) ^ key * 0x9E3779B97F4A7C15) mod world.  The
  * key-sharded word histogram of the multi-GPU wordcount sends

@@ -287,3 +287,38 @@ def test_lb_replication_device_matches_host(gpu):
         replicate_local(o, bs)
         for r in range(W):
             assert not _same(g[r].export(), o[r].export()), (s, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wdc", [False, True])
+def test_sharded_wordcount_device_exchange_gpu(gpu, wdc):
+    """The device-side exchange (ccrdt_wc_partition_device / _merge_device)
+    gives each shard exactly the words word_owner assigns it."""
+    from antidote_ccrdt_amd.cluster import exchange_local_device
+    for W in (2, 3):
+        shards = [ShardedWordcount(WC_KEYS, wdc, rank=r, world=W) for r in range(W)]
+        for s in range(2):
+            for r, sh in enumerate(shards):
+                sh.apply(*_docs(W, r, s)[:3])
+            exchange_local_device(shards)
+        exp = _wc_expected(W, wdc)
+        for r, sh in enumerate(shards):
+            assert _flat(sh.export()) == _owned_part(exp, W, r)
+
+
+@pytest.mark.gpu
+def test_wc_merge_device_rejects_bad_rows(gpu):
+    import torch
+
+    from antidote_ccrdt_amd import _lib
+    from antidote_ccrdt_amd.cluster import _wc_merge_device
+    from antidote_ccrdt_amd.types import WordcountEngine
+    e = WordcountEngine(2)
+    e.apply_docs([[b"a b"], [b"c"]])
+    before = e.export()
+    for meta in ([[0, 1, 0]], [[5, 1, 1]]):  # count 0; key outside [0, n_keys)
+        with pytest.raises(_lib.CcrdtError) as ei:
+            _wc_merge_device(e, torch.tensor(meta, dtype=torch.int64).cuda(),
+                             torch.tensor([120], dtype=torch.uint8).cuda())
+        assert ei.value.code == _lib.EINVAL
+    assert all(np.array_equal(x, y) for x, y in zip(e.export(), before))
