@@ -35,6 +35,7 @@
 //       rmv/3 (impact, promotion, Min) with per-player LDS state;
 //   K5  Obs/largest positions of replayed players, player records, Vc, meta.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "trmv_kernels.hpp"
@@ -94,12 +95,26 @@ struct Log2<1> {
   static constexpr int v = 0;
 };
 
+// Hash slots hold a player index, a claim (S_CLAIM | lane) or S_NONE; u16 for
+// up to 256 players (LDS is what bounds the waves per CU), u32 above.
 template <int PCAP>
+struct HSlot {
+  using T = typename std::conditional<(PCAP <= 256), uint16_t, uint32_t>::type;
+  static constexpr uint32_t NONE = (uint32_t)(T)~(T)0;
+  static constexpr uint32_t CLAIM = (uint32_t)1 << (8 * sizeof(T) - 1);
+};
+
+// RANKED (K <= 128): Obs[Id]'s Score / Ts live with Observed's sorted entries
+// (tsc/tts by rank, ork = a player's rank), not per player, which keeps the
+// 256-player class at 4 workgroups (8 waves) per CU.
+template <int PCAP, bool RANKED>
 struct alignas(16) SLds {
   static constexpr int HS = 2 * PCAP;
-  uint32_t hs[HS];                       // Id hash: player | S_CLAIM|lane | S_NONE
+  static constexpr int NP = RANKED ? 0 : PCAP + 1;  // per-player Obs[Id] arrays (unranked only)
+  static constexpr int NR = RANKED ? 128 : 0;       // Observed entries (ranked only)
+  typename HSlot<PCAP>::T hs[HS];        // Id hash: player | CLAIM|lane | NONE
   int64_t pid[PCAP + 1];                 // player Ids
-  int64_t osc[PCAP + 1], ots[PCAP + 1];  // Obs[Id]: Score, Ts
+  int64_t osc[NP], ots[NP];              // Obs[Id]: Score, Ts (unranked)
   int64_t gsc[PCAP + 1], gts[PCAP + 1];  // gb_sets:largest(Masked[Id]): Score, Ts
   uint32_t opd[PCAP + 1];                // flags | Obs dc << 8 | Obs position << 16
   uint32_t gpd[PCAP + 1];                // largest: dc << 8 | position << 16
@@ -119,26 +134,46 @@ struct alignas(16) SLds {
     uint8_t cws[S_CH], cwe[S_CH];        // and their sorted ranges
     uint32_t mark[S_CH];                 // K3: player (+1) whose slab starts at a position
   };
-  struct Build {                         // old Observed, before it is sorted into registers
-    int64_t bsc[128], bid[128];
-    uint32_t bp[128];
+  struct K2 {
+    uint32_t nops[PCAP + 1];             // ops of each player in the batch
+    int64_t claim[S_CH];                 // Ids being claimed
   };
   union {
-    uint32_t nops[PCAP + 1];             // K2: ops of each player in the batch
+    K2 k;
     Chunk c;
-    Build b;
   } u;
-  int64_t claim[S_CH];                   // K2: Ids being claimed (beside nops)
-  int64_t tsc[128], tid[128];            // Observed merge: entries at their new rank
-  uint32_t tp[128];
+  int64_t tsc[NR], tid[NR], tts[NR];     // Observed, sorted by (Score, Id): Score, Id, Ts
+  uint16_t tp[NR];                       // and player
+  uint8_t ork[RANKED ? PCAP + 1 : 0];    // rank of an observed player's entry
   unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
   uint32_t nex;
+  uint32_t nob;                          // K1: old Observed entries gathered
 };
 
 template <int PCAP>
 __device__ __forceinline__ uint32_t shash(int64_t id) {
   constexpr int B = Log2<2 * PCAP>::v;
   return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> (64 - B));
+}
+
+// Compare-and-swap on one hash slot (u16 slots: on their 32-bit word);
+// returns the slot's value before (== expect on success).
+template <int PCAP, bool RK>
+__device__ __forceinline__ uint32_t hs_cas(SLds<PCAP, RK>& L, uint32_t h, uint32_t expect, uint32_t val) {
+  if constexpr (sizeof(L.hs[0]) == 4) {
+    return atomicCAS(reinterpret_cast<uint32_t*>(&L.hs[h]), expect, val);
+  } else {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&L.hs[h & ~1u]);
+    const uint32_t sh = (h & 1u) * 16u;
+    uint32_t old = *w;
+    for (;;) {
+      const uint32_t cur = (old >> sh) & 0xFFFFu;
+      if (cur != expect) return cur;
+      const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (val << sh));
+      if (prev == old) return expect;
+      old = prev;
+    }
+  }
 }
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -200,8 +235,8 @@ __device__ __forceinline__ bool gb_gt(int64_t s1, uint32_t d1, int64_t t1, int64
   return s1 > s2 || (s1 == s2 && (d1 > d2 || (d1 == d2 && t1 > t2)));
 }
 
-template <int PCAP>
-__device__ __forceinline__ void s_emit(const TrmvApplyArgs& a, SLds<PCAP>& L, uint64_t op0, uint64_t op,
+template <int PCAP, bool RK>
+__device__ __forceinline__ void s_emit(const TrmvApplyArgs& a, SLds<PCAP, RK>& L, uint64_t op0, uint64_t op,
                                        uint8_t kind, int64_t id, int64_t sc, uint32_t dc, int64_t ts,
                                        const Row8* vc) {
   const uint32_t pos = atomicAdd(&L.nex, 1u);
@@ -220,27 +255,28 @@ __device__ __forceinline__ void s_emit(const TrmvApplyArgs& a, SLds<PCAP>& L, ui
 
 // Player of each lane's Id (v lanes); new Ids are claimed and numbered
 // np, np+1, ... in lane order.  Returns false if the key outgrows PCAP.
-template <int PCAP>
-__device__ __forceinline__ bool s_resolve(SLds<PCAP>& L, int64_t id, bool v, uint32_t& np, uint32_t& p) {
-  constexpr int HS = SLds<PCAP>::HS;
+template <int PCAP, bool RK>
+__device__ __forceinline__ bool s_resolve(SLds<PCAP, RK>& L, int64_t id, bool v, uint32_t& np, uint32_t& p) {
+  constexpr int HS = SLds<PCAP, RK>::HS;
   const int lane = lane_id();
-  L.claim[lane] = id;
+  L.u.k.claim[lane] = id;
   wave_lds_sync();
   uint32_t h = shash<PCAP>(id);
   bool resolved = !v, claimed = false;
   int follow = -1;
   p = 0;
+  constexpr uint32_t HNONE = HSlot<PCAP>::NONE, HCLAIM = HSlot<PCAP>::CLAIM;
   while (ballot(!resolved)) {
     if (!resolved) {
       const uint32_t s = L.hs[h];
-      if (s == S_NONE) {
-        if (atomicCAS(&L.hs[h], S_NONE, S_CLAIM | (uint32_t)lane) == S_NONE) {
+      if (s == HNONE) {
+        if (hs_cas(L, h, HNONE, HCLAIM | (uint32_t)lane) == HNONE) {
           claimed = true;
           resolved = true;
         }  // lost the race: read the slot again
-      } else if (s & S_CLAIM) {
+      } else if (s & HCLAIM) {
         const int c = (int)(s & 63u);
-        if (L.claim[c] == id) {
+        if (L.u.k.claim[c] == id) {
           follow = c;
           resolved = true;
         } else {
@@ -261,13 +297,14 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP>& L, int64_t id, bool v, uin
   if (claimed) {
     p = np + mbcnt(cm);
     L.pid[p] = id;
-    L.hs[h] = p;
+    L.hs[h] = (typename HSlot<PCAP>::T)p;
     L.oslab[p] = 0u;
     L.orow[p] = S_NONE;
-    L.u.nops[p] = 0u;
+    L.u.k.nops[p] = 0u;
     L.opd[p] = NONE16 << 16;
     L.gpd[p] = 0u;
-    L.osc[p] = L.ots[p] = L.gsc[p] = L.gts[p] = 0;
+    L.gsc[p] = L.gts[p] = 0;
+    if constexpr (!RK) L.osc[p] = L.ots[p] = 0;
   }
   const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
   if (follow >= 0) p = fp;
@@ -276,14 +313,14 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP>& L, int64_t id, bool v, uin
   return true;
 }
 
-template <int PCAP>
-__device__ __forceinline__ uint32_t s_lookup(const SLds<PCAP>& L, int64_t id, bool v) {
-  constexpr int HS = SLds<PCAP>::HS;
+template <int PCAP, bool RK>
+__device__ __forceinline__ uint32_t s_lookup(const SLds<PCAP, RK>& L, int64_t id, bool v) {
+  constexpr int HS = SLds<PCAP, RK>::HS;
   uint32_t h = shash<PCAP>(id), p = (uint32_t)PCAP;
   if (v) {
     for (;;) {
       const uint32_t s = L.hs[h];
-      if (s == S_NONE) break;  // cannot happen: K2 resolved every Id
+      if (s == HSlot<PCAP>::NONE) break;  // cannot happen: K2 resolved every Id
       if (L.pid[s] == id) {
         p = s;
         break;
@@ -301,8 +338,8 @@ struct SMin {
 
 // min_observed/1 (:398-406): term-order smallest Observed value; Ids are
 // distinct, so (Score, Id) decides.
-template <int PCAP>
-__device__ __forceinline__ void s_min(const SLds<PCAP>& L, uint32_t np, SMin& m) {
+template <int PCAP, bool RK>
+__device__ __forceinline__ void s_min(const SLds<PCAP, RK>& L, uint32_t np, SMin& m) {
   const int lane = lane_id();
   uint32_t bp = S_NONE;
   int64_t bs = INT64_MAX, bi = INT64_MAX;
@@ -334,8 +371,8 @@ __device__ __forceinline__ void s_min(const SLds<PCAP>& L, uint32_t np, SMin& m)
 // Promotion candidate of rmv/3 (:276-281, :291): the Id outside Observed
 // whose largest Masked element is the term-order largest, i.e. the largest
 // (max Score, Id); S_NONE if no Id outside Observed has Masked elements.
-template <int PCAP>
-__device__ __forceinline__ uint32_t s_promote(const SLds<PCAP>& L, uint32_t np) {
+template <int PCAP, bool RK>
+__device__ __forceinline__ uint32_t s_promote(const SLds<PCAP, RK>& L, uint32_t np) {
   const int lane = lane_id();
   uint32_t bp = S_NONE;
   int64_t bs = INT64_MIN, bi = INT64_MIN;
@@ -366,6 +403,7 @@ __device__ __forceinline__ uint32_t s_promote(const SLds<PCAP>& L, uint32_t np) 
 // Ts / dc / slab position live in LDS (ots, opd), written on every change.
 struct ObsTab {
   int64_t sc[2], id[2];  // Obs[Id] score, Id
+  int64_t ts[2];         // Obs[Id] Ts
   uint32_t p[2];         // player
   uint32_t n;            // |Observed|
   uint32_t mi;           // entry of Min: 0, or S_NONE ({nil, nil, nil}) when empty
@@ -377,6 +415,10 @@ __device__ __forceinline__ uint32_t ot_find(const ObsTab& o, uint32_t q) {
   const uint64_t m0 = ballot((uint32_t)lane < o.n && o.p[0] == q);
   const uint64_t m1 = ballot((uint32_t)(64 + lane) < o.n && o.p[1] == q);
   return m0 ? (uint32_t)__builtin_ctzll(m0) : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : S_NONE);
+}
+__device__ __forceinline__ int64_t ot_get64(const int64_t f[2], uint32_t i) {
+  const int64_t a = rl64(f[0], (int)(i & 63u)), b = rl64(f[1], (int)(i & 63u));
+  return i < 64 ? a : b;
 }
 __device__ __forceinline__ uint32_t ot_get32(const uint32_t f[2], uint32_t i) {
   const uint32_t a = rl32(f[0], (int)(i & 63u)), b = rl32(f[1], (int)(i & 63u));
@@ -399,9 +441,9 @@ __device__ __forceinline__ void ot_set_min(ObsTab& o) {
 // within a player the caller applies its adds one merge step each.  Players
 // of evicted old entries lose F_OBS here; returns each `ins` lane's new rank,
 // -1 if evicted (and -1 on the other lanes).
-template <int PCAP>
-__device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP>& L, uint32_t K, bool del, uint32_t dr,
-                                            bool ins, int64_t is, int64_t iid, uint32_t ip) {
+template <int PCAP, bool RK>
+__device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP, RK>& L, uint32_t K, bool del, uint32_t dr,
+                                            bool ins, int64_t is, int64_t iid, int64_t its, uint32_t ip) {
   const int lane = lane_id();
   bool d0 = false, d1 = false;
   uint64_t dm = ballot(del);
@@ -438,17 +480,23 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP>& L, uint32_t K
   if (v0 && pos0 >= 0) {
     L.tsc[pos0] = o.sc[0];
     L.tid[pos0] = o.id[0];
-    L.tp[pos0] = o.p[0];
+    L.tts[pos0] = o.ts[0];
+    L.tp[pos0] = (uint16_t)o.p[0];
+    L.ork[o.p[0]] = (uint8_t)pos0;
   }
   if (v1 && pos1 >= 0) {
     L.tsc[pos1] = o.sc[1];
     L.tid[pos1] = o.id[1];
-    L.tp[pos1] = o.p[1];
+    L.tts[pos1] = o.ts[1];
+    L.tp[pos1] = (uint16_t)o.p[1];
+    L.ork[o.p[1]] = (uint8_t)pos1;
   }
   if (ins && posi >= 0) {
     L.tsc[posi] = is;
     L.tid[posi] = iid;
-    L.tp[posi] = ip;
+    L.tts[posi] = its;
+    L.tp[posi] = (uint16_t)ip;
+    L.ork[ip] = (uint8_t)posi;
   }
   if (v0 && pos0 < 0) atomicAnd(&L.opd[o.p[0]], ~F_OBS);  // evicted (:325-331)
   if (v1 && pos1 < 0) atomicAnd(&L.opd[o.p[1]], ~F_OBS);
@@ -459,10 +507,11 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP>& L, uint32_t K
     const uint32_t k = (uint32_t)(t * 64 + lane);
     const bool ok = k < o.n;
     const uint32_t kk = ok ? k : 0u;
-    const int64_t sv = L.tsc[kk], iv = L.tid[kk];
+    const int64_t sv = L.tsc[kk], iv = L.tid[kk], tv = L.tts[kk];
     const uint32_t pv = L.tp[kk];
     o.sc[t] = ok ? sv : INT64_MAX;
     o.id[t] = ok ? iv : INT64_MAX;
+    o.ts[t] = ok ? tv : 0;
     o.p[t] = ok ? pv : (uint32_t)PCAP;
   }
   wave_lds_sync();
@@ -477,8 +526,8 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP>& L, uint32_t K
 // resets it, and the rmv itself sets the player's largest from its replay).
 // One writer per player, so no two lanes race.  Called before a promotion
 // reads the players' largest elements, and at the end of a chunk.
-template <int PCAP>
-__device__ __forceinline__ void s_catch_up(SLds<PCAP>& L, uint32_t lo, uint32_t hi, uint32_t kd, uint32_t nxt,
+template <int PCAP, bool RK>
+__device__ __forceinline__ void s_catch_up(SLds<PCAP, RK>& L, uint32_t lo, uint32_t hi, uint32_t kd, uint32_t nxt,
                                            bool rok, int64_t rsc, int64_t rts, uint32_t rd) {
   const uint32_t l = (uint32_t)lane_id();
   if (l >= lo && l < hi && nxt >= hi && rok) {
@@ -499,8 +548,8 @@ __device__ __forceinline__ void s_catch_up(SLds<PCAP>& L, uint32_t lo, uint32_t 
 // One key.  Writes nothing to the new side before its last early return
 // that hands the key on (S_NEXT).
 template <int PCAP, bool RANKED>
-__device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>& L) {
-  constexpr int HS = SLds<PCAP>::HS;
+__device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, RANKED>& L) {
+  constexpr int HS = SLds<PCAP, RANKED>::HS;
   const int lane = lane_id();
   const int D = a.n_dc;
 #ifdef TRMV_PROF
@@ -520,15 +569,19 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
   }
   if (om.np > (uint32_t)PCAP) return S_NEXT;
 
-  for (int i = lane; i < HS; i += 64) L.hs[i] = S_NONE;
+  for (int i = lane; i < HS; i += 64) L.hs[i] = (typename HSlot<PCAP>::T)HSlot<PCAP>::NONE;
   if (lane <= TRMV_DPAD)
     L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
-  if (lane == 0) L.nex = 0u;
+  if (lane == 0) {
+    L.nex = 0u;
+    L.nob = 0u;
+  }
   // sinks (PCAP) read by lanes without a player
   if (lane == 0) {
     L.opd[PCAP] = 0u;
-    L.osc[PCAP] = L.gsc[PCAP] = L.pid[PCAP] = 0;
-    L.ots[PCAP] = 0;
+    L.gsc[PCAP] = L.pid[PCAP] = 0;
+    if constexpr (RANKED) L.ork[PCAP] = 0u;
+    else L.osc[PCAP] = L.ots[PCAP] = 0;
   }
   wave_lds_sync();
 
@@ -558,9 +611,19 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       L.pid[p] = id;
       L.oslab[p] = slab;
       L.orow[p] = info;
-      L.u.nops[p] = 0u;
-      L.osc[p] = os;
-      L.ots[p] = ot;
+      L.u.k.nops[p] = 0u;
+      if constexpr (RANKED) {  // Observed's entries, gathered for the build
+        if (ob != NONE16) {
+          const uint32_t k = atomicAdd(&L.nob, 1u);
+          L.tsc[k] = os;
+          L.tid[k] = id;
+          L.tts[k] = ot;
+          L.tp[k] = (uint16_t)p;
+        }
+      } else {
+        L.osc[p] = os;
+        L.ots[p] = ot;
+      }
       L.gsc[p] = gs;
       L.gts[p] = gt;
       L.opd[p] = (ob != NONE16 ? F_OBS : 0u) | (cnt ? F_HASM : 0u) |
@@ -568,7 +631,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       L.gpd[p] = (gd << 8) | (gb << 16);
       span = off + cnt > span ? off + cnt : span;
       uint32_t h = shash<PCAP>(id);
-      while (atomicCAS(&L.hs[h], S_NONE, p) != S_NONE) h = (h + 1) & (HS - 1);
+      while (hs_cas(L, h, HSlot<PCAP>::NONE, p) != HSlot<PCAP>::NONE) h = (h + 1) & (HS - 1);
     }
   }
   span = wave_max_u32_dpp(span);
@@ -583,9 +646,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     const int64_t id = v ? a.id[op0 + l] : 0;
     const uint32_t kind = v ? (uint32_t)a.kind[op0 + l] : 0u;
     uint32_t p;
-    if (!s_resolve<PCAP>(L, id, v, np, p)) return S_NEXT;
+    if (!s_resolve<PCAP, RANKED>(L, id, v, np, p)) return S_NEXT;
     if (v) {
-      atomicAdd(&L.u.nops[p], 1u);
+      atomicAdd(&L.u.k.nops[p], 1u);
       if (kind == 2 || kind == 3) atomicOr(&L.opd[p], F_RMV);
     }
   }
@@ -602,7 +665,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
     if (newrow) L.orow[p] = (info & 0xFFFFu) | ((nr + mbcnt(m)) << 16);
     nr += (uint32_t)__builtin_popcountll(m);
     const uint32_t ocnt = act ? (L.oslab[q] >> 16) : 0u;
-    const uint32_t cap = act ? ocnt + L.u.nops[q] : 0u;
+    const uint32_t cap = act ? ocnt + L.u.k.nops[q] : 0u;
     uint32_t tot;
     const uint32_t ex = wave_excl_scan_dpp(cap, tot);
     if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
@@ -674,44 +737,35 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       mn.ts = ufl64(L.ots[mn.p]);
     }
   } else {
-    // the old Observed -> LDS list -> registers
-    uint32_t c = 0;
-    for (uint32_t b = 0; b < om.np; b += 64) {
-      const uint32_t p = b + lane;
-      const bool ok = p < om.np && (L.opd[p] & F_OBS);
-      const uint64_t m = ballot(ok);
-      if (ok) {
-        const uint32_t k = c + mbcnt(m);
-        L.u.b.bsc[k] = L.osc[p];
-        L.u.b.bid[k] = L.pid[p];
-        L.u.b.bp[k] = p;
-      }
-      c += (uint32_t)__builtin_popcountll(m);
-    }
-    wave_lds_sync();
-    // sorted by (Score, Id): each entry's rank is the number of entries
-    // below it (broadcast LDS reads, independent across j)
-    int64_t es[2], ei[2];
+    // the old Observed (gathered by K1) -> sorted by (Score, Id): each
+    // entry's rank is the number of entries below it (broadcast LDS reads,
+    // independent across j)
+    const uint32_t c = ufl(L.nob);
+    int64_t es[2], ei[2], et[2];
     uint32_t ep[2], rk[2] = {0u, 0u};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t k = (uint32_t)(t * 64 + lane);
       const uint32_t kk = k < c ? k : 0u;
-      es[t] = L.u.b.bsc[kk];
-      ei[t] = L.u.b.bid[kk];
-      ep[t] = L.u.b.bp[kk];
+      es[t] = L.tsc[kk];
+      ei[t] = L.tid[kk];
+      et[t] = L.tts[kk];
+      ep[t] = L.tp[kk];
     }
     for (uint32_t j = 0; j < c; ++j) {
-      const int64_t js = L.u.b.bsc[j], ji = L.u.b.bid[j];
+      const int64_t js = L.tsc[j], ji = L.tid[j];
       rk[0] += key_lt(js, ji, es[0], ei[0]) ? 1u : 0u;
       rk[1] += key_lt(js, ji, es[1], ei[1]) ? 1u : 0u;
     }
+    wave_lds_sync();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if ((uint32_t)(t * 64 + lane) < c) {
         L.tsc[rk[t]] = es[t];
         L.tid[rk[t]] = ei[t];
-        L.tp[rk[t]] = ep[t];
+        L.tts[rk[t]] = et[t];
+        L.tp[rk[t]] = (uint16_t)ep[t];
+        L.ork[ep[t]] = (uint8_t)rk[t];
       }
     }
     wave_lds_sync();
@@ -722,7 +776,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       const uint32_t kk = ok ? k : 0u;
       ob.sc[t] = ok ? L.tsc[kk] : INT64_MAX;
       ob.id[t] = ok ? L.tid[kk] : INT64_MAX;
-      ob.p[t] = ok ? L.tp[kk] : (uint32_t)PCAP;
+      ob.ts[t] = ok ? L.tts[kk] : 0;
+      ob.p[t] = ok ? (uint32_t)L.tp[kk] : (uint32_t)PCAP;
     }
     ob.n = c;
     ot_set_min(ob);
@@ -757,7 +812,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       if (err) atomicOr(&a.status[1], err);
       return S_REJECT;
     }
-    const uint32_t p = s_lookup<PCAP>(L, id, v);
+    const uint32_t p = s_lookup<PCAP, RANKED>(L, id, v);
     // the rmvs' clocks (8 lanes per row)
     const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
     if (isr) L.u.c.crow[rk] = (uint32_t)ts;
@@ -854,7 +909,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       Row8 rv = (Row8)(0);
       for (int d = 0; d < D; ++d) rv[d] = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + d];
       L.u.c.cres[so] = R_DOM;
-      s_emit<PCAP>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
+      s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
     }
     wave_lds_sync();
     if (sv && !walk && lane + 1 == (int)shi) {
@@ -903,7 +958,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         if ((kd & 3u) < 2) {  // add/4
           if (has_row && pick8(R, edc) >= ets) {  // dominated (:234-237)
             L.u.c.cres[o] = R_DOM;
-            s_emit<PCAP>(a, L, op0, op0 + c0 + o, CCRDT_TRMV_RMV, wid, 0, 0, 0, &R);
+            s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + o, CCRDT_TRMV_RMV, wid, 0, 0, 0, &R);
             continue;
           }
           uint32_t pos = S_NONE;
@@ -1034,7 +1089,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
           wave_lds_sync();
           const uint32_t pq = inr ? (kdr >> 8) : (uint32_t)PCAP;
           const uint32_t f = L.opd[pq];
-          const int64_t os = L.osc[pq], ot = L.ots[pq];
+          const uint32_t rq = L.ork[pq];  // meaningful with F_OBS
+          const int64_t os = L.tsc[rq], ot = L.tts[rq];
           rel = inr && ((f & F_OBS) ? (scr > os || (scr == os && tsr > ot))
                                     : (ob.n < K || scr > ob.msc || (scr == ob.msc && id > ob.mid)));
         }
@@ -1056,7 +1112,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
             wave_lds_sync();
             const uint32_t qq = mine ? q : (uint32_t)PCAP;
             const uint32_t f = L.opd[qq];
-            const int64_t os = L.osc[qq], ot = L.ots[qq];
+            const uint32_t rq = L.ork[qq];  // meaningful with F_OBS
+            const int64_t os = L.tsc[rq], ot = L.tts[rq];
             // Id in Observed: a better element replaces Obs[Id] (:303-315);
             // else it competes for a place (:317-331)
             const bool up = mine && (f & F_OBS) && (scr > os || (scr == os && tsr > ot));
@@ -1068,12 +1125,10 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
               dr = lane == x ? r : dr;
             }
             SPROF(14);
-            const int32_t pos = ot_merge<PCAP>(ob, L, K, up, dr, up || en, scr, id, q);
+            const int32_t pos = ot_merge<PCAP, RANKED>(ob, L, K, up, dr, up || en, scr, id, tsr, q);
             SPROF(15);
             const uint32_t obits = (((kdr >> 2) & 7u) << 8) | ((crr >> 16) << 16);
             if ((up || en) && pos >= 0) {
-              L.osc[q] = scr;
-              L.ots[q] = tsr;
               L.opd[q] = (f & 0xFFu) | F_OBS | obits;
             } else if (up) {
               atomicAnd(&L.opd[q], ~F_OBS);
@@ -1129,7 +1184,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
             }
             if (lane == 0) L.opd[q] = (L.opd[q] & F_HASM) | (f & ~F_HASM);
             wave_lds_sync();
-            if (need_min) s_min<PCAP>(L, np, mn);
+            if (need_min) s_min<PCAP, RANKED>(L, np, mn);
           }
         }
       }
@@ -1162,7 +1217,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         else ix = (f & F_OBS) ? 0u : S_NONE;
         if (ix == S_NONE) continue;
         const uint32_t odc = (f >> 8) & 7u;
-        const int64_t ot = ufl64(L.ots[q]);
+        int64_t ot;
+        if constexpr (RANKED) ot = ot_get64(ob.ts, ix);
+        else ot = ufl64(L.ots[q]);
         const int vl = (int)(((r & 7u) << 3) | odc);
         const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
         if ((r < 8 ? va : vb) < ot) continue;
@@ -1173,36 +1230,38 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
         --nobs;
       }
       if (lane == 0) atomicAnd(&L.opd[q], ~F_OBS);
-      s_catch_up<PCAP>(L, last, jr + 1, kdr, nxt, rok, rsc, rts, rd);
+      s_catch_up<PCAP, RANKED>(L, last, jr + 1, kdr, nxt, rok, rsc, rts, rd);
       last = jr + 1;
       SPROF(11);
-      const uint32_t w = s_promote<PCAP>(L, np);
+      const uint32_t w = s_promote<PCAP, RANKED>(L, np);
       if (w == S_NONE) {  // (:283-289): Obs[Id] dropped, Min of the rest
-        if (RANKED) (void)ot_merge<PCAP>(ob, L, K, lane == 0, ix, false, 0, 0, 0u);
-        else if (was_min) s_min<PCAP>(L, np, mn);
+        if (RANKED) (void)ot_merge<PCAP, RANKED>(ob, L, K, lane == 0, ix, false, 0, 0, 0, 0u);
+        else if (was_min) s_min<PCAP, RANKED>(L, np, mn);
       } else {  // promote the largest (:290-295)
         const int64_t gs = ufl64(L.gsc[w]), gt = ufl64(L.gts[w]), wid = ufl64(L.pid[w]);
         const uint32_t gd = ufl(L.gpd[w]);
         if (lane == 0) {
-          L.osc[w] = gs;
-          L.ots[w] = gt;
+          if constexpr (!RANKED) {
+            L.osc[w] = gs;
+            L.ots[w] = gt;
+          }
           L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
         }
         if (RANKED) {  // Obs[Id] dropped and the promoted entry placed in one step
           wave_lds_sync();
-          (void)ot_merge<PCAP>(ob, L, K, lane == 0, ix, lane == 0, gs, wid, w);
+          (void)ot_merge<PCAP, RANKED>(ob, L, K, lane == 0, ix, lane == 0, gs, wid, gt, w);
         } else {
           ++nobs;
           wave_lds_sync();
-          s_min<PCAP>(L, np, mn);
+          s_min<PCAP, RANKED>(L, np, mn);
         }
         if (lane == 0)
-          s_emit<PCAP>(a, L, op0, op0 + c0 + jr, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt, nullptr);
+          s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + jr, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt, nullptr);
       }
       wave_lds_sync();
       SPROF(12);
     }
-    s_catch_up<PCAP>(L, last, n, kdr, nxt, rok, rsc, rts, rd);
+    s_catch_up<PCAP, RANKED>(L, last, n, kdr, nxt, rok, rsc, rts, rd);
     wave_lds_sync();
     c0 += n;
     SPROF(7);
@@ -1221,7 +1280,15 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
       const uint32_t ns = L.nslab[p], cnt = ns >> 16;
       if ((f & F_WALK) && cnt) {
         const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
-        const int64_t os = L.osc[p], ot = L.ots[p];
+        int64_t os, ot;
+        if constexpr (RANKED) {
+          const uint32_t r = L.ork[p];  // meaningful with F_OBS
+          os = L.tsc[r];
+          ot = L.tts[r];
+        } else {
+          os = L.osc[p];
+          ot = L.ots[p];
+        }
         const uint32_t od = (f >> 8) & 0xFFu;
         uint32_t opos = NONE16, bpos = 0, bdc = 0;
         int64_t bsc = 0, bts = 0;
@@ -1268,9 +1335,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP>&
 
 template <int PCAP, int WAVES, bool RANKED>
 __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a) {
-  __shared__ SLds<PCAP> lds[WAVES];
+  __shared__ SLds<PCAP, RANKED> lds[WAVES];
   const uint32_t wv = ufl(threadIdx.x >> 6);
-  SLds<PCAP>& L = lds[wv];
+  SLds<PCAP, RANKED>& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x * WAVES + wv; w < n; w += gridDim.x * WAVES) {
     const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
