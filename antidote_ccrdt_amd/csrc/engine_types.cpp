@@ -3,6 +3,7 @@
 // Host code only sizes buffers, launches kernels (types_kernels.hip) and
 // converts canonical images; every update/2 runs on the GPU.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <tuple>
@@ -671,6 +672,10 @@ int ccrdt_lb_apply_device(ccrdt_engine* e, const ccrdt_lb_ops* ops) {
   a.ex_cnt = T.ex_cnt.as<uint32_t>();
   a.ex = T.ex.as<LbExtraRec>();
   a.status = T.status.as<uint32_t>();
+  {
+    const char* sq = getenv("CCRDT_LB_SEQ");
+    a.seq = (sq && sq[0] == '1') ? 1 : 0;
+  }
   uint64_t n_work = nk;
   const uint32_t* list = nullptr;
   float total_ms = 0.f;

@@ -74,7 +74,6 @@ namespace {
 constexpr int S_CH = 64;    // ops per chunk
 constexpr int S_CHR = 16;   // rmvs per chunk (rows of the clock table)
 constexpr uint32_t S_NONE = 0xFFFFFFFFu;
-constexpr uint32_t S_CLAIM = 0x80000000u;
 // opd[p] = flags (8) | Obs[Id] dc (8) | Obs[Id] slab position (16)
 constexpr uint32_t F_OBS = 1u;    // Id in Observed
 constexpr uint32_t F_HASM = 2u;   // Masked[Id] is not empty
@@ -95,7 +94,7 @@ struct Log2<1> {
   static constexpr int v = 0;
 };
 
-// Hash slots hold a player index, a claim (S_CLAIM | lane) or S_NONE; u16 for
+// Hash slots hold a player index, a claim (CLAIM | lane) or NONE; u16 for
 // up to 256 players (LDS is what bounds the waves per CU), u32 above.
 template <int PCAP>
 struct HSlot {

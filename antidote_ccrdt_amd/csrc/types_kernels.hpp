@@ -107,6 +107,7 @@ struct LbArgs {
   int64_t* g_esc;
   uint8_t* g_est;
   uint32_t* g_hslot;
+  int32_t seq;  // 1: sequential replay only (diagnostic, CCRDT_LB_SEQ=1)
 };
 enum : uint32_t { LB_ERR_KIND = 1u };
 

@@ -72,6 +72,25 @@ def test_leaderboard_random(gpu, cfg):
     assert not e2.export().diff(st)
 
 
+@pytest.mark.parametrize("seq", ["0", "1"])
+def test_leaderboard_bench_shape(gpu, seq, monkeypatch):
+    """The benchmark's board shape (~500 ops per board, Ids U[0,1e4), 1% bans,
+    K=100) over three batches, through the op-parallel boards (seq=0) and the
+    sequential replay (seq=1, CCRDT_LB_SEQ=1)."""
+    monkeypatch.setenv("CCRDT_LB_SEQ", seq)
+    rng = np.random.default_rng(0x1B)
+    nk, K = 300, 100
+    e, o = LeaderboardEngine(nk, K), orc.LbOracle(nk, K)
+    for _ in range(3):
+        b = _lb_stream(rng, 150_000, nk, 10**4, 10**6, 0.01)
+        xe, xo = e.apply(*b), o.apply(*b)
+        assert np.array_equal(xe["kind"], xo["kind"])
+        m = xo["kind"] == 0
+        assert np.array_equal(xe["id"][m], xo["id"][m])
+        assert np.array_equal(xe["score"][m], xo["score"][m])
+        assert not e.export().diff(o.export())
+
+
 # ----------------------------------------------------------------------- topk
 def test_topk_golden(gpu):
     for f in FIX["topk"]:
