@@ -674,6 +674,8 @@ struct LbPar {
   ET tid[LB_PK];
   uint16_t te[LB_PK];
   ET cid[64];       // the chunk's Ids (hash-slot claims name the claiming lane)
+  ET isc[64];       // a merge step's inserts, compacted
+  ET iid[64];
 };
 
 // Observed as a register table, entry r in lane r % 64 of slot r / 64,
@@ -698,15 +700,40 @@ __device__ __forceinline__ uint32_t lb_obs_find(const LbObs& o, uint32_t e) {
   return m0 ? (uint32_t)__builtin_ctzll(m0) : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : 0xFFFFFFFFu);
 }
 
+// Rank of (sc, id) in the sorted table staging [0, n): the number of entries
+// below it (lower_bound, at most 8 steps for n <= 128).
+template <typename ET>
+__device__ __forceinline__ uint32_t lb_rank(const LbPar<ET>& P, uint32_t n, int64_t sc, int64_t id) {
+  uint32_t first = 0, count = n;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t step = count >> 1, mid = first + step;
+    const bool lt = count > 0 && lb_key_lt((int64_t)P.tsc[mid], (int64_t)P.tid[mid], sc, id);
+    first = lt ? mid + 1 : first;
+    count = count > 0 ? (lt ? count - step - 1 : step) : 0u;
+  }
+  return first;
+}
+
 // One merge step: drop the table entries whose ranks the `del` lanes hold in
-// dr, add the `ins` lanes' (is, iid, ie), keep the K largest.  Evicted table
+// dr, add the `ins` lanes' (is, iid, ie), keep the K largest.  The staging
+// (P.tsc/tid/te) holds the table on entry and on exit.  Evicted table
 // entries become Masked here; returns each `ins` lane's rank, -1 if it did
 // not make the table.
 template <typename ET, typename V>
 __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, uint32_t K, bool del,
                                             uint32_t dr, bool ins, int64_t is, int64_t iid, uint32_t ie) {
   const int lane = lane_id();
+  const uint64_t im = ballot(ins);
+  const uint32_t ni = (uint32_t)__builtin_popcountll(im);
+  if (ins) {
+    P.isc[mbcnt(im)] = (ET)is;
+    P.iid[mbcnt(im)] = (ET)iid;
+  }
+  // table entries below each insert (deleted ones subtracted below)
+  const uint32_t lo_all = ins ? lb_rank(P, o.n, is, iid) : 0u;
   bool d0 = false, d1 = false;
+  uint32_t ld = 0;
   uint64_t dm = ballot(del);
   const uint32_t nd = (uint32_t)__builtin_popcountll(dm);
   while (dm) {
@@ -715,22 +742,19 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
     const uint32_t r = rl32(dr, x);
     d0 |= r == (uint32_t)lane;
     d1 |= r == (uint32_t)(64 + lane);
+    ld += r < lo_all ? 1u : 0u;
   }
   const bool v0 = (uint32_t)lane < o.n && !d0, v1 = (uint32_t)(64 + lane) < o.n && !d1;
-  uint64_t im = ballot(ins);
-  const uint32_t ni = (uint32_t)__builtin_popcountll(im);
-  uint32_t li0 = 0, li1 = 0, ri = 0, lo = 0;
-  while (im) {
-    const int x = (int)__builtin_ctzll(im);
-    im &= im - 1;
-    const int64_t xs = rl64(is, x), xi = rl64(iid, x);
+  wave_lds_sync();
+  // inserts below each table entry and each insert (broadcast reads)
+  uint32_t li0 = 0, li1 = 0, ri = 0;
+  for (uint32_t x = 0; x < ni; ++x) {
+    const int64_t xs = (int64_t)P.isc[x], xi = (int64_t)P.iid[x];
     li0 += lb_key_lt(xs, xi, o.sc[0], o.id[0]) ? 1u : 0u;
     li1 += lb_key_lt(xs, xi, o.sc[1], o.id[1]) ? 1u : 0u;
-    ri += (ins && lb_key_lt(xs, xi, is, iid)) ? 1u : 0u;
-    const uint32_t c = (uint32_t)__builtin_popcountll(ballot(v0 && lb_key_lt(o.sc[0], o.id[0], xs, xi))) +
-                       (uint32_t)__builtin_popcountll(ballot(v1 && lb_key_lt(o.sc[1], o.id[1], xs, xi)));
-    lo = lane == x ? c : lo;
+    ri += lb_key_lt(xs, xi, is, iid) ? 1u : 0u;
   }
+  const uint32_t lo = lo_all - ld;
   const uint64_t dm0 = ballot(d0), dm1 = ballot(d1);
   const uint32_t db0 = mbcnt(dm0), db1 = (uint32_t)__builtin_popcountll(dm0) + mbcnt(dm1);
   const uint32_t tot = o.n - nd + ni;
@@ -775,7 +799,8 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
 // One board, op-parallel.  Returns false (nothing written) when the board
 // must take the sequential replay instead.
 template <typename ET, typename V>
-__device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, const V& L, LbPar<ET>& P) {
+__device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, const V& L, LbPar<ET>& P,
+                             uint8_t* lead_of) {
   const int lane = lane_id();
   const uint32_t K = a.k;
   if (a.seq || K == 0 || K > LB_PK || om.nobs > K) return false;
@@ -951,19 +976,13 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
         // can reach Observed: a rise of an Observed entry (:222-229), a place
         // while not full (:252-258), or beating Min (:235)
         const bool rel = act && (st == LB_OBS ? nbst > ob : (o.n < K || lb_cmp(id, nbst, mid, msc)));
-        bool later = false;  // one lane per entry: the first
-        for (uint64_t t = ballot(rel); t; t &= t - 1) {
-          const int x = (int)__builtin_ctzll(t);
-          later |= lane > x && e == rl32(e, x);
-        }
-        const bool lead = rel && !later;
+        // one lane per entry leads (any of them: they share nbst)
+        if (rel) lead_of[e] = (uint8_t)lane;
+        wave_lds_sync();
+        const bool lead = rel && lead_of[e] == (uint8_t)lane;
         const bool up = lead && st == LB_OBS;
-        uint32_t dr = 0;
-        for (uint64_t t = ballot(up); t; t &= t - 1) {
-          const int x = (int)__builtin_ctzll(t);
-          const uint32_t r = lb_obs_find(o, rl32(e, x));
-          dr = lane == x ? r : dr;
-        }
+        // an Observed entry's rank: its old key's place in the sorted table
+        const uint32_t dr = up ? lb_rank(P, o.n, ob, id) : 0u;
         if (ballot(lead)) {
           const int32_t pos = lb_merge<ET>(o, P, L, K, up, dr, lead, nbst, id, e);
           if (lead) L.est[e] = pos >= 0 ? LB_OBS : LB_MASKED;
@@ -1052,10 +1071,14 @@ __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
     if (lane_id() == 0) a.ovf_list[atomicAdd(&a.status[0], 1u)] = k;
     return;
   }
-  __shared__ uint16_t OL[LB_OL];
+  // the sequential replay's Observed list and the op-parallel path's
+  // per-entry lead bytes share their LDS
+  constexpr int UB = (2 * LB_OL > E) ? 2 * LB_OL : E;
+  __shared__ alignas(16) uint8_t U[UB];
   __shared__ LbPar<ET> PL;
+  uint16_t* OL = reinterpret_cast<uint16_t*>(U);
   const LbView<uint16_t, ET> view{S.eid, S.esc, S.est, S.hslot, H - 1, OL, a.k <= LB_OL && om.nobs <= LB_OL};
-  if (lb_board_par<ET>(a, k, om, view, PL)) return;
+  if (lb_board_par<ET>(a, k, om, view, PL, U)) return;
   lb_board(a, k, om, view);
 }
 
