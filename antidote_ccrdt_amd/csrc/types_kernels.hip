@@ -665,18 +665,81 @@ __device__ __forceinline__ bool lb_fits32(int64_t x) { return x == (int64_t)(int
 // entries whose new max can reach Observed.  ban/2 stays sequential (one
 // step each, 1% of the ops in the benchmark).  A board whose imported state
 // breaks (L1)/(L2), or Size outside [1, LB_PK], takes the sequential replay.
+// Diagnostic build only (-DTRMV_PROF): per-phase s_memtime sums of the
+// op-parallel boards, read with ccrdt_debug_lb_prof().
+#ifdef TRMV_PROF
+__device__ unsigned long long g_lb_prof[16];
+#define LB_MARK(i)                                                                        \
+  do {                                                                                    \
+    unsigned long long _t;                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (lane == 0 && (k & 63u) == 3) atomicAdd(&g_lb_prof[i], _t - lb_t);                 \
+    lb_t = _t;                                                                            \
+  } while (0)
+#define LB_MSTAMP(i)                                                                      \
+  do {                                                                                    \
+    unsigned long long _t;                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (lane == 0 && (blockIdx.x & 63u) == 3) atomicAdd(&g_lb_prof[i], _t - m_t);         \
+    m_t = _t;                                                                             \
+  } while (0)
+#else
+#define LB_MARK(i) (void)0
+#define LB_MSTAMP(i) (void)0
+#endif
 constexpr uint32_t LB_PK = 128;  // Observed table capacity (two slots of 64 lanes)
 constexpr uint8_t LB_NEW = 3;    // entry created by this chunk, its first op not applied yet
 
 template <typename ET>
 struct LbPar {
-  ET tsc[LB_PK];    // merge staging: Observed sorted ascending by (Score, Id)
-  ET tid[LB_PK];
+  // NARROW boards compare (Score, Id) as one packed int64 key (lb_pack);
+  // 64-bit boards keep (Score, Id) pairs.
+  static constexpr bool PK = sizeof(ET) == 4;
+  static constexpr int W = PK ? 1 : 2;
+  int64_t tk[LB_PK * W];  // merge staging: Observed sorted ascending by (Score, Id)
   uint16_t te[LB_PK];
-  ET cid[64];       // the chunk's Ids (hash-slot claims name the claiming lane)
-  ET isc[64];       // a merge step's inserts, compacted
-  ET iid[64];
+  ET cid[64];             // the chunk's Ids (hash-slot claims name the claiming lane)
+  int64_t ik[68 * W];     // a merge step's inserts, compacted, then sentinels up to a multiple of 4
 };
+
+__device__ __forceinline__ int64_t lb_pack(int64_t sc, int64_t id) {
+  return (int64_t)(((uint64_t)sc << 32) | ((uint32_t)id ^ 0x80000000u));
+}
+template <typename ET>
+__device__ __forceinline__ void lb_tput(LbPar<ET>& P, uint32_t i, int64_t sc, int64_t id, uint32_t e) {
+  if constexpr (LbPar<ET>::PK) {
+    P.tk[i] = lb_pack(sc, id);
+  } else {
+    P.tk[2 * i] = sc;
+    P.tk[2 * i + 1] = id;
+  }
+  P.te[i] = (uint16_t)e;
+}
+template <typename ET>
+__device__ __forceinline__ void lb_tget(const LbPar<ET>& P, uint32_t i, int64_t& sc, int64_t& id, uint32_t& e) {
+  if constexpr (LbPar<ET>::PK) {
+    const int64_t k = P.tk[i];
+    sc = k >> 32;
+    id = (int64_t)(int32_t)((uint32_t)k ^ 0x80000000u);
+  } else {
+    sc = P.tk[2 * i];
+    id = P.tk[2 * i + 1];
+  }
+  e = P.te[i];
+}
+template <typename ET>
+__device__ __forceinline__ void lb_iput(LbPar<ET>& P, uint32_t i, int64_t sc, int64_t id) {
+  if constexpr (LbPar<ET>::PK) {
+    P.ik[i] = lb_pack(sc, id);
+  } else {
+    P.ik[2 * i] = sc;
+    P.ik[2 * i + 1] = id;
+  }
+}
 
 // Observed as a register table, entry r in lane r % 64 of slot r / 64,
 // ascending by (Score, Id); entries >= n hold (INT64_MAX, INT64_MAX).
@@ -708,7 +771,9 @@ __device__ __forceinline__ uint32_t lb_rank(const LbPar<ET>& P, uint32_t n, int6
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const uint32_t step = count >> 1, mid = first + step;
-    const bool lt = count > 0 && lb_key_lt((int64_t)P.tsc[mid], (int64_t)P.tid[mid], sc, id);
+    bool lt;
+    if constexpr (LbPar<ET>::PK) lt = count > 0 && P.tk[mid] < lb_pack(sc, id);
+    else lt = count > 0 && lb_key_lt(P.tk[2 * mid], P.tk[2 * mid + 1], sc, id);
     first = lt ? mid + 1 : first;
     count = count > 0 ? (lt ? count - step - 1 : step) : 0u;
   }
@@ -717,21 +782,31 @@ __device__ __forceinline__ uint32_t lb_rank(const LbPar<ET>& P, uint32_t n, int6
 
 // One merge step: drop the table entries whose ranks the `del` lanes hold in
 // dr, add the `ins` lanes' (is, iid, ie), keep the K largest.  The staging
-// (P.tsc/tid/te) holds the table on entry and on exit.  Evicted table
+// (P.tk/te) holds the table on entry and on exit.  Evicted table
 // entries become Masked here; returns each `ins` lane's rank, -1 if it did
 // not make the table.
 template <typename ET, typename V>
 __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, uint32_t K, bool del,
                                             uint32_t dr, bool ins, int64_t is, int64_t iid, uint32_t ie) {
   const int lane = lane_id();
+#ifdef TRMV_PROF
+  unsigned long long m_t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(m_t)::"memory");
+#endif
   const uint64_t im = ballot(ins);
   const uint32_t ni = (uint32_t)__builtin_popcountll(im);
-  if (ins) {
-    P.isc[mbcnt(im)] = (ET)is;
-    P.iid[mbcnt(im)] = (ET)iid;
+  if (ins) lb_iput(P, mbcnt(im), is, iid);
+  if ((uint32_t)lane >= ni && (uint32_t)lane < ni + 4) {  // sentinels: never below anything
+    if constexpr (LbPar<ET>::PK) {
+      P.ik[lane] = INT64_MAX;
+    } else {
+      P.ik[2 * lane] = INT64_MAX;
+      P.ik[2 * lane + 1] = INT64_MAX;
+    }
   }
   // table entries below each insert (deleted ones subtracted below)
   const uint32_t lo_all = ins ? lb_rank(P, o.n, is, iid) : 0u;
+  LB_MSTAMP(8);
   bool d0 = false, d1 = false;
   uint32_t ld = 0;
   uint64_t dm = ballot(del);
@@ -746,15 +821,40 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
   }
   const bool v0 = (uint32_t)lane < o.n && !d0, v1 = (uint32_t)(64 + lane) < o.n && !d1;
   wave_lds_sync();
+  LB_MSTAMP(9);
   // inserts below each table entry and each insert (broadcast reads)
   uint32_t li0 = 0, li1 = 0, ri = 0;
-  for (uint32_t x = 0; x < ni; ++x) {
-    const int64_t xs = (int64_t)P.isc[x], xi = (int64_t)P.iid[x];
-    li0 += lb_key_lt(xs, xi, o.sc[0], o.id[0]) ? 1u : 0u;
-    li1 += lb_key_lt(xs, xi, o.sc[1], o.id[1]) ? 1u : 0u;
-    ri += lb_key_lt(xs, xi, is, iid) ? 1u : 0u;
+  if constexpr (LbPar<ET>::PK) {
+    const int64_t k0 = lb_pack(o.sc[0], o.id[0]), k1 = lb_pack(o.sc[1], o.id[1]), ki = lb_pack(is, iid);
+    for (uint32_t x0 = 0; x0 < ni; x0 += 4) {  // four independent broadcast reads in flight
+      int64_t xk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xk[u] = P.ik[x0 + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        li0 += xk[u] < k0 ? 1u : 0u;
+        li1 += xk[u] < k1 ? 1u : 0u;
+        ri += xk[u] < ki ? 1u : 0u;
+      }
+    }
+  } else {
+    for (uint32_t x0 = 0; x0 < ni; x0 += 4) {
+      int64_t xs[4], xi[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xs[u] = P.ik[2 * (x0 + u)];
+        xi[u] = P.ik[2 * (x0 + u) + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        li0 += lb_key_lt(xs[u], xi[u], o.sc[0], o.id[0]) ? 1u : 0u;
+        li1 += lb_key_lt(xs[u], xi[u], o.sc[1], o.id[1]) ? 1u : 0u;
+        ri += lb_key_lt(xs[u], xi[u], is, iid) ? 1u : 0u;
+      }
+    }
   }
   const uint32_t lo = lo_all - ld;
+  LB_MSTAMP(10);
   const uint64_t dm0 = ballot(d0), dm1 = ballot(d1);
   const uint32_t db0 = mbcnt(dm0), db1 = (uint32_t)__builtin_popcountll(dm0) + mbcnt(dm1);
   const uint32_t tot = o.n - nd + ni;
@@ -762,21 +862,9 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
   const int32_t pos0 = (int32_t)((uint32_t)lane - db0 + li0) - m;
   const int32_t pos1 = (int32_t)((uint32_t)(64 + lane) - db1 + li1) - m;
   const int32_t posi = (int32_t)(ri + lo) - m;
-  if (v0 && pos0 >= 0) {
-    P.tsc[pos0] = (ET)o.sc[0];
-    P.tid[pos0] = (ET)o.id[0];
-    P.te[pos0] = (uint16_t)o.e[0];
-  }
-  if (v1 && pos1 >= 0) {
-    P.tsc[pos1] = (ET)o.sc[1];
-    P.tid[pos1] = (ET)o.id[1];
-    P.te[pos1] = (uint16_t)o.e[1];
-  }
-  if (ins && posi >= 0) {
-    P.tsc[posi] = (ET)is;
-    P.tid[posi] = (ET)iid;
-    P.te[posi] = (uint16_t)ie;
-  }
+  if (v0 && pos0 >= 0) lb_tput(P, (uint32_t)pos0, o.sc[0], o.id[0], o.e[0]);
+  if (v1 && pos1 >= 0) lb_tput(P, (uint32_t)pos1, o.sc[1], o.id[1], o.e[1]);
+  if (ins && posi >= 0) lb_tput(P, (uint32_t)posi, is, iid, ie);
   if (v0 && pos0 < 0) L.est[o.e[0]] = LB_MASKED;  // evicted Min into Masked (:236-242)
   if (v1 && pos1 < 0) L.est[o.e[1]] = LB_MASKED;
   wave_lds_sync();
@@ -786,13 +874,15 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
     const uint32_t k = (uint32_t)(t * 64 + lane);
     const bool ok = k < o.n;
     const uint32_t kk = ok ? k : 0u;
-    const int64_t sv = (int64_t)P.tsc[kk], iv = (int64_t)P.tid[kk];
-    const uint32_t ev = P.te[kk];
+    int64_t sv, iv;
+    uint32_t ev;
+    lb_tget(P, kk, sv, iv, ev);
     o.sc[t] = ok ? sv : INT64_MAX;
     o.id[t] = ok ? iv : INT64_MAX;
     o.e[t] = ok ? ev : 0xFFFFFFFFu;
   }
   wave_lds_sync();
+  LB_MSTAMP(11);
   return ins ? posi : -1;
 }
 
@@ -804,6 +894,10 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
   const int lane = lane_id();
   const uint32_t K = a.k;
   if (a.seq || K == 0 || K > LB_PK || om.nobs > K) return false;
+#ifdef TRMV_PROF
+  unsigned long long lb_t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lb_t)::"memory");
+#endif
   const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
   for (uint32_t i = lane; i <= L.hmask; i += 64) L.hslot[i] = 0;
   wave_lds_sync();
@@ -829,11 +923,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     const bool ob = v && st == LB_OBS;
     const uint64_t m = ballot(ob);
     const uint32_t p = cnt + mbcnt(m);
-    if (ob && p < LB_PK) {
-      P.tsc[p] = (ET)sc;
-      P.tid[p] = (ET)id;
-      P.te[p] = (uint16_t)j;
-    }
+    if (ob && p < LB_PK) lb_tput(P, p, sc, id, j);
     cnt += (uint32_t)__builtin_popcountll(m);
     if (v && st == LB_MASKED && (!hasm || lb_key_lt(mms, mmi, sc, id))) {
       mms = sc;
@@ -854,13 +944,13 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     for (int t = 0; t < 2; ++t) {
       const uint32_t r = t * 64 + lane;
       const uint32_t rr = r < cnt ? r : 0u;
-      s[t] = (int64_t)P.tsc[rr];
-      d[t] = (int64_t)P.tid[rr];
-      e[t] = P.te[rr];
+      lb_tget(P, rr, s[t], d[t], e[t]);
       rk[t] = 0;
     }
     for (uint32_t x = 0; x < cnt; ++x) {
-      const int64_t xs = (int64_t)P.tsc[x], xi = (int64_t)P.tid[x];
+      int64_t xs, xi;
+      uint32_t xe;
+      lb_tget(P, x, xs, xi, xe);
       rk[0] += lb_key_lt(xs, xi, s[0], d[0]) ? 1u : 0u;
       rk[1] += lb_key_lt(xs, xi, s[1], d[1]) ? 1u : 0u;
     }
@@ -868,9 +958,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       if ((uint32_t)(t * 64 + lane) < cnt) {
-        P.tsc[rk[t]] = (ET)s[t];
-        P.tid[rk[t]] = (ET)d[t];
-        P.te[rk[t]] = (uint16_t)e[t];
+        lb_tput(P, rk[t], s[t], d[t], e[t]);
       }
     wave_lds_sync();
 #pragma unroll
@@ -878,8 +966,9 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       const uint32_t r = t * 64 + lane;
       const bool ok = r < cnt;
       const uint32_t rr = ok ? r : 0u;
-      const int64_t sv = (int64_t)P.tsc[rr], iv = (int64_t)P.tid[rr];
-      const uint32_t ev = P.te[rr];
+      int64_t sv, iv;
+      uint32_t ev;
+      lb_tget(P, rr, sv, iv, ev);
       o.sc[t] = ok ? sv : INT64_MAX;
       o.id[t] = ok ? iv : INT64_MAX;
       o.e[t] = ok ? ev : 0xFFFFFFFFu;
@@ -893,6 +982,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     if (!lb_key_lt(ms, mi, rl64(o.sc[0], 0), rl64(o.id[0], 0))) return false;
   }
 
+  LB_MARK(0);
   uint32_t n = om.n, nex = 0;
   uint32_t nkd = 0;
   int64_t nid = 0, nsc = 0;
@@ -926,9 +1016,12 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     bool pend = v, mine = false;
     while (ballot(pend)) {
       if (pend) {
-        const uint32_t s = L.hslot[h];
+        // the slot's 32-bit word: one read, then (empty) one CAS on it
+        uint32_t* w = reinterpret_cast<uint32_t*>(&L.hslot[h & ~1u]);
+        const uint32_t sh = (h & 1u) * 16u, wv = *w;
+        const uint32_t s = (wv >> sh) & 0xFFFFu;
         if (s == 0) {
-          if (lb_claim(&L.hslot[h], 0x8000u | (uint32_t)lane)) {
+          if (atomicCAS(w, wv, wv | ((0x8000u | (uint32_t)lane) << sh)) == wv) {
             pend = false;
             mine = true;
             slot = h;
@@ -959,6 +1052,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     n += (uint32_t)__builtin_popcountll(cm);
     wave_lds_sync();
     if (v && e == 0xFFFFFFFFu) e = (uint32_t)L.hslot[slot] - 1u;
+    LB_MARK(1);
     // ---- runs of adds between the chunk's bans
     const uint64_t bm = ballot(v && kd == 2);
     for (uint32_t j = 0; j < cn;) {
@@ -983,12 +1077,23 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
         const bool up = lead && st == LB_OBS;
         // an Observed entry's rank: its old key's place in the sorted table
         const uint32_t dr = up ? lb_rank(P, o.n, ob, id) : 0u;
+        LB_MARK(2);
         if (ballot(lead)) {
+#ifdef TRMV_PROF
+          {
+            const unsigned long long nl = (unsigned long long)__builtin_popcountll(ballot(lead));
+            if (lane == 0 && (k & 63u) == 3) {
+              atomicAdd(&g_lb_prof[6], 1ull);
+              atomicAdd(&g_lb_prof[7], nl);
+            }
+          }
+#endif
           const int32_t pos = lb_merge<ET>(o, P, L, K, up, dr, lead, nbst, id, e);
           if (lead) L.est[e] = pos >= 0 ? LB_OBS : LB_MASKED;
         }
         if (act && !rel && st == LB_NEW) L.est[e] = LB_MASKED;  // Masked[Id] (:243-250)
         wave_lds_sync();
+        LB_MARK(3);
       }
       if (hi >= cn) break;
       // ---- ban/2 at hi (:264-286)
@@ -1030,6 +1135,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       }
       if (lane == 0) L.est[xe] = LB_BANNED;
       wave_lds_sync();
+      LB_MARK(4);
       j = hi + 1;
     }
   }
@@ -1046,6 +1152,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     a.meta_out[k] = m;
     a.ex_cnt[k] = nex;
   }
+  LB_MARK(5);
   return true;
 }
 
@@ -1871,3 +1978,14 @@ int topk_launch_value(const TopkValueArgs& a, int cls, uint64_t n_work, hipStrea
 }
 
 }  // namespace ccrdt
+
+#ifdef TRMV_PROF
+extern "C" int ccrdt_debug_lb_prof(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(ccrdt::g_lb_prof), 16 * 8) != hipSuccess) return 4;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ccrdt::g_lb_prof), z, sizeof(z)) != hipSuccess) return 4;
+  }
+  return 0;
+}
+#endif
