@@ -154,11 +154,22 @@ __device__ __forceinline__ uint32_t wave_excl_scan_dpp(uint32_t v, uint32_t& tot
   return inc - v;
 }
 // Orders one wavefront's LDS accesses across lanes without a workgroup
-// barrier (the LDS executes a wave's DS instructions in issue order; this
-// only stops the compiler from moving them across the point).
+// barrier.  The LDS executes (and returns) a wave's DS instructions in issue
+// order, so a later DS instruction of the wave sees every earlier one's
+// effect; all this has to stop is the compiler moving accesses across the
+// point (it reasons per lane and cannot see that lanes share addresses).
+// No s_waitcnt: a wavefront-scope fence would wait for every outstanding DS
+// op (a full LDS round trip) at each such point.  -DCCRDT_LDS_FENCE builds
+// the fenced form instead.
 __device__ __forceinline__ void wave_lds_sync() {
+#ifdef CCRDT_LDS_FENCE
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+#else
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 // Wave maximum of an int64 (DPP, identity INT64_MIN), wave-uniform result.
