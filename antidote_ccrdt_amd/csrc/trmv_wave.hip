@@ -99,7 +99,7 @@ struct alignas(16) WaveLds {
   int64_t rows[W_RCAP][TRMV_DPAD];       // [0, old nr) old Removals rows, then rmv clocks
   unsigned long long vc[TRMV_DPAD + 2];  // replica Vc; [TRMV_DPAD] sink
   uint32_t pcnt2[W_PCAP / 2 + 4];        // ops per player (two u16 counters per word)
-  uint32_t rsrc[W_RCAP + 4];             // rmv_vc row of each rmv op of the key being prefetched
+  uint32_t rsrc[W_RCAP];                 // rmv_vc row of each rmv op of the key being prefetched
   uint16_t ekd[W_ECAP + 8];              // kind | dc << 2 | player << 8
   uint8_t hp[W_HCAP];                    // hash slot -> player
   uint8_t pslot[W_PCAP + 8];             // player -> hash slot
@@ -267,7 +267,11 @@ template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
                                               WaveLds<FRESH>& L, bool has_next, const ChunkHdr& hdr,
                                               uint32_t nj, KeyIn& nxt) {
-  const int lane = lane_id();
+  // opaque per key: lane-derived addresses are formed where they are used
+  // instead of being hoisted out of the key loop into VGPR pairs that live
+  // (and spill) across every key
+  int lane = lane_id();
+  asm volatile("" : "+v"(lane));
   const int D = a.n_dc;
 #ifdef TRMV_PROF
   unsigned long long prof_t;
@@ -275,7 +279,12 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #endif
   const uint64_t op0 = in.op0;
   const uint32_t nops = in.nops;
-  const KeyMeta nmeta = in.nmeta;
+  // the new-side offsets are wave-uniform: SGPRs, so every output address is
+  // a scalar base plus a 32-bit lane offset (no 64-bit VGPR bases to spill)
+  KeyMeta nmeta = in.nmeta;
+  nmeta.p_off = __builtin_amdgcn_readfirstlane(nmeta.p_off);
+  nmeta.m_off = __builtin_amdgcn_readfirstlane(nmeta.m_off);
+  nmeta.r_off = __builtin_amdgcn_readfirstlane(nmeta.r_off);
   KeyMeta om;
   if (FRESH) {
     om.p_off = om.m_off = om.r_off = 0;
@@ -647,6 +656,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t st = L.pstart[p], c = act ? pcnt_of(L, p) : 0u;
       const uint32_t me = q - st;
       bool fb = false, beaten = false, risk = false, seen = false, first = true;
+      bool gbeaten = false, gtie = false;  // gb_sets:largest of the segment (by Score; a tie replays)
       const uint32_t maxc = wave_max_u32_dpp(c);
       // software-pipelined: position x+1 is read while position x's clock
       // entry (its address depends on x's element) is in flight
@@ -671,12 +681,19 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         first &= !(isr && before);
         risk = risk && !isr;
         beaten = beaten && !isr;
+        gbeaten = gbeaten && !isr;
+        gtie = gtie && !isr;
         const bool both = ya && valid && !isr;
         risk |= both && before && tx >= tm;
         beaten |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
+        gbeaten |= both && sx > sm;
+        gtie |= both && sx == sm;
       }
-      if (act && (fb || risk)) L.pflag[p] = 1;
+      // equal Scores in the last segment: gb_sets order goes on to DcId and
+      // Ts, which the replay settles
+      if (act && (fb || risk || (ya && !seen && gtie))) L.pflag[p] = 1;
       if (ya && !seen && !beaten) L.pobs[p] = (uint8_t)q;
+      if (ya && !seen && !gbeaten) L.pgb[p] = (uint8_t)q;  // largest of the last segment (by Score)
       if (yr && first) L.prow[p] = (uint8_t)sm;  // a rmv's "score" is its clock row
       if (yr && !seen) L.plr[p] = (uint8_t)(q + 1);
       if (act) mrg[k] = (uint8_t)(yr && !first);
@@ -919,15 +936,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
       const int64_t id = (int64_t)L.htab[L.pslot[pp]];
-      // gb_sets:largest of a decided player's slab (its last segment, strictly
-      // rising Ts, so no two elements tie): term order (Score, DcId, Ts)
-      uint32_t gb = replayed ? (uint32_t)L.pgb[pp] - off : 0u;
-      if (!replayed && cnt > 1)
-        for (uint32_t j = 1; j < cnt; ++j) {
-          const int64_t s2 = L.esc[off + j], t2 = L.ets[off + j], bs = L.esc[off + gb], bt = L.ets[off + gb];
-          const uint32_t d2 = (L.ekd[off + j] >> 2) & 7u, bd = (L.ekd[off + gb] >> 2) & 7u;
-          if (s2 > bs || (s2 == bs && (d2 > bd || (d2 == bd && t2 > bt)))) gb = j;
-        }
+      // gb_sets:largest of the slab: step 5 (a decided player: its last
+      // segment, strictly rising Ts, so no two elements tie) or 5b (replayed)
+      const uint32_t gb = (replayed || cnt > 1) ? (uint32_t)L.pgb[pp] - off : 0u;
       if (act) {
         (a.new_s.pl_id + nmeta.p_off)[p] = id;
         (a.new_s.pl_slab + nmeta.p_off)[p] = off | (cnt << 16);
