@@ -115,6 +115,10 @@ SIGNATURES = {
     "ccrdt_timer_start": (INT, [P]),
     "ccrdt_timer_stop": (INT, [P, C.POINTER(C.c_float)]),
     "ccrdt_trmv_apply": (INT, [P, C.POINTER(TrmvOps), C.POINTER(TrmvExtra)]),
+    # ccrdt_*_batch outputs share the layout of the ops structs
+    "ccrdt_trmv_compact": (INT, [INT, I64, C.POINTER(TrmvOps), C.POINTER(TrmvOps)]),
+    "ccrdt_lb_compact": (INT, [I64, C.POINTER(LbOps), C.POINTER(LbOps)]),
+    "ccrdt_avg_compact": (INT, [I64, C.POINTER(AvgOps), C.POINTER(AvgOps)]),
     "ccrdt_trmv_apply_device": (INT, [P, C.POINTER(TrmvOps)]),
     "ccrdt_trmv_extra_count": (INT, [P, C.POINTER(I64)]),
     "ccrdt_trmv_fetch_extra": (INT, [P, C.POINTER(TrmvExtra)]),

@@ -392,6 +392,25 @@ class TopkRmvEngine(_Engine):
         return out, vc
 
 
+def compact_trmv(b: TrmvBatch, n_dc: int) -> TrmvBatch:
+    """Host log compaction of a batch before upload (ccrdt_trmv_compact): per
+    key, can_compact/2 + compact_ops/2 (topk_rmv.erl:178-223) folded over
+    adjacent effects; every output rmv gets its own clock row."""
+    b = b.normalized()
+    n, nk = b.n_ops, b.n_keys
+    out = TrmvBatch(np.zeros(nk + 1, np.uint64), np.zeros(n, np.uint8), np.zeros(n, np.int64),
+                    np.zeros(n, np.int64), np.zeros(n, np.uint8), np.zeros(n, np.int64),
+                    np.zeros((max(n, 1), n_dc), np.int64))
+    ci = _lib.TrmvOps(n, int(b.rmv_vc.shape[0]), ptr(b.key_ptr), ptr(b.kind), ptr(b.id), ptr(b.score),
+                      ptr(b.dc), ptr(b.ts), ptr(b.rmv_vc))
+    co = _lib.TrmvOps(0, 0, ptr(out.key_ptr), ptr(out.kind), ptr(out.id), ptr(out.score), ptr(out.dc),
+                      ptr(out.ts), ptr(out.rmv_vc))
+    check(lib.ccrdt_trmv_compact(n_dc, nk, C.byref(ci), C.byref(co)), "trmv_compact")
+    m, r = int(co.n_ops), int(co.n_rmv_rows)
+    return TrmvBatch(out.key_ptr, out.kind[:m].copy(), out.id[:m].copy(), out.score[:m].copy(),
+                     out.dc[:m].copy(), out.ts[:m].copy(), out.rmv_vc[:r].copy())
+
+
 def gen_trmv(n_ops: int, n_keys: int, n_dc: int = 8, n_players: int = 256,
              score_max: int = 10**6, rmv_pm: int = 100, lag_max: int = 64, dup_pm: int = 0,
              swap_pm: int = 0, seed: int = 0xCC0DE + 2, clock0: int = 0) -> TrmvBatch:

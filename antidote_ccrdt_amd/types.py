@@ -314,3 +314,30 @@ class DeviceBatch:
     def close(self):
         for b in self.bufs.values():
             b.close()
+
+
+def compact_lb(key_ptr, kind, id, score):
+    """Host log compaction of a leaderboard batch (ccrdt_lb_compact,
+    leaderboard.erl:163-205).  Returns (key_ptr, kind, id, score)."""
+    kp, kd, i, sc = (_c(key_ptr, np.uint64), _c(kind, np.uint8), _c(id, np.int64), _c(score, np.int64))
+    n, nk = kd.shape[0], kp.shape[0] - 1
+    okp, okd, oi, osc = np.zeros(nk + 1, np.uint64), np.zeros(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64)
+    co = _lib.LbOps(0, ptr(okp), ptr(okd), ptr(oi), ptr(osc))
+    check(lib.ccrdt_lb_compact(nk, C.byref(_lib.LbOps(n, ptr(kp), ptr(kd), ptr(i), ptr(sc))), C.byref(co)),
+          "lb_compact")
+    m = int(co.n_ops)
+    return okp, okd[:m].copy(), oi[:m].copy(), osc[:m].copy()
+
+
+def compact_avg(key_ptr, value, n):
+    """Host log compaction of an average batch (ccrdt_avg_compact,
+    average.erl:122-127): one {add, {Sum V, Sum N}} per key.  Returns
+    (key_ptr, value, n)."""
+    kp, v, nn = _c(key_ptr, np.uint64), _c(value, np.int64), _c(n, np.int64)
+    nk = kp.shape[0] - 1
+    okp, ov, on = np.zeros(nk + 1, np.uint64), np.zeros(v.shape[0], np.int64), np.zeros(v.shape[0], np.int64)
+    co = _lib.AvgOps(0, ptr(okp), ptr(ov), ptr(on))
+    check(lib.ccrdt_avg_compact(nk, C.byref(_lib.AvgOps(v.shape[0], ptr(kp), ptr(v), ptr(nn))), C.byref(co)),
+          "avg_compact")
+    m = int(co.n_ops)
+    return okp, ov[:m].copy(), on[:m].copy()

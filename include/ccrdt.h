@@ -142,6 +142,26 @@ typedef struct {
   const int64_t* rmv_vc;   /* [n_rmv_rows * n_dc] */
 } ccrdt_trmv_ops;
 
+/* Host log compaction before upload: per key, can_compact/2
+ * + compact_ops/2 (topk_rmv.erl:178-223) folded over adjacent effects in
+ * stream order (an effect is tried once against the last kept one; {noop}
+ * halves are dropped).  `out` arrays have the input's capacity (n_ops ops,
+ * n_ops * n_dc clock values); out->key_ptr has n_keys + 1 entries.  Every
+ * output rmv gets its own clock row (merged Vcs included), numbered in
+ * stream order; out->n_ops / out->n_rmv_rows are set.  Host only. */
+typedef struct {
+  int64_t n_ops;
+  int64_t n_rmv_rows;
+  uint64_t* key_ptr;
+  uint8_t* kind;
+  int64_t* id;
+  int64_t* score;
+  uint8_t* dc;
+  int64_t* ts;
+  int64_t* rmv_vc;
+} ccrdt_trmv_batch;
+int ccrdt_trmv_compact(int n_dc, int64_t n_keys, const ccrdt_trmv_ops* in, ccrdt_trmv_batch* out);
+
 /* Extra effects ({ok, State, [Effect]}, at most one per op — SURVEY Q3),
  * indexed by op.  kind[i] = CCRDT_NOOP when op i returned {ok, State}.
  *   CCRDT_TRMV_ADD -> {add, {Id, Score, {Dc, Ts}}}   promotion (topk_rmv.erl:295)
@@ -248,6 +268,15 @@ typedef struct {
 } ccrdt_avg_ops;
 /* update/2 over a batch (host arrays).  Sums that leave int64 give ERANGE. */
 int ccrdt_avg_apply(ccrdt_engine* e, const ccrdt_avg_ops* ops);
+/* Host log compaction (average.erl:122-127): every pair compacts, so each
+ * key's effects become one {add, {Sum V, Sum N}}; ERANGE past int64. */
+typedef struct {
+  int64_t n_ops;
+  uint64_t* key_ptr;
+  int64_t* value;
+  int64_t* n;
+} ccrdt_avg_batch;
+int ccrdt_avg_compact(int64_t n_keys, const ccrdt_avg_ops* in, ccrdt_avg_batch* out);
 int ccrdt_avg_apply_device(ccrdt_engine* e, const ccrdt_avg_ops* dev_ops);
 /* State {Sum, Num} of every key (to_binary/from_binary analogues). */
 int ccrdt_avg_export(ccrdt_engine* e, int64_t* sum, int64_t* num);
@@ -301,6 +330,17 @@ typedef struct {
   const int64_t* id;       /* [n_ops] */
   const int64_t* score;    /* [n_ops] (ignored for ban) */
 } ccrdt_lb_ops;
+/* Host log compaction (leaderboard.erl:163-205), folded like
+ * ccrdt_trmv_compact: of two adds of one Id the higher score survives, a ban
+ * absorbs an earlier add or ban of its Id. */
+typedef struct {
+  int64_t n_ops;
+  uint64_t* key_ptr;
+  uint8_t* kind;
+  int64_t* id;
+  int64_t* score;
+} ccrdt_lb_batch;
+int ccrdt_lb_compact(int64_t n_keys, const ccrdt_lb_ops* in, ccrdt_lb_batch* out);
 /* Extra effects, op-indexed: kind CCRDT_LB_ADD = {add, {Id, Score}} from a
  * ban that promoted a Masked player (:279-283), CCRDT_NOOP = none. */
 typedef struct {
