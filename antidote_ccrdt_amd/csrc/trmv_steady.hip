@@ -462,11 +462,14 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP, RK>& L, uint32
     const int x = (int)__builtin_ctzll(im);
     im &= im - 1;
     const int64_t xs = rl64(is, x), xi = rl64(iid, x);
-    li0 += key_lt(xs, xi, o.sc[0], o.id[0]) ? 1u : 0u;
-    li1 += key_lt(xs, xi, o.sc[1], o.id[1]) ? 1u : 0u;
+    const bool lt0 = key_lt(xs, xi, o.sc[0], o.id[0]), lt1 = key_lt(xs, xi, o.sc[1], o.id[1]);
+    li0 += lt0 ? 1u : 0u;
+    li1 += lt1 ? 1u : 0u;
     ri += (ins && key_lt(xs, xi, is, iid)) ? 1u : 0u;
-    const uint32_t c = (uint32_t)__builtin_popcountll(ballot(v0 && key_lt(o.sc[0], o.id[0], xs, xi))) +
-                       (uint32_t)__builtin_popcountll(ballot(v1 && key_lt(o.sc[1], o.id[1], xs, xi)));
+    // table entries below the insert: the kept entries have other Ids than
+    // the inserted ones, so their keys differ and "below" is "not above"
+    const uint32_t c = (uint32_t)__builtin_popcountll(ballot(v0 && !lt0)) +
+                       (uint32_t)__builtin_popcountll(ballot(v1 && !lt1));
     lo = lane == x ? c : lo;
   }
   const uint64_t dm0 = ballot(d0), dm1 = ballot(d1);
@@ -1117,12 +1120,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
             // else it competes for a place (:317-331)
             const bool up = mine && (f & F_OBS) && (scr > os || (scr == os && tsr > ot));
             const bool en = mine && !(f & F_OBS);
-            uint32_t dr = 0;
-            for (uint64_t t = ballot(up); t; t &= t - 1) {
-              const int x = (int)__builtin_ctzll(t);
-              const uint32_t r = ot_find(ob, rl32(kdr, x) >> 8);
-              dr = lane == x ? r : dr;
-            }
+            const uint32_t dr = rq;  // an Observed player's rank (ork)
             SPROF(14);
             const int32_t pos = ot_merge<PCAP, RANKED>(ob, L, K, up, dr, up || en, scr, id, tsr, q);
             SPROF(15);
