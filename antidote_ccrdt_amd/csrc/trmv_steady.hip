@@ -375,16 +375,28 @@ __device__ __forceinline__ uint32_t s_promote(const SLds<PCAP, RK>& L, uint32_t 
   const int lane = lane_id();
   uint32_t bp = S_NONE;
   int64_t bs = INT64_MIN, bi = INT64_MIN;
-  for (uint32_t b = 0; b < np; b += 64) {
-    const uint32_t p = b + lane;
-    const uint32_t q = p < np ? p : (uint32_t)PCAP;
-    const uint32_t f = L.opd[q];
-    const bool ok = p < np && !(f & F_OBS) && (f & F_HASM);
-    const int64_t sc = L.gsc[q], id = L.pid[q];
-    if (ok && (bp == S_NONE || sc > bs || (sc == bs && id > bi))) {
-      bp = p;
-      bs = sc;
-      bi = id;
+  // four slots of players per round, their loads issued together (one LDS
+  // round trip per round instead of one per slot)
+  for (uint32_t b0 = 0; b0 < np; b0 += 256) {
+    uint32_t f[4];
+    int64_t sc[4], id[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t p = b0 + 64 * u + lane;
+      const uint32_t q = p < np ? p : (uint32_t)PCAP;
+      f[u] = L.opd[q];
+      sc[u] = L.gsc[q];
+      id[u] = L.pid[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t p = b0 + 64 * u + lane;
+      const bool ok = p < np && !(f[u] & F_OBS) && (f[u] & F_HASM);
+      if (ok && (bp == S_NONE || sc[u] > bs || (sc[u] == bs && id[u] > bi))) {
+        bp = p;
+        bs = sc[u];
+        bi = id[u];
+      }
     }
   }
   const bool has = bp != S_NONE;
