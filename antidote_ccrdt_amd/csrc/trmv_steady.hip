@@ -599,53 +599,66 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   }
   wave_lds_sync();
 
-  // ---- K1. old players
+  // ---- K1. old players: four slots per round, each round's HBM loads
+  // issued together (records, then the Obs[Id] / largest elements they name)
   uint32_t span = 0;
-  for (uint32_t b = 0; b < om.np; b += 64) {
-    const uint32_t p = b + lane;
-    if (p < om.np) {
-      const uint64_t pp = (uint64_t)om.p_off + p;
-      const int64_t id = a.old_s.pl_id[pp];
-      const uint32_t info = a.old_s.pl_info[pp], slab = a.old_s.pl_slab[pp];
-      const uint32_t gb = (slab >> 16) > 1 ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
-      const uint32_t off = slab & 0xFFFFu, cnt = slab >> 16, ob = info & 0xFFFFu;
+  for (uint32_t b0 = 0; b0 < om.np; b0 += 256) {
+    int64_t id[4];
+    uint32_t info[4], slab[4], gb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t p = b0 + 64 * u + lane;
+      const uint64_t pp = (uint64_t)om.p_off + (p < om.np ? p : 0u);
+      const bool v = p < om.np;
+      id[u] = v ? a.old_s.pl_id[pp] : 0;
+      info[u] = v ? a.old_s.pl_info[pp] : NONE32;
+      slab[u] = v ? a.old_s.pl_slab[pp] : 0u;
+      gb[u] = (v && (slab[u] >> 16) > 1) ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
+    }
+    int64_t os[4], ot[4], gs[4], gt[4];
+    uint32_t od[4], gd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
       const uint64_t g0 = (uint64_t)om.m_off + off;
-      int64_t os = 0, ot = 0, gs = 0, gt = 0;
-      uint32_t od = 0, gd = 0;
-      if (ob != NONE16) {
-        os = a.old_s.m_score[g0 + ob];
-        ot = a.old_s.m_ts[g0 + ob];
-        od = a.old_s.m_dc[g0 + ob];
-      }
-      if (cnt) {
-        gs = a.old_s.m_score[g0 + gb];
-        gt = a.old_s.m_ts[g0 + gb];
-        gd = a.old_s.m_dc[g0 + gb];
-      }
-      L.pid[p] = id;
-      L.oslab[p] = slab;
-      L.orow[p] = info;
-      L.u.k.nops[p] = 0u;
-      if constexpr (RANKED) {  // Observed's entries, gathered for the build
-        if (ob != NONE16) {
-          const uint32_t k = atomicAdd(&L.nob, 1u);
-          L.tsc[k] = os;
-          L.tid[k] = id;
-          L.tts[k] = ot;
-          L.tp[k] = (uint16_t)p;
+      const bool ho = obx != NONE16, hg = cnt != 0;
+      os[u] = ho ? a.old_s.m_score[g0 + obx] : 0;
+      ot[u] = ho ? a.old_s.m_ts[g0 + obx] : 0;
+      od[u] = ho ? (uint32_t)a.old_s.m_dc[g0 + obx] : 0u;
+      gs[u] = hg ? a.old_s.m_score[g0 + gb[u]] : 0;
+      gt[u] = hg ? a.old_s.m_ts[g0 + gb[u]] : 0;
+      gd[u] = hg ? (uint32_t)a.old_s.m_dc[g0 + gb[u]] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t p = b0 + 64 * u + lane;
+      if (p < om.np) {
+        const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
+        L.pid[p] = id[u];
+        L.oslab[p] = slab[u];
+        L.orow[p] = info[u];
+        L.u.k.nops[p] = 0u;
+        if constexpr (RANKED) {  // Observed's entries, gathered for the build
+          if (obx != NONE16) {
+            const uint32_t k = atomicAdd(&L.nob, 1u);
+            L.tsc[k] = os[u];
+            L.tid[k] = id[u];
+            L.tts[k] = ot[u];
+            L.tp[k] = (uint16_t)p;
+          }
+        } else {
+          L.osc[p] = os[u];
+          L.ots[p] = ot[u];
         }
-      } else {
-        L.osc[p] = os;
-        L.ots[p] = ot;
+        L.gsc[p] = gs[u];
+        L.gts[p] = gt[u];
+        L.opd[p] = (obx != NONE16 ? F_OBS : 0u) | (cnt ? F_HASM : 0u) |
+                   ((info[u] >> 16) != NONE16 ? F_ROWV : 0u) | (od[u] << 8) | (obx << 16);
+        L.gpd[p] = (gd[u] << 8) | (gb[u] << 16);
+        span = off + cnt > span ? off + cnt : span;
+        uint32_t h = shash<PCAP>(id[u]);
+        while (hs_cas(L, h, HSlot<PCAP>::NONE, p) != HSlot<PCAP>::NONE) h = (h + 1) & (HS - 1);
       }
-      L.gsc[p] = gs;
-      L.gts[p] = gt;
-      L.opd[p] = (ob != NONE16 ? F_OBS : 0u) | (cnt ? F_HASM : 0u) |
-                 ((info >> 16) != NONE16 ? F_ROWV : 0u) | (od << 8) | (ob << 16);
-      L.gpd[p] = (gd << 8) | (gb << 16);
-      span = off + cnt > span ? off + cnt : span;
-      uint32_t h = shash<PCAP>(id);
-      while (hs_cas(L, h, HSlot<PCAP>::NONE, p) != HSlot<PCAP>::NONE) h = (h + 1) & (HS - 1);
     }
   }
   span = wave_max_u32_dpp(span);
@@ -692,15 +705,23 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   // ---- K3. old slabs (except replayed players') and old Removals rows
   if (!a.fresh && span) {
     int32_t prev = -1;  // owner of the position before the window
+    // the next window's elements load while this one is placed
+    int64_t nsc = 0, nts = 0;
+    uint32_t ndc = 0;
+    if ((uint32_t)lane < span) {
+      nsc = a.old_s.m_score[(uint64_t)om.m_off + lane];
+      nts = a.old_s.m_ts[(uint64_t)om.m_off + lane];
+      ndc = a.old_s.m_dc[(uint64_t)om.m_off + lane];
+    }
     for (uint32_t q0 = 0; q0 < span; q0 += 64) {
       const uint32_t q = q0 + lane;
-      const uint64_t src = (uint64_t)om.m_off + q;
-      int64_t sc = 0, ts = 0;
-      uint32_t dc = 0;
-      if (q < span) {
-        sc = a.old_s.m_score[src];
-        ts = a.old_s.m_ts[src];
-        dc = a.old_s.m_dc[src];
+      const int64_t sc = nsc, ts = nts;
+      const uint32_t dc = ndc;
+      if (q + 64 < span) {
+        const uint64_t src = (uint64_t)om.m_off + q + 64;
+        nsc = a.old_s.m_score[src];
+        nts = a.old_s.m_ts[src];
+        ndc = a.old_s.m_dc[src];
       }
       L.u.c.mark[lane] = 0u;
       wave_lds_sync();
