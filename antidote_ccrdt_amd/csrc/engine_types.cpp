@@ -1093,9 +1093,10 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   const uint64_t words_old = e->fresh ? 0 : top[1], arena_used = e->fresh ? 0 : top[0];
   // arena: room for every byte of the batch (upper bound of new word bytes)
-  if (arena_used + docs->n_bytes > T.arena_cap) {
+  // (+32: the verify pass reads three aligned 8-byte words around a word)
+  if (arena_used + docs->n_bytes + 32 > T.arena_cap) {
     DevBuf grown;
-    const uint64_t cap = std::max<uint64_t>(2 * (arena_used + docs->n_bytes), 4096);
+    const uint64_t cap = std::max<uint64_t>(2 * (arena_used + docs->n_bytes) + 32, 4096);
     CCRDT_TRY(grown.ensure(cap));
     if (arena_used)
       CCRDT_HIP(hipMemcpyAsync(grown.p, T.arena.p, arena_used, hipMemcpyDeviceToDevice, e->stream));
@@ -1157,21 +1158,33 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       set_error("wc_apply: word table overflow");
       return CCRDT_ENOMEM;
     }
-    // exactness: every token equals its word's representative
+    // the batch's new words into the arena first (the verify pass then
+    // compares every token against a compact, cache-resident copy)
     a.doc_key = T.stage[0].as<uint64_t>();
     a.doc_off = docs->doc_off;
     a.n_docs = (int64_t)nd;
     a.tile_ptr = T.stage[4].as<uint64_t>();
     a.tile0 = 0;
+    a.arena = T.arena.as<uint8_t>();
+    CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
+    CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));
+    // exactness: every token equals its word's representative
+    {
+      const char* dg = getenv("CCRDT_WC_DBG");
+      a.dbg = dg ? atoi(dg) : 0;
+    }
     CCRDT_TRY(wc_launch_verify(a, tptr[nd], e->stream));
     CCRDT_TRY(read_status(e, st));
     if (st[1]) {
+      // the state is unchanged: the new table side is dropped, the arena
+      // top goes back to the words it held
+      const uint64_t back[2] = {arena_used, words_old};
+      CCRDT_TRY(h2d(T.arena_top, back, 16, e->stream));
+      CCRDT_HIP(hipStreamSynchronize(e->stream));
       set_error(st[1] & 1 ? "wc_apply: 64-bit word hash collision between distinct words"
                           : "wc_apply: token lost (table overflow)");
       return CCRDT_ERANGE;
     }
-    CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
-    CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));
     CCRDT_HIP(hipStreamSynchronize(e->stream));
     break;
   }

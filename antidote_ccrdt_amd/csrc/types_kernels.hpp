@@ -153,6 +153,7 @@ struct WcArgs {
   uint64_t* d_hash;
   uint64_t d_mask;
   uint32_t* status;          // [0] table overflow, [1] hash collision
+  int32_t dbg;               // diagnostic (CCRDT_WC_DBG): 1 verify without the byte compare, 2 without the probe
 };
 
 }  // namespace ccrdt
