@@ -25,7 +25,7 @@ struct TypeBufs {
   DevBuf lb_meta[2], lb_id[2], lb_score[2], lb_st[2];
   // wordcount / worddocumentcount: word table (open addressing on the
   // 64-bit word hash) + byte arena of the words
-  DevBuf t_hash[2], t_key[2], t_len[2], t_pos[2], t_arena[2], t_cnt[2];
+  DevBuf t_tab[2], t_cnt[2];  // word table: WcSlot[t_slots], counts[t_slots]
   uint64_t t_slots[2] = {0, 0};
   DevBuf arena, arena_top, d_hash;
   uint64_t arena_cap = 0;

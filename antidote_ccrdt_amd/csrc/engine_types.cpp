@@ -41,8 +41,8 @@ int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_
                          hipStream_t st);
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
                     int verify, hipStream_t st);
-int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
-                     const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st);
+int wc_launch_rehash(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
+                     hipStream_t st);
 }  // namespace ccrdt
 
 using namespace ccrdt;
@@ -108,8 +108,7 @@ void ccrdt_engine::release_types() {
   for (int s = 0; s < 2; ++s) {
     for (DevBuf* d : {&tb.avg_sum[s], &tb.avg_num[s], &tb.tk_off[s], &tb.tk_cnt[s], &tb.tk_id[s],
                       &tb.tk_score[s], &tb.lb_meta[s], &tb.lb_id[s], &tb.lb_score[s], &tb.lb_st[s],
-                      &tb.t_hash[s], &tb.t_key[s], &tb.t_len[s], &tb.t_pos[s], &tb.t_arena[s],
-                      &tb.t_cnt[s]})
+                      &tb.t_tab[s], &tb.t_cnt[s]})
       d->release();
   }
   for (DevBuf* d : {&tb.hb_off, &tb.hb_cap, &tb.hb_a, &tb.hb_b, &tb.hb_c, &tb.hb_d})
@@ -147,10 +146,8 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
                           {&tb.tk_cnt[c], &s.tk_cnt[c]}, {&tb.tk_id[c], &s.tk_id[c]},
                           {&tb.tk_score[c], &s.tk_score[c]}, {&tb.lb_meta[c], &s.lb_meta[c]},
                           {&tb.lb_id[c], &s.lb_id[c]}, {&tb.lb_score[c], &s.lb_score[c]},
-                          {&tb.lb_st[c], &s.lb_st[c]}, {&tb.t_hash[c], &s.t_hash[c]},
-                          {&tb.t_key[c], &s.t_key[c]}, {&tb.t_len[c], &s.t_len[c]},
-                          {&tb.t_pos[c], &s.t_pos[c]}, {&tb.t_arena[c], &s.t_arena[c]},
-                          {&tb.t_cnt[c], &s.t_cnt[c]}, {&tb.arena, &s.arena},
+                          {&tb.lb_st[c], &s.lb_st[c]}, {&tb.t_tab[c], &s.t_tab[c]}, {&tb.t_cnt[c], &s.t_cnt[c]},
+                          {&tb.arena, &s.arena},
                           {&tb.arena_top, &s.arena_top}})
       CCRDT_TRY(copy_buf(*dd, *ss, stream));
     tb.t_slots[c] = s.t_slots[c];
@@ -1029,11 +1026,7 @@ static WcArgs wc_table_args(ccrdt_engine* e, int side) {
   WcArgs a{};
   a.n_keys = e->n_keys;
   a.wdc = e->type == CCRDT_WORDDOCUMENTCOUNT;
-  a.t_hash = T.t_hash[side].as<uint64_t>();
-  a.t_key = T.t_key[side].as<uint32_t>();
-  a.t_len = T.t_len[side].as<uint32_t>();
-  a.t_pos = T.t_pos[side].as<uint64_t>();
-  a.t_arena = T.t_arena[side].as<uint64_t>();
+  a.t = T.t_tab[side].as<WcSlot>();
   a.t_cnt = T.t_cnt[side].as<unsigned long long>();
   a.t_mask = T.t_slots[side] ? T.t_slots[side] - 1 : 0;
   a.arena = T.arena.as<uint8_t>();
@@ -1043,13 +1036,9 @@ static WcArgs wc_table_args(ccrdt_engine* e, int side) {
 
 static int wc_alloc_table(ccrdt_engine* e, int side, uint64_t slots) {
   TypeBufs& T = e->tb;
-  CCRDT_TRY(T.t_hash[side].ensure(slots * 8));
-  CCRDT_TRY(T.t_key[side].ensure(slots * 4));
-  CCRDT_TRY(T.t_len[side].ensure(slots * 4));
-  CCRDT_TRY(T.t_pos[side].ensure(slots * 8));
-  CCRDT_TRY(T.t_arena[side].ensure(slots * 8));
+  CCRDT_TRY(T.t_tab[side].ensure(slots * sizeof(WcSlot)));
   CCRDT_TRY(T.t_cnt[side].ensure(slots * 8));
-  CCRDT_HIP(hipMemsetAsync(T.t_hash[side].p, 0, slots * 8, e->stream));
+  CCRDT_HIP(hipMemsetAsync(T.t_tab[side].p, 0, slots * sizeof(WcSlot), e->stream));
   CCRDT_HIP(hipMemsetAsync(T.t_cnt[side].p, 0, slots * 8, e->stream));
   T.t_slots[side] = slots;
   return CCRDT_OK;
@@ -1113,9 +1102,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     CCRDT_TRY(wc_alloc_table(e, out, slots));
     WcArgs a = wc_table_args(e, out);
     if (!e->fresh && T.t_slots[in])
-      CCRDT_TRY(wc_launch_rehash(T.t_hash[in].as<uint64_t>(), T.t_key[in].as<uint32_t>(),
-                                 T.t_len[in].as<uint32_t>(), T.t_arena[in].as<uint64_t>(),
-                                 T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
     CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
     a.doc_off = docs->doc_off;
     a.bytes = docs->bytes;
@@ -1286,9 +1273,7 @@ static int wc_merge_core(ccrdt_engine* e, uint64_t nw, const uint64_t* wk, const
   CCRDT_TRY(wc_alloc_table(e, out, slots));
   WcArgs a = wc_table_args(e, out);
   if (!start_empty && T.t_slots[in])
-    CCRDT_TRY(wc_launch_rehash(T.t_hash[in].as<uint64_t>(), T.t_key[in].as<uint32_t>(),
-                               T.t_len[in].as<uint32_t>(), T.t_arena[in].as<uint64_t>(),
-                               T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+    CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
   CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
   a.bytes = bytes;
   a.n_bytes = nb;
@@ -1446,20 +1431,18 @@ int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint
   TypeBufs& T = e->tb;
   const int c = T.tcur;
   const uint64_t n = T.t_slots[c];
-  std::vector<uint64_t> h, ar, top;
-  std::vector<uint32_t> key, len;
+  std::vector<WcSlot> tab;
   std::vector<unsigned long long> cnt;
+  std::vector<uint64_t> top;
   std::vector<uint8_t> arena;
-  CCRDT_TRY(d2h(h, T.t_hash[c], n, e->stream));
-  CCRDT_TRY(d2h(key, T.t_key[c], n, e->stream));
-  CCRDT_TRY(d2h(len, T.t_len[c], n, e->stream));
-  CCRDT_TRY(d2h(ar, T.t_arena[c], n, e->stream));
+  CCRDT_TRY(d2h(tab, T.t_tab[c], n, e->stream));
   CCRDT_TRY(d2h(cnt, T.t_cnt[c], n, e->stream));
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   CCRDT_TRY(d2h(arena, T.arena, top[0], e->stream));
   std::vector<std::tuple<uint32_t, std::string, uint64_t>> words;
   for (uint64_t i = 0; i < n; ++i)
-    if (h[i]) words.emplace_back(key[i], std::string((const char*)arena.data() + ar[i], len[i]), cnt[i]);
+    if (tab[i].h)
+      words.emplace_back(tab[i].key, std::string((const char*)arena.data() + tab[i].ref, tab[i].len), cnt[i]);
   std::sort(words.begin(), words.end());
   uint64_t w = 0, b = 0, p = 0;
   for (uint64_t k = 0; k < nk; ++k) {

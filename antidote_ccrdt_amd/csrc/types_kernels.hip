@@ -1494,18 +1494,17 @@ __device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h
   for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
     // read first: a slot goes 0 -> h once, so a (possibly stale) nonzero
     // value is final and only an empty-looking slot needs the CAS
-    const uint64_t seen = __hip_atomic_load(&a.t_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (seen == h) return sl;
     if (seen != 0ull) {
       sl = (sl + 1) & a.t_mask;
       continue;
     }
-    const unsigned long long prev = atomicCAS((unsigned long long*)&a.t_hash[sl], 0ull, (unsigned long long)h);
+    const unsigned long long prev = atomicCAS(&a.t[sl].h, 0ull, (unsigned long long)h);
     if (prev == 0ull) {  // new word: this token is its representative
-      a.t_key[sl] = key;
-      a.t_len[sl] = len;
-      a.t_pos[sl] = pos;
-      a.t_arena[sl] = ~0ull;
+      a.t[sl].key = key;
+      a.t[sl].len = len;
+      a.t[sl].ref = WC_REF_BATCH | pos;
       return sl;
     }
     if (prev == h) return sl;
@@ -1654,28 +1653,29 @@ __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
     }
     // probe: the slot's fields are loaded together with its hash
     uint64_t sl = h & a.t_mask;
-    uint64_t th, tar, tpos;
+    uint64_t th, tref;
     uint32_t tk, tln;
     for (;;) {
-      th = a.t_hash[sl];
-      tar = a.t_arena[sl];
-      tpos = a.t_pos[sl];
-      tk = a.t_key[sl];
-      tln = a.t_len[sl];
+      const WcSlot ts = a.t[sl];
+      th = ts.h;
+      tref = ts.ref;
+      tk = ts.key;
+      tln = ts.len;
       if (th == h || th == 0ull) break;
       sl = (sl + 1) & a.t_mask;
     }
+    const bool tar = !(tref & WC_REF_BATCH);  // persisted: an arena offset
     if (th != h) {
       atomicOr(&a.status[1], 2u);  // lost token (table overflow)
       continue;
     }
-    const uint8_t* rep = tar != ~0ull ? a.arena + tar : a.bytes + tpos;
+    const uint8_t* rep = tar ? a.arena + tref : a.bytes + (tref & ~WC_REF_BATCH);
     bool eq = tk == key && tln == tl;
     if (a.dbg == 1) {
       if (!eq) atomicOr(&a.status[1], 1u);
       continue;
     }
-    if (eq && fast && tar != ~0ull) {
+    if (eq && fast && tar) {
       // the representative in the arena (persisted before this pass; the
       // arena keeps 32 bytes of slack past its top): three aligned 8-byte
       // loads against the token's registers
@@ -1708,14 +1708,15 @@ __global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
 // arena_top[1] counts the table's words.
 __global__ void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* arena_top) {
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
+  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
   atomicAdd(&arena_top[1], 1ull);
-  if (a.t_arena[sl] != ~0ull) return;
-  const uint32_t n = a.t_len[sl];
+  const uint64_t ref = a.t[sl].ref;
+  if (!(ref & WC_REF_BATCH)) return;
+  const uint32_t n = a.t[sl].len;
   const uint64_t at = atomicAdd(arena_top, (unsigned long long)n);
-  const uint8_t* src = a.bytes + a.t_pos[sl];
+  const uint8_t* src = a.bytes + (ref & ~WC_REF_BATCH);
   for (uint32_t j = 0; j < n; ++j) arena[at + j] = src[j];
-  a.t_arena[sl] = at;
+  a.t[sl].ref = at;
 }
 
 // token count of every document (sizes the worddocumentcount dedupe table)
@@ -1808,14 +1809,15 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
     return;
   }
   uint64_t sl = h & a.t_mask;
-  for (uint64_t probe = 0; probe <= a.t_mask && a.t_hash[sl] != h && a.t_hash[sl] != 0ull; ++probe)
+  for (uint64_t probe = 0; probe <= a.t_mask && a.t[sl].h != h && a.t[sl].h != 0ull; ++probe)
     sl = (sl + 1) & a.t_mask;
-  if (a.t_hash[sl] != h) {
+  if (a.t[sl].h != h) {
     atomicOr(&a.status[1], 2u);
     return;
   }
-  const uint8_t* rep = a.t_arena[sl] != ~0ull ? a.arena + a.t_arena[sl] : a.bytes + a.t_pos[sl];
-  bool eq = a.t_key[sl] == key && a.t_len[sl] == len;
+  const uint64_t ref = a.t[sl].ref;
+  const uint8_t* rep = !(ref & WC_REF_BATCH) ? a.arena + ref : a.bytes + (ref & ~WC_REF_BATCH);
+  bool eq = a.t[sl].key == key && a.t[sl].len == len;
   for (uint32_t j = 0; eq && j < len; ++j) eq = rep[j] == a.bytes[s + j];
   if (!eq) atomicOr(&a.status[1], 1u);
 }
@@ -1832,29 +1834,29 @@ __device__ __forceinline__ uint64_t wc_owner_mix(uint64_t z) {  // splitmix64
   return z ^ (z >> 31);
 }
 __device__ __forceinline__ uint32_t wc_slot_owner(const WcArgs& a, uint64_t sl, uint32_t world) {
-  const uint8_t* w = a.arena + a.t_arena[sl];
+  const uint8_t* w = a.arena + a.t[sl].ref;
   uint64_t f = 0xCBF29CE484222325ull;
-  for (uint32_t j = 0; j < a.t_len[sl]; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
-  return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)a.t_key[sl] * 0x9E3779B97F4A7C15ull)) % world);
+  for (uint32_t j = 0; j < a.t[sl].len; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
+  return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)a.t[sl].key * 0x9E3779B97F4A7C15ull)) % world);
 }
 __global__ void wc_owner_count_kernel(WcArgs a, uint32_t world, uint32_t* owner, unsigned long long* cur) {
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
+  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
   const uint32_t o = wc_slot_owner(a, sl, world);
   owner[sl] = o;
-  atomicAdd(&cur[o], (1ull << 40) + a.t_len[sl]);
+  atomicAdd(&cur[o], (1ull << 40) + a.t[sl].len);
 }
 __global__ void wc_owner_scatter_kernel(WcArgs a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
                                         uint8_t* out) {
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t_hash[sl] == 0ull) return;
-  const uint32_t len = a.t_len[sl];
+  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
+  const uint32_t len = a.t[sl].len;
   const unsigned long long c = atomicAdd(&cur[owner[sl]], (1ull << 40) + len);
   const uint64_t w = c >> 40, b = c & ((1ull << 40) - 1);
-  meta[w * 3] = a.t_key[sl];
+  meta[w * 3] = a.t[sl].key;
   meta[w * 3 + 1] = len;
   meta[w * 3 + 2] = (int64_t)a.t_cnt[sl];
-  const uint8_t* src = a.arena + a.t_arena[sl];
+  const uint8_t* src = a.arena + a.t[sl].ref;
   for (uint32_t j = 0; j < len; ++j) out[b + j] = src[j];
 }
 // rows (key, len, count) -> the merge kernel's per-word arrays
@@ -1898,25 +1900,22 @@ int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff,
 }
 
 // Re-insert the words of an old table into a fresh (larger) table.
-__global__ void wc_rehash_kernel(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen,
-                                 const uint64_t* oarena, const unsigned long long* ocnt, uint64_t on,
-                                 WcArgs a) {
+__global__ void wc_rehash_kernel(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, WcArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= on || oh[i] == 0ull) return;
-  uint64_t sl = oh[i] & a.t_mask;
-  while (atomicCAS((unsigned long long*)&a.t_hash[sl], 0ull, (unsigned long long)oh[i]) != 0ull)
-    sl = (sl + 1) & a.t_mask;
-  a.t_key[sl] = okey[i];
-  a.t_len[sl] = olen[i];
-  a.t_pos[sl] = 0;
-  a.t_arena[sl] = oarena[i];
+  if (i >= on) return;
+  const WcSlot o = old[i];
+  if (o.h == 0ull) return;
+  uint64_t sl = o.h & a.t_mask;
+  while (atomicCAS(&a.t[sl].h, 0ull, o.h) != 0ull) sl = (sl + 1) & a.t_mask;
+  a.t[sl].key = o.key;
+  a.t[sl].len = o.len;
+  a.t[sl].ref = o.ref;
   a.t_cnt[sl] = ocnt[i];
 }
-int wc_launch_rehash(const uint64_t* oh, const uint32_t* okey, const uint32_t* olen, const uint64_t* oarena,
-                     const unsigned long long* ocnt, uint64_t on, const WcArgs& a, hipStream_t st) {
+int wc_launch_rehash(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
+                     hipStream_t st) {
   if (!on) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_rehash_kernel, dim3((unsigned)((on + 255) / 256)), dim3(256), 0, st, oh, okey, olen,
-                     oarena, ocnt, on, a);
+  hipLaunchKernelGGL(wc_rehash_kernel, dim3((unsigned)((on + 255) / 256)), dim3(256), 0, st, old, ocnt, on, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -130,6 +130,22 @@ struct LbDownArgs {
 constexpr uint64_t WC_TILE = 4096;  // bytes of a document per wave step (64 per lane)
 constexpr uint64_t WC_TPW = 16;     // tiles per wave (a chunk)
 
+// A word-table slot: everything one probe or one compare needs lies in one
+// 32-byte record (one cache sector), not in five arrays.  The counts live in
+// their own array: the Zipf head's atomics would otherwise keep the lines
+// every probe reads busy.
+//   ref: the word's bytes, an arena offset once persisted, or
+//        WC_REF_BATCH | the batch byte position of its first occurrence
+struct alignas(32) WcSlot {
+  unsigned long long h;  // 0 = empty
+  uint64_t ref;
+  uint32_t key;
+  uint32_t len;
+  uint64_t spare;
+};
+static_assert(sizeof(WcSlot) == 32, "WcSlot is 32 bytes");
+constexpr uint64_t WC_REF_BATCH = 1ull << 63;
+
 struct WcArgs {
   int64_t n_keys;
   int64_t n_docs;
@@ -140,12 +156,8 @@ struct WcArgs {
   const uint8_t* bytes;
   uint64_t n_bytes;
   int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)
-  // word table (persistent across batches)
-  uint64_t* t_hash;          // 0 = empty
-  uint32_t* t_key;
-  uint32_t* t_len;
-  uint64_t* t_pos;           // batch byte position of first occurrence (this batch)
-  uint64_t* t_arena;         // arena offset (persistent words) or ~0
+  // word table (persistent across batches): one 32-byte slot per word
+  WcSlot* t;
   unsigned long long* t_cnt;
   uint64_t t_mask;
   const uint8_t* arena;
