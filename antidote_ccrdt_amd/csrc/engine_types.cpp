@@ -1063,11 +1063,19 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   CCRDT_TRY(T.stage[0].ensure(nd * 8 + 8));
   CCRDT_TRY(T.stage[1].ensure(nd * 8 + 8));
   CCRDT_TRY(wc_launch_doc_key(docs->key_ptr, nk, nd, T.stage[0].as<uint64_t>(), e->stream));
-  CCRDT_TRY(wc_launch_count(docs->doc_off, docs->bytes, nd, T.stage[1].as<uint64_t>(), e->stream));
+  // tokens per document: worddocumentcount sizes its (document, word) dedupe
+  // table by them; wordcount only sizes its word table, for which the bound
+  // bytes + documents will do (the table regrows if a batch overflows it)
   std::vector<uint64_t> ntok;
-  CCRDT_TRY(d2h(ntok, T.stage[1], nd, e->stream));
   uint64_t tokens = 0;
-  for (uint64_t t : ntok) tokens += t;
+  if (e->type == CCRDT_WORDDOCUMENTCOUNT) {
+    CCRDT_TRY(wc_launch_count(docs->doc_off, docs->bytes, nd, T.stage[1].as<uint64_t>(), e->stream));
+    CCRDT_TRY(d2h(ntok, T.stage[1], nd, e->stream));
+    for (uint64_t t : ntok) tokens += t;
+  } else {
+    ntok.assign(nd, 0);
+    tokens = docs->n_bytes + nd;
+  }
   // documents -> chunks of WC_TPW tiles of WC_TILE bytes (one wave each)
   std::vector<uint64_t> doff(nd + 1), tptr(nd + 1);
   if (nd) {
