@@ -1086,6 +1086,14 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   for (uint64_t d = 0; d < nd; ++d)
     tptr[d + 1] = tptr[d] + ((doff[d + 1] - doff[d]) / WC_TILE + WC_TPW) / WC_TPW;
   CCRDT_TRY(h2d(T.stage[4], tptr.data(), (nd + 1) * 8, e->stream));
+  if (nd > 0xFFFFFFFFull) {
+    set_error("wc_apply: more than 2^32 documents in one batch");
+    return CCRDT_EINVAL;
+  }
+  std::vector<uint32_t> cdoc(tptr[nd] + 1, 0u);  // chunk -> document (lives until the batch is done)
+  for (uint64_t d = 0; d < nd; ++d)
+    for (uint64_t c = tptr[d]; c < tptr[d + 1]; ++c) cdoc[c] = (uint32_t)d;
+  CCRDT_TRY(h2d(T.stage[5], cdoc.data(), cdoc.size() * 4, e->stream));
   std::vector<uint64_t> top;
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   const uint64_t words_old = e->fresh ? 0 : top[1], arena_used = e->fresh ? 0 : top[0];
@@ -1104,7 +1112,11 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     T.arena_cap = cap;
   }
   const int in = T.tcur, out = 1 - T.tcur;
-  uint64_t slots = pow2_at_least(2 * (words_old + std::min<uint64_t>(tokens, 1ull << 22)));
+  // (a batch's new words are guessed at <= 2^20: the table then stays
+  // resident in the 256 MiB Infinity Cache; a batch with more overflows it and
+  // is re-run on a table four times larger)
+  uint64_t slots = pow2_at_least(2 * (words_old + std::min<uint64_t>(tokens, 1ull << 20)));
+  if (getenv("CCRDT_WC_SLOTS")) slots = strtoull(getenv("CCRDT_WC_SLOTS"), nullptr, 0);
   for (int attempt = 0;; ++attempt) {
     // new table (rehash of the current words), then the batch
     CCRDT_TRY(wc_alloc_table(e, out, slots));
@@ -1131,6 +1143,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       a.doc_off = docs->doc_off + d0;
       a.tile_ptr = T.stage[4].as<uint64_t>() + d0;
       a.tile0 = tptr[d0];
+      a.chunk_doc = T.stage[5].as<uint32_t>();
+      a.doc0 = d0;
       if (a.wdc) {
         const uint64_t ds = pow2_at_least(2 * tk);
         CCRDT_TRY(T.d_hash.ensure(ds * 8));
@@ -1138,7 +1152,9 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.d_hash = T.d_hash.as<uint64_t>();
         a.d_mask = ds - 1;
       }
+      a.dbg = getenv("CCRDT_WC_IDBG") ? atoi(getenv("CCRDT_WC_IDBG")) : 0;
       CCRDT_TRY(wc_launch_insert(a, tptr[d1] - tptr[d0], e->stream));
+      a.dbg = 0;
       d0 = d1;
     }
     CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
@@ -1160,6 +1176,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     a.n_docs = (int64_t)nd;
     a.tile_ptr = T.stage[4].as<uint64_t>();
     a.tile0 = 0;
+    a.chunk_doc = T.stage[5].as<uint32_t>();
+    a.doc0 = 0;
     a.arena = T.arena.as<uint8_t>();
     CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
     CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));

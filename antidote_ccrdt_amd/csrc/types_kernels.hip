@@ -1312,7 +1312,7 @@ int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
 // (worddocumentcount); misses go to the global table (CAS on h).  Exactness
 // does not rest on the hash: wc_verify_kernel byte-compares every token with
 // its word's representative and flags any collision.
-constexpr int WC_PROBE = 8;
+constexpr int WC_BPROBE = 2;  // LDS buckets (of 4 slots) probed per token
 
 __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
 
@@ -1324,18 +1324,27 @@ __device__ __forceinline__ uint64_t wc_mix(uint64_t fnv, uint64_t key, uint64_t 
   return x ? x : 1;
 }
 
-// Token starting at s (byte index in the document): returns its end.
-__device__ __forceinline__ uint64_t wc_token(const uint8_t* doc, uint64_t len, uint64_t s, uint64_t& fnv) {
-  uint64_t h = 0xCBF29CE484222325ull;
-  uint64_t e = s;
-  while (e < len) {
-    const uint8_t c = doc[e];
-    if (wc_sep(c)) break;
-    h = (h ^ c) * 0x100000001B3ull;
-    ++e;
+// A token's word hash, before wc_mix adds its key and length: the token's
+// bytes as little-endian 8-byte words (the last one zero-padded) folded by
+// multiply-xorshift -- two folds for a token of up to 16 bytes, instead of a
+// dependent multiply per byte.  Every site that hashes a word (tokenizer fast
+// and slow paths, wc_merge_kernel) uses this one definition.
+constexpr uint64_t WC_SEED = 0x9E3779B97F4A7C15ull;
+__device__ __forceinline__ uint64_t wc_fold(uint64_t x, uint64_t w) {
+  x = (x ^ w) * 0xFF51AFD7ED558CCDull;
+  return x ^ (x >> 29);
+}
+// bytes p[0..n) from global memory
+__device__ __forceinline__ uint64_t wc_hash_bytes(const uint8_t* p, uint64_t n) {
+  uint64_t x = WC_SEED, acc = 0;
+  for (uint64_t j = 0; j < n; ++j) {
+    acc |= (uint64_t)p[j] << (8 * (j & 7));
+    if ((j & 7) == 7) {
+      x = wc_fold(x, acc);
+      acc = 0;
+    }
   }
-  fnv = h;
-  return e;
+  return (n & 7) ? wc_fold(x, acc) : x;
 }
 
 // A tile staged in LDS: bytes [tile - 16 + sh .. ) of the document, read as
@@ -1356,37 +1365,68 @@ struct WcTileView {
   }
 };
 
-__device__ __forceinline__ WcTileView wc_stage(const WcArgs& a, uint8_t* buf, uint64_t b0, uint64_t len,
-                                               uint64_t tile) {
+// Staging is split so the next tile's loads fly while the current tile is
+// worked on: wc_stage_load issues a tile's 16-byte pieces into registers
+// (global address space, no flat loads), wc_stage_store writes them to LDS.
+constexpr int WC_NPC = (WC_STAGE + 1023) / 1024;  // 16-byte pieces per lane
+typedef unsigned int __attribute__((ext_vector_type(4))) wc_u32x4;
+__device__ __forceinline__ uint4 wc_gload16(const uint8_t* p) {  // global_load_dwordx4, not flat
+  const wc_u32x4 v = *(const __attribute__((address_space(1))) wc_u32x4*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+struct WcStageRegs {
+  uint4 r[WC_NPC];
+  uint64_t abs0, want1;
+};
+
+__device__ __forceinline__ void wc_stage_load(const WcArgs& a, uint64_t b0, uint64_t len, uint64_t tile,
+                                              WcStageRegs& g) {
   // window: document positions [tile - 1, tile + WC_TILE + WC_HALO), clipped
   // to the document, starting at a 16-byte aligned absolute address
   const uint64_t want0 = b0 + (tile ? tile - 1 : 0);
   const uint64_t mis = (uint64_t)(uintptr_t)a.bytes & 15u;  // the batch array need not be aligned
-  const uint64_t abs0 = ((want0 + mis) & ~15ull) - mis;    // may wrap below 0: guarded below
-  const uint64_t want1 = b0 + (tile + WC_TILE + WC_HALO < len ? tile + WC_TILE + WC_HALO : len);
+  g.abs0 = ((want0 + mis) & ~15ull) - mis;                  // may wrap below 0: guarded below
+  g.want1 = b0 + (tile + WC_TILE + WC_HALO < len ? tile + WC_TILE + WC_HALO : len);
   const int lane = lane_id();
-  for (int i = lane * 16; i < WC_STAGE; i += 64 * 16) {
-    const uint64_t p = abs0 + (uint64_t)i;
-    if ((int64_t)p >= (int64_t)want1) break;
+#pragma unroll
+  for (int k = 0; k < WC_NPC; ++k) {
+    const int i = (k * 64 + lane) * 16;
+    const uint64_t p = g.abs0 + (uint64_t)i;
+    if (i < WC_STAGE && (int64_t)p < (int64_t)g.want1 && (int64_t)p >= 0 && p + 16 <= a.n_bytes)
+      g.r[k] = wc_gload16(a.bytes + p);
+    else
+      g.r[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+__device__ __forceinline__ WcTileView wc_stage_store(const WcArgs& a, uint8_t* buf, uint64_t b0,
+                                                     const WcStageRegs& g) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < WC_NPC; ++k) {
+    const int i = (k * 64 + lane) * 16;
+    if (i >= WC_STAGE) continue;
+    const uint64_t p = g.abs0 + (uint64_t)i;
+    if ((int64_t)p >= (int64_t)g.want1) continue;
     if ((int64_t)p >= 0 && p + 16 <= a.n_bytes) {
-      *reinterpret_cast<uint4*>(buf + i) = *reinterpret_cast<const uint4*>(a.bytes + p);
-    } else {
+      *reinterpret_cast<uint4*>(buf + i) = g.r[k];
+    } else {  // the batch array's first or last bytes
       for (int j = 0; j < 16; ++j) {
         const int64_t q = (int64_t)p + j;
         buf[i + j] = (q >= 0 && (uint64_t)q < a.n_bytes) ? a.bytes[q] : (uint8_t)0;
       }
     }
   }
-  __syncthreads();
+  wave_lds_sync();  // the stage is this wave's own
   WcTileView v;
   v.lds = buf;
   v.doc = a.bytes + b0;
-  v.lo = abs0 - b0;  // document position of buf[0] (wraps when abs0 < b0)
-  const uint64_t staged_end = abs0 + (uint64_t)WC_STAGE < want1 ? abs0 + (uint64_t)WC_STAGE : want1;
-  // valid window: [want0, staged_end) in absolute terms
+  v.lo = g.abs0 - b0;  // document position of buf[0] (wraps when abs0 < b0)
+  const uint64_t staged_end = g.abs0 + (uint64_t)WC_STAGE < g.want1 ? g.abs0 + (uint64_t)WC_STAGE : g.want1;
+  // valid window: [want0, staged_end) in absolute terms; positions below want0
+  // (other documents' bytes) are never asked for: callers only read s in
+  // [tile - 1, len)
   v.n = staged_end - b0 - v.lo;
-  // positions below want0 (other documents' bytes) are never asked for:
-  // callers only read s in [tile - 1, len)
   return v;
 }
 
@@ -1402,7 +1442,7 @@ __device__ __forceinline__ uint64_t wc_sep_mask(uint64_t x) {
 // Token starting at document position s: returns its end.  Fast path: the
 // 16 staged bytes from s, read as three aligned 8-byte LDS words, hold the
 // token's end (a separator, or the document end); the token's bytes are then
-// in tb[0..1] (little-endian) and the FNV-1a runs on registers.  Otherwise
+// in tb[0..1] (little-endian) and the hash runs on registers.  Otherwise
 // (a token of 16+ bytes, or one running out of the staged window) the byte
 // loop; *fast says which.
 __device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len, uint64_t s, uint64_t& fnv,
@@ -1421,11 +1461,11 @@ __device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len
     // a separator among the staged bytes, or the document's end right after them
     if (k < nb || len - s == nb) {
       const uint32_t tl = k < nb ? k : nb;
-      uint64_t h = 0xCBF29CE484222325ull;
-      for (uint32_t j = 0; j < tl; ++j) {
-        const uint64_t w = j < 8 ? lo : hi;
-        h = (h ^ ((w >> (8 * (j & 7))) & 0xFFull)) * 0x100000001B3ull;
-      }
+      const uint64_t mlo = tl >= 8 ? ~0ull : ((1ull << (8 * tl)) - 1);
+      const uint64_t mhi = tl >= 16 ? ~0ull : (tl > 8 ? ((1ull << (8 * (tl - 8))) - 1) : 0ull);
+      uint64_t h = WC_SEED;
+      if (tl) h = wc_fold(h, lo & mlo);
+      if (tl > 8) h = wc_fold(h, hi & mhi);
       fnv = h;
       if (tb) {
         tb[0] = lo;
@@ -1435,33 +1475,63 @@ __device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len
       return s + tl;
     }
   }
-  uint64_t h = 0xCBF29CE484222325ull;
+  uint64_t h = WC_SEED, acc = 0;
   uint64_t e = s;
   while (e < len) {
     const uint8_t c = v.at(e);
     if (wc_sep(c)) break;
-    h = (h ^ c) * 0x100000001B3ull;
+    acc |= (uint64_t)c << (8 * ((e - s) & 7));
+    if (((e - s) & 7) == 7) {
+      h = wc_fold(h, acc);
+      acc = 0;
+    }
     ++e;
   }
-  fnv = h;
+  fnv = ((e - s) & 7) ? wc_fold(h, acc) : h;
   if (fast) *fast = false;
   return e;
+}
+
+// Separator flags of 8 bytes packed into 8 bits (bit i = byte i is 0x20 or
+// 0x0A), exact for every byte (no borrow between bytes).
+__device__ __forceinline__ uint32_t wc_sep_bits8(uint64_t x) {
+  constexpr uint64_t L7 = 0x7F7F7F7F7F7F7F7Full, L1 = 0x0101010101010101ull;
+  const uint64_t a = x ^ (0x20ull * L1), b = x ^ (0x0Aull * L1);
+  const uint64_t za = ~(((a & L7) + L7) | a | L7), zb = ~(((b & L7) + L7) | b | L7);
+  return (uint32_t)((((za | zb) >> 7) * 0x0102040810204080ull) >> 56);
 }
 
 // Token starts of the staged tile as per-lane bitmasks (a lane owns
 // WC_TILE/64 consecutive positions) with each lane's exclusive offset in the
 // tile's token order.  Returns the lane's mask; tot = tokens in the tile.
-__device__ __forceinline__ uint64_t wc_start_mask(const WcTileView& v, uint64_t len, uint64_t tile, uint32_t& o,
-                                                  uint32_t& tot) {
+// The lane's 64 bytes are read as nine aligned 8-byte LDS words (every lane
+// of a wave has the same alignment) and turned into separator bits by SWAR;
+// a start is a position after a separator (the previous lane's last bit
+// carries across lanes), the document start, or the end position len.
+__device__ __forceinline__ uint64_t wc_start_mask(const WcTileView& v, const uint8_t* sbuf, uint64_t len,
+                                                  uint64_t tile, uint32_t& o, uint32_t& tot) {
+  static_assert(WC_TILE / 64 == 64, "one 64-bit mask per lane");
   const int lane = lane_id();
-  const uint64_t s0 = tile + (uint64_t)lane * (WC_TILE / 64);
-  uint64_t m = 0;
-#pragma unroll 8
-  for (int i = 0; i < (int)(WC_TILE / 64); ++i) {
-    const uint64_t s = s0 + (uint64_t)i;
-    const bool st = s <= len && (s == 0 || wc_sep(v.at(s - 1)));
-    m |= (uint64_t)st << i;
+  const uint64_t s0 = tile + (uint64_t)lane * 64u;
+  const uint32_t j = (uint32_t)(s0 - v.lo);  // staged index of position s0 (>= 0, +72 inside the stage)
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(sbuf + (j & ~7u));
+  const uint32_t sh = (j & 7u) * 8u;
+  uint64_t sep = 0;
+  uint64_t prev = w[0];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t nx = w[k + 1];
+    const uint64_t x = sh ? (prev >> sh) | (nx << (64u - sh)) : prev;
+    sep |= (uint64_t)wc_sep_bits8(x) << (8 * k);
+    prev = nx;
   }
+  // bit i of sep: byte s0 + i is a separator (bytes past len: don't care)
+  uint64_t carry = __shfl_up(sep >> 63, 1, 64);
+  if (lane == 0) carry = tile == 0 ? 1ull : (uint64_t)wc_sep(sbuf[(uint32_t)(tile - 1 - v.lo)]);
+  uint64_t m = (sep << 1) | carry;
+  // positions s0 + i <= len only
+  if (s0 > len) m = 0;
+  else if (len - s0 < 63) m &= (2ull << (len - s0)) - 1;
   o = wave_excl_scan_u32((uint32_t)__builtin_popcountll(m), tot);
   return m;
 }
@@ -1474,7 +1544,7 @@ __device__ __forceinline__ uint64_t wc_start_mask(const WcTileView& v, uint64_t 
 constexpr uint32_t WC_LIST = 512;
 __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot, uint32_t base, uint16_t* list) {
   const int lane = lane_id();
-  __syncthreads();  // the previous round's list is no longer read
+  wave_lds_sync();  // the previous round's list is no longer read (the list is this wave's own)
   while (m && o < base) {
     m &= m - 1;
     ++o;
@@ -1484,23 +1554,26 @@ __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot
     m &= m - 1;
     list[o++ - base] = (uint16_t)(lane * (WC_TILE / 64) + i);
   }
-  __syncthreads();
+  wave_lds_sync();
   return tot - base < WC_LIST ? tot - base : WC_LIST;
 }
 
+template <int SCOPE = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
                                                      uint64_t pos) {
   uint64_t sl = h & a.t_mask;
   for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
     // read first: a slot goes 0 -> h once, so a (possibly stale) nonzero
     // value is final and only an empty-looking slot needs the CAS
-    const uint64_t seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, SCOPE);
     if (seen == h) return sl;
     if (seen != 0ull) {
       sl = (sl + 1) & a.t_mask;
       continue;
     }
-    const unsigned long long prev = atomicCAS(&a.t[sl].h, 0ull, (unsigned long long)h);
+    unsigned long long prev = 0ull;
+    __hip_atomic_compare_exchange_strong(&a.t[sl].h, &prev, (unsigned long long)h, __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, SCOPE);
     if (prev == 0ull) {  // new word: this token is its representative
       a.t[sl].key = key;
       a.t[sl].len = len;
@@ -1531,176 +1604,294 @@ __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64
   return false;
 }
 
-// Chunk of the launch -> (document, first byte of the chunk in it).  Wave-
-// uniform binary search over the launch's tile_ptr.  Documents are split
-// into chunks of WC_TPW tiles of WC_TILE bytes, one wave each, so every wave
-// has a bounded share and stays inside one document.
+// Chunk of the batch -> (document of the launch, first byte of the chunk in
+// it): two loads through the host-built chunk -> document map (a binary
+// search over tile_ptr was 13 dependent loads per chunk).  Documents are
+// split into chunks of WC_TPW tiles of WC_TILE bytes, one wave each, so every
+// wave has a bounded share and stays inside one document.
 __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d, uint64_t& s0) {
-  uint64_t lo = 0, hi = (uint64_t)a.n_docs;  // tile_ptr[lo] <= t < tile_ptr[hi]
-  while (hi - lo > 1) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (a.tile_ptr[mid] <= t) lo = mid;
-    else hi = mid;
-  }
-  d = lo;
-  s0 = (t - a.tile_ptr[lo]) * (uint64_t)(WC_TILE * WC_TPW);
+  d = (uint64_t)a.chunk_doc[t] - a.doc0;
+  s0 = (t - a.tile_ptr[d]) * (uint64_t)(WC_TILE * WC_TPW);
 }
 
-// One wave per tile: the tokens that START in bytes [s0, s0 + WC_TILE) of
-// document d (the position len counts: a document ending in a separator, or
-// an empty one, has a trailing empty token).  Each lane owns 64 bytes.
-// WC_LDS = per-chunk LDS table entries: 512 for wordcount (the Zipf head is
-// counted in LDS), 256 for worddocumentcount (measured: the smaller table's
-// occupancy beats its extra dedupe-table probes, 138 -> 122 ms; wordcount is
-// 2% slower at 256).
-template <int WC_LDS>
-__global__ __launch_bounds__(64) void wc_insert_kernel(WcArgs a) {
-  __shared__ unsigned long long lh[WC_LDS];
-  __shared__ uint32_t lc[WC_LDS];
-  __shared__ uint64_t lpos[WC_LDS];  // representative: position << 16 | length
-  __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
-  __shared__ uint16_t tlist[WC_LIST];
-  const int lane = lane_id();
-  // a wave takes up to WC_TPW consecutive tiles of ONE document and keeps its
-  // LDS table across them (the Zipf head costs one global atomic per word
-  // per WC_TPW tiles)
-  uint64_t d, tile;
-  wc_tile(a, a.tile0 + blockIdx.x, d, tile);
-  const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
-  const uint32_t key = (uint32_t)a.doc_key[d];
-  for (int i = lane; i < WC_LDS; i += 64) {
+// The tokens that START in a chunk (WC_TPW tiles of WC_TILE bytes of one
+// document; the position len counts: a document ending in a separator, or an
+// empty one, has a trailing empty token), one wave per chunk, each lane owning
+// 64 bytes of a tile.  The WAVES waves of a workgroup take consecutive chunks
+// and share one LDS table of TAB words (hash, count, representative), so the
+// Zipf head is counted in LDS and costs one global insert per word per
+// workgroup; LDS misses and tokens of 2 KiB or more go to the global table.
+// The waves never wait for each other inside the chunk loop (each has its own
+// staging buffer and token list); only the table's set-up and its final flush
+// are workgroup-wide.
+// wordcount: TAB 2048, 4 waves (chunks of different documents may share the
+// workgroup: the table keys on the hash, which includes the key, and each
+// entry remembers its wave for the document);  worddocumentcount: 1 wave and
+// 256 entries (its LDS entries are per (document, word), so a workgroup never
+// spans two documents).
+// (a.dbg 3 / 4: diagnostic builds of the step, CCRDT_WC_IDBG -- LDS only /
+// tokenizer only; their counts are wrong by design)
+// An entry's representative is one u32: position - group base (RELB bits) |
+// length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
+template <int TAB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES == 8 && TAB <= 2048 ? 4 : 1))) void wc_insert_kernel(WcArgs a) {
+  constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : 3;
+  constexpr uint32_t WC_RELB = 17 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
+  static_assert(WAVES == (1 << WB) && WAVES * WC_TPW * WC_TILE < (1ull << WC_RELB), "group span");
+  __shared__ unsigned long long lh[TAB];
+  __shared__ uint32_t lc[TAB];
+  __shared__ uint32_t lp[TAB];
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf_w[WAVES][WC_STAGE];
+  __shared__ uint16_t tlist_w[WAVES][WC_LIST];
+  __shared__ uint64_t gdoc[WAVES];
+  __shared__ uint64_t gbase;
+  const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+  uint8_t* sbuf = sbuf_w[wv];
+  uint16_t* tlist = tlist_w[wv];
+  const uint64_t chunk = (uint64_t)blockIdx.x * WAVES + (uint64_t)wv;  // launch-local
+  const bool act = chunk < a.n_chunks;
+  uint64_t d = 0, tile = 1, b0 = 0, len = 0;
+  if (act) {
+    wc_tile(a, a.tile0 + chunk, d, tile);
+    b0 = a.doc_off[d];
+    len = a.doc_off[d + 1] - b0;
+  }
+  const uint32_t key = act ? (uint32_t)a.doc_key[d] : 0u;
+  for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
     lh[i] = 0ull;
     lc[i] = 0u;
   }
+  if (lane == 0) {
+    gdoc[wv] = d;
+    if (wv == 0) gbase = b0 + tile;
+  }
+  WcStageRegs g;
+  if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
   __syncthreads();
-  for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
-    __syncthreads();  // the previous tile's staged bytes are no longer read
-    const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
+  const uint64_t base_pos = gbase;
+  for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
+    wave_lds_sync();  // the previous tile's staged bytes are no longer read
+    const WcTileView v = wc_stage_store(a, sbuf, b0, g);
+    if (ti + 1 < (int)WC_TPW && tile + WC_TILE <= len) wc_stage_load(a, b0, len, tile + WC_TILE, g);
     uint32_t mo, tot;
-    const uint64_t mm = wc_start_mask(v, len, tile, mo, tot);
+    const uint64_t mm = wc_start_mask(v, sbuf, len, tile, mo, tot);
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
-    const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
-    for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
-      const uint64_t s = tile + tlist[k];
-      uint64_t fnv;
-      const uint64_t e = wc_token_v(v, len, s, fnv);
-      const uint32_t tl = (uint32_t)(e - s);
-      const uint64_t h = wc_mix(fnv, key, tl);
-      // per-tile LDS table
-      uint32_t sl = (uint32_t)(h >> 17) & (WC_LDS - 1);
-      int where = -1;  // 0: counted in LDS, 1: global
-      // (tokens of 64 KiB or more go straight to the global table)
-      for (int p = 0; p < (tl < 0xFFFFu ? WC_PROBE : 0); ++p) {
-        const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
-        if (prev == 0ull) {
-          lpos[sl] = (b0 + s) << 16 | tl;
-          where = 0;
-          if (!a.wdc) atomicAdd(&lc[sl], 1u);
-          else lc[sl] = 1u;
-          break;
+      const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
+      for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
+        const uint64_t s = tile + tlist[k];
+        uint64_t wh;
+        const uint64_t e = wc_token_v(v, len, s, wh);
+        const uint32_t tl = (uint32_t)(e - s);
+        const uint64_t h = wc_mix(wh, key, tl);
+        if (a.dbg == 4) {  // diagnostic: tokenizer only
+          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
+          continue;
         }
-        if (prev == h) {  // same word already seen in this tile
-          where = 0;
-          if (!a.wdc) atomicAdd(&lc[sl], 1u);
-          break;
+        // buckets of 4 slots (32 B): one pair of 16-byte reads finds a word
+        // already in the table (the common case) without an atomic; the CAS
+        // only claims an empty slot
+        uint32_t bk = (uint32_t)(h >> 17) & (TAB / 4 - 1);
+        bool counted = false;
+        const int nprobe = tl < (1u << WC_LENB) - 1 ? WC_BPROBE : 0;
+        for (int p = 0; p < nprobe && !counted; ++p, bk = (bk + 1) & (TAB / 4 - 1)) {
+          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&lh[bk * 4]);
+          const ulonglong2 x0 = q[0], x1 = q[1];
+          uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
+          int hit = -1;
+#pragma unroll
+          for (int i = 3; i >= 0; --i)
+            if (e4[i] == h) hit = i;
+          if (hit >= 0) {
+            if (!a.wdc) atomicAdd(&lc[bk * 4 + hit], 1u);
+            counted = true;
+            break;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (counted || e4[i] != 0ull) continue;
+            const uint32_t sl = bk * 4 + (uint32_t)i;
+            const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
+            if (prev == 0ull) {  // new word of the group: this token represents it
+              lp[sl] = (uint32_t)(b0 + s - base_pos) | tl << WC_RELB | ((uint32_t)wv << WS);
+              if (!a.wdc) atomicAdd(&lc[sl], 1u);
+              else lc[sl] = 1u;
+              counted = true;
+            } else if (prev == h) {
+              if (!a.wdc) atomicAdd(&lc[sl], 1u);
+              counted = true;
+            }
+          }
         }
-        sl = (sl + 1) & (WC_LDS - 1);
+        if (!counted && a.dbg == 3) {  // diagnostic: no global path
+          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
+          continue;
+        }
+        if (!counted) {  // LDS table full (or a long token): global path
+          const uint64_t gs = wc_global_insert(a, h, key, tl, b0 + s);
+          if (gs != ~0ull && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
+        }
       }
-      if (where < 0) {  // LDS table full: global path
-        const uint64_t g = wc_global_insert(a, h, key, tl, b0 + s);
-        if (g != ~0ull && (!a.wdc || wc_doc_first(a, g, d))) atomicAdd(&a.t_cnt[g], 1ull);
-      }
-    }
     }
   }
   __syncthreads();
-  for (int i = lane; i < WC_LDS; i += 64) {
+  for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
     const uint64_t h = lh[i];
     if (h == 0ull) continue;
-    // worddocumentcount: other tiles of the document may hold the word too;
-    // the (document, word) dedupe table admits one of them
-    const uint64_t g = wc_global_insert(a, h, key, (uint32_t)(lpos[i] & 0xFFFFu), lpos[i] >> 16);
-    if (g != ~0ull && (!a.wdc || wc_doc_first(a, g, d))) atomicAdd(&a.t_cnt[g], (unsigned long long)lc[i]);
+    const uint32_t u = lp[i];
+    const uint64_t dd = gdoc[WB ? u >> WS : 0u];
+    const uint32_t tl = (u >> WC_RELB) & ((1u << WC_LENB) - 1);
+    const uint64_t gs = wc_global_insert(a, h, (uint32_t)a.doc_key[dd], tl, base_pos + (u & ((1u << WC_RELB) - 1)));
+    // worddocumentcount: other workgroups of the document may hold the word
+    // too; the (document, word) dedupe table admits one of them
+    if (gs != ~0ull && (!a.wdc || wc_doc_first(a, gs, dd))) atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
   }
 }
 
 // Exactness: every token must equal its word's representative byte-for-byte.
-__global__ __launch_bounds__(64) void wc_verify_kernel(WcArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sbuf[WC_STAGE];
-  __shared__ uint16_t tlist[WC_LIST];
-  const int lane = lane_id();
-  uint64_t d, tile;
-  wc_tile(a, a.tile0 + blockIdx.x, d, tile);
-  const uint64_t b0 = a.doc_off[d], b1 = a.doc_off[d + 1], len = b1 - b0;
-  const uint32_t key = (uint32_t)a.doc_key[d];
-  for (int ti = 0; ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
+// The WAVES waves of a workgroup take consecutive chunks and share an LDS
+// cache of VTAB words already checked against the table (hash, key | length,
+// the 16 bytes): a repeated word of up to 16 bytes is compared with the cache
+// instead of probing the global table and reading its representative again.
+// An entry is usable once its key | length word is set (its writer stores the
+// bytes first; LDS runs a wave's stores in order), so a reader that finds it
+// unset just takes the global path.
+template <int VTAB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
+  __shared__ unsigned long long vh[VTAB];
+  __shared__ unsigned long long vkl[VTAB];  // key << 32 | (length + 1); 0 = not ready
+  __shared__ ulonglong2 vb[VTAB];
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf_w[WAVES][WC_STAGE];
+  __shared__ uint16_t tlist_w[WAVES][WC_LIST];
+  const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+  uint8_t* sbuf = sbuf_w[wv];
+  uint16_t* tlist = tlist_w[wv];
+  for (int i = (int)threadIdx.x; i < VTAB; i += 64 * WAVES) {
+    vh[i] = 0ull;
+    vkl[i] = 0ull;
+  }
+  const uint64_t chunk = (uint64_t)blockIdx.x * WAVES + (uint64_t)wv;
+  const bool act = chunk < a.n_chunks;
+  uint64_t d = 0, tile = 1, b0 = 0, len = 0;
+  if (act) {
+    wc_tile(a, a.tile0 + chunk, d, tile);
+    b0 = a.doc_off[d];
+    len = a.doc_off[d + 1] - b0;
+  }
+  const uint32_t key = act ? (uint32_t)a.doc_key[d] : 0u;
+  WcStageRegs g;
+  if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
   __syncthreads();
-  const WcTileView v = wc_stage(a, sbuf, b0, len, tile);
-  uint32_t mo, tot;
-  const uint64_t mm = wc_start_mask(v, len, tile, mo, tot);
-  for (uint32_t base = 0; base < tot; base += WC_LIST) {
-  const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
-  for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
-    const uint64_t s = tile + tlist[k];
-    uint64_t fnv, tb[2];
-    bool fast;
-    const uint64_t e = wc_token_v(v, len, s, fnv, tb, &fast);
-    const uint32_t tl = (uint32_t)(e - s);
-    const uint64_t h = wc_mix(fnv, key, tl);
-    if (a.dbg == 2) {
-      if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);  // keeps the hash live
-      continue;
-    }
-    // probe: the slot's fields are loaded together with its hash
-    uint64_t sl = h & a.t_mask;
-    uint64_t th, tref;
-    uint32_t tk, tln;
-    for (;;) {
-      const WcSlot ts = a.t[sl];
-      th = ts.h;
-      tref = ts.ref;
-      tk = ts.key;
-      tln = ts.len;
-      if (th == h || th == 0ull) break;
-      sl = (sl + 1) & a.t_mask;
-    }
-    const bool tar = !(tref & WC_REF_BATCH);  // persisted: an arena offset
-    if (th != h) {
-      atomicOr(&a.status[1], 2u);  // lost token (table overflow)
-      continue;
-    }
-    const uint8_t* rep = tar ? a.arena + tref : a.bytes + (tref & ~WC_REF_BATCH);
-    bool eq = tk == key && tln == tl;
-    if (a.dbg == 1) {
-      if (!eq) atomicOr(&a.status[1], 1u);
-      continue;
-    }
-    if (eq && fast && tar) {
-      // the representative in the arena (persisted before this pass; the
-      // arena keeps 32 bytes of slack past its top): three aligned 8-byte
-      // loads against the token's registers
-      const uintptr_t ra = (uintptr_t)rep & ~(uintptr_t)7;
-      const uint32_t sh = (uint32_t)((uintptr_t)rep & 7) * 8;
-      const uint64_t* rp = reinterpret_cast<const uint64_t*>(ra);
-      const uint64_t r0 = rp[0], r1 = rp[1], r2 = rp[2];
-      const uint64_t rlo = sh ? (r0 >> sh) | (r1 << (64 - sh)) : r0;
-      const uint64_t rhi = sh ? (r1 >> sh) | (r2 << (64 - sh)) : r1;
-      const uint64_t mlo = tl >= 8 ? ~0ull : ((1ull << (8 * tl)) - 1);
-      const uint64_t mhi = tl >= 16 ? ~0ull : (tl > 8 ? ((1ull << (8 * (tl - 8))) - 1) : 0ull);
-      if (((tb[0] ^ rlo) & mlo) | ((tb[1] ^ rhi) & mhi)) atomicOr(&a.status[1], 1u);
-      continue;
-    }
-    // 8 independent byte loads per step (one latency per 8 bytes)
-    for (uint32_t j0 = 0; eq && j0 < tl; j0 += 8) {
-      uint8_t r[8];
+  for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
+    wave_lds_sync();
+    const WcTileView v = wc_stage_store(a, sbuf, b0, g);
+    if (ti + 1 < (int)WC_TPW && tile + WC_TILE <= len) wc_stage_load(a, b0, len, tile + WC_TILE, g);
+    uint32_t mo, tot;
+    const uint64_t mm = wc_start_mask(v, sbuf, len, tile, mo, tot);
+    for (uint32_t base = 0; base < tot; base += WC_LIST) {
+      const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
+      for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
+        const uint64_t s = tile + tlist[k];
+        uint64_t wh, tb[2];
+        bool fast;
+        const uint64_t e = wc_token_v(v, len, s, wh, tb, &fast);
+        const uint32_t tl = (uint32_t)(e - s);
+        const uint64_t h = wc_mix(wh, key, tl);
+        if (a.dbg == 2) {
+          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);  // keeps the hash live
+          continue;
+        }
+        const uint64_t mlo = tl >= 8 ? ~0ull : ((1ull << (8 * tl)) - 1);
+        const uint64_t mhi = tl >= 16 ? ~0ull : (tl > 8 ? ((1ull << (8 * (tl - 8))) - 1) : 0ull);
+        const uint64_t kl = (uint64_t)key << 32 | (tl + 1);
+        // the LDS cache (one bucket of 4)
+        const uint32_t bk = (uint32_t)(h >> 17) & (VTAB / 4 - 1);
+        if (fast) {
+          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&vh[bk * 4]);
+          const ulonglong2 x0 = q[0], x1 = q[1];
+          const uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
+          int hit = -1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = j0 + j < tl ? rep[j0 + j] : 0;
+          for (int i = 3; i >= 0; --i)
+            if (e4[i] == h) hit = i;
+          if (hit >= 0) {
+            const uint64_t ckl = vkl[bk * 4 + hit];
+            wave_lds_sync();  // the bytes are read after their ready word
+            if (ckl != 0ull) {
+              const ulonglong2 cb = vb[bk * 4 + hit];
+              if (ckl != kl || ((tb[0] ^ cb.x) & mlo) | ((tb[1] ^ cb.y) & mhi)) atomicOr(&a.status[1], 1u);
+              continue;
+            }
+          }
+        }
+        // probe: the slot's fields are loaded together with its hash
+        uint64_t sl = h & a.t_mask;
+        uint64_t th, tref;
+        uint32_t tk, tln;
+        for (;;) {  // (global loads: a generic WcSlot load would be a flat load)
+          const uint4 q0 = wc_gload16(reinterpret_cast<const uint8_t*>(a.t + sl));
+          const uint4 q1 = wc_gload16(reinterpret_cast<const uint8_t*>(a.t + sl) + 16);
+          th = (uint64_t)q0.y << 32 | q0.x;
+          tref = (uint64_t)q0.w << 32 | q0.z;
+          tk = q1.x;
+          tln = q1.y;
+          if (th == h || th == 0ull) break;
+          sl = (sl + 1) & a.t_mask;
+        }
+        const bool tar = !(tref & WC_REF_BATCH);  // persisted: an arena offset
+        if (th != h) {
+          atomicOr(&a.status[1], 2u);  // lost token (table overflow)
+          continue;
+        }
+        const uint8_t* rep = tar ? a.arena + tref : a.bytes + (tref & ~WC_REF_BATCH);
+        bool eq = tk == key && tln == tl;
+        if (a.dbg == 1) {
+          if (!eq) atomicOr(&a.status[1], 1u);
+          continue;
+        }
+        if (eq && fast && tar) {
+          // the representative in the arena (persisted before this pass; the
+          // arena keeps 32 bytes of slack past its top): three aligned 8-byte
+          // loads against the token's registers
+          const uintptr_t ra = (uintptr_t)rep & ~(uintptr_t)7;
+          const uint32_t sh = (uint32_t)((uintptr_t)rep & 7) * 8;
+          const __attribute__((address_space(1))) uint64_t* rp = (const __attribute__((address_space(1))) uint64_t*)ra;
+          const uint64_t r0 = rp[0], r1 = rp[1], r2 = rp[2];
+          const uint64_t rlo = sh ? (r0 >> sh) | (r1 << (64 - sh)) : r0;
+          const uint64_t rhi = sh ? (r1 >> sh) | (r2 << (64 - sh)) : r1;
+          if (((tb[0] ^ rlo) & mlo) | ((tb[1] ^ rhi) & mhi)) {
+            atomicOr(&a.status[1], 1u);
+            continue;
+          }
+          // checked: into the cache (claim an empty slot of the bucket; the
+          // bytes go in before the ready word)
+          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&vh[bk * 4]);
+          const ulonglong2 x0 = q[0], x1 = q[1];
+          const uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
+          bool done = false;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) eq = eq && (j0 + j >= tl || r[j] == v.at(s + j0 + j));
+          for (int i = 0; i < 4; ++i) {
+            if (done || e4[i] != 0ull) continue;
+            const unsigned long long prev = atomicCAS(&vh[bk * 4 + i], 0ull, (unsigned long long)h);
+            if (prev == 0ull) {
+              vb[bk * 4 + i] = make_ulonglong2(tb[0] & mlo, tb[1] & mhi);
+              wave_lds_sync();
+              vkl[bk * 4 + i] = kl;
+            }
+            done = prev == 0ull || prev == h;
+          }
+          continue;
+        }
+        // 8 independent byte loads per step (one latency per 8 bytes)
+        for (uint32_t j0 = 0; eq && j0 < tl; j0 += 8) {
+          uint8_t r[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = j0 + j < tl ? rep[j0 + j] : 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) eq = eq && (j0 + j >= tl || r[j] == v.at(s + j0 + j));
+        }
+        if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+      }
     }
-    if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
-  }
-  }
   }
 }
 
@@ -1760,21 +1951,42 @@ int wc_launch_doc_key(const uint64_t* key_ptr, uint64_t n_keys, uint64_t n_docs,
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-int wc_launch_insert(const WcArgs& a, uint64_t n_tiles, hipStream_t st) {
-  if (!a.n_docs || !n_tiles) return CCRDT_OK;
-  if (a.wdc)
-    hipLaunchKernelGGL(wc_insert_kernel<256>, dim3((unsigned)n_tiles), dim3(64), 0, st, a);
+int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
+  if (!n_chunks) return CCRDT_OK;
+  WcArgs b = a;
+  b.n_chunks = n_chunks;
+  if (a.wdc) {
+    hipLaunchKernelGGL((wc_insert_kernel<256, 1>), dim3((unsigned)n_chunks), dim3(64), 0, st, b);
+  } else {
+    const char* t = getenv("CCRDT_WC_TAB");
+    const char* w = getenv("CCRDT_WC_WAVES");
+    if (w && atoi(w) == 8) {
+      if (t && atoi(t) == 4096)
+        hipLaunchKernelGGL((wc_insert_kernel<4096, 8>), dim3((unsigned)((n_chunks + 7) / 8)), dim3(512), 0, st, b);
+      else
+        hipLaunchKernelGGL((wc_insert_kernel<2048, 8>), dim3((unsigned)((n_chunks + 7) / 8)), dim3(512), 0, st, b);
+    } else if (t && atoi(t) == 1024)
+      hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL((wc_insert_kernel<2048, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+  }
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
+  if (!n_chunks) return CCRDT_OK;
+  WcArgs b = a;
+  b.n_chunks = n_chunks;
+  const char* t = getenv("CCRDT_WC_VTAB");
+  if (t && atoi(t) == 1024)
+    hipLaunchKernelGGL((wc_verify_kernel<1024, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
   else
-    hipLaunchKernelGGL(wc_insert_kernel<512>, dim3((unsigned)n_tiles), dim3(64), 0, st, a);
+    hipLaunchKernelGGL((wc_verify_kernel<512, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
-int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st) {
-  if (!a.n_docs || !n_tiles) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_verify_kernel, dim3((unsigned)n_tiles), dim3(64), 0, st, a);
-  CCRDT_HIP(hipGetLastError());
-  return CCRDT_OK;
-}
+
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st) {
   const uint64_t n = a.t_mask + 1;
   hipLaunchKernelGGL(wc_persist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, arena, top);
@@ -1792,9 +2004,7 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
   if (i >= n) return;
   const uint64_t s = woff[i], e = woff[i + 1];
   const uint32_t len = (uint32_t)(e - s), key = (uint32_t)wkey[i];
-  uint64_t f = 0xCBF29CE484222325ull;
-  for (uint64_t j = s; j < e; ++j) f = (f ^ a.bytes[j]) * 0x100000001B3ull;
-  const uint64_t h = wc_mix(f, key, len);
+  const uint64_t h = wc_mix(wc_hash_bytes(a.bytes + s, len), key, len);
   if (!verify) {
     if (cnt[i] < 1 || key >= (uint64_t)a.n_keys) {  // a map entry counts at least one token
       atomicOr(&a.status[1], 8u);

@@ -153,6 +153,8 @@ struct WcArgs {
   const uint64_t* doc_off;   // [n_docs+1] byte offsets
   const uint64_t* tile_ptr;  // [n_docs+1] first chunk (WC_TPW tiles) of each document, global index
   uint64_t tile0;            // first chunk of this launch (= tile_ptr[0])
+  const uint32_t* chunk_doc; // [chunks of the batch] document of each chunk (batch index)
+  uint64_t doc0;             // batch index of this launch's first document
   const uint8_t* bytes;
   uint64_t n_bytes;
   int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)
@@ -166,6 +168,7 @@ struct WcArgs {
   uint64_t d_mask;
   uint32_t* status;          // [0] table overflow, [1] hash collision
   int32_t dbg;               // diagnostic (CCRDT_WC_DBG): 1 verify without the byte compare, 2 without the probe
+  uint64_t n_chunks;         // chunks of this insert launch
 };
 
 }  // namespace ccrdt
