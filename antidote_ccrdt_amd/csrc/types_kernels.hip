@@ -1316,24 +1316,26 @@ constexpr int WC_BPROBE = 2;  // LDS buckets (of 4 slots) probed per token
 
 __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
 
-__device__ __forceinline__ uint64_t wc_mix(uint64_t fnv, uint64_t key, uint64_t len) {
-  uint64_t x = fnv ^ (key * 0x9E3779B97F4A7C15ull) ^ (len * 0xC2B2AE3D27D4EB4Full);
-  x ^= x >> 31;
-  x *= 0xBF58476D1CE4E5B9ull;
+// h = wc_mix(word hash, key, length): the key's and the length's products
+// (the key's is wave-uniform, so a scalar multiply) folded in, then one
+// multiply-xorshift avalanche so every bit the tables index by depends on
+// every input bit.
+__device__ __forceinline__ uint64_t wc_mix(uint64_t wh, uint64_t key, uint32_t len) {
+  uint64_t x = wh ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len * 0xC2B2AE3D27D4EB4Full);
   x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 32;
   return x ? x : 1;
 }
 
 // A token's word hash, before wc_mix adds its key and length: the token's
-// bytes as little-endian 8-byte words (the last one zero-padded) folded by
-// multiply-xorshift -- two folds for a token of up to 16 bytes, instead of a
-// dependent multiply per byte.  Every site that hashes a word (tokenizer fast
-// and slow paths, wc_merge_kernel) uses this one definition.
-constexpr uint64_t WC_SEED = 0x9E3779B97F4A7C15ull;
-__device__ __forceinline__ uint64_t wc_fold(uint64_t x, uint64_t w) {
-  x = (x ^ w) * 0xFF51AFD7ED558CCDull;
-  return x ^ (x >> 29);
-}
+// bytes as little-endian 8-byte words (the last one zero-padded), folded as
+// x = (x ^ w) * M from x = 0 -- one multiply per 8 bytes, instead of a
+// dependent multiply per byte (a token of up to 8 bytes costs one).  Every
+// site that hashes a word (tokenizer fast and slow paths, wc_merge_kernel)
+// uses this one definition.
+constexpr uint64_t WC_SEED = 0ull;
+__device__ __forceinline__ uint64_t wc_fold(uint64_t x, uint64_t w) { return (x ^ w) * 0xFF51AFD7ED558CCDull; }
 // bytes p[0..n) from global memory
 __device__ __forceinline__ uint64_t wc_hash_bytes(const uint8_t* p, uint64_t n) {
   uint64_t x = WC_SEED, acc = 0;
@@ -1445,51 +1447,57 @@ __device__ __forceinline__ uint64_t wc_sep_mask(uint64_t x) {
 // in tb[0..1] (little-endian) and the hash runs on registers.  Otherwise
 // (a token of 16+ bytes, or one running out of the staged window) the byte
 // loop; *fast says which.
-__device__ __forceinline__ uint64_t wc_token_v(const WcTileView& v, uint64_t len, uint64_t s, uint64_t& fnv,
-                                               uint64_t* tb = nullptr, bool* fast = nullptr) {
-  const uint64_t i = s - v.lo;
-  if (i < v.n && (i & ~7ull) + 24 <= (uint64_t)WC_STAGE) {
-    const uint64_t avail = v.n - i;  // staged bytes from s (all inside the document)
-    const uint32_t nb = avail < 16 ? (uint32_t)avail : 16u;
-    const uint64_t* p = reinterpret_cast<const uint64_t*>(v.lds + (i & ~7ull));
-    const uint32_t sh = (uint32_t)(i & 7) * 8;
+// Token at tile offset t (tile position s = tile + t): returns its length.
+// Fast path (32-bit offsets): the 16 staged bytes from the token's stage index
+// i = toff + t, read as three aligned 8-byte LDS words, hold the token's end
+// (a separator, or the document end: rem = bytes from s to the document end,
+// clamped to 32 bits); the token's bytes are then in lo / hi (little-endian)
+// and the hash runs on registers.  Otherwise (16+ bytes, or past the staged
+// window) the byte loop; fast says which.
+__device__ __forceinline__ uint32_t wc_token_t(const WcTileView& v, const uint8_t* sbuf, uint32_t toff, uint32_t vn,
+                                               uint32_t rem, uint32_t t, uint64_t tile, uint64_t len, uint64_t& wh,
+                                               uint64_t& lo, uint64_t& hi, bool& fast) {
+  const uint32_t i = toff + t;
+  if (i < vn && (i & ~7u) + 24u <= (uint32_t)WC_STAGE) {
+    const uint32_t avail = vn - i;  // staged bytes from s (all inside the document)
+    const uint32_t nb = avail < 16u ? avail : 16u;
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(sbuf + (i & ~7u));
+    const uint32_t sh = (i & 7u) * 8u;
     const uint64_t w0 = p[0], w1 = p[1], w2 = p[2];
-    const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-    const uint64_t hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+    lo = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+    hi = sh ? (w1 >> sh) | (w2 << (64u - sh)) : w1;
     const uint64_t m0 = wc_sep_mask(lo), m1 = wc_sep_mask(hi);
     const uint32_t k = m0 ? (uint32_t)__builtin_ctzll(m0) >> 3 : (m1 ? 8u + ((uint32_t)__builtin_ctzll(m1) >> 3) : 16u);
     // a separator among the staged bytes, or the document's end right after them
-    if (k < nb || len - s == nb) {
+    if (k < nb || rem == nb) {
       const uint32_t tl = k < nb ? k : nb;
       const uint64_t mlo = tl >= 8 ? ~0ull : ((1ull << (8 * tl)) - 1);
       const uint64_t mhi = tl >= 16 ? ~0ull : (tl > 8 ? ((1ull << (8 * (tl - 8))) - 1) : 0ull);
-      uint64_t h = WC_SEED;
-      if (tl) h = wc_fold(h, lo & mlo);
-      if (tl > 8) h = wc_fold(h, hi & mhi);
-      fnv = h;
-      if (tb) {
-        tb[0] = lo;
-        tb[1] = hi;
-      }
-      if (fast) *fast = true;
-      return s + tl;
+      lo &= mlo;
+      hi &= mhi;
+      uint64_t x = tl ? wc_fold(WC_SEED, lo) : WC_SEED;
+      if (tl > 8) x = wc_fold(x, hi);
+      wh = x;
+      fast = true;
+      return tl;
     }
   }
-  uint64_t h = WC_SEED, acc = 0;
+  const uint64_t s = tile + t;
+  uint64_t x = WC_SEED, acc = 0;
   uint64_t e = s;
   while (e < len) {
     const uint8_t c = v.at(e);
     if (wc_sep(c)) break;
     acc |= (uint64_t)c << (8 * ((e - s) & 7));
     if (((e - s) & 7) == 7) {
-      h = wc_fold(h, acc);
+      x = wc_fold(x, acc);
       acc = 0;
     }
     ++e;
   }
-  fnv = ((e - s) & 7) ? wc_fold(h, acc) : h;
-  if (fast) *fast = false;
-  return e;
+  wh = ((e - s) & 7) ? wc_fold(x, acc) : x;
+  fast = false;
+  return (uint32_t)(e - s);
 }
 
 // Separator flags of 8 bytes packed into 8 bits (bit i = byte i is 0x20 or
@@ -1558,33 +1566,36 @@ __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot
   return tot - base < WC_LIST ? tot - base : WC_LIST;
 }
 
-template <int SCOPE = __HIP_MEMORY_SCOPE_AGENT>
-__device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
-                                                     uint64_t pos) {
-  uint64_t sl = h & a.t_mask;
+// Insert (or find) h in the word table, probing from slot sl whose hash was
+// already read as `seen` (the caller issues that first read early, so its
+// latency overlaps other work).
+__device__ __forceinline__ uint64_t wc_global_insert_at(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
+                                                        uint64_t pos, uint64_t sl, uint64_t seen) {
   for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
-    // read first: a slot goes 0 -> h once, so a (possibly stale) nonzero
-    // value is final and only an empty-looking slot needs the CAS
-    const uint64_t seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, SCOPE);
+    // a slot goes 0 -> h once, so a (possibly stale) nonzero value is final
+    // and only an empty-looking slot needs the CAS
     if (seen == h) return sl;
-    if (seen != 0ull) {
-      sl = (sl + 1) & a.t_mask;
-      continue;
+    if (seen == 0ull) {
+      const unsigned long long prev = atomicCAS(&a.t[sl].h, 0ull, (unsigned long long)h);
+      if (prev == 0ull) {  // new word: this token is its representative
+        a.t[sl].key = key;
+        a.t[sl].len = len;
+        a.t[sl].ref = WC_REF_BATCH | pos;
+        return sl;
+      }
+      if (prev == h) return sl;
     }
-    unsigned long long prev = 0ull;
-    __hip_atomic_compare_exchange_strong(&a.t[sl].h, &prev, (unsigned long long)h, __ATOMIC_RELAXED,
-                                         __ATOMIC_RELAXED, SCOPE);
-    if (prev == 0ull) {  // new word: this token is its representative
-      a.t[sl].key = key;
-      a.t[sl].len = len;
-      a.t[sl].ref = WC_REF_BATCH | pos;
-      return sl;
-    }
-    if (prev == h) return sl;
     sl = (sl + 1) & a.t_mask;
+    seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   atomicOr(&a.status[0], 1u);  // table full
   return ~0ull;
+}
+__device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
+                                                     uint64_t pos) {
+  const uint64_t sl = h & a.t_mask;
+  return wc_global_insert_at(a, h, key, len, pos, sl,
+                             __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64_t doc) {
@@ -1629,8 +1640,12 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // entry remembers its wave for the document);  worddocumentcount: 1 wave and
 // 256 entries (its LDS entries are per (document, word), so a workgroup never
 // spans two documents).
-// (a.dbg 3 / 4: diagnostic builds of the step, CCRDT_WC_IDBG -- LDS only /
-// tokenizer only; their counts are wrong by design)
+// (a.dbg 3-6: diagnostic builds of the step, CCRDT_WC_IDBG -- 3 LDS only,
+// 4 tokenizer only, 5 global lookups without the count adds, 6 the count adds
+// alone; their counts are wrong by design.  Measured on the 8 GiB corpus:
+// tokenizer 9.9 ms, + LDS table 18.8, + global lookups 25.7, full 29.2 -- the
+// device-scope count adds of the LDS misses (~40% of the Zipf tokens) are a
+// third of the kernel, and take the same time at workgroup scope)
 // An entry's representative is one u32: position - group base (RELB bits) |
 // length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
 template <int TAB, int WAVES>
@@ -1669,19 +1684,23 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVE
   if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
   __syncthreads();
   const uint64_t base_pos = gbase;
+
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();  // the previous tile's staged bytes are no longer read
     const WcTileView v = wc_stage_store(a, sbuf, b0, g);
     if (ti + 1 < (int)WC_TPW && tile + WC_TILE <= len) wc_stage_load(a, b0, len, tile + WC_TILE, g);
     uint32_t mo, tot;
     const uint64_t mm = wc_start_mask(v, sbuf, len, tile, mo, tot);
+    const uint32_t toff = (uint32_t)(tile - v.lo), vn = (uint32_t)v.n;  // stage index of the tile start, staged bytes
+    const uint32_t lrc = len - tile < 0xFFFFFFFFull ? (uint32_t)(len - tile) : 0xFFFFFFFFu;
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
       const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
       for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
-        const uint64_t s = tile + tlist[k];
-        uint64_t wh;
-        const uint64_t e = wc_token_v(v, len, s, wh);
-        const uint32_t tl = (uint32_t)(e - s);
+        const uint32_t t = tlist[k];
+        const uint64_t s = tile + t;
+        uint64_t wh, lo, hi;
+        bool fast;
+        const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
         const uint64_t h = wc_mix(wh, key, tl);
         if (a.dbg == 4) {  // diagnostic: tokenizer only
           if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
@@ -1727,8 +1746,12 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVE
           continue;
         }
         if (!counted) {  // LDS table full (or a long token): global path
+          if (a.dbg == 6) {  // diagnostic: the count add alone
+            atomicAdd(&a.t_cnt[h & a.t_mask], 1ull);
+            continue;
+          }
           const uint64_t gs = wc_global_insert(a, h, key, tl, b0 + s);
-          if (gs != ~0ull && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
+          if (gs != ~0ull && a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
         }
       }
     }
@@ -1787,14 +1810,16 @@ __global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
     if (ti + 1 < (int)WC_TPW && tile + WC_TILE <= len) wc_stage_load(a, b0, len, tile + WC_TILE, g);
     uint32_t mo, tot;
     const uint64_t mm = wc_start_mask(v, sbuf, len, tile, mo, tot);
+    const uint32_t toff = (uint32_t)(tile - v.lo), vn = (uint32_t)v.n;  // stage index of the tile start, staged bytes
+    const uint32_t lrc = len - tile < 0xFFFFFFFFull ? (uint32_t)(len - tile) : 0xFFFFFFFFu;
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
       const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
       for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
-        const uint64_t s = tile + tlist[k];
+        const uint32_t t = tlist[k];
+        const uint64_t s = tile + t;
         uint64_t wh, tb[2];
         bool fast;
-        const uint64_t e = wc_token_v(v, len, s, wh, tb, &fast);
-        const uint32_t tl = (uint32_t)(e - s);
+        const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, tb[0], tb[1], fast);
         const uint64_t h = wc_mix(wh, key, tl);
         if (a.dbg == 2) {
           if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);  // keeps the hash live
