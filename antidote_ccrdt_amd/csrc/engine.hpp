@@ -29,6 +29,7 @@ struct TypeBufs {
   uint64_t t_slots[2] = {0, 0};
   DevBuf arena, arena_top, d_hash;
   uint64_t arena_cap = 0;
+  uint64_t wc_seed = 0;  // word-hash seed; a batch that meets a collision is re-run once with a new one
   // scratch shared by the types
   DevBuf caps, part, ovf_a, ovf_b, status, ex_cnt, ex, kp, stage[6];
   // HBM class of topk / leaderboard (keys beyond the LDS classes)

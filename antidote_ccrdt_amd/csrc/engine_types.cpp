@@ -1021,6 +1021,13 @@ static uint64_t pow2_at_least(uint64_t x) {
   return p;
 }
 
+static uint64_t wc_next_seed(uint64_t z) {  // splitmix64 step
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 static WcArgs wc_table_args(ccrdt_engine* e, int side) {
   TypeBufs& T = e->tb;
   WcArgs a{};
@@ -1029,6 +1036,8 @@ static WcArgs wc_table_args(ccrdt_engine* e, int side) {
   a.t = T.t_tab[side].as<WcSlot>();
   a.t_cnt = T.t_cnt[side].as<unsigned long long>();
   a.t_mask = T.t_slots[side] ? T.t_slots[side] - 1 : 0;
+  a.seed = T.wc_seed;
+  a.weak0 = getenv("CCRDT_WC_WEAK0") ? 1 : 0;
   a.arena = T.arena.as<uint8_t>();
   a.status = T.status.as<uint32_t>();
   return a;
@@ -1116,6 +1125,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   // resident in the 256 MiB Infinity Cache; a batch with more overflows it and
   // is re-run on a table four times larger)
   uint64_t slots = pow2_at_least(2 * (words_old + std::min<uint64_t>(tokens, 1ull << 20)));
+  bool reseeded = false;
   if (getenv("CCRDT_WC_SLOTS")) slots = strtoull(getenv("CCRDT_WC_SLOTS"), nullptr, 0);
   for (int attempt = 0;; ++attempt) {
     // new table (rehash of the current words), then the batch
@@ -1194,7 +1204,15 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       const uint64_t back[2] = {arena_used, words_old};
       CCRDT_TRY(h2d(T.arena_top, back, 16, e->stream));
       CCRDT_HIP(hipStreamSynchronize(e->stream));
-      set_error(st[1] & 1 ? "wc_apply: 64-bit word hash collision between distinct words"
+      if ((st[1] & 1) && !reseeded) {
+        // two distinct words met on one 64-bit hash: the collision depends on
+        // the bytes and the seed only, so the batch is re-run once under a
+        // new seed (the rehash recomputes every old word's hash)
+        reseeded = true;
+        T.wc_seed = wc_next_seed(T.wc_seed);
+        continue;
+      }
+      set_error(st[1] & 1 ? "wc_apply: 64-bit word hash collision between distinct words (also under a second seed)"
                           : "wc_apply: token lost (table overflow)");
       return CCRDT_ERANGE;
     }
@@ -1296,17 +1314,25 @@ static int wc_merge_core(ccrdt_engine* e, uint64_t nw, const uint64_t* wk, const
   }
   const int in = T.tcur, out = 1 - T.tcur;
   const uint64_t slots = pow2_at_least(2 * (words_old + nw));
-  CCRDT_TRY(wc_alloc_table(e, out, slots));
-  WcArgs a = wc_table_args(e, out);
-  if (!start_empty && T.t_slots[in])
-    CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
-  CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
-  a.bytes = bytes;
-  a.n_bytes = nb;
-  CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 0, e->stream));
-  CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 1, e->stream));
+  WcArgs a;
   uint32_t st[2];
-  CCRDT_TRY(read_status(e, st));
+  for (int attempt = 0;; ++attempt) {
+    CCRDT_TRY(wc_alloc_table(e, out, slots));
+    a = wc_table_args(e, out);
+    if (!start_empty && T.t_slots[in])
+      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+    a.bytes = bytes;
+    a.n_bytes = nb;
+    CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 0, e->stream));
+    CCRDT_TRY(wc_launch_merge(a, wk, wo, wc, nw, 1, e->stream));
+    CCRDT_TRY(read_status(e, st));
+    if (st[1] == 1u && attempt == 0) {  // a hash collision alone: once more under a new seed
+      T.wc_seed = wc_next_seed(T.wc_seed);
+      continue;
+    }
+    break;
+  }
   if (st[0] || st[1]) {
     set_error(st[1] & 8   ? "wc_merge: a count < 1 or a key outside [0, n_keys)"
               : st[1] & 1 ? "wc_merge: 64-bit word hash collision between distinct words"

@@ -1320,12 +1320,19 @@ __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x2
 // (the key's is wave-uniform, so a scalar multiply) folded in, then one
 // multiply-xorshift avalanche so every bit the tables index by depends on
 // every input bit.
-__device__ __forceinline__ uint64_t wc_mix(uint64_t wh, uint64_t key, uint32_t len) {
-  uint64_t x = wh ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len * 0xC2B2AE3D27D4EB4Full);
+__device__ __forceinline__ uint64_t wc_mix(uint64_t wh, uint64_t key, uint32_t len, uint64_t seed = 0) {
+  uint64_t x = wh ^ seed ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)len * 0xC2B2AE3D27D4EB4Full);
   x ^= x >> 29;
   x *= 0xBF58476D1CE4E5B9ull;
   x ^= x >> 32;
   return x ? x : 1;
+}
+
+// The table hash of a word under the table's seed.  (a.weak0: test hook --
+// under seed 0 every word of one length and key collides, so the re-seeded
+// retry of a batch can be exercised.)
+__device__ __forceinline__ uint64_t wc_hkey(const WcArgs& a, uint64_t wh, uint64_t key, uint32_t len) {
+  return wc_mix(a.weak0 && a.seed == 0 ? 0ull : wh, key, len, a.seed);
 }
 
 // A token's word hash, before wc_mix adds its key and length: the token's
@@ -1701,7 +1708,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVE
         uint64_t wh, lo, hi;
         bool fast;
         const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
-        const uint64_t h = wc_mix(wh, key, tl);
+        const uint64_t h = wc_hkey(a, wh, key, tl);
         if (a.dbg == 4) {  // diagnostic: tokenizer only
           if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
           continue;
@@ -1820,7 +1827,7 @@ __global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
         uint64_t wh, tb[2];
         bool fast;
         const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, tb[0], tb[1], fast);
-        const uint64_t h = wc_mix(wh, key, tl);
+        const uint64_t h = wc_hkey(a, wh, key, tl);
         if (a.dbg == 2) {
           if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);  // keeps the hash live
           continue;
@@ -2029,7 +2036,7 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
   if (i >= n) return;
   const uint64_t s = woff[i], e = woff[i + 1];
   const uint32_t len = (uint32_t)(e - s), key = (uint32_t)wkey[i];
-  const uint64_t h = wc_mix(wc_hash_bytes(a.bytes + s, len), key, len);
+  const uint64_t h = wc_hkey(a, wc_hash_bytes(a.bytes + s, len), key, len);
   if (!verify) {
     if (cnt[i] < 1 || key >= (uint64_t)a.n_keys) {  // a map entry counts at least one token
       atomicOr(&a.status[1], 8u);
@@ -2134,14 +2141,17 @@ int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff,
   return CCRDT_OK;
 }
 
-// Re-insert the words of an old table into a fresh (larger) table.
+// Re-insert the words of an old table into a fresh (larger) table.  The hash
+// is recomputed from the word's persisted bytes under the table's seed, so a
+// re-seeded batch (a collision) starts from a consistent table.
 __global__ void wc_rehash_kernel(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, WcArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= on) return;
   const WcSlot o = old[i];
   if (o.h == 0ull) return;
-  uint64_t sl = o.h & a.t_mask;
-  while (atomicCAS(&a.t[sl].h, 0ull, o.h) != 0ull) sl = (sl + 1) & a.t_mask;
+  const uint64_t h = wc_hkey(a, wc_hash_bytes(a.arena + o.ref, o.len), o.key, o.len);
+  uint64_t sl = h & a.t_mask;
+  while (atomicCAS(&a.t[sl].h, 0ull, h) != 0ull) sl = (sl + 1) & a.t_mask;
   a.t[sl].key = o.key;
   a.t[sl].len = o.len;
   a.t[sl].ref = o.ref;

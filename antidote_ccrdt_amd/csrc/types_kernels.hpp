@@ -162,6 +162,8 @@ struct WcArgs {
   WcSlot* t;
   unsigned long long* t_cnt;
   uint64_t t_mask;
+  uint64_t seed;             // word-hash seed of the table (every h of the table is under it)
+  int32_t weak0;             // test hook (CCRDT_WC_WEAK0): a degenerate hash under seed 0
   const uint8_t* arena;
   // per-document dedupe table (worddocumentcount)
   uint64_t* d_hash;

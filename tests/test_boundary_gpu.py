@@ -257,3 +257,29 @@ def test_topk_lb_ranges(gpu):
     for k0, k1 in ((0, 1500), (1500, nk)):
         lb2.import_range(k0, k1, lb.export_range(k0, k1))
     assert not lb2.export().diff(full)
+
+
+@pytest.mark.parametrize("E", [WordcountEngine, WordDocumentCountEngine])
+def test_wc_reseed_on_hash_collision(gpu, E, monkeypatch):
+    """A 64-bit word-hash collision between distinct words is re-run once under
+    a new seed instead of failing the batch.  The test hook
+    CCRDT_WC_WEAK0 makes every word of one length and key collide under the
+    engine's first seed, so the first attempt of each path below collides."""
+    monkeypatch.setenv("CCRDT_WC_WEAK0", "1")
+    docs = [[b"abc abd abe abc\nxyz", b"abd q r"], [b"abc"]]
+    e, o = E(2), orc.WcOracle(2, E is WordDocumentCountEngine)
+    e.apply_docs(docs)
+    o.apply_docs(docs)
+    for x, y in zip(e.export(), o.export()):
+        assert np.array_equal(x, y)
+    # the next batch runs under the new seed (the rehash recomputes the words)
+    more = [[b"abf abc zz"], [b"qq qr abc"]]
+    e.apply_docs(more)
+    o.apply_docs(more)
+    for x, y in zip(e.export(), o.export()):
+        assert np.array_equal(x, y)
+    # the (word, count) import path takes the same retry
+    f = E(2)
+    maps = [{b"aa": 3, b"ab": 4, b"ac": 5}, {b"aa": 1}]
+    f.import_state(*_import(f, maps))
+    assert [f.value(k) for k in range(2)] == maps
