@@ -31,7 +31,7 @@ struct TypeBufs {
   uint64_t arena_cap = 0;
   uint64_t wc_seed = 0;  // word-hash seed; a batch that meets a collision is re-run once with a new one
   // scratch shared by the types
-  DevBuf caps, part, ovf_a, ovf_b, status, ex_cnt, ex, kp, stage[6];
+  DevBuf caps, part, ovf_a, ovf_b, status, ex_cnt, ex, kp, stage[8];
   // HBM class of topk / leaderboard (keys beyond the LDS classes)
   DevBuf hb_off, hb_cap, hb_a, hb_b, hb_c, hb_d;
 };

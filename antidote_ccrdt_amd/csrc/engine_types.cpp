@@ -1103,6 +1103,17 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   for (uint64_t d = 0; d < nd; ++d)
     for (uint64_t c = tptr[d]; c < tptr[d + 1]; ++c) cdoc[c] = (uint32_t)d;
   CCRDT_TRY(h2d(T.stage[5], cdoc.data(), cdoc.size() * 4, e->stream));
+  // worddocumentcount: groups of 4 chunks of one document (one workgroup each)
+  std::vector<uint64_t> gptr(nd + 1, 0);
+  std::vector<uint32_t> gdoc;
+  if (e->type == CCRDT_WORDDOCUMENTCOUNT) {
+    for (uint64_t d = 0; d < nd; ++d) gptr[d + 1] = gptr[d] + (tptr[d + 1] - tptr[d] + 3) / 4;
+    gdoc.resize(gptr[nd] + 1, 0u);
+    for (uint64_t d = 0; d < nd; ++d)
+      for (uint64_t g = gptr[d]; g < gptr[d + 1]; ++g) gdoc[g] = (uint32_t)d;
+    CCRDT_TRY(h2d(T.stage[6], gptr.data(), (nd + 1) * 8, e->stream));
+    CCRDT_TRY(h2d(T.stage[7], gdoc.data(), gdoc.size() * 4, e->stream));
+  }
   std::vector<uint64_t> top;
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   const uint64_t words_old = e->fresh ? 0 : top[1], arena_used = e->fresh ? 0 : top[0];
@@ -1156,6 +1167,12 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       a.chunk_doc = T.stage[5].as<uint32_t>();
       a.doc0 = d0;
       if (a.wdc) {
+        a.group_doc = T.stage[7].as<uint32_t>();
+        a.group_ptr = T.stage[6].as<uint64_t>() + d0;
+        a.group0 = gptr[d0];
+        a.n_groups = gptr[d1] - gptr[d0];
+      }
+      if (a.wdc) {
         const uint64_t ds = pow2_at_least(2 * tk);
         CCRDT_TRY(T.d_hash.ensure(ds * 8));
         CCRDT_HIP(hipMemsetAsync(T.d_hash.p, 0, ds * 8, e->stream));
@@ -1188,6 +1205,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     a.tile0 = 0;
     a.chunk_doc = T.stage[5].as<uint32_t>();
     a.doc0 = 0;
+    a.group_doc = nullptr;
     a.arena = T.arena.as<uint8_t>();
     CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
     CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));

@@ -1642,11 +1642,12 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // The waves never wait for each other inside the chunk loop (each has its own
 // staging buffer and token list); only the table's set-up and its final flush
 // are workgroup-wide.
-// wordcount: TAB 2048, 4 waves (chunks of different documents may share the
-// workgroup: the table keys on the hash, which includes the key, and each
-// entry remembers its wave for the document);  worddocumentcount: 1 wave and
-// 256 entries (its LDS entries are per (document, word), so a workgroup never
-// spans two documents).
+// 4 waves; TAB 2048 (wordcount) / 1024 (worddocumentcount).  wordcount: chunks of different documents may share the
+// workgroup (the table keys on the hash, which includes the key, and each
+// entry remembers its wave for the document); worddocumentcount: its LDS
+// entries are per (document, word), so a workgroup's chunks are chunks of one
+// document (group_doc / group_ptr; the last group of a document may leave
+// waves idle).
 // (a.dbg 3-6: diagnostic builds of the step, CCRDT_WC_IDBG -- 3 LDS only,
 // 4 tokenizer only, 5 global lookups without the count adds, 6 the count adds
 // alone; their counts are wrong by design.  Measured on the 8 GiB corpus:
@@ -1670,11 +1671,20 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVE
   const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
   uint8_t* sbuf = sbuf_w[wv];
   uint16_t* tlist = tlist_w[wv];
-  const uint64_t chunk = (uint64_t)blockIdx.x * WAVES + (uint64_t)wv;  // launch-local
-  const bool act = chunk < a.n_chunks;
+  uint64_t chunk;  // batch index
+  bool act;
+  if (a.group_doc) {  // worddocumentcount: WAVES consecutive chunks of ONE document
+    const uint64_t gi = a.group0 + blockIdx.x;
+    const uint64_t dl = (uint64_t)a.group_doc[gi] - a.doc0;
+    chunk = a.tile_ptr[dl] + (gi - a.group_ptr[dl]) * WAVES + (uint64_t)wv;
+    act = blockIdx.x < a.n_groups && chunk < a.tile_ptr[dl + 1];
+  } else {
+    chunk = a.tile0 + (uint64_t)blockIdx.x * WAVES + (uint64_t)wv;
+    act = chunk < a.tile0 + a.n_chunks;
+  }
   uint64_t d = 0, tile = 1, b0 = 0, len = 0;
   if (act) {
-    wc_tile(a, a.tile0 + chunk, d, tile);
+    wc_tile(a, chunk, d, tile);
     b0 = a.doc_off[d];
     len = a.doc_off[d + 1] - b0;
   }
@@ -1988,7 +1998,10 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   WcArgs b = a;
   b.n_chunks = n_chunks;
   if (a.wdc) {
-    hipLaunchKernelGGL((wc_insert_kernel<256, 1>), dim3((unsigned)n_chunks), dim3(64), 0, st, b);
+    if (!a.n_groups) return CCRDT_OK;
+    // (measured on the 8 GiB corpus: 1024 entries 48.6 ms, 512 51.2, 2048 58.4 --
+    // the dedupe path of the misses wants the occupancy of the smaller table)
+    hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)a.n_groups), dim3(256), 0, st, b);
   } else {
     const char* t = getenv("CCRDT_WC_TAB");
     const char* w = getenv("CCRDT_WC_WAVES");

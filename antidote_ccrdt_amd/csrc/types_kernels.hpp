@@ -155,6 +155,11 @@ struct WcArgs {
   uint64_t tile0;            // first chunk of this launch (= tile_ptr[0])
   const uint32_t* chunk_doc; // [chunks of the batch] document of each chunk (batch index)
   uint64_t doc0;             // batch index of this launch's first document
+  // worddocumentcount: workgroups of WAVES chunks of one document
+  const uint32_t* group_doc; // [groups of the batch] document of each group (batch index), or nullptr
+  const uint64_t* group_ptr; // [launch docs + 1] first group of each document (batch index)
+  uint64_t group0;           // first group of this launch
+  uint64_t n_groups;         // groups of this launch
   const uint8_t* bytes;
   uint64_t n_bytes;
   int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)
