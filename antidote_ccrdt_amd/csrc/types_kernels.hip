@@ -1657,7 +1657,7 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // An entry's representative is one u32: position - group base (RELB bits) |
 // length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
 template <int TAB, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES == 8 && TAB <= 2048 ? 4 : 1))) void wc_insert_kernel(WcArgs a) {
+__global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : 3;
   constexpr uint32_t WC_RELB = 17 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
   static_assert(WAVES == (1 << WB) && WAVES * WC_TPW * WC_TILE < (1ull << WC_RELB), "group span");
@@ -2003,17 +2003,9 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     // the dedupe path of the misses wants the occupancy of the smaller table)
     hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)a.n_groups), dim3(256), 0, st, b);
   } else {
-    const char* t = getenv("CCRDT_WC_TAB");
-    const char* w = getenv("CCRDT_WC_WAVES");
-    if (w && atoi(w) == 8) {
-      if (t && atoi(t) == 4096)
-        hipLaunchKernelGGL((wc_insert_kernel<4096, 8>), dim3((unsigned)((n_chunks + 7) / 8)), dim3(512), 0, st, b);
-      else
-        hipLaunchKernelGGL((wc_insert_kernel<2048, 8>), dim3((unsigned)((n_chunks + 7) / 8)), dim3(512), 0, st, b);
-    } else if (t && atoi(t) == 1024)
-      hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
-    else
-      hipLaunchKernelGGL((wc_insert_kernel<2048, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+    // (measured: 2048 entries 29.2 ms, 1024 33.9 ms; 8 waves sharing 2048 or
+    // 4096 entries 32.8 / 33.4 ms before the bucketed probes)
+    hipLaunchKernelGGL((wc_insert_kernel<2048, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
   }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
@@ -2023,11 +2015,8 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   if (!n_chunks) return CCRDT_OK;
   WcArgs b = a;
   b.n_chunks = n_chunks;
-  const char* t = getenv("CCRDT_WC_VTAB");
-  if (t && atoi(t) == 1024)
-    hipLaunchKernelGGL((wc_verify_kernel<1024, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
-  else
-    hipLaunchKernelGGL((wc_verify_kernel<512, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+  // (measured: a 512-word cache at 16 waves per CU beats 1024 words at 8)
+  hipLaunchKernelGGL((wc_verify_kernel<512, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
