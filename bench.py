@@ -121,6 +121,8 @@ class Exchange:
                 rows = torch.from_numpy(h)
             outs = [torch.empty_like(rows) for _ in range(self.world)]
             dist.all_gather(outs, rows)
+            if self.on_dev:  # the next step's extras overwrite the rows this gather reads
+                torch.cuda.current_stream().synchronize()
         self.n_gathered = tot
 
 
