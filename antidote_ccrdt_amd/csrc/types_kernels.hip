@@ -1953,15 +1953,39 @@ __global__ void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* 
 }
 
 // token count of every document (sizes the worddocumentcount dedupe table)
+// (the document's 16-byte aligned interior read as global_load_dwordx4, four
+// in flight per lane, separators counted by SWAR; the unaligned head and tail
+// byte by byte)
 __global__ __launch_bounds__(64) void wc_count_kernel(const uint64_t* doc_off, const uint8_t* bytes,
                                                       uint64_t* ntok) {
   const uint64_t d = blockIdx.x;
   const uint64_t b0 = doc_off[d], b1 = doc_off[d + 1];
-  uint32_t c = 0;
-  for (uint64_t i = b0 + lane_id(); i < b1; i += 64) c += wc_sep(bytes[i]);
-  uint32_t tot;
-  (void)wave_excl_scan_u32(c, tot);
-  if (lane_id() == 0) ntok[d] = (uint64_t)tot + 1;
+  const int lane = lane_id();
+  const uint64_t mis = (uint64_t)(uintptr_t)bytes & 15u;
+  uint64_t i0 = ((b0 + mis + 15) & ~15ull) - mis, i1 = ((b1 + mis) & ~15ull) - mis;
+  if (i0 > b1) i0 = b1;
+  if (i1 < i0) i1 = i0;
+  uint64_t c = 0;
+  if (b0 + (uint64_t)lane < i0) c += wc_sep(bytes[b0 + lane]);
+  if (i1 + (uint64_t)lane < b1) c += wc_sep(bytes[i1 + lane]);
+  uint64_t j = i0 + 16u * (uint64_t)lane;
+  for (; j + 3 * 1024 < i1; j += 4 * 1024) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = wc_gload16(bytes + j + 1024u * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      c += __builtin_popcount(wc_sep_bits8((uint64_t)v[u].y << 32 | v[u].x)) +
+           __builtin_popcount(wc_sep_bits8((uint64_t)v[u].w << 32 | v[u].z));
+  }
+  for (; j < i1; j += 1024) {
+    const uint4 v = wc_gload16(bytes + j);
+    c += __builtin_popcount(wc_sep_bits8((uint64_t)v.y << 32 | v.x)) +
+         __builtin_popcount(wc_sep_bits8((uint64_t)v.w << 32 | v.z));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += (uint64_t)__shfl_xor((unsigned long long)c, m, 64);
+  if (lane == 0) ntok[d] = c + 1;
 }
 // key of every document from the key -> documents CSR (thread per document,
 // binary search: a key may own thousands of documents)
