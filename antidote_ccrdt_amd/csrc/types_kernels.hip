@@ -1312,6 +1312,9 @@ int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
 // (worddocumentcount); misses go to the global table (CAS on h).  Exactness
 // does not rest on the hash: wc_verify_kernel byte-compares every token with
 // its word's representative and flags any collision.
+// linear probes of the global tables before an insert reports the table full
+// (the batch is then re-run on a table four times larger)
+constexpr uint64_t WC_MAXPROBE = 4096;
 constexpr int WC_BPROBE = 2;  // LDS buckets (of 4 slots) probed per token
 
 __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
@@ -1578,7 +1581,7 @@ __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot
 // latency overlaps other work).
 __device__ __forceinline__ uint64_t wc_global_insert_at(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
                                                         uint64_t pos, uint64_t sl, uint64_t seen) {
-  for (uint64_t probe = 0; probe <= a.t_mask; ++probe) {
+  for (uint64_t probe = 0; probe <= a.t_mask && probe < WC_MAXPROBE; ++probe) {
     // a slot goes 0 -> h once, so a (possibly stale) nonzero value is final
     // and only an empty-looking slot needs the CAS
     if (seen == h) return sl;
@@ -1612,7 +1615,7 @@ __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64
   // share an entry; the hash only picks where to probe.
   const uint64_t dh = ((doc + 1) << 40) | g;
   uint64_t sl = wc_mix(dh, 0x5151, 0) & a.d_mask;
-  for (uint64_t probe = 0; probe <= a.d_mask; ++probe) {
+  for (uint64_t probe = 0; probe <= a.d_mask && probe < WC_MAXPROBE; ++probe) {
     const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], 0ull, (unsigned long long)dh);
     if (prev == 0ull) return true;
     if (prev == dh) return false;

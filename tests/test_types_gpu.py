@@ -273,6 +273,17 @@ def test_wordcount_lds_overflow_path(gpu):
         assert e.value() == o.value()
 
 
+def test_wdc_all_distinct_words(gpu):
+    """worddocumentcount on documents of all-distinct words: every (document,
+    word) pair reaches the global dedupe table (same counts as the oracle)."""
+    docs = [b" ".join(b"u%06d" % (d * 100000 + i) for i in range(20000)) for d in range(3)]
+    docs.append(docs[0])  # the same words in a second document count again
+    e, o = WordDocumentCountEngine(1), orc.WcOracle(1, True)
+    e.apply_docs([docs])
+    o.apply_docs([docs])
+    assert e.value() == o.value()
+
+
 # ------------------------------------------------- HBM classes (beyond LDS)
 def test_topk_hbm_class(gpu):
     """A key with 30000 ops / 9000 distinct Ids goes through the HBM hash and
