@@ -36,7 +36,7 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_tiles, hipStream_t st);
 int wc_launch_persist(const WcArgs& a, uint8_t* arena, unsigned long long* top, hipStream_t st);
 int wc_launch_owner_count(const WcArgs& a, uint32_t world, uint32_t* owner, unsigned long long* cur, hipStream_t st);
 int wc_launch_owner_scatter(const WcArgs& a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
-                            uint8_t* out, hipStream_t st);
+                            uint8_t* out, uint32_t world, hipStream_t st);
 int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_t* wcnt, uint32_t* wlen,
                          hipStream_t st);
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
@@ -1449,7 +1449,7 @@ int ccrdt_wc_partition_device(ccrdt_engine* e, int world, int64_t* d_meta, uint8
     b += (uint64_t)owner_bytes[o];
   }
   CCRDT_HIP(hipMemcpyAsync(cur, base.data(), (size_t)world * 8, hipMemcpyHostToDevice, e->stream));
-  CCRDT_TRY(wc_launch_owner_scatter(a, T.caps.as<uint32_t>(), cur, d_meta, d_bytes, e->stream));
+  CCRDT_TRY(wc_launch_owner_scatter(a, T.caps.as<uint32_t>(), cur, d_meta, d_bytes, (uint32_t)world, e->stream));
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   return CCRDT_OK;
 }

@@ -1942,14 +1942,31 @@ __global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
 
 // New words of this batch: copy their bytes into the persistent arena.
 // arena_top[1] counts the table's words.
-__global__ void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* arena_top) {
+// (words and new bytes are summed per workgroup in LDS; one device atomic per
+// workgroup reserves its arena range and adds its word count)
+__global__ __launch_bounds__(256) void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* arena_top) {
+  __shared__ unsigned long long bw, bf, bb, bbase;
+  if (threadIdx.x == 0) bw = bf = bb = 0ull;
+  __syncthreads();
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
-  atomicAdd(&arena_top[1], 1ull);
-  const uint64_t ref = a.t[sl].ref;
-  if (!(ref & WC_REF_BATCH)) return;
-  const uint32_t n = a.t[sl].len;
-  const uint64_t at = atomicAdd(arena_top, (unsigned long long)n);
+  const bool v = sl <= a.t_mask && a.t[sl].h != 0ull;
+  const uint64_t ref = v ? a.t[sl].ref : 0ull;
+  const bool fresh = v && (ref & WC_REF_BATCH);
+  const uint32_t n = fresh ? a.t[sl].len : 0u;
+  unsigned long long loc = 0;
+  if (v) atomicAdd(&bw, 1ull);
+  if (fresh) {
+    atomicAdd(&bf, 1ull);
+    loc = atomicAdd(&bb, (unsigned long long)n);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (bw) atomicAdd(&arena_top[1], bw);
+    if (bf) bbase = atomicAdd(arena_top, bb);  // (also for a block of empty words only)
+  }
+  __syncthreads();
+  if (!fresh) return;
+  const uint64_t at = bbase + loc;
   const uint8_t* src = a.bytes + (ref & ~WC_REF_BATCH);
   for (uint32_t j = 0; j < n; ++j) arena[at + j] = src[j];
   a.t[sl].ref = at;
@@ -2110,19 +2127,51 @@ __device__ __forceinline__ uint32_t wc_slot_owner(const WcArgs& a, uint64_t sl, 
   for (uint32_t j = 0; j < a.t[sl].len; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
   return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)a.t[sl].key * 0x9E3779B97F4A7C15ull)) % world);
 }
-__global__ void wc_owner_count_kernel(WcArgs a, uint32_t world, uint32_t* owner, unsigned long long* cur) {
+// Both passes add per owner into LDS first and reserve with one device
+// atomic per (workgroup, owner): a device-scope cursor per owner taking one
+// add per word was ~6 ms per pass (every word of a shard on the same few
+// addresses).  Worlds above WC_OWN_LDS fall back to the per-word adds.
+constexpr uint32_t WC_OWN_LDS = 64;
+__global__ __launch_bounds__(256) void wc_owner_count_kernel(WcArgs a, uint32_t world, uint32_t* owner,
+                                                             unsigned long long* cur) {
+  __shared__ unsigned long long lcur[WC_OWN_LDS];
+  const bool lds = world <= WC_OWN_LDS;
+  if (lds && threadIdx.x < world) lcur[threadIdx.x] = 0ull;
+  __syncthreads();
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
-  const uint32_t o = wc_slot_owner(a, sl, world);
-  owner[sl] = o;
-  atomicAdd(&cur[o], (1ull << 40) + a.t[sl].len);
+  if (sl <= a.t_mask && a.t[sl].h != 0ull) {
+    const uint32_t o = wc_slot_owner(a, sl, world);
+    owner[sl] = o;
+    const unsigned long long v = (1ull << 40) + a.t[sl].len;
+    if (lds) atomicAdd(&lcur[o], v);
+    else atomicAdd(&cur[o], v);
+  }
+  __syncthreads();
+  if (lds && threadIdx.x < world && lcur[threadIdx.x]) atomicAdd(&cur[threadIdx.x], lcur[threadIdx.x]);
 }
-__global__ void wc_owner_scatter_kernel(WcArgs a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
-                                        uint8_t* out) {
+__global__ __launch_bounds__(256) void wc_owner_scatter_kernel(WcArgs a, const uint32_t* owner,
+                                                               unsigned long long* cur, int64_t* meta,
+                                                               uint8_t* out, uint32_t world) {
+  __shared__ unsigned long long lcur[WC_OWN_LDS], lbase[WC_OWN_LDS];
+  const bool lds = world <= WC_OWN_LDS;
+  if (lds && threadIdx.x < world) lcur[threadIdx.x] = 0ull;
+  __syncthreads();
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl > a.t_mask || a.t[sl].h == 0ull) return;
-  const uint32_t len = a.t[sl].len;
-  const unsigned long long c = atomicAdd(&cur[owner[sl]], (1ull << 40) + len);
+  const bool v = sl <= a.t_mask && a.t[sl].h != 0ull;
+  uint32_t len = 0, o = 0;
+  unsigned long long c = 0;
+  if (v) {
+    len = a.t[sl].len;
+    o = owner[sl];
+    // rows and bytes advance together in one packed cursor, so a row's bytes
+    // start at the sum of the lengths of the rows before it
+    c = lds ? atomicAdd(&lcur[o], (1ull << 40) + len) : atomicAdd(&cur[o], (1ull << 40) + len);
+  }
+  __syncthreads();
+  if (lds && threadIdx.x < world && lcur[threadIdx.x]) lbase[threadIdx.x] = atomicAdd(&cur[threadIdx.x], lcur[threadIdx.x]);
+  __syncthreads();
+  if (!v) return;
+  if (lds) c += lbase[o];
   const uint64_t w = c >> 40, b = c & ((1ull << 40) - 1);
   meta[w * 3] = a.t[sl].key;
   meta[w * 3 + 1] = len;
@@ -2145,10 +2194,10 @@ int wc_launch_owner_count(const WcArgs& a, uint32_t world, uint32_t* owner, unsi
   return CCRDT_OK;
 }
 int wc_launch_owner_scatter(const WcArgs& a, const uint32_t* owner, unsigned long long* cur, int64_t* meta,
-                            uint8_t* out, hipStream_t st) {
+                            uint8_t* out, uint32_t world, hipStream_t st) {
   const uint64_t n = a.t_mask + 1;
   hipLaunchKernelGGL(wc_owner_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, owner, cur,
-                     meta, out);
+                     meta, out, world);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
