@@ -595,31 +595,22 @@ def _lb_rows_device(kp, kind, id_, score, origin: int, seq0: int):
     return r
 
 
-def _lb_apply_rows_device(engine, rows):
-    """Apply effect rows in canonical order (key, origin, seq) on the device;
-    returns the extras as rows (origin/seq left to the caller) and the sorted
-    batch size."""
+def _lb_apply_csr_device(engine, kp, kind, id_, score):
+    """Apply a batch already in canonical order (CSR by key) on the device;
+    returns the extras as rows (origin/seq left to the caller)."""
     import torch
-    nk = engine.n_keys
-    if nk >= (1 << 23):
-        raise ValueError("device replication packs keys into 23 bits")
-    order = torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])
-    r = rows[order]
-    kp = torch.zeros(nk + 1, dtype=torch.int64, device=rows.device)
-    kp[1:] = torch.cumsum(torch.bincount(r[:, 0], minlength=nk), 0)
-    kind = r[:, 3].to(torch.uint8).contiguous()
-    id_, score = r[:, 4].contiguous(), r[:, 5].contiguous()
-    n = int(r.shape[0])
+    n = int(kind.shape[0])
+    dev = kind.device
     torch.cuda.synchronize()
     engine.apply_device(_TorchBatch(n, key_ptr=kp, kind=kind, id=id_, score=score))
-    ex = torch.empty((max(n, 1), 4), dtype=torch.int64, device=rows.device)
-    cnt = torch.zeros(1, dtype=torch.int32, device=rows.device)
+    ex = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     from . import _lib
     _lib.check(_lib.lib.ccrdt_lb_extras_device(engine.h, ex.data_ptr(), max(n, 1), cnt.data_ptr()),
                "lb_extras_device")
     engine.sync()
     m = int(cnt.item())
-    out = torch.empty((m, 6), dtype=torch.int64, device=rows.device)
+    out = torch.empty((m, 6), dtype=torch.int64, device=dev)
     if m:
         e = ex[:m]
         out[:, 0] = e[:, 0]
@@ -628,6 +619,39 @@ def _lb_apply_rows_device(engine, rows):
         out[:, 5] = e[:, 3]
         out[:, 2] = e[:, 1]  # op index in the applied batch: stream order of the extras
     return out
+
+
+def _lb_canonical(rows):
+    """rows sorted by (key, origin, seq) (a 64-bit radix sort: for the small
+    row sets of the extras rounds)."""
+    import torch
+    return rows[torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])]
+
+
+def _lb_apply_rows_device(engine, rows, by_key_only: bool = False):
+    """Apply effect rows in canonical order (key, origin, seq) on the device;
+    returns the extras as rows (origin/seq left to the caller).
+    by_key_only: the rows are already in (origin, seq) order within every key
+    (origins concatenated in order, each in seq order), so a stable sort by
+    the 32-bit key alone puts them in canonical order."""
+    import torch
+    nk = engine.n_keys
+    if nk >= (1 << 23):
+        raise ValueError("device replication packs keys into 23 bits")
+    if by_key_only:
+        ks, order = torch.sort(rows[:, 0].to(torch.int32), stable=True)
+        kind = rows[:, 3].index_select(0, order).to(torch.uint8)
+        id_ = rows[:, 4].index_select(0, order)
+        score = rows[:, 5].index_select(0, order)
+        keys = ks.long()
+    else:
+        r = _lb_canonical(rows)
+        keys = r[:, 0]
+        kind = r[:, 3].to(torch.uint8).contiguous()
+        id_, score = r[:, 4].contiguous(), r[:, 5].contiguous()
+    kp = torch.zeros(nk + 1, dtype=torch.int64, device=rows.device)
+    kp[1:] = torch.cumsum(torch.bincount(keys, minlength=nk), 0)
+    return _lb_apply_csr_device(engine, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
 
 
 def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
@@ -640,16 +664,34 @@ def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
     seq = [0] * W
     outs = []
     # seq: a replica's rows are numbered in the order it sends them; extras
-    # take the counter + their op index in the batch that produced them
+    # take the counter + their op index in the batch that produced them.
+    # Round 0: a replica's own batch is already in canonical order (CSR by
+    # key, stream order), so it is applied as it is; its rows go out with its
+    # extras, the extras sorted by (key, seq), so every origin's rows are in
+    # (key, seq) order within a key and round 1 needs only a stable sort by key.
     for o, (e, b) in enumerate(zip(engines, batches)):
-        own = _lb_rows_device(*b, origin=o, seq0=0)
+        kp, kind, id_, score = b
+        own = _lb_rows_device(kp, kind, id_, score, origin=o, seq0=0)
         seq[o] = int(own.shape[0])
-        ex = _lb_apply_rows_device(e, own)
+        ex = _lb_apply_csr_device(e, kp.long(), kind.contiguous(), id_.contiguous(), score.contiguous())
         ex[:, 1] = o
         ex[:, 2] += seq[o]
         seq[o] += int(own.shape[0])
-        outs.append(torch.cat([own, ex]))
-    for rounds in range(max_rounds):
+        outs.append((own, _lb_canonical(ex) if ex.shape[0] else ex))
+    # round 1: every other origin's rows, origins in order
+    nxt = []
+    for r, e in enumerate(engines):
+        mine = torch.cat([x for o, (own, ex) in enumerate(outs) if o != r for x in (own, ex)])
+        if not mine.shape[0]:
+            nxt.append(mine)
+            continue
+        ex = _lb_apply_rows_device(e, mine, by_key_only=True)
+        ex[:, 1] = r
+        ex[:, 2] += seq[r]
+        seq[r] += int(mine.shape[0])
+        nxt.append(ex)
+    outs = nxt
+    for rounds in range(1, max_rounds):
         allr = torch.cat(outs)
         if not allr.shape[0]:
             return rounds

@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/wcx
-timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats -d gpurun_out/wcx -o wcx --output-format csv -- python3 bench_types.py --types wc_sharded --no-cpu --steps 2 --warmup 1 > gpurun_out/wcx/run.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats -d gpurun_out/wcx -o wcx --output-format csv -- python3 bench_types.py --types ${WCX_TYPES:-wc_sharded} --no-cpu --steps 2 --warmup 1 > gpurun_out/wcx/run.log 2>&1 || exit $?
 tail -1 gpurun_out/wcx/run.log | cut -c1-300
 f=$(find gpurun_out/wcx -name '*kernel_stats.csv' | head -1); python3 -c "
 import csv,sys
