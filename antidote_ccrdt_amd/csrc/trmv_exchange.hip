@@ -43,10 +43,19 @@ __global__ __launch_bounds__(256) void trmv_pack_extras_kernel(const uint64_t* k
                                                                const int64_t* ex_vc, uint64_t n_keys,
                                                                int n_dc, int64_t* rows, int64_t cap,
                                                                uint32_t* count) {
+  // (the workgroup's keys reserve their rows with one device atomic: a
+  // per-key add on the single count serialized every key with extras)
+  __shared__ uint32_t bsum, bbase;
+  if (threadIdx.x == 0) bsum = 0u;
+  __syncthreads();
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = k < n_keys ? ex_cnt[k] : 0u;
+  const uint32_t loc = c ? atomicAdd(&bsum, c) : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0 && bsum) bbase = atomicAdd(count, bsum);
+  __syncthreads();
   if (c == 0) return;
-  const uint32_t pos = atomicAdd(count, c);
+  const uint32_t pos = bbase + loc;
   const uint64_t op0 = key_ptr[k];
   const int w = 6 + n_dc;
   for (uint32_t j = 0; j < c; ++j) {

@@ -1267,10 +1267,19 @@ int lb_launch_apply(const LbArgs& a, int cls, uint64_t n_work, hipStream_t st) {
 __global__ __launch_bounds__(256) void lb_pack_extras_kernel(const uint64_t* key_ptr, const uint32_t* ex_cnt,
                                                              const LbExtraRec* ex, uint64_t n_keys,
                                                              int64_t* rows, int64_t cap, uint32_t* count) {
+  // (the workgroup's keys reserve their rows with one device atomic: a
+  // per-key add on the single count serialized every key with extras)
+  __shared__ uint32_t bsum, bbase;
+  if (threadIdx.x == 0) bsum = 0u;
+  __syncthreads();
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = k < n_keys ? ex_cnt[k] : 0u;
+  const uint32_t loc = c ? atomicAdd(&bsum, c) : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0 && bsum) bbase = atomicAdd(count, bsum);
+  __syncthreads();
   if (c == 0) return;
-  const uint32_t pos = atomicAdd(count, c);
+  const uint32_t pos = bbase + loc;
   const uint64_t op0 = key_ptr[k];
   for (uint32_t j = 0; j < c && (int64_t)pos + j < cap; ++j) {
     const LbExtraRec e = ex[op0 + j];
