@@ -621,6 +621,13 @@ def _lb_apply_csr_device(engine, kp, kind, id_, score):
     return out
 
 
+def _lb_cols(rows):
+    """Effect rows [n, 6] as columns (key int32, kind uint8, id, score)."""
+    import torch
+    return (rows[:, 0].to(torch.int32), rows[:, 3].to(torch.uint8), rows[:, 4].contiguous(),
+            rows[:, 5].contiguous())
+
+
 def _lb_canonical(rows):
     """rows sorted by (key, origin, seq) (a 64-bit radix sort: for the small
     row sets of the extras rounds)."""
@@ -662,35 +669,46 @@ def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
     import torch
     W = len(engines)
     seq = [0] * W
-    outs = []
     # seq: a replica's rows are numbered in the order it sends them; extras
     # take the counter + their op index in the batch that produced them.
     # Round 0: a replica's own batch is already in canonical order (CSR by
-    # key, stream order), so it is applied as it is; its rows go out with its
-    # extras, the extras sorted by (key, seq), so every origin's rows are in
-    # (key, seq) order within a key and round 1 needs only a stable sort by key.
+    # key, stream order), so it is applied as it is.  What it sends is kept as
+    # columns (key, kind, id, score): its own batch, then its extras sorted by
+    # (key, seq); every origin's rows are then in (key, seq) order within a key
+    # and round 1 needs only a stable sort of the origins' concatenation by key.
+    cols = []
     for o, (e, b) in enumerate(zip(engines, batches)):
         kp, kind, id_, score = b
-        own = _lb_rows_device(kp, kind, id_, score, origin=o, seq0=0)
-        seq[o] = int(own.shape[0])
+        n = int(kind.shape[0])
+        nk = int(kp.shape[0]) - 1
+        key = torch.repeat_interleave(torch.arange(nk, dtype=torch.int32, device=kind.device),
+                                      (kp[1:] - kp[:-1]).long(), output_size=n)
         ex = _lb_apply_csr_device(e, kp.long(), kind.contiguous(), id_.contiguous(), score.contiguous())
         ex[:, 1] = o
-        ex[:, 2] += seq[o]
-        seq[o] += int(own.shape[0])
-        outs.append((own, _lb_canonical(ex) if ex.shape[0] else ex))
+        ex[:, 2] += n
+        seq[o] = 2 * n
+        ex = _lb_canonical(ex) if ex.shape[0] else ex
+        cols.append(((key, kind, id_, score), _lb_cols(ex)))
     # round 1: every other origin's rows, origins in order
-    nxt = []
+    outs = []
     for r, e in enumerate(engines):
-        mine = torch.cat([x for o, (own, ex) in enumerate(outs) if o != r for x in (own, ex)])
-        if not mine.shape[0]:
-            nxt.append(mine)
+        parts = [c for o, (own, exc) in enumerate(cols) if o != r for c in (own, exc)]
+        key = torch.cat([c[0] for c in parts])
+        n = int(key.shape[0])
+        if not n:
+            outs.append(torch.empty((0, 6), dtype=torch.int64, device=key.device))
             continue
-        ex = _lb_apply_rows_device(e, mine, by_key_only=True)
+        ks, order = torch.sort(key, stable=True)
+        kind = torch.cat([c[1] for c in parts]).index_select(0, order)
+        id_ = torch.cat([c[2] for c in parts]).index_select(0, order)
+        score = torch.cat([c[3] for c in parts]).index_select(0, order)
+        nk = e.n_keys
+        kp = torch.searchsorted(ks, torch.arange(nk + 1, dtype=torch.int32, device=ks.device)).long()
+        ex = _lb_apply_csr_device(e, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
         ex[:, 1] = r
         ex[:, 2] += seq[r]
-        seq[r] += int(mine.shape[0])
-        nxt.append(ex)
-    outs = nxt
+        seq[r] += n
+        outs.append(ex)
     for rounds in range(1, max_rounds):
         allr = torch.cat(outs)
         if not allr.shape[0]:
