@@ -441,6 +441,15 @@ class ShardedWordcount:
         """Histogram this rank's documents (CSR by key, as ccrdt_wc_apply)."""
         self.local.apply(key_ptr, doc_off, data)
 
+    def restart_local(self) -> None:
+        """The local histogram starts over after an exchange: a reset engine
+        keeps its stream and device buffers (a new one cost ~5 ms of stream
+        creation plus the buffers' first allocation per exchange)."""
+        if hasattr(self.local, "reset"):
+            self.local.reset()
+        else:
+            self.local = self.local_factory()
+
     def partition(self):
         """The local histogram cut by owner: (send_meta [n, 3] = key, length,
         count in destination order, send_bytes, per-rank word counts)."""
@@ -465,7 +474,7 @@ class ShardedWordcount:
         rmeta, _ = a2a(meta.reshape(-1), [int(c) * 3 for c in per_rank])
         rdata, _ = a2a(data, bsplit)
         self.merge_received(rmeta.reshape(-1, 3), rdata)
-        self.local = self.local_factory()
+        self.restart_local()
 
     def merge_received(self, meta: np.ndarray, data: np.ndarray) -> None:
         if not meta.shape[0]:
@@ -530,7 +539,7 @@ def exchange_device(shard: ShardedWordcount) -> None:
         dist.all_to_all_single(rdata, data.contiguous(), [int(x) for x in r[:, 1]], [int(x) for x in ob])
         meta, data = rmeta, rdata
     _wc_merge_device(shard.owned, meta, data)
-    shard.local = shard.local_factory()
+    shard.restart_local()
 
 
 def exchange_local_device(shards: list[ShardedWordcount]) -> None:
@@ -546,7 +555,7 @@ def exchange_local_device(shards: list[ShardedWordcount]) -> None:
             datas.append(data[b0:b0 + int(ob[dst])])
         _wc_merge_device(s.owned, torch.cat(metas), torch.cat(datas))
     for s in shards:
-        s.local = s.local_factory()
+        s.restart_local()
 
 
 def exchange_local(shards: list[ShardedWordcount]) -> None:
@@ -563,7 +572,7 @@ def exchange_local(shards: list[ShardedWordcount]) -> None:
             datas.append(data[b0:b0 + int(lens[w0:w1].sum())])
         s.merge_received(np.concatenate(metas), np.concatenate(datas))
     for s in shards:
-        s.local = s.local_factory()
+        s.restart_local()
 
 
 # ------------------------------------- replication mode, on the device
