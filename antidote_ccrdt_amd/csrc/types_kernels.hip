@@ -1660,12 +1660,12 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // entries are per (document, word), so a workgroup's chunks are chunks of one
 // document (group_doc / group_ptr; the last group of a document may leave
 // waves idle).
-// (a.dbg 3-6: diagnostic builds of the step, CCRDT_WC_IDBG -- 3 LDS only,
-// 4 tokenizer only, 5 global lookups without the count adds, 6 the count adds
-// alone; their counts are wrong by design.  Measured on the 8 GiB corpus:
-// tokenizer 9.9 ms, + LDS table 18.8, + global lookups 25.7, full 29.2 -- the
-// device-scope count adds of the LDS misses (~40% of the Zipf tokens) are a
-// third of the kernel, and take the same time at workgroup scope)
+// (Measured on the 8 GiB corpus with diagnostic builds of the step, now
+// removed -- their early exits made the loop-carried miss below cost a full
+// vmcnt(0) wait per round: tokenizer 9.9 ms, + LDS table 18.8, + global
+// lookups 25.7, full 29.2; the device-scope count adds of the LDS misses
+// (~40% of the Zipf tokens) took the same time at workgroup scope.  a.dbg 5,
+// CCRDT_WC_IDBG: the global lookups without the count adds.)
 // An entry's representative is one u32: position - group base (RELB bits) |
 // length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
 template <int TAB, int WAVES>
@@ -1713,6 +1713,9 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
   __syncthreads();
   const uint64_t base_pos = gbase;
+  uint64_t ph = 0, ppos = 0, pseen = 0, pseen2 = 0;  // this lane's miss of the previous round
+  uint32_t ptl = 0;
+  bool pend = false;
 
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();  // the previous tile's staged bytes are no longer read
@@ -1724,66 +1727,84 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
     const uint32_t lrc = len - tile < 0xFFFFFFFFull ? (uint32_t)(len - tile) : 0xFFFFFFFFu;
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
       const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
-      for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
-        const uint32_t t = tlist[k];
-        const uint64_t s = tile + t;
-        uint64_t wh, lo, hi;
-        bool fast;
-        const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
-        const uint64_t h = wc_hkey(a, wh, key, tl);
-        if (a.dbg == 4) {  // diagnostic: tokenizer only
-          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
-          continue;
-        }
-        // buckets of 4 slots (32 B): one pair of 16-byte reads finds a word
-        // already in the table (the common case) without an atomic; the CAS
-        // only claims an empty slot
-        uint32_t bk = (uint32_t)(h >> 17) & (TAB / 4 - 1);
-        bool counted = false;
-        const int nprobe = tl < (1u << WC_LENB) - 1 ? WC_BPROBE : 0;
-        for (int p = 0; p < nprobe && !counted; ++p, bk = (bk + 1) & (TAB / 4 - 1)) {
-          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&lh[bk * 4]);
-          const ulonglong2 x0 = q[0], x1 = q[1];
-          uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
-          int hit = -1;
+      // One round per 64 tokens, two rounds per iteration: a round issues its
+      // misses' first-slot reads into one register and resolves the previous
+      // round's misses from the other, so the loop carries no copy of an
+      // in-flight load (a copy at the latch waited for it every round).
+      auto round = [&](uint32_t k, uint64_t& seen_prev, uint64_t& seen_new) {
+        const bool valid = k < ntk;
+        bool counted = true;
+        uint64_t h = 0, s = 0;
+        uint32_t tl = 0;
+        if (valid) {
+          const uint32_t t = tlist[k];
+          s = tile + t;
+          uint64_t wh, lo, hi;
+          bool fast;
+          tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
+          h = wc_hkey(a, wh, key, tl);
+          // buckets of 4 slots (32 B): one pair of 16-byte reads finds a word
+          // already in the table (the common case) without an atomic; the CAS
+          // only claims an empty slot
+          uint32_t bk = (uint32_t)(h >> 17) & (TAB / 4 - 1);
+          counted = false;
+          const int nprobe = tl < (1u << WC_LENB) - 1 ? WC_BPROBE : 0;
+          for (int p = 0; p < nprobe && !counted; ++p, bk = (bk + 1) & (TAB / 4 - 1)) {
+            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&lh[bk * 4]);
+            const ulonglong2 x0 = q[0], x1 = q[1];
+            uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
+            int hit = -1;
 #pragma unroll
-          for (int i = 3; i >= 0; --i)
-            if (e4[i] == h) hit = i;
-          if (hit >= 0) {
-            if (!a.wdc) atomicAdd(&lc[bk * 4 + hit], 1u);
-            counted = true;
-            break;
-          }
+            for (int i = 3; i >= 0; --i)
+              if (e4[i] == h) hit = i;
+            if (hit >= 0) {
+              if (!a.wdc) atomicAdd(&lc[bk * 4 + hit], 1u);
+              counted = true;
+              break;
+            }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (counted || e4[i] != 0ull) continue;
-            const uint32_t sl = bk * 4 + (uint32_t)i;
-            const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
-            if (prev == 0ull) {  // new word of the group: this token represents it
-              lp[sl] = (uint32_t)(b0 + s - base_pos) | tl << WC_RELB | ((uint32_t)wv << WS);
-              if (!a.wdc) atomicAdd(&lc[sl], 1u);
-              else lc[sl] = 1u;
-              counted = true;
-            } else if (prev == h) {
-              if (!a.wdc) atomicAdd(&lc[sl], 1u);
-              counted = true;
+            for (int i = 0; i < 4; ++i) {
+              if (counted || e4[i] != 0ull) continue;
+              const uint32_t sl = bk * 4 + (uint32_t)i;
+              const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
+              if (prev == 0ull) {  // new word of the group: this token represents it
+                lp[sl] = (uint32_t)(b0 + s - base_pos) | tl << WC_RELB | ((uint32_t)wv << WS);
+                if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                else lc[sl] = 1u;
+                counted = true;
+              } else if (prev == h) {
+                if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                counted = true;
+              }
             }
           }
         }
-        if (!counted && a.dbg == 3) {  // diagnostic: no global path
-          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);
-          continue;
-        }
-        if (!counted) {  // LDS table full (or a long token): global path
-          if (a.dbg == 6) {  // diagnostic: the count add alone
-            atomicAdd(&a.t_cnt[h & a.t_mask], 1ull);
-            continue;
-          }
-          const uint64_t gs = wc_global_insert(a, h, key, tl, b0 + s);
+        // global path (LDS table full, or a long token), one round behind:
+        // every lane issues this round's first-slot read (a lane without a
+        // miss reads slot 0), then the previous round's misses are resolved
+        seen_new = __hip_atomic_load(&a.t[counted ? 0ull : (h & a.t_mask)].h, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (pend) {
+          // (the common case -- the word at its first slot -- stays out of the
+          // probe loop, whose header would wait for every outstanding load)
+          const uint64_t gs = seen_prev == ph ? (ph & a.t_mask)
+                                              : wc_global_insert_at(a, ph, key, ptl, ppos, ph & a.t_mask, seen_prev);
           if (gs != ~0ull && a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
         }
+        pend = !counted;
+        ph = h;
+        ptl = tl;
+        ppos = b0 + s;
+      };
+      for (uint32_t k0 = 0; k0 < ntk; k0 += 128) {
+        round(k0 + (uint32_t)lane, pseen, pseen2);
+        round(k0 + 64u + (uint32_t)lane, pseen2, pseen);
       }
     }
+  }
+  if (pend) {
+    const uint64_t gs = wc_global_insert_at(a, ph, key, ptl, ppos, ph & a.t_mask, pseen);
+    if (gs != ~0ull && a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
   }
   __syncthreads();
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
