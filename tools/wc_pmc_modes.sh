@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/wcpmc
 mkdir -p $OUT
-for mode in 0 4 3; do
+for mode in 0 5; do  # (5: global lookups without the count adds; the tokenizer-only and LDS-only builds were removed)
   echo "== IDBG=$mode"
   timeout -k 10 240 env CCRDT_WC_IDBG=$mode CCRDT_WC_DBG=$([ $mode = 0 ] && echo 0 || echo 2) rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH -d $OUT/m$mode -o m$mode --output-format csv -- python3 bench_types.py --types wordcount --no-cpu --steps 1 --warmup 0 > $OUT/m$mode.log 2>&1 || exit $?
   python3 - $OUT/m$mode <<'PY'
