@@ -1656,7 +1656,8 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // The waves never wait for each other inside the chunk loop (each has its own
 // staging buffer and token list); only the table's set-up and its final flush
 // are workgroup-wide.
-// 4 waves; TAB 2048 (wordcount) / 1024 (worddocumentcount).  wordcount: chunks of different documents may share the
+// TAB x WAVES: 4096 x 16 (wordcount: one workgroup per CU), 1024 x 4
+// (worddocumentcount).  wordcount: chunks of different documents may share the
 // workgroup (the table keys on the hash, which includes the key, and each
 // entry remembers its wave for the document); worddocumentcount: its LDS
 // entries are per (document, word), so a workgroup's chunks are chunks of one
@@ -1672,7 +1673,7 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
 template <int TAB, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
-  constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : 3;
+  constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : WAVES == 8 ? 3 : 4;
   constexpr uint32_t WC_RELB = 17 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
   static_assert(WAVES == (1 << WB) && WAVES * WC_TPW * WC_TILE < (1ull << WC_RELB), "group span");
   __shared__ unsigned long long lh[TAB];
@@ -2077,11 +2078,12 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     if (!a.n_groups) return CCRDT_OK;
     // (measured on the 8 GiB corpus: 1024 entries 48.6 ms, 512 51.2, 2048 58.4 --
     // the dedupe path of the misses wants the occupancy of the smaller table)
+    // (one-document groups of 16 waves on 4096 / 2048 entries: 61.6 / 63.6 ms)
     hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)a.n_groups), dim3(256), 0, st, b);
   } else {
-    // (measured: 2048 entries 29.2 ms, 1024 33.9 ms; 8 waves sharing 2048 or
-    // 4096 entries 32.8 / 33.4 ms before the bucketed probes)
-    hipLaunchKernelGGL((wc_insert_kernel<2048, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+    // (one 16-wave workgroup per CU sharing 4096 entries: 26.2 ms; 4 waves
+    // sharing 2048: 29.0; 8 sharing 4096: 27.0; 16 sharing 2048: 29.4)
+    hipLaunchKernelGGL((wc_insert_kernel<4096, 16>), dim3((unsigned)((n_chunks + 15) / 16)), dim3(1024), 0, st, b);
   }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
