@@ -1674,7 +1674,8 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 template <int TAB, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : WAVES == 8 ? 3 : 4;
-  constexpr uint32_t WC_RELB = 17 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
+  constexpr uint32_t CB = WC_TPW == 8 ? 15 : WC_TPW == 16 ? 16 : 17;  // log2(chunk bytes)
+  constexpr uint32_t WC_RELB = CB + 1 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
   static_assert(WAVES == (1 << WB) && WAVES * WC_TPW * WC_TILE < (1ull << WC_RELB), "group span");
   __shared__ unsigned long long lh[TAB];
   __shared__ uint32_t lc[TAB];
