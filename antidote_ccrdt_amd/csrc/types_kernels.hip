@@ -2096,7 +2096,13 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   b.n_chunks = n_chunks;
   // (measured: a 512-word cache at 16 waves per CU beats 1024 words at 8)
   // (16 waves sharing 2048 / 1024 cached words: +1 ms)
-  hipLaunchKernelGGL((wc_verify_kernel<512, 4>), dim3((unsigned)((n_chunks + 3) / 4)), dim3(256), 0, st, b);
+#ifndef WC_VTAB
+#define WC_VTAB 512
+#endif
+#ifndef WC_VW
+#define WC_VW 4
+#endif
+  hipLaunchKernelGGL((wc_verify_kernel<WC_VTAB, WC_VW>), dim3((unsigned)((n_chunks + WC_VW - 1) / WC_VW)), dim3(64 * WC_VW), 0, st, b);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
