@@ -193,7 +193,8 @@ class topk:
                 return topk.new()
             st = Topk(TopkEngine(1, size), size, terms.TermInterner())
             if m:
-                codes = sorted((st.ids.code(i), m[i]) for i in m)
+                ids = list(m)
+                codes = sorted(zip(st.ids.codes(ids), (m[i] for i in ids)))
                 st.engine.import_state(_kp1(len(codes)), np.array([c for c, _ in codes], np.int64),
                                        np.array([v for _, v in codes], np.int64))
             return st
@@ -225,7 +226,7 @@ class topk:
             ids, scores = list(p), [p[i] for i in p]
         else:
             raise FunctionClause("update/2")
-        codes = [st.ids.code(i) for i in ids]  # may re-code st (and its chain) first
+        codes = st.ids.codes(ids)  # may re-code st (and its chain) first
         new = Topk(st.engine.clone(), st.size, st.ids)
         if ids:
             new.engine.apply(_kp1(len(ids)), codes, scores)

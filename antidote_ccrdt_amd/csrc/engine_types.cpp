@@ -1429,6 +1429,16 @@ int ccrdt_wc_partition_device(ccrdt_engine* e, int world, int64_t* d_meta, uint8
     set_error("wc_partition_device: output buffers smaller than ccrdt_wc_sizes");
     return CCRDT_EINVAL;
   }
+  // the owner cursors pack (rows << 40 | bytes) into one 64-bit word, so the
+  // rows of one table must stay below 2^24 and its bytes below 2^40
+  // (test hook CCRDT_WC_PART_MAX_WORDS lowers the row limit)
+  uint64_t max_words = 1ull << 24;
+  if (const char* s = getenv("CCRDT_WC_PART_MAX_WORDS")) max_words = std::min<uint64_t>(max_words, strtoull(s, nullptr, 0));
+  if ((uint64_t)nw >= max_words || (uint64_t)nb >= (1ull << 40)) {
+    set_error("wc_partition_device: more than 2^24 - 1 words or 2^40 - 1 bytes in one table "
+              "(export with ccrdt_wc_export and partition on the host)");
+    return CCRDT_ERANGE;
+  }
   TypeBufs& T = e->tb;
   const int c = T.tcur;
   WcArgs a = wc_table_args(e, c);

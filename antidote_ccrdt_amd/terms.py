@@ -174,6 +174,15 @@ class TermInterner:
         self._term[c] = t
         return c
 
+    def codes(self, ts) -> list:
+        """The codes of several terms, read after every one of them is
+        interned: interning a later term can re-space the codes of the earlier
+        ones, so codes are never collected while terms are still being added."""
+        ts = list(ts)
+        for t in ts:
+            self.code(t)
+        return [self._code[term_key(t)] for t in ts]
+
     def term(self, c: int):
         return self._term[int(c)]
 

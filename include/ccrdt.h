@@ -404,7 +404,9 @@ int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint
  * word of the maps, grouped by owner rank (the ccrdt_wc_owner function),
  * into device rows d_meta[n_words][3] = {key, length, count} and their bytes
  * d_bytes in the same order; owner_words / owner_bytes (host, [world]) get
- * each owner's share.  Buffers sized by ccrdt_wc_sizes. */
+ * each owner's share.  Buffers sized by ccrdt_wc_sizes.  CCRDT_ERANGE for a
+ * table of 2^24 words or more (or 2^40 bytes): partition the export on the
+ * host instead (cluster.ShardedWordcount.partition). */
 int ccrdt_wc_partition_device(ccrdt_engine* e, int world, int64_t* d_meta, uint8_t* d_bytes, int64_t cap_words,
                               int64_t cap_bytes, int64_t* owner_words, int64_t* owner_bytes);
 /* ccrdt_wc_merge of device rows {key, length, count} and their bytes (the

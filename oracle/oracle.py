@@ -159,6 +159,7 @@ def _setup_types(l):
     l.orc_wc_create.argtypes = [I64, INT]
     l.orc_wc_destroy.argtypes = [P]
     l.orc_wc_apply.argtypes = [P, P, P, P]
+    l.orc_wc_apply_mt.argtypes = [P, P, P, P, INT]
     l.orc_wc_sizes.argtypes = [P, P, P]
     l.orc_wc_export.argtypes = [P, P, P, P, P]
 
@@ -276,11 +277,16 @@ class WcOracle:
         if getattr(self, "h", None):
             tlib().orc_wc_destroy(self.h)
 
-    def apply(self, key_ptr, doc_off, data):
+    def apply(self, key_ptr, doc_off, data, n_threads: int = 1):
+        """add/2 of every document, CSR by key; n_threads > 1 splits each
+        key's documents over threads (per-thread maps, then summed)."""
         b = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
         b = np.ascontiguousarray(b) if b.shape[0] else np.zeros(1, np.uint8)
         kp, do = _a(key_ptr, np.uint64), _a(doc_off, np.uint64)
-        tlib().orc_wc_apply(self.h, _p(kp), _p(do), _p(b))
+        if n_threads > 1:
+            tlib().orc_wc_apply_mt(self.h, _p(kp), _p(do), _p(b), int(n_threads))
+        else:
+            tlib().orc_wc_apply(self.h, _p(kp), _p(do), _p(b))
 
     def apply_docs(self, docs_per_key):
         kp = np.zeros(self.n_keys + 1, np.uint64)

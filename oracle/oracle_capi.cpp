@@ -346,6 +346,40 @@ void orc_wc_apply(void* h, const uint64_t* key_ptr, const uint64_t* doc_off, con
       }
     }
 }
+// The same fold with each key's documents split over n_threads threads: every
+// thread folds add/2 over its documents into a map of its own (the +1s of
+// wordcount.erl:78-85 / worddocumentcount.erl:78-86 commute), then the maps
+// are summed into the key's map.  Used for the corpus-sized parity tests.
+void orc_wc_apply_mt(void* h, const uint64_t* key_ptr, const uint64_t* doc_off, const uint8_t* bytes,
+                     int n_threads) {
+  auto* s = (WcSet*)h;
+  if (n_threads < 1) n_threads = 1;
+  for (size_t k = 0; k < s->keys.size(); ++k) {
+    const uint64_t d0 = key_ptr[k], d1 = key_ptr[k + 1];
+    std::vector<std::map<std::string, i64>> part(n_threads);
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t)
+      th.emplace_back([&, t] {
+        for (uint64_t d = d0 + t; d < d1; d += n_threads) {
+          std::string f((const char*)bytes + doc_off[d], doc_off[d + 1] - doc_off[d]);
+          if (s->wdc) {
+            WordDocCount w;
+            w.counts.swap(part[t]);
+            w.add(f);
+            w.counts.swap(part[t]);
+          } else {
+            Wordcount w;
+            w.counts.swap(part[t]);
+            w.add(f);
+            w.counts.swap(part[t]);
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+    for (auto& m : part)
+      for (auto& [w, c] : m) s->keys[k][w] += c;
+  }
+}
 void orc_wc_sizes(void* h, int64_t* n_words, int64_t* n_bytes) {
   int64_t w = 0, b = 0;
   for (auto& m : ((WcSet*)h)->keys)

@@ -166,3 +166,22 @@ def test_term_interner_order_and_respace():
     assert seen, "codes were re-spaced"
     assert sorted(t._term.values(), key=t.code) == sorted(t._term.values(), key=term_key)
     assert all(t.term(t.code(x)) == x for x in xs)
+
+
+def test_term_interner_codes_across_respace():
+    """codes() of one batch whose own terms use up a gap: every
+    returned code is live after the re-space and keeps term order."""
+    from antidote_ccrdt_amd.terms import TermInterner, term_key
+    t = TermInterner()
+    t.code(b"")
+    t.code(b"\x01")
+    ids = [b"\x00" + b"\x01" * i for i in range(200)]  # all between b"" and b"\x01"
+    codes = t.codes(ids)
+    assert [t.term(c) for c in codes] == ids
+    assert sorted(ids, key=term_key) == [t.term(c) for c in sorted(codes)]
+    # the old per-term loop would have kept stale codes
+    t2 = TermInterner()
+    t2.code(b"")
+    t2.code(b"\x01")
+    stale = [t2.code(i) for i in ids]
+    assert any(c not in t2._term for c in stale)

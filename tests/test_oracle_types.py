@@ -108,3 +108,23 @@ def test_wordcount_empty_tokens_unpinned():
     o = orc.WcOracle(1, True)
     o.apply_docs([[b"a  b\nc ", b"", b"a\ta"]])
     assert o.value() == {b"a": 1, b"b": 1, b"c": 1, b"": 2, b"a\ta": 1}
+
+
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_threaded_oracle_matches(wdc):
+    """orc_wc_apply_mt (documents split over threads, maps summed) gives the
+    sequential fold's maps, two keys, documents with repeated words."""
+    rng = np.random.default_rng(5)
+    vocab = [b"w%d" % i for i in range(300)] + [b""]
+    docs = [[b" ".join(vocab[j] for j in rng.integers(0, len(vocab), rng.integers(0, 80)))
+             for _ in range(int(rng.integers(1, 40)))] for _ in range(2)]
+    a, b = orc.WcOracle(2, wdc), orc.WcOracle(2, wdc)
+    a.apply_docs(docs)
+    kp = np.zeros(3, np.uint64)
+    kp[1:] = np.cumsum([len(d) for d in docs])
+    flat = [d for ds in docs for d in ds]
+    off = np.zeros(len(flat) + 1, np.uint64)
+    off[1:] = np.cumsum([len(d) for d in flat])
+    b.apply(kp, off, b"".join(flat), n_threads=7)
+    for x, y in zip(a.export(), b.export()):
+        assert np.array_equal(x, y)

@@ -322,3 +322,21 @@ def test_wc_merge_device_rejects_bad_rows(gpu):
                              torch.tensor([120], dtype=torch.uint8).cuda())
         assert ei.value.code == _lib.EINVAL
     assert all(np.array_equal(x, y) for x, y in zip(e.export(), before))
+
+
+@pytest.mark.gpu
+def test_wc_partition_device_row_limit(gpu, monkeypatch):
+    """The device partition packs (rows << 40 | bytes) per owner: a table at
+    the row limit is refused with ERANGE (limit lowered by the test hook)."""
+    from antidote_ccrdt_amd import _lib
+    from antidote_ccrdt_amd.cluster import _wc_partition_device
+    from antidote_ccrdt_amd.types import WordcountEngine
+    e = WordcountEngine(1)
+    e.apply_docs([[b"a b c"]])
+    monkeypatch.setenv("CCRDT_WC_PART_MAX_WORDS", "3")
+    with pytest.raises(_lib.CcrdtError) as ei:
+        _wc_partition_device(e, 2)
+    assert ei.value.code == _lib.ERANGE
+    monkeypatch.setenv("CCRDT_WC_PART_MAX_WORDS", "4")
+    meta, data, ow, ob = _wc_partition_device(e, 2)
+    assert int(ow.sum()) == 3 and int(ob.sum()) == 3
