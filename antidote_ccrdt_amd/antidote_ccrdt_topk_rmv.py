@@ -71,11 +71,14 @@ def new(size: int = 100) -> TopkRmv:
 
 
 def value(state: TopkRmv):
-    """value/1 (topk_rmv.erl:91-95): [{Id, Score}] sorted by Id.  The
-    reference builds the list with maps:fold, so its order is the map's
-    iteration order (an implementation detail of the BEAM, Q7): compare
-    value/1 results as sets."""
-    return [(i, sc) for i, sc, _, _ in state._export()["obs"]]
+    """value/1 (topk_rmv.erl:91-95): [{Id, Score}], built as the reference
+    builds it: maps:fold over Observed, prepending each pair.  A map of at
+    most 32 keys iterates in ascending key order, so the fold yields the
+    pairs in DESCENDING Id order; a larger map iterates in the BEAM's HAMT
+    hash order (Q7), which this keeps as descending Id order too (compare
+    larger lists as sets)."""
+    obs = sorted(((i, sc) for i, sc, _, _ in state._export()["obs"]), key=lambda p: terms.term_key(p[0]))
+    return obs[::-1]
 
 
 def _vc_dense(vc: dict):

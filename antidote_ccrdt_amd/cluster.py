@@ -21,7 +21,7 @@ same ``apply``/``export`` interface.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -79,6 +79,21 @@ def route(batch: TrmvBatch, keys: np.ndarray) -> Shard:
     sub = TrmvBatch(lkp.astype(np.uint64), kind, batch.id[op_index], batch.score[op_index],
                     batch.dc[op_index], ts, np.ascontiguousarray(rvc, dtype=np.int64))
     return Shard(keys, sub, op_index)
+
+
+def _apply_keycap(engine, batch, host_keys: set, key_ids=None):
+    """engine.apply(batch, want_extra=True), with CCRDT_EKEYCAP turned into a
+    record: the batch committed for every key but the listed ones, whose
+    extras are in err.extra; their (global) ids join host_keys."""
+    from ._lib import KeyCapacityError
+    try:
+        return engine.apply(batch, want_extra=True)
+    except KeyCapacityError as err:
+        keys = np.asarray(err.keys if err.keys is not None else [], np.int64)
+        if key_ids is not None:
+            keys = np.asarray(key_ids, np.int64)[keys]
+        host_keys.update(int(k) for k in keys)
+        return err.extra
 
 
 def _dist():
@@ -160,15 +175,26 @@ class ShardedTopkRmv:
             def engine_factory(nk, kk, d):
                 return TopkRmvEngine(nk, kk, d, device=device)
         self.engine = engine_factory(len(self.keys), k, n_dc)
+        self.host_keys: set[int] = set()
 
     def apply(self, batch: TrmvBatch) -> np.ndarray:
         """update/2 over this rank's keys of a global batch; returns the
-        rank's extra effects as packed rows (global op index first)."""
+        rank's extra effects as packed rows (global op index first).  Keys
+        over the engine's per-key capacity (CCRDT_EKEYCAP: the batch
+        committed for every other key) are recorded, as global ids, in
+        `host_keys` for the host path, and the rank goes on with the
+        collectives like the others."""
         sh = route(batch, self.keys)
-        x = self.engine.apply(sh.batch, want_extra=True)
+        x = _apply_keycap(self.engine, sh.batch, self.host_keys, self.keys)
         if isinstance(x, dict):
             x = TrmvExtra(**x)
         return pack_extras(x, sh.op_index)
+
+    def host_keys_all(self) -> np.ndarray:
+        """Every rank's host-path keys (CCRDT_EKEYCAP), all-gathered: the same
+        sorted global ids on every rank."""
+        mine = np.array(sorted(self.host_keys), np.int64).reshape(-1, 1)
+        return np.unique(all_gather_rows(mine)[:, 0]) if self.world > 1 else mine[:, 0]
 
     def exchange_extras(self, rows: np.ndarray) -> np.ndarray:
         """Every rank's extras, in stream order (identical on all ranks)."""
@@ -210,9 +236,11 @@ def all_reduce_sum(v: int) -> int:
 
 @dataclass
 class _TrmvCodec:
-    """topk_rmv effects as rows: origin, seq, key, kind, id, score, dc, ts, vc[n_dc]."""
+    """topk_rmv effects as rows: origin, seq, key, kind, id, score, dc, ts, vc[n_dc].
+    host_keys: keys the engine handed to the host path (CCRDT_EKEYCAP)."""
     n_keys: int
     n_dc: int
+    host_keys: set = field(default_factory=set)
     COLS = 8
 
     def rows_of_batch(self, b: TrmvBatch) -> np.ndarray:
@@ -241,7 +269,7 @@ class _TrmvCodec:
         """Apply rows (already in canonical order); the extras as rows
         (origin/seq left for the caller)."""
         b = self.batch_of_rows(r)
-        x = engine.apply(b, want_extra=True)
+        x = _apply_keycap(engine, b, self.host_keys)
         if isinstance(x, dict):
             x = TrmvExtra(**x)
         sel = np.nonzero(x.kind != 255)[0]
@@ -494,6 +522,52 @@ class ShardedWordcount:
         return self.owned.export()
 
 
+class TorchCollective:
+    """The collectives the multi-GPU steps inject, on device tensors, over
+    torch.distributed: RCCL (``nccl``) moves the device tensors over xGMI
+    directly; any other backend (gloo: the multi-process tests on one GPU)
+    stages them through the host and hands back tensors on their device.
+    The single-process drivers (replicas or shards held by one process)
+    call the same step functions with the exchange done by slicing."""
+
+    def __init__(self, dist=None):
+        self.dist = dist or _dist()
+        if self.dist is None:
+            raise RuntimeError("TorchCollective needs an initialised process group")
+        self.rank, self.world = self.dist.get_rank(), self.dist.get_world_size()
+        self.staged = self.dist.get_backend() != "nccl"
+
+    def _wire(self, t):
+        return t.cpu() if self.staged else t
+
+    def all_gather_v(self, t):
+        """Rank r's t (variable first dimension) -> [t of rank 0, ..., t of rank W-1]."""
+        import torch
+        w = self._wire(t)
+        n = torch.tensor([w.shape[0]], dtype=torch.int64, device=w.device)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n)
+        counts = [int(c) for c in torch.cat(ns).cpu()]
+        buf = torch.zeros((max(max(counts), 1),) + tuple(w.shape[1:]), dtype=w.dtype, device=w.device)
+        buf[:w.shape[0]] = w
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(outs, buf)
+        return [o[:c].to(t.device) for o, c in zip(outs, counts)]
+
+    def all_to_all_v(self, t, splits):
+        """Rank r sends t[sum(splits[:d]) : sum(splits[:d+1])] to rank d;
+        returns (what every rank sent to r, in rank order; its sizes)."""
+        import torch
+        w = self._wire(t.contiguous())
+        sz = torch.tensor([int(x) for x in splits], dtype=torch.int64, device=w.device)
+        rsz = torch.empty(self.world, dtype=torch.int64, device=w.device)
+        self.dist.all_to_all_single(rsz, sz)
+        rsplits = [int(x) for x in rsz.cpu()]
+        out = torch.empty((sum(rsplits),) + tuple(w.shape[1:]), dtype=w.dtype, device=w.device)
+        self.dist.all_to_all_single(out, w, rsplits, [int(x) for x in splits])
+        return out.to(t.device), rsplits
+
+
 def _wc_partition_device(engine, world: int):
     """(meta [n, 3] int64, bytes uint8, per-owner word counts, per-owner byte
     counts) of an engine's maps, grouped by owner, all on the device."""
@@ -519,24 +593,19 @@ def _wc_merge_device(engine, meta, data) -> None:
                "wc_merge_device")
 
 
-def exchange_device(shard: ShardedWordcount) -> None:
-    """ShardedWordcount.exchange with the words kept on the device: partition
-    by owner on the GPU, one all_to_all_single each for the rows and their
-    bytes (RCCL), merge on the GPU.  The local histogram starts over."""
-    import torch
-    dist = _dist()
+def exchange_device(shard: ShardedWordcount, coll=None) -> None:
+    """ShardedWordcount.exchange with the words kept on the device: the
+    shard's maps partitioned by owner on the GPU (ccrdt_wc_partition_device),
+    one variable all-to-all each for the rows and their bytes through the
+    injected collective (TorchCollective: RCCL, or gloo staged through the
+    host), the received words merged on the GPU (ccrdt_wc_merge_device).
+    The local histogram starts over.  exchange_local_device runs the same
+    partition and merge with the all-to-all done by slicing."""
+    coll = coll if coll is not None else (TorchCollective() if _dist() is not None else None)
     meta, data, ow, ob = _wc_partition_device(shard.local, shard.world)
-    if dist is not None:
-        world = dist.get_world_size()
-        sz = torch.tensor(np.concatenate([ow, ob]), dtype=torch.int64, device=meta.device)
-        rsz = torch.empty(2 * world, dtype=torch.int64, device=meta.device)
-        dist.all_to_all_single(rsz, sz, [2] * world, [2] * world)
-        r = rsz.view(world, 2).cpu().numpy()
-        rmeta = torch.empty((int(r[:, 0].sum()), 3), dtype=torch.int64, device=meta.device)
-        rdata = torch.empty(int(r[:, 1].sum()), dtype=torch.uint8, device=meta.device)
-        dist.all_to_all_single(rmeta.view(-1), meta.contiguous().view(-1), [int(x) * 3 for x in r[:, 0]],
-                               [int(x) * 3 for x in ow])
-        dist.all_to_all_single(rdata, data.contiguous(), [int(x) for x in r[:, 1]], [int(x) for x in ob])
+    if coll is not None and coll.world > 1:
+        rmeta, _ = coll.all_to_all_v(meta, [int(x) for x in ow])
+        rdata, _ = coll.all_to_all_v(data, [int(x) for x in ob])
         meta, data = rmeta, rdata
     _wc_merge_device(shard.owned, meta, data)
     shard.restart_local()
@@ -586,35 +655,19 @@ class _TorchBatch:
         return self.cols[k].data_ptr()
 
 
-def _lb_rows_device(kp, kind, id_, score, origin: int, seq0: int):
-    """Effect rows [n, 6] = key, origin, seq, kind, id, score of a CSR batch
-    (device tensors), seq = seq0 + position in the batch."""
-    import torch
-    dev = kp.device
-    n = kind.shape[0]
-    nk = kp.shape[0] - 1
-    key = torch.repeat_interleave(torch.arange(nk, device=dev), (kp[1:] - kp[:-1]).long(), output_size=n)
-    r = torch.empty((n, 6), dtype=torch.int64, device=dev)
-    r[:, 0] = key
-    r[:, 1] = origin
-    r[:, 2] = torch.arange(seq0, seq0 + n, device=dev)
-    r[:, 3] = kind.long()
-    r[:, 4] = id_
-    r[:, 5] = score
-    return r
-
-
 def _lb_apply_csr_device(engine, kp, kind, id_, score):
     """Apply a batch already in canonical order (CSR by key) on the device;
-    returns the extras as rows (origin/seq left to the caller)."""
+    returns the extras as rows [m, 6] (key, -, op index in the batch, kind,
+    id, score; origin and seq are the caller's)."""
     import torch
+
+    from . import _lib
     n = int(kind.shape[0])
     dev = kind.device
     torch.cuda.synchronize()
     engine.apply_device(_TorchBatch(n, key_ptr=kp, kind=kind, id=id_, score=score))
     ex = torch.empty((max(n, 1), 4), dtype=torch.int64, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    from . import _lib
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)  # zeroed on the engine stream by the launcher
     _lib.check(_lib.lib.ccrdt_lb_extras_device(engine.h, ex.data_ptr(), max(n, 1), cnt.data_ptr()),
                "lb_extras_device")
     engine.sync()
@@ -623,114 +676,123 @@ def _lb_apply_csr_device(engine, kp, kind, id_, score):
     if m:
         e = ex[:m]
         out[:, 0] = e[:, 0]
-        out[:, 3] = 0  # {add, {Id, Score}}
+        out[:, 2] = e[:, 1]  # op index in the applied batch: stream order of the extras
+        out[:, 3] = 0        # {add, {Id, Score}} (leaderboard.erl:282-284)
         out[:, 4] = e[:, 2]
         out[:, 5] = e[:, 3]
-        out[:, 2] = e[:, 1]  # op index in the applied batch: stream order of the extras
     return out
 
 
-def _lb_cols(rows):
-    """Effect rows [n, 6] as columns (key int32, kind uint8, id, score)."""
-    import torch
-    return (rows[:, 0].to(torch.int32), rows[:, 3].to(torch.uint8), rows[:, 4].contiguous(),
-            rows[:, 5].contiguous())
-
-
 def _lb_canonical(rows):
-    """rows sorted by (key, origin, seq) (a 64-bit radix sort: for the small
-    row sets of the extras rounds)."""
+    """rows sorted by (key, origin, seq): one sort of a packed 64-bit key
+    when key < 2^23, origin < 16 and seq < 2^36, else three stable sorts."""
     import torch
-    return rows[torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])]
+    if not rows.shape[0]:
+        return rows
+    if (int(rows[:, 0].max()) < (1 << 23) and int(rows[:, 1].max()) < 16 and int(rows[:, 2].max()) < (1 << 36)
+            and int(rows[:, :3].min()) >= 0):
+        return rows[torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])]
+    order = torch.argsort(rows[:, 2], stable=True)
+    for c in (1, 0):
+        order = order[torch.argsort(rows[order, c], stable=True)]
+    return rows[order]
 
 
 def _lb_apply_rows_device(engine, rows, by_key_only: bool = False):
     """Apply effect rows in canonical order (key, origin, seq) on the device;
     returns the extras as rows (origin/seq left to the caller).
     by_key_only: the rows are already in (origin, seq) order within every key
-    (origins concatenated in order, each in seq order), so a stable sort by
-    the 32-bit key alone puts them in canonical order."""
+    (origins concatenated in order, each in (key, seq) order), so a stable
+    sort by the key alone puts them in canonical order."""
     import torch
     nk = engine.n_keys
-    if nk >= (1 << 23):
-        raise ValueError("device replication packs keys into 23 bits")
     if by_key_only:
-        ks, order = torch.sort(rows[:, 0].to(torch.int32), stable=True)
-        kind = rows[:, 3].index_select(0, order).to(torch.uint8)
-        id_ = rows[:, 4].index_select(0, order)
-        score = rows[:, 5].index_select(0, order)
-        keys = ks.long()
+        ks, order = torch.sort(rows[:, 0], stable=True)
+        r = rows.index_select(0, order)
     else:
         r = _lb_canonical(rows)
-        keys = r[:, 0]
-        kind = r[:, 3].to(torch.uint8).contiguous()
-        id_, score = r[:, 4].contiguous(), r[:, 5].contiguous()
-    kp = torch.zeros(nk + 1, dtype=torch.int64, device=rows.device)
-    kp[1:] = torch.cumsum(torch.bincount(keys, minlength=nk), 0)
-    return _lb_apply_csr_device(engine, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
+        ks = r[:, 0].contiguous()
+    kp = torch.searchsorted(ks, torch.arange(nk + 1, dtype=ks.dtype, device=ks.device))
+    return _lb_apply_csr_device(engine, kp, r[:, 3].to(torch.uint8).contiguous(), r[:, 4].contiguous(),
+                                r[:, 5].contiguous())
+
+
+class LbDeviceReplica:
+    """One DC replica of n_keys leaderboards with its effect rows on the
+    device (BASELINE configs[3]; the protocol of ReplicatedLeaderboard,
+    leaderboard.erl:128-134,282-284).  Rows are int64 [n, 6] = key, origin,
+    seq, kind, id, score.  A step is originate() and then deliver() per
+    round; the exchange between them is injected: lb_replicate_step with a
+    TorchCollective (one process per GPU) or lb_replicate_device_local
+    (replicas held by one process, exchange = the list of every replica's
+    rows).  Both run exactly these two methods."""
+
+    def __init__(self, engine, rank: int, world: int):
+        self.engine, self.rank, self.world = engine, rank, world
+        self.seq = 0
+        self.first = True
+
+    def originate(self, batch):
+        """Apply this replica's own batch (device (key_ptr, kind, id, score),
+        CSR by key, stream order) -- already canonical for one origin -- and
+        return the rows it sends: the batch, then its extras, each in (key,
+        seq) order."""
+        import torch
+        kp, kind, id_, score = batch
+        kp = kp.long()
+        n, nk = int(kind.shape[0]), int(kp.shape[0]) - 1
+        dev = kind.device
+        ex = _lb_apply_csr_device(self.engine, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
+        own = torch.empty((n, 6), dtype=torch.int64, device=dev)
+        own[:, 0] = torch.repeat_interleave(torch.arange(nk, device=dev), kp[1:] - kp[:-1], output_size=n)
+        own[:, 1] = self.rank
+        own[:, 2] = torch.arange(n, device=dev)
+        own[:, 3] = kind.long()
+        own[:, 4] = id_
+        own[:, 5] = score
+        ex[:, 1] = self.rank
+        ex[:, 2] += n  # extras: seq = n + op index
+        self.seq, self.first = 2 * n, True
+        return torch.cat([own, _lb_canonical(ex)])
+
+    def deliver(self, parts):
+        """Apply the rows of every other origin (parts[o] = origin o's rows)
+        in canonical order; returns the extras that produced, stamped as
+        this replica's rows."""
+        import torch
+        rows = torch.cat([p for o, p in enumerate(parts) if o != self.rank])
+        first, self.first = self.first, False
+        if not rows.shape[0]:
+            return rows
+        ex = _lb_apply_rows_device(self.engine, rows, by_key_only=first)
+        ex[:, 1] = self.rank
+        ex[:, 2] += self.seq
+        self.seq += int(rows.shape[0])
+        return ex
+
+
+def lb_replicate_step(replica: LbDeviceReplica, batch, coll, max_rounds: int = 64) -> int:
+    """One replication step of this rank's replica over a collective
+    (TorchCollective: RCCL over xGMI, or gloo staged through the host);
+    returns the number of delivery rounds."""
+    out = replica.originate(batch)
+    for rounds in range(max_rounds):
+        parts = coll.all_gather_v(out)
+        if not any(int(p.shape[0]) for p in parts):
+            return rounds
+        out = replica.deliver(parts)
+    raise RuntimeError("replication did not quiesce")
 
 
 def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
-    """ReplicatedLeaderboard's step with every row on the device, for several
-    replicas held by one process (exchange = concatenation).  `batches` are
-    (key_ptr, kind, id, score) device tensors, CSR by key.  Returns the number
-    of delivery rounds."""
-    import torch
-    W = len(engines)
-    seq = [0] * W
-    # seq: a replica's rows are numbered in the order it sends them; extras
-    # take the counter + their op index in the batch that produced them.
-    # Round 0: a replica's own batch is already in canonical order (CSR by
-    # key, stream order), so it is applied as it is.  What it sends is kept as
-    # columns (key, kind, id, score): its own batch, then its extras sorted by
-    # (key, seq); every origin's rows are then in (key, seq) order within a key
-    # and round 1 needs only a stable sort of the origins' concatenation by key.
-    cols = []
-    for o, (e, b) in enumerate(zip(engines, batches)):
-        kp, kind, id_, score = b
-        n = int(kind.shape[0])
-        nk = int(kp.shape[0]) - 1
-        key = torch.repeat_interleave(torch.arange(nk, dtype=torch.int32, device=kind.device),
-                                      (kp[1:] - kp[:-1]).long(), output_size=n)
-        ex = _lb_apply_csr_device(e, kp.long(), kind.contiguous(), id_.contiguous(), score.contiguous())
-        ex[:, 1] = o
-        ex[:, 2] += n
-        seq[o] = 2 * n
-        ex = _lb_canonical(ex) if ex.shape[0] else ex
-        cols.append(((key, kind, id_, score), _lb_cols(ex)))
-    # round 1: every other origin's rows, origins in order
-    outs = []
-    for r, e in enumerate(engines):
-        parts = [c for o, (own, exc) in enumerate(cols) if o != r for c in (own, exc)]
-        key = torch.cat([c[0] for c in parts])
-        n = int(key.shape[0])
-        if not n:
-            outs.append(torch.empty((0, 6), dtype=torch.int64, device=key.device))
-            continue
-        ks, order = torch.sort(key, stable=True)
-        kind = torch.cat([c[1] for c in parts]).index_select(0, order)
-        id_ = torch.cat([c[2] for c in parts]).index_select(0, order)
-        score = torch.cat([c[3] for c in parts]).index_select(0, order)
-        nk = e.n_keys
-        kp = torch.searchsorted(ks, torch.arange(nk + 1, dtype=torch.int32, device=ks.device)).long()
-        ex = _lb_apply_csr_device(e, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
-        ex[:, 1] = r
-        ex[:, 2] += seq[r]
-        seq[r] += n
-        outs.append(ex)
-    for rounds in range(1, max_rounds):
-        allr = torch.cat(outs)
-        if not allr.shape[0]:
+    """lb_replicate_step for several replicas held by one process (the
+    all-gather is the list of every replica's rows).  `batches` are
+    (key_ptr, kind, id, score) device tensors, CSR by key.  Returns the
+    number of delivery rounds."""
+    reps = [LbDeviceReplica(e, r, len(engines)) for r, e in enumerate(engines)]
+    outs = [r.originate(b) for r, b in zip(reps, batches)]
+    for rounds in range(max_rounds):
+        if not any(int(o.shape[0]) for o in outs):
             return rounds
-        outs = []
-        for r, e in enumerate(engines):
-            mine = allr[allr[:, 1] != r]
-            if not mine.shape[0]:
-                outs.append(mine)
-                continue
-            ex = _lb_apply_rows_device(e, mine)
-            ex[:, 1] = r
-            ex[:, 2] += seq[r]
-            seq[r] += int(mine.shape[0])
-            outs.append(ex)
+        outs = [r.deliver(outs) for r in reps]
     raise RuntimeError("replication did not quiesce")

@@ -74,7 +74,8 @@ def test_value_equal_binary_roundtrip(gpu, mocks):
     t = trmv.new(3)
     for i, (pid, sc) in enumerate([(1, 5), (2, 7), (3, 1), (4, 9)]):
         t = trmv.update(("add", (pid, sc, (names[0], i + 1))), t)[1]
-    assert sorted(trmv.value(t)) == [(1, 5), (2, 7), (4, 9)]
+    # maps:fold with prepend over a small map: descending Id (topk_rmv.erl:92-95)
+    assert trmv.value(t) == [(4, 9), (2, 7), (1, 5)]
     ok, t2 = trmv.from_binary(trmv.to_binary(t))
     assert ok == "ok" and trmv.equal(t, t2) and t2.to_term() == t.to_term()
     res = trmv.update(("rmv", (4, {names[0]: 4})), t)  # promotes player 3

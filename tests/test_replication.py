@@ -340,3 +340,192 @@ def test_wc_partition_device_row_limit(gpu, monkeypatch):
     monkeypatch.setenv("CCRDT_WC_PART_MAX_WORDS", "4")
     meta, data, ow, ob = _wc_partition_device(e, 2)
     assert int(ow.sum()) == 3 and int(ob.sum()) == 3
+
+
+# ------------------------------------------------ injected collectives
+class ThreadCollective:
+    """In-process stand-in for TorchCollective: W threads, one per rank,
+    meet at a barrier and read each other's tensors (the exchange by
+    slicing), so the per-rank drivers run unchanged."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.box = [None] * world
+
+    def view(self, rank):
+        coll = self
+
+        class _V:
+            world = coll.world
+
+            def all_gather_v(self, t):
+                coll.box[rank] = t
+                coll.bar.wait()
+                out = list(coll.box)
+                coll.bar.wait()
+                return out
+
+            def all_to_all_v(self, t, splits):
+                import torch
+                coll.box[rank] = (t, [int(x) for x in splits])
+                coll.bar.wait()
+                parts, sizes = [], []
+                for src, sp in coll.box:
+                    o = sum(sp[:rank])
+                    parts.append(src[o:o + sp[rank]])
+                    sizes.append(sp[rank])
+                coll.bar.wait()
+                return torch.cat(parts), sizes
+        return _V()
+
+
+def _coll_worker(rank, world, port, errf):
+    """TorchCollective over gloo (CPU tensors): variable all-gather and
+    all-to-all."""
+    import torch
+    import torch.distributed as dist
+
+    from antidote_ccrdt_amd.cluster import TorchCollective
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = TorchCollective()
+        t = torch.arange(3 * (rank + 1), dtype=torch.int64).reshape(-1, 3) + 100 * rank
+        got = c.all_gather_v(t)
+        assert [g.shape[0] for g in got] == [r + 1 for r in range(world)]
+        assert all(torch.equal(g, torch.arange(3 * (r + 1)).reshape(-1, 3) + 100 * r) for r, g in enumerate(got))
+        splits = [d + 1 for d in range(world)]  # rank r sends d+1 rows to d
+        src = torch.full((sum(splits), 2), rank, dtype=torch.int64)
+        out, rs = c.all_to_all_v(src, splits)
+        assert rs == [rank + 1] * world and out.shape[0] == world * (rank + 1)
+        assert torch.equal(out[:, 0], torch.arange(world).repeat_interleave(rank + 1))
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_torch_collective_gloo(world, tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_coll_worker, args=(world, _free_port(), errf), nprocs=world, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+def _lb_dev(bs):
+    import torch
+    return [tuple(torch.as_tensor(np.asarray(x, dt)).cuda() for x, dt in
+                  zip(b, (np.int64, np.uint8, np.int64, np.int64))) for b in bs]
+
+
+@pytest.mark.gpu
+def test_lb_replicate_step_threads_gpu(gpu):
+    """The per-rank driver lb_replicate_step (the nccl path's code) with an
+    in-process collective: one thread per replica, device rows exchanged by
+    slicing; every replica equals the host protocol on oracle replicas."""
+    import threading
+
+    from antidote_ccrdt_amd.cluster import LbDeviceReplica, lb_replicate_step
+    from antidote_ccrdt_amd.types import LeaderboardEngine
+    W = 3
+    engs = [LeaderboardEngine(NK, K) for _ in range(W)]
+    o = [ReplicatedLeaderboard(NK, K, rank=r, world=W, engine=orc.LbOracle(NK, K)) for r in range(W)]
+    tc = ThreadCollective(W)
+    for s in range(STEPS):
+        bs = _lb_batches(W, s)
+        dev = _lb_dev(bs)
+        rounds, errs = [None] * W, []
+
+        def run(r):
+            try:
+                rounds[r] = lb_replicate_step(LbDeviceReplica(engs[r], r, W), dev[r], tc.view(r))
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                tc.bar.abort()
+        th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        assert rounds[0] == replicate_local(o, bs) and len(set(rounds)) == 1
+        for r in range(W):
+            assert not _same(engs[r].export(), o[r].export()), (s, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wc_exchange_device_threads_gpu(gpu, wdc):
+    """exchange_device (the nccl path's code) per shard, one thread each,
+    with the in-process collective."""
+    import threading
+
+    from antidote_ccrdt_amd.cluster import exchange_device
+    W = 2
+    shards = [ShardedWordcount(WC_KEYS, wdc, rank=r, world=W) for r in range(W)]
+    tc = ThreadCollective(W)
+    for s in range(2):
+        for r, sh in enumerate(shards):
+            sh.apply(*_docs(W, r, s)[:3])
+        errs = []
+
+        def run(r):
+            try:
+                exchange_device(shards[r], tc.view(r))
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                tc.bar.abort()
+        th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+    exp = _wc_expected(W, wdc)
+    for r, sh in enumerate(shards):
+        assert _flat(sh.export()) == _owned_part(exp, W, r)
+
+
+def _gpu_gloo_worker(rank, world, port, errf):
+    """One process per replica / shard on the GPU box's one GPU, gloo
+    staging the device tensors through the host: lb_replicate_step and
+    exchange_device, the functions the nccl path runs."""
+    import torch.distributed as dist
+
+    from antidote_ccrdt_amd.cluster import LbDeviceReplica, TorchCollective, exchange_device, lb_replicate_step
+    from antidote_ccrdt_amd.types import LeaderboardEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        coll = TorchCollective()
+        assert coll.staged
+        eng = LeaderboardEngine(NK, K)
+        o = [ReplicatedLeaderboard(NK, K, rank=r, world=world, engine=orc.LbOracle(NK, K)) for r in range(world)]
+        for s in range(STEPS):
+            bs = _lb_batches(world, s)
+            rounds = lb_replicate_step(LbDeviceReplica(eng, rank, world), _lb_dev(bs)[rank], coll)
+            assert rounds == replicate_local(o, bs)
+            bad = _same(eng.export(), o[rank].export())
+            assert not bad, (s, bad)
+        sh = ShardedWordcount(WC_KEYS, False, rank=rank, world=world)
+        for s in range(2):
+            sh.apply(*_docs(world, rank, s)[:3])
+            exchange_device(sh, coll)
+        assert _flat(sh.export()) == _owned_part(_wc_expected(world, False), world, rank)
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_device_steps_gloo_two_processes_gpu(gpu, tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_gpu_gloo_worker, args=(2, _free_port(), errf), nprocs=2, join=True)
+    assert not os.path.exists(errf), open(errf).read()
