@@ -28,6 +28,7 @@ int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
+int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
                            hipStream_t st);
 int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
@@ -35,10 +36,14 @@ int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, con
                             int64_t cap, uint32_t* count, hipStream_t st);
 
 // Tiers of the apply chain: 0 = trmv_wave (tier 0), 1 / 2 = trmv_steady with
-// up to 256 / 1024 players per key (tier S).
-static constexpr int TRMV_N_TIERS = 3;
+// up to 256 / 1024 players per key (tier S), 3 = trmv_resident (tier R).  A
+// batch runs one chain: onto fresh keys 0 -> 1 -> 2, onto resident keys
+// 3 -> 1 -> 2 (tier R needs K <= 128; else 1 -> 2).  Tier 2 is always last:
+// the keys it hands on are over the per-key capacity (CCRDT_EKEYCAP).
+static constexpr int TRMV_N_TIERS = 4;
+static constexpr int TRMV_TIER_LAST = 2;
 static constexpr uint32_t TRMV_MAX_PLAYERS = 1024u;  // players per key (tier S, last class)
-static constexpr int TRMV_STATUS_WORDS = 8;  // [0,2) scan, [2+2t, 4+2t) tier t
+static constexpr int TRMV_STATUS_WORDS = 2 + 2 * TRMV_N_TIERS;  // [0,2) scan, [2+2t, 4+2t) tier t
 static constexpr uint32_t TRMV_LATER_GRID = 4096;  // keys the grids of the later tiers cover
 
 }  // namespace ccrdt
@@ -344,29 +349,39 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
   for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
+  if (!E.fresh) CCRDT_TRY(E.op_pl.ensure(n_ops + 1));
+  a.op_pl = E.op_pl.as<uint8_t>();
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
   a.ex_vc = E.ex_vc.as<int64_t>();
-  // 2) tier 0 over every key, then tier S (256, then 1024 players per key) for
-  //    the keys each tier hands on.  Every later tier reads its list length
-  //    from the device, so the whole chain is queued without a host round
-  //    trip; one sync at the end reads the status.
-  // Keys with more ops than tier 0 takes are handed on by it like the others
-  // (tier S runs them after it, ~0.1 ms for a bench batch).
-  // CCRDT_TRMV_FIRST_TIER (tuning knob): -1 = tier 0 for fresh batches and
-  // tier S for batches onto resident state (default), 0 = always tier 0 first,
-  // 1 = always tier S.
+  // 2) the chain: its first tier over every key, then each later tier over
+  //    the keys the one before handed on.  Every later tier reads its list
+  //    length from the device, so the whole chain is queued without a host
+  //    round trip; one sync at the end reads the status.
+  // CCRDT_TRMV_FIRST_TIER (tuning knob): -1 = the default chain, 0 = tier 0
+  // first (fresh batches only), 1 = tier S first, 3 = tier R first (resident
+  // batches only).
   static const int first_env = [] {
     const char* v = getenv("CCRDT_TRMV_FIRST_TIER");
     return v ? atoi(v) : -1;
   }();
-  const int first_tier = first_env >= 0 ? std::min(first_env, 1) : (E.fresh ? 0 : 1);
+  int chain[3], n_chain = 0;
+  {
+    int first = E.fresh ? 0 : (E.k <= 128 ? 3 : 1);
+    if (first_env == 1 || (first_env == 0 && E.fresh) || (first_env == 3 && !E.fresh && E.k <= 128)) first = first_env;
+    chain[n_chain++] = first;
+    chain[n_chain++] = 1;
+    chain[n_chain++] = 2;
+    if (first == 1) n_chain = 2, chain[1] = 2;
+  }
+  const int first_tier = chain[0];
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
   DevBuf* work = nullptr;
   const uint32_t* n_dev = nullptr;
   int ev = 0;
   CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-  for (int t = first_tier; t < TRMV_N_TIERS && nk; ++t) {
+  for (int ci = 0; ci < n_chain && nk; ++ci) {
+    const int t = chain[ci];
     DevBuf* ovf = &E.tier_ovf[t];
     a.key_list = work ? work->as<uint32_t>() : nullptr;
     a.n_list = work ? 0u : (uint32_t)nk;
@@ -375,6 +390,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     a.status = status + 2 + 2 * t;
     const uint64_t grid = work ? later_grid : nk;
     if (t == 0) CCRDT_TRY(trmv_launch_wave(a, grid, E.stream));
+    else if (t == 3) CCRDT_TRY(trmv_launch_resident(a, grid, E.stream));
     else CCRDT_TRY(trmv_launch_steady(a, t - 1, grid, E.stream));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     work = ovf;
@@ -385,7 +401,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
   uint32_t err = 0;
-  for (int t = first_tier; t < TRMV_N_TIERS; ++t) err |= hs[3 + 2 * t];
+  for (int ci = 0; ci < n_chain; ++ci) err |= hs[3 + 2 * chain[ci]];
   if (err) {
     std::string m = "trmv_apply: invalid op in batch:";
     if (err & TRMV_ERR_KIND) m += " kind>3";
@@ -401,19 +417,20 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   E.trmv_overflow_keys.clear();
   E.trmv_tier_ms.clear();
   E.trmv_first_tier = first_tier;
-  for (int t = first_tier, i = 1; t < TRMV_N_TIERS && nk; ++t, ++i) {
+  for (int ci = 0; ci < n_chain && nk; ++ci) {
+    const int t = chain[ci];
     float ms = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[i - 1], E.evt[i]));
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[ci], E.evt[ci + 1]));
     E.trmv_tier_ms[t] = ms;
     E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
   // Keys over the per-key capacity (the last tier's hand-ons) keep their old
   // state; every other key commits.
-  const uint32_t n_over = nk ? hs[2 + 2 * (TRMV_N_TIERS - 1)] : 0u;
+  const uint32_t n_over = nk ? hs[2 + 2 * TRMV_TIER_LAST] : 0u;
   if (n_over) {
-    a.key_list = E.tier_ovf[TRMV_N_TIERS - 1].as<uint32_t>();
+    a.key_list = E.tier_ovf[TRMV_TIER_LAST].as<uint32_t>();
     a.n_list = 0;
-    a.n_list_dev = status + 2 + 2 * (TRMV_N_TIERS - 1);
+    a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>(n_over, TRMV_LATER_GRID), E.stream));
   }
   float kernel_ms = 0.f;

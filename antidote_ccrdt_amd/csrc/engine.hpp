@@ -64,8 +64,8 @@ struct ccrdt_engine {
   // topk_rmv
   ccrdt::TrmvBufs trmv[2];
   int cur = 0;
-  ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status;
-  ccrdt::DevBuf tier_ovf[3];    // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
+  ccrdt::DevBuf tier_ovf[4];    // keys each topk_rmv tier handed on (last batch)
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held

@@ -97,6 +97,7 @@ struct TrmvApplyArgs {
                                // (the previous tier's overflow count)
   uint32_t* ovf_list;
   uint32_t* status;  // [0] overflow count, [1] error flags
+  uint8_t* op_pl;    // [n_ops] tier R scratch: each op's player index in its key
 };
 
 // New-side metadata of key k before its tier writes it.  A fresh batch's

@@ -1,0 +1,1326 @@
+// trmv_resident.hip — tier R of the topk_rmv apply: a batch onto RESIDENT
+// keys (the steady state Antidote drives: the same keys receive batch after
+// batch, Observed full, more players than K, evictions and promotions).  One
+// wavefront per key; the class: at most 256 players, K <= 128, Ids and Scores
+// that fit in 32 bits.  A key outside it is handed on to tier S
+// (trmv_steady.hip), which redoes it from the old side.
+//
+// The reference state machine (src/antidote_ccrdt_topk_rmv.erl:231-334) keeps
+// two invariants after every op: Obs[Id] has the largest
+// Score of Masked[Id], and Observed is the top K players by (largest Score,
+// Id).  Every per-player effect — Removals merges, rmv filters, dominated adds
+// (:234-237), set semantics (:240-246), gb_sets:largest — depends on the
+// player's own ops only and is decided per player (op-parallel, or one lane
+// per replayed player).  What depends on the order of ops ACROSS players is
+// Observed: which element Obs[Id] holds, Min, and the promotions of rmv/3.
+// Tier R keeps Observed as an array SORTED ascending by (Score, Id) in two
+// register slots (entry r in lane r % 64 of slot r / 64, one packed 64-bit key
+// per entry): Min is entry 0 (min_observed/1, :398-406; Ids are distinct), an
+// eviction (:325-331), an upgrade (:303-315) or a promotion (:276-295) is one
+// shift of a range of entries (DPP wave shifts).  Per run of adds between two
+// rmvs, a lane-parallel filter keeps only the adds that can change Observed
+// given the state at the run's start (inside a run Min and every Obs[Id] only
+// rise); those run one by one in stream order on the register array alone.
+// gb_sets:largest of every player — what a promotion needs — is brought up to
+// date lane-parallel at each rmv (one segmented scan per chunk).  Players are
+// written back with Observed first, in sorted order, so the next batch starts
+// from the sorted array as it is (a key last written by tier 0 or tier S is
+// sorted once, in registers).
+//
+// Phases per key:
+//   P1  old players -> LDS / registers, the Id hash, the sorted Observed;
+//   P2  every op's player (new Ids numbered in claim order; recorded per op),
+//       ops per player, new slab offsets (old count + ops) and Removals rows;
+//   P3  old Masked slabs and Removals rows -> the new side, position-parallel;
+//   per chunk of <= 64 ops (<= 16 rmvs):
+//     P3c validation, clocks, dominance and appends of the players without a
+//         rmv (op-parallel), replays of the players with one (a lane each);
+//     P4  the Observed half in stream order;
+//   P5  player records (Observed first, sorted), positions, Vc, meta.
+#include "common.hpp"
+#include "trmv_kernels.hpp"
+
+// Diagnostic build only (-DTRMV_PROF): per-phase s_memtime stamps summed over
+// a sample of keys; read with ccrdt_debug_resident_prof().
+#ifdef TRMV_PROF
+__device__ unsigned long long g_resident_prof[16];
+#define RPROF_STAMP(v)                                                        \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#define RPROF(i)                                                                         \
+  do {                                                                                   \
+    unsigned long long _t;                                                               \
+    RPROF_STAMP(_t);                                                                     \
+    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_resident_prof[i], _t - prof_t); \
+    prof_t = _t;                                                                         \
+  } while (0)
+#define RCOUNT(i, v)                                                                              \
+  do {                                                                                            \
+    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_resident_prof[i], (unsigned long long)(v)); \
+  } while (0)
+#else
+#define RPROF(i) (void)0
+#define RCOUNT(i, v) (void)0
+#endif
+
+namespace ccrdt {
+
+namespace {
+
+constexpr int RP = 256;        // players per key
+constexpr int RSL = RP / 64;   // player slots per lane
+constexpr int RCH = 64;        // ops per chunk
+constexpr int RCHR = 16;       // rmvs per chunk (rows of the clock table)
+constexpr uint32_t RNONE = 0xFFFFFFFFu;
+constexpr uint32_t RH_NONE = 0xFFFFu, RH_CLAIM = 0x8000u;  // hash slots: player | CLAIM|lane | NONE
+enum : int { R_DONE = 0, R_NEXT = 1, R_REJECT = 2 };
+
+// pf[p] flags
+constexpr uint32_t Q_OBS = 1u;   // Id in Observed
+constexpr uint32_t Q_HASM = 2u;  // Masked[Id] is not empty
+constexpr uint32_t Q_ROWV = 4u;  // Removals[Id] exists
+constexpr uint32_t Q_RMV = 8u;   // a rmv of Id in this batch: its slab is replayed by one lane
+constexpr uint32_t Q_WALK = 16u; // a replay compacted the slab: positions restated in P5
+constexpr uint32_t Q_DUP = 32u;  // a possibly duplicated element: replayed too
+constexpr uint32_t R_DOM = 1u;   // cres: dominated add (:234-237)
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int64_t ufl64(int64_t v) {
+  const uint32_t lo = ufl((uint32_t)v), hi = ufl((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t perm32(uint32_t v, uint32_t dst) {
+  return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)v);
+}
+// Lane i <- v of lane i + 1 (lane 63 <- fill): DPP wave_shl:1.
+__device__ __forceinline__ uint32_t wshl1(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xf, 0xf, false);
+}
+// Lane i <- v of lane i - 1 (lane 0 <- fill): DPP wave_shr:1.
+__device__ __forceinline__ uint32_t wshr1(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lo32(int64_t v) { return (uint32_t)v; }
+__device__ __forceinline__ uint32_t hi32(int64_t v) { return (uint32_t)((uint64_t)v >> 32); }
+__device__ __forceinline__ int64_t mk64(uint32_t lo, uint32_t hi) { return (int64_t)(((uint64_t)hi << 32) | lo); }
+__device__ __forceinline__ bool fits32(int64_t v) { return v == (int64_t)(int32_t)v; }
+
+// (Score, Id) of 32-bit values as one signed 64-bit key: comparing keys
+// compares Score, then Id (the Id's sign bit flipped so it orders unsigned).
+__device__ __forceinline__ int64_t mkkey(int64_t score, int64_t id) {
+  return (int64_t)(((uint64_t)(uint32_t)(int32_t)score << 32) | ((uint32_t)(int32_t)id ^ 0x80000000u));
+}
+__device__ __forceinline__ int64_t key_score(int64_t k) { return (int64_t)(int32_t)(uint32_t)((uint64_t)k >> 32); }
+__device__ __forceinline__ int64_t key_id(int64_t k) { return (int64_t)(int32_t)((uint32_t)k ^ 0x80000000u); }
+
+// gb_sets term order of two elements of one Id: (Score, DcId, Ts).
+__device__ __forceinline__ bool gb_gt(int64_t s1, uint32_t d1, int64_t t1, int64_t s2, uint32_t d2, int64_t t2) {
+  return s1 > s2 || (s1 == s2 && (d1 > d2 || (d1 == d2 && t1 > t2)));
+}
+
+typedef int64_t Row8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ int64_t pick8(const Row8& v, uint32_t d) {
+  int64_t r = v[0];
+#pragma unroll
+  for (int k = 1; k < TRMV_DPAD; ++k) r = d == (uint32_t)k ? v[k] : r;
+  return r;
+}
+
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_radix_sort(uint32_t kv) {  // by bits [6, 6 + BITS); payload 6 bits
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const bool bit = (kv >> (6 + b)) & 1u;
+    const uint64_t ones = ballot(bit);
+    const uint32_t nz = 64u - (uint32_t)__builtin_popcountll(ones);
+    const uint32_t dst = bit ? nz + mbcnt(ones) : mbcnt(~ones);
+    kv = perm32(kv, dst);
+  }
+  return kv;
+}
+
+// Position of the k-th (0-based) set bit of m (k < popcount(m)).
+__device__ __forceinline__ uint32_t kth_bit(uint64_t m, uint32_t k) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t s = 32; s >= 1; s >>= 1) {
+    const uint64_t low = pos + s >= 64 ? ~0ull : ((1ull << (pos + s)) - 1);
+    if ((uint32_t)__builtin_popcountll(m & low) <= k) pos += s;
+  }
+  return pos;
+}
+
+__device__ __forceinline__ uint32_t rhash(int64_t id) {
+  return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> (64 - 9));  // 512 slots
+}
+
+struct alignas(16) RLds {
+  int64_t gts[RP];     // gb_sets:largest(Masked[Id]): Ts
+  int64_t ots[RP];     // Obs[Id]: Ts (players in Observed)
+  int32_t msc[RP];     // largest Score of Masked[Id] (= Obs[Id]'s Score in Observed, or below it mid-run)
+  uint32_t pf[RP];     // flags
+  uint32_t oslab[RP];  // old slab: offset | count << 16
+  uint32_t nslab[RP];  // new slab: offset | current count << 16
+  uint16_t prow[RP];   // Removals row (new side), NONE16
+  uint16_t opos[RP];   // Obs[Id]'s position in the new slab
+  uint16_t gpos[RP];   // the largest's position in the new slab
+  uint8_t odc[RP];     // Obs[Id]: DcId
+  uint8_t gdc[RP];     // the largest: DcId
+  union {
+    struct {  // P1 / P2
+      uint16_t hs[2 * RP];
+      int64_t pid[RP];
+      int64_t claim[64];
+      uint16_t nops[RP];
+    } r;
+    struct {  // chunks
+      int64_t csc[RCH], cts[RCH];
+      int64_t cid[RCH];    // Ids, (player, stream) order
+      uint32_t ckd[RCH];   // kind | dc << 2 | dup candidate << 5 | player << 8
+      uint32_t cres[RCH];  // add: R_DOM | slab position << 16; rmv: its rank in the chunk
+      int64_t vtab[RCHR][TRMV_DPAD];
+      uint32_t crow[RCHR];
+      int64_t rgs[RCHR], rgt[RCHR];  // Masked[Id]'s largest survivor after each rmv
+      uint32_t rgd[RCHR];            // non-empty | dc << 8 | position << 16
+      uint16_t cwp[RCH];
+      uint8_t cws[RCH], cwe[RCH], csrt[RCH];
+      uint32_t mark[RCH];
+    } c;
+    struct {  // P5
+      uint16_t nidx[RP];  // a player's index in the new record order
+    } f;
+  } u;
+  unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
+  uint32_t nex;
+};
+
+// --------------------------------------------------- the sorted Observed
+// Entry r = lane r % 64 of slot r / 64, ascending by key = (Score, Id);
+// pl = player | Obs[Id]'s DcId << 16; entries >= n hold (INT64_MAX, RNONE).
+struct Obs {
+  int64_t key[2], ts[2];
+  uint32_t pl[2];
+  uint32_t n;
+};
+
+__device__ __forceinline__ void ob_clear_tail(Obs& o) {
+  const uint32_t l = (uint32_t)lane_id();
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    if (64u * t + l >= o.n) {
+      o.key[t] = INT64_MAX;
+      o.ts[t] = 0;
+      o.pl[t] = RNONE;
+    }
+}
+
+// Entries i in [lo, hi) take entry i + 1 (down) or entries i in [lo, hi]
+// take entry i - 1 (up); both slots always shift (no branches on the range).
+template <bool DOWN>
+__device__ __forceinline__ void ob_shift(Obs& o, uint32_t lo, uint32_t hi) {
+  const uint32_t l = (uint32_t)lane_id();
+  const bool in0 = DOWN ? (l >= lo && l < hi) : (l >= lo && l <= hi);
+  const bool in1 = DOWN ? (64u + l >= lo && 64u + l < hi) : (64u + l >= lo && 64u + l <= hi);
+  uint32_t w0[5] = {lo32(o.key[0]), hi32(o.key[0]), lo32(o.ts[0]), hi32(o.ts[0]), o.pl[0]};
+  uint32_t w1[5] = {lo32(o.key[1]), hi32(o.key[1]), lo32(o.ts[1]), hi32(o.ts[1]), o.pl[1]};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    uint32_t n0, n1;
+    if (DOWN) {
+      n0 = wshl1(w0[k], rl32(w1[k], 0));
+      n1 = wshl1(w1[k], 0u);
+    } else {
+      n0 = wshr1(w0[k], 0u);
+      n1 = wshr1(w1[k], rl32(w0[k], 63));
+    }
+    w0[k] = in0 ? n0 : w0[k];
+    w1[k] = in1 ? n1 : w1[k];
+  }
+  o.key[0] = mk64(w0[0], w0[1]);
+  o.ts[0] = mk64(w0[2], w0[3]);
+  o.pl[0] = w0[4];
+  o.key[1] = mk64(w1[0], w1[1]);
+  o.ts[1] = mk64(w1[2], w1[3]);
+  o.pl[1] = w1[4];
+}
+
+__device__ __forceinline__ void ob_put(Obs& o, uint32_t q, int64_t key, int64_t ts, uint32_t pl) {
+  const uint32_t l = (uint32_t)lane_id();
+  if (l == (q & 63u)) {
+    if (q < 64u) {
+      o.key[0] = key;
+      o.ts[0] = ts;
+      o.pl[0] = pl;
+    } else {
+      o.key[1] = key;
+      o.ts[1] = ts;
+      o.pl[1] = pl;
+    }
+  }
+}
+
+// Entries below key, skipping entry `skip` (RNONE: none).
+__device__ __forceinline__ uint32_t ob_rank(const Obs& o, int64_t key, uint32_t skip) {
+  const uint32_t l = (uint32_t)lane_id();
+  const bool b0 = l < o.n && l != skip && o.key[0] < key;
+  const bool b1 = 64u + l < o.n && 64u + l != skip && o.key[1] < key;
+  return (uint32_t)__builtin_popcountll(ballot(b0)) + (uint32_t)__builtin_popcountll(ballot(b1));
+}
+
+__device__ __forceinline__ uint32_t ob_find(const Obs& o, uint32_t p) {
+  const uint64_t m0 = ballot((o.pl[0] & 0xFFFFu) == p), m1 = ballot((o.pl[1] & 0xFFFFu) == p);
+  return m0 ? (uint32_t)__builtin_ctzll(m0) : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : RNONE);
+}
+__device__ __forceinline__ int64_t ob_get64(const int64_t f[2], uint32_t i) {
+  const int64_t a = rl64(f[0], (int)(i & 63u)), b = rl64(f[1], (int)(i & 63u));
+  return i < 64u ? a : b;
+}
+__device__ __forceinline__ uint32_t ob_get32(const uint32_t f[2], uint32_t i) {
+  const uint32_t a = rl32(f[0], (int)(i & 63u)), b = rl32(f[1], (int)(i & 63u));
+  return i < 64u ? a : b;
+}
+
+// Entry r removed and (key, ts, pl) inserted, in one range shift.
+__device__ __forceinline__ void ob_replace(Obs& o, uint32_t r, int64_t key, int64_t ts, uint32_t pl) {
+  const uint32_t q = ob_rank(o, key, r);
+  if (q >= r) ob_shift<true>(o, r, q);
+  else ob_shift<false>(o, q + 1, r);
+  ob_put(o, q, key, ts, pl);
+}
+__device__ __forceinline__ void ob_insert(Obs& o, int64_t key, int64_t ts, uint32_t pl) {
+  const uint32_t q = ob_rank(o, key, RNONE);
+  ob_shift<false>(o, q + 1, o.n);
+  ob_put(o, q, key, ts, pl);
+  ++o.n;
+}
+__device__ __forceinline__ void ob_remove(Obs& o, uint32_t r) {
+  ob_shift<true>(o, r, o.n - 1);
+  --o.n;
+  ob_clear_tail(o);
+}
+
+// Bitonic sort of the 128 positions ascending by key (sentinels last).  Used
+// once for a key whose players were not written in sorted-Observed order.
+__device__ __forceinline__ void ob_sort(Obs& o) {
+  const uint32_t l = (uint32_t)lane_id();
+#pragma unroll 1
+  for (uint32_t k = 2; k <= 128; k <<= 1) {
+#pragma unroll 1
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j == 64) {  // partner = the other slot, same lane (k == 128: ascending)
+        if (o.key[1] < o.key[0]) {
+          int64_t t;
+          t = o.key[0]; o.key[0] = o.key[1]; o.key[1] = t;
+          t = o.ts[0]; o.ts[0] = o.ts[1]; o.ts[1] = t;
+          const uint32_t u = o.pl[0]; o.pl[0] = o.pl[1]; o.pl[1] = u;
+        }
+        continue;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t i = 64u * s + l;
+        const int src = (int)(l ^ j);
+        const int64_t pk = shfl64(o.key[s], src), pt = shfl64(o.ts[s], src);
+        const uint32_t pp = shfl32(o.pl[s], src);
+        const bool lower = (i & j) == 0;  // this position is the lower of its pair
+        const bool asc = (i & k) == 0;    // this block sorts ascending
+        const bool take = (lower == asc) ? pk < o.key[s] : o.key[s] < pk;
+        if (take) {
+          o.key[s] = pk;
+          o.ts[s] = pt;
+          o.pl[s] = pp;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void r_emit(const TrmvApplyArgs& a, RLds& L, uint64_t op0, uint64_t op, uint8_t kind,
+                                       int64_t id, int64_t sc, uint32_t dc, int64_t ts, const Row8* vc) {
+  const uint32_t pos = atomicAdd(&L.nex, 1u);
+  TrmvExtraRec r;
+  r.op = (uint32_t)op;
+  r.kind = kind;
+  r.dc = (uint8_t)dc;
+  r.pad = 0;
+  r.id = id;
+  r.score = sc;
+  r.ts = ts;
+  a.ex[op0 + pos] = r;
+  if (vc)
+    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = pick8(*vc, (uint32_t)d);
+}
+
+// P2: the player of each lane's Id; new Ids claimed and numbered np, np+1,
+// ... in lane order.  False if the key outgrows RP players.
+__device__ __forceinline__ bool r_resolve(RLds& L, int64_t id, bool v, uint32_t& np, uint32_t& p) {
+  const int lane = lane_id();
+  L.u.r.claim[lane] = id;
+  wave_lds_sync();
+  uint32_t h = rhash(id);
+  bool resolved = !v, claimed = false;
+  int follow = -1;
+  p = 0;
+  while (ballot(!resolved)) {
+    if (!resolved) {
+      uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[h & ~1u]);
+      const uint32_t sh = (h & 1u) * 16u;
+      const uint32_t s = (*w >> sh) & 0xFFFFu;
+      if (s == RH_NONE) {
+        uint32_t old = *w;
+        bool won = false;
+        for (;;) {
+          if (((old >> sh) & 0xFFFFu) != RH_NONE) break;
+          const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | ((RH_CLAIM | (uint32_t)lane) << sh));
+          if (prev == old) {
+            won = true;
+            break;
+          }
+          old = prev;
+        }
+        if (won) {
+          claimed = true;
+          resolved = true;
+        }  // else: read the slot again
+      } else if (s & RH_CLAIM) {
+        const int c = (int)(s & 63u);
+        if (L.u.r.claim[c] == id) {
+          follow = c;
+          resolved = true;
+        } else {
+          h = (h + 1) & (2 * RP - 1);
+        }
+      } else if (L.u.r.pid[s] == id) {
+        p = s;
+        resolved = true;
+      } else {
+        h = (h + 1) & (2 * RP - 1);
+      }
+    }
+  }
+  wave_lds_sync();
+  const uint64_t cm = ballot(claimed);
+  const uint32_t nn = np + (uint32_t)__builtin_popcountll(cm);
+  if (nn > (uint32_t)RP) return false;
+  if (claimed) {
+    p = np + mbcnt(cm);
+    L.u.r.pid[p] = id;
+    L.u.r.hs[h] = (uint16_t)p;
+    L.u.r.nops[p] = 0;
+    L.oslab[p] = 0u;
+    L.prow[p] = (uint16_t)NONE16;
+    L.pf[p] = 0u;
+    L.msc[p] = 0;
+    L.gts[p] = 0;
+    L.ots[p] = 0;
+    L.opos[p] = (uint16_t)NONE16;
+    L.gpos[p] = 0;
+    L.odc[p] = 0;
+    L.gdc[p] = 0;
+  }
+  const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
+  if (follow >= 0) p = fp;
+  np = nn;
+  wave_lds_sync();
+  return true;
+}
+
+// Promotion candidate of rmv/3 (:276-281, :291): the player outside Observed
+// with Masked elements whose (largest Score, Id) is largest; RNONE if none.
+// Its key in `wk`.
+__device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[RSL], uint32_t np, int64_t& wk) {
+  const uint32_t l = (uint32_t)lane_id();
+  uint32_t bp = RNONE;
+  int64_t best = INT64_MIN;
+  uint32_t f[RSL];
+  int32_t sc[RSL];
+#pragma unroll
+  for (int u = 0; u < RSL; ++u) {
+    const uint32_t p = 64u * u + l;
+    f[u] = p < np ? L.pf[p] : 0u;
+    sc[u] = L.msc[p];
+  }
+#pragma unroll
+  for (int u = 0; u < RSL; ++u) {
+    const int64_t k = mkkey(sc[u], pid[u]);
+    if ((f[u] & (Q_OBS | Q_HASM)) == Q_HASM && (bp == RNONE || k > best)) {
+      bp = 64u * u + l;
+      best = k;
+    }
+  }
+  if (!ballot(bp != RNONE)) return RNONE;
+  const int64_t m = wave_max_i64_dpp(bp != RNONE ? best : INT64_MIN);
+  const uint64_t hit = ballot(bp != RNONE && best == m);
+  wk = m;
+  return rl32(bp, (int)__builtin_ctzll(hit));
+}
+
+// One key.  Returns R_NEXT for a key outside the class; the next tier redoes
+// it from the old side (whatever this one wrote of it is rewritten).
+__device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) {
+  const uint32_t lane = (uint32_t)lane_id();
+  const int D = a.n_dc;
+#ifdef TRMV_PROF
+  unsigned long long prof_t;
+  RPROF_STAMP(prof_t);
+#endif
+  const uint64_t op0 = a.key_ptr[key];
+  const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
+  const KeyMeta nm = a.new_s.meta[key];
+  const KeyMeta om = a.old_s.meta[key];
+  // (per-player op counts are 16-bit here)
+  if (om.np > (uint32_t)RP || om.nobs > 128u || nops > 0xFFFFu) return R_NEXT;
+  const uint32_t K = a.k;
+
+  for (uint32_t i = lane; i < (uint32_t)RP; i += 64) reinterpret_cast<uint32_t*>(L.u.r.hs)[i] = 0xFFFFFFFFu;
+  if (lane <= (uint32_t)TRMV_DPAD)
+    L.vc[lane] = lane < (uint32_t)D ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+  if (lane == 0) L.nex = 0u;
+  wave_lds_sync();
+
+  // ---- P1. old players: records, then the Obs[Id] / largest elements they
+  // name (two halves of two slots: fewer loads in flight at once).
+  // Observed's entries are players 0..nobs-1 when the key was last written
+  // by tier R (checked), else gathered and sorted here.
+  int64_t pid[RSL];
+  uint32_t span = 0, inobs = 0;  // inobs: bit u = player of slot u in Observed
+  int64_t k01[2], t01[2];        // slots 0-1: Obs[Id]'s key and Ts
+  bool wide = false;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t info[2], slab[2], gb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t p = 64u * (2 * h + t) + lane;
+      const bool v = p < om.np;
+      const uint64_t pp = (uint64_t)om.p_off + (v ? p : 0u);
+      pid[2 * h + t] = v ? a.old_s.pl_id[pp] : 0;
+      info[t] = v ? a.old_s.pl_info[pp] : RNONE;
+      slab[t] = v ? a.old_s.pl_slab[pp] : 0u;
+      gb[t] = (v && (slab[t] >> 16) > 1) ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int u = 2 * h + t;
+      const uint32_t p = 64u * u + lane;
+      const uint32_t off = slab[t] & 0xFFFFu, cnt = slab[t] >> 16, obx = info[t] & 0xFFFFu;
+      const uint64_t g0 = (uint64_t)om.m_off + off;
+      const bool ho = obx != NONE16, hg = cnt != 0;
+      const int64_t os = ho ? a.old_s.m_score[g0 + obx] : 0;
+      const int64_t ot = ho ? a.old_s.m_ts[g0 + obx] : 0;
+      const uint32_t od = ho ? (uint32_t)a.old_s.m_dc[g0 + obx] : 0u;
+      const int64_t gs = hg ? a.old_s.m_score[g0 + gb[t]] : 0;
+      const int64_t gt = hg ? a.old_s.m_ts[g0 + gb[t]] : 0;
+      const uint32_t gd = hg ? (uint32_t)a.old_s.m_dc[g0 + gb[t]] : 0u;
+      if (h == 0) {
+        k01[t] = mkkey(os, pid[u]);
+        t01[t] = ot;
+      }
+      if (p < om.np) {
+        wide |= !fits32(pid[u]) || !fits32(os) || !fits32(gs);
+        L.msc[p] = (int32_t)gs;
+        L.gts[p] = gt;
+        L.ots[p] = ot;
+        L.pf[p] = (ho ? Q_OBS : 0u) | (cnt ? Q_HASM : 0u) | ((info[t] >> 16) != NONE16 ? Q_ROWV : 0u);
+        L.odc[p] = (uint8_t)od;
+        L.gdc[p] = (uint8_t)gd;
+        L.opos[p] = (uint16_t)obx;
+        L.gpos[p] = (uint16_t)gb[t];
+        L.oslab[p] = slab[t];
+        L.prow[p] = (uint16_t)(info[t] >> 16);
+        L.u.r.pid[p] = pid[u];
+        L.u.r.nops[p] = 0;
+        span = off + cnt > span ? off + cnt : span;
+        uint32_t hh = rhash(pid[u]);
+        for (;;) {  // insert into the hash (slots of 16 bits: CAS on the word)
+          uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[hh & ~1u]);
+          const uint32_t sh = (hh & 1u) * 16u;
+          uint32_t old = *w;
+          bool done = false;
+          while (((old >> sh) & 0xFFFFu) == RH_NONE) {
+            const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (p << sh));
+            if (prev == old) {
+              done = true;
+              break;
+            }
+            old = prev;
+          }
+          if (done) break;
+          hh = (hh + 1) & (2 * RP - 1);
+        }
+      }
+      inobs |= (ho ? 1u : 0u) << u;
+    }
+  }
+  if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
+  span = wave_max_u32_dpp(span);
+  Obs ob;
+  ob.n = om.nobs;
+  {
+    // players 0..nobs-1 in Observed and ascending?
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t i = 64u * t + lane;
+      const uint32_t nlo = t == 0 ? wshl1(lo32(k01[0]), rl32(lo32(k01[1]), 0)) : wshl1(lo32(k01[1]), 0u);
+      const uint32_t nhi = t == 0 ? wshl1(hi32(k01[0]), rl32(hi32(k01[1]), 0)) : wshl1(hi32(k01[1]), 0u);
+      const bool io = (inobs >> t) & 1u;
+      if (i < ob.n) bad |= !io || (i + 1 < ob.n && !(k01[t] < mk64(nlo, nhi)));
+      else bad |= io;
+    }
+    bad |= (inobs >> 2) != 0;  // an Observed player past 127
+    if (!ballot(bad)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        ob.key[t] = k01[t];
+        ob.ts[t] = t01[t];
+        ob.pl[t] = (64u * t + lane) | ((uint32_t)L.odc[64u * t + lane] << 16);
+      }
+    } else {
+      // the r-th Observed player in player order is pulled by entry r; then sort
+      uint64_t mk[RSL];
+      uint32_t base[RSL + 1];
+      base[0] = 0;
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        mk[u] = ballot((inobs >> u) & 1u);
+        base[u + 1] = base[u] + (uint32_t)__builtin_popcountll(mk[u]);
+      }
+      ob.n = base[RSL];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t r = 64u * t + lane;
+        ob.key[t] = INT64_MAX;
+        ob.ts[t] = 0;
+        ob.pl[t] = RNONE;
+#pragma unroll
+        for (int u = 0; u < RSL; ++u) {
+          const bool here = r >= base[u] && r < base[u + 1];
+          const uint32_t src = here ? kth_bit(mk[u], r - base[u]) : lane;
+          const int64_t vi = shfl64(pid[u], (int)src);
+          if (here) {
+            const uint32_t p = 64u * u + src;
+            ob.key[t] = mkkey(L.msc[p], vi);  // Obs[Id]'s Score = the largest (I1)
+            ob.ts[t] = L.ots[p];
+            ob.pl[t] = p | ((uint32_t)L.odc[p] << 16);
+          }
+        }
+      }
+      ob_sort(ob);
+    }
+  }
+  ob_clear_tail(ob);
+  wave_lds_sync();
+  RPROF(0);
+  {
+    // ---- P2. every op's player; ops per player; rmv players
+    uint32_t np = om.np;
+    for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
+      const uint32_t l = c0 + lane;
+      const bool v = l < nops;
+      const int64_t id = v ? a.id[op0 + l] : 0;
+      const uint32_t kind = v ? (uint32_t)a.kind[op0 + l] : 0u;
+      if (ballot(v && !fits32(id))) return R_NEXT;  // a wide Id: tier S
+      uint32_t p;
+      if (!r_resolve(L, id, v, np, p)) return R_NEXT;
+      if (v) {
+        a.op_pl[op0 + l] = (uint8_t)p;
+        atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
+        if (kind == 2 || kind == 3) atomicOr(&L.pf[p], Q_RMV);
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t p = 64u * u + lane;
+      if (p >= om.np && p < np) pid[u] = L.u.r.pid[p];
+    }
+    // new Removals rows, new slab offsets (old count + ops: the new segment)
+    uint32_t nr = om.nr, mtot = 0;
+#pragma unroll
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t p = 64u * u + lane;
+      const bool act = p < np;
+      const uint32_t q = act ? p : 0u;
+      const uint32_t f = act ? L.pf[q] : 0u;
+      const uint32_t row = L.prow[q];
+      const bool newrow = act && (f & Q_RMV) && row == NONE16;
+      const uint64_t m = ballot(newrow);
+      if (newrow) L.prow[p] = (uint16_t)(nr + mbcnt(m));
+      nr += (uint32_t)__builtin_popcountll(m);
+      const uint32_t ocnt = act ? (L.oslab[q] >> 16) : 0u;
+      const uint32_t cap = act ? ocnt + L.u.r.nops[q] : 0u;
+      uint32_t tot;
+      const uint32_t ex = wave_excl_scan_dpp(cap, tot);
+      if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
+      mtot += tot;
+    }
+    if (nr >= NONE16 || mtot > TRMV_SEG_MAX) return R_NEXT;  // over the per-key capacity
+    wave_lds_sync();
+    RPROF(1);
+
+    // ---- P3. old slabs and old Removals rows -> the new side
+    // (start map: u16 per pool position of the span, player + 1 at each slab
+    // start, in the P1/P2 union, which is free from here on)
+    constexpr uint32_t SMAP = (uint32_t)(sizeof(L.u.r) / 2);
+    uint16_t* smap16 = reinterpret_cast<uint16_t*>(&L.u.r);
+    const bool smap = span <= SMAP;
+    if (span && smap) {
+      for (uint32_t i = lane; i < (span + 1) / 2; i += 64) reinterpret_cast<uint32_t*>(smap16)[i] = 0u;
+      wave_lds_sync();
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        const uint32_t sl = p < om.np ? L.oslab[p] : 0u;
+        if (sl >> 16) smap16[sl & 0xFFFFu] = (uint16_t)(p + 1);
+      }
+      wave_lds_sync();
+    }
+    bool wide = false;
+    if (span) {
+      int32_t prev = -1;
+      int64_t nsc = 0, nts = 0;
+      uint32_t ndc = 0;
+      if (lane < span) {
+        nsc = a.old_s.m_score[(uint64_t)om.m_off + lane];
+        nts = a.old_s.m_ts[(uint64_t)om.m_off + lane];
+        ndc = a.old_s.m_dc[(uint64_t)om.m_off + lane];
+      }
+      for (uint32_t q0 = 0; q0 < span; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const int64_t sc = nsc, ts = nts;
+        const uint32_t dc = ndc;
+        if (q + 64 < span) {
+          const uint64_t src = (uint64_t)om.m_off + q + 64;
+          nsc = a.old_s.m_score[src];
+          nts = a.old_s.m_ts[src];
+          ndc = a.old_s.m_dc[src];
+        }
+        // the owner of a position is the player whose slab starts last at or
+        // before it (slabs are not in player order: tier R writes players in
+        // Observed order); starts come from the start map, or for a span past
+        // its size from a sweep of every player
+        uint32_t st = 0;
+        if (smap) {
+          st = q < span ? (uint32_t)smap16[q] : 0u;
+        } else {
+          L.u.c.mark[lane] = 0u;
+          wave_lds_sync();
+          for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const uint32_t sl = j < om.np ? L.oslab[j] : 0u;
+            const uint32_t off = sl & 0xFFFFu;
+            if ((sl >> 16) && off >= q0 && off < q0 + 64) L.u.c.mark[off - q0] = j + 1;
+          }
+          wave_lds_sync();
+          st = L.u.c.mark[lane];
+        }
+        uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
+        {  // inclusive max-scan (DPP): the last start at or before the lane
+          uint32_t o;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x111, 0xf, 0xf, false);
+          own = o > own ? o : own;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x112, 0xf, 0xf, false);
+          own = o > own ? o : own;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x114, 0xf, 0xf, false);
+          own = o > own ? o : own;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x118, 0xf, 0xf, false);
+          own = o > own ? o : own;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x142, 0xa, 0xf, false);
+          own = o > own ? o : own;
+          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x143, 0xc, 0xf, false);
+          own = o > own ? o : own;
+        }
+        own &= 0xFFFFu;
+        const int32_t o = own ? (int32_t)own - 1 : prev;
+        prev = (int32_t)rl32((uint32_t)o, 63);
+        if (q < span && o >= 0) {
+          const uint32_t sl = L.oslab[o];
+          const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
+          if (q < off + cnt) {
+            wide |= !fits32(sc);
+            const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
+            a.new_s.m_score[dst] = sc;
+            a.new_s.m_ts[dst] = ts;
+            a.new_s.m_dc[dst] = (uint8_t)dc;
+          }
+        }
+        wave_lds_sync();
+      }
+    }
+    if (ballot(wide)) return R_NEXT;  // a wide Score in Masked: tier S
+    for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
+      const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
+      if (r < om.nr && (int)d < D)
+        a.new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
+    RPROF(2);
+
+    // ---- chunks
+    for (uint32_t c0 = 0; c0 < nops;) {
+      uint32_t n = nops - c0 < (uint32_t)RCH ? nops - c0 : (uint32_t)RCH;
+      bool v = lane < n;
+      const uint64_t gi = op0 + c0 + lane;
+      const uint32_t kind = v ? (uint32_t)a.kind[gi] : 0u;
+      const int64_t id = v ? a.id[gi] : 0;
+      const int64_t sc = v ? a.score[gi] : 0;
+      const int64_t ts = v ? a.ts[gi] : 0;
+      const uint32_t dc = v ? (uint32_t)a.dc[gi] : 0u;
+      const uint32_t p = v ? (uint32_t)a.op_pl[gi] : (uint32_t)RP;
+      bool isr = v && (kind == 2 || kind == 3);
+      uint64_t rm = ballot(isr);
+      if (__builtin_popcountll(rm) > RCHR) {  // cut before the chunk's 17th rmv
+        uint64_t m = rm;
+        for (int k = 0; k < RCHR; ++k) m &= m - 1;
+        n = (uint32_t)__builtin_ctzll(m);
+        v = lane < n;
+        isr = isr && v;
+        rm = ballot(isr);
+      }
+      const bool add = v && kind < 2;
+      uint32_t err = 0;
+      err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
+      err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
+      err |= (add && ts < 1) ? TRMV_ERR_TS : 0u;
+      err |= (isr && (ts < 0 || ts >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
+      if (ballot(err != 0)) {
+        if (err) atomicOr(&a.status[1], err);
+        return R_REJECT;
+      }
+      if (ballot(v && (!fits32(id) || (add && !fits32(sc))))) return R_NEXT;  // wide values: tier S
+      const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
+      if (isr) L.u.c.crow[rk] = (uint32_t)ts;
+      wave_lds_sync();
+      for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
+        const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
+        if (r < nrm) {
+          const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
+          err |= x < 0 ? TRMV_ERR_VC : 0u;
+          L.u.c.vtab[r][d] = x;
+        }
+      }
+      if (ballot(err != 0)) {
+        if (err) atomicOr(&a.status[1], err);
+        return R_REJECT;
+      }
+      // Elements that may already be in Masked[Id] (:240-246): every element
+      // of dc in the key has Ts <= Vc[dc], so an add above the key's Vc[dc]
+      // before it is new.  Exact when the chunk's adds of each dc have rising
+      // Ts; otherwise every add of that dc after the first fall is a candidate.
+      bool dupc;
+      {
+        const int64_t vcs = (int64_t)L.vc[add ? dc : (uint32_t)TRMV_DPAD];
+        const uint32_t kv = wave_radix_sort<4>(((add ? dc : 8u) << 6) | lane);
+        const uint32_t src = kv & 63u, sdc = kv >> 6;
+        const int64_t sts = shfl64(ts, (int)src);
+        const uint32_t lkv = shfl32(kv, lane ? (int)lane - 1 : 0);
+        const int64_t lts = shfl64(sts, lane ? (int)lane - 1 : 0);
+        const bool fall = lane > 0 && sdc < 8u && (lkv >> 6) == sdc && lts >= sts;
+        const uint64_t fm = ballot(fall);
+        bool taint = false;
+        if (fm) {
+          const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+          const uint64_t f = fm & below;
+          const uint32_t hi = f ? 63u - (uint32_t)__builtin_clzll(f) : lane;
+          const uint32_t fkv = shfl32(kv, (int)hi);
+          taint = f != 0 && (fkv >> 6) == sdc;
+        }
+        const bool taint_src = perm32(taint ? 1u : 0u, src) != 0;
+        dupc = add && (ts <= vcs || taint_src);
+      }
+      wave_lds_sync();
+      if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
+      if (dupc) atomicOr(&L.pf[p], Q_DUP);
+      L.u.c.csc[lane] = sc;
+      L.u.c.cts[lane] = ts;
+      L.u.c.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)RP << 8);
+      L.u.c.cres[lane] = isr ? rk : 0u;
+      wave_lds_sync();
+      RPROF(3);
+
+      // ---- P3c. ops in (player, stream) order: appends of players without
+      // a rmv or duplicate candidate (op-parallel), replays of the others
+      const uint32_t kvs = wave_radix_sort<9>(((v ? p : (uint32_t)RP) << 6) | lane);
+      const uint32_t sp = kvs >> 6, so = kvs & 63u;
+      const bool sv = sp < (uint32_t)RP;
+      const uint32_t lkvs = shfl32(kvs, lane ? (int)lane - 1 : 0);
+      const bool start = sv && (lane == 0 || (lkvs >> 6) != sp);
+      L.u.c.csrt[lane] = (uint8_t)so;
+      const uint64_t ss = ballot(start);
+      const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+      const uint64_t sb = ss & incl;
+      const uint32_t slo = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
+      const uint64_t above = ss & ~incl;
+      const uint32_t shi = above ? (uint32_t)__builtin_ctzll(above) : n;
+      const uint64_t segm = (shi >= 64 ? ~0ull : ((1ull << shi) - 1)) & ~((1ull << slo) - 1);
+      const uint32_t skd = L.u.c.ckd[so];
+      const int64_t ssc = L.u.c.csc[so], sts = L.u.c.cts[so];
+      const uint32_t sdc = (skd >> 2) & 7u;
+      const int64_t sid = shfl64(id, (int)so);
+      L.u.c.cid[lane] = sid;
+      const uint32_t pf0 = L.pf[sv ? sp : 0u];
+      const bool walk = sv && (pf0 & (Q_RMV | Q_DUP));
+      bool dom = false;
+      uint32_t orw = NONE16;
+      if (sv && !walk && (pf0 & Q_ROWV)) {
+        orw = L.prow[sp];
+        dom = a.new_s.r_vc[((uint64_t)nm.r_off + orw) * D + sdc] >= sts;
+      }
+      const bool app = sv && !walk && !dom;
+      const uint64_t nd = ballot(app);
+      if (app) {
+        const uint32_t ns = L.nslab[sp];
+        const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << lane) - 1));
+        const uint64_t dst = (uint64_t)nm.m_off + (ns & 0xFFFFu) + pos;
+        a.new_s.m_score[dst] = ssc;
+        a.new_s.m_ts[dst] = sts;
+        a.new_s.m_dc[dst] = (uint8_t)sdc;
+        L.u.c.cres[so] = pos << 16;
+      }
+      if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
+        Row8 rv = (Row8)(0);
+        for (int d = 0; d < D; ++d) rv[d] = a.new_s.r_vc[((uint64_t)nm.r_off + orw) * D + d];
+        L.u.c.cres[so] = R_DOM;
+        r_emit(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, sid, 0, 0, 0, &rv);
+      }
+      wave_lds_sync();
+      if (sv && !walk && lane + 1 == shi) {
+        const uint32_t ns = L.nslab[sp];
+        L.nslab[sp] = ns + ((uint32_t)__builtin_popcountll(nd & segm) << 16);
+      }
+      RPROF(4);
+      const uint64_t wm = ballot(start && walk);
+      if (start && walk) {
+        const uint32_t k = mbcnt(wm);
+        L.u.c.cwp[k] = (uint16_t)sp;
+        L.u.c.cws[k] = (uint8_t)lane;
+        L.u.c.cwe[k] = (uint8_t)shi;
+      }
+      wave_lds_sync();
+      if (lane < (uint32_t)__builtin_popcountll(wm)) {
+        const uint32_t wp = L.u.c.cwp[lane], ws = L.u.c.cws[lane], we = L.u.c.cwe[lane];
+        uint32_t f = L.pf[wp];
+        const uint32_t ns = L.nslab[wp];
+        const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
+        uint32_t cnt = ns >> 16;
+        const uint32_t row = L.prow[wp];
+        bool has_row = (f & Q_ROWV) != 0;
+        Row8 R = (Row8)(0);
+        const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
+        if (has_row)
+          for (int d = 0; d < D; ++d) R[d] = a.new_s.r_vc[rbase + d];
+        const int64_t wid = L.u.c.cid[ws];
+        bool moved = false;
+        for (uint32_t x = ws; x < we; ++x) {
+          const uint32_t o = L.u.c.csrt[x];
+          const uint32_t kd = L.u.c.ckd[o];
+          const int64_t esc = L.u.c.csc[o], ets = L.u.c.cts[o];
+          const uint32_t edc = (kd >> 2) & 7u;
+          if ((kd & 3u) < 2) {  // add/4
+            if (has_row && pick8(R, edc) >= ets) {  // dominated (:234-237)
+              L.u.c.cres[o] = R_DOM;
+              r_emit(a, L, op0, op0 + c0 + o, CCRDT_TRMV_RMV, wid, 0, 0, 0, &R);
+              continue;
+            }
+            uint32_t pos = RNONE;
+            if ((kd >> 5) & 1u)  // set semantics: the element may be there
+              for (uint32_t j = 0; j < cnt; ++j)
+                if (a.new_s.m_ts[base + j] == ets && a.new_s.m_dc[base + j] == edc &&
+                    a.new_s.m_score[base + j] == esc) {
+                  pos = j;
+                  break;
+                }
+            if (pos == RNONE) {
+              pos = cnt++;
+              a.new_s.m_score[base + pos] = esc;
+              a.new_s.m_ts[base + pos] = ets;
+              a.new_s.m_dc[base + pos] = (uint8_t)edc;
+            }
+            L.u.c.cres[o] = pos << 16;
+          } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
+            const uint32_t r = L.u.c.cres[o];
+            Row8 V;
+#pragma unroll
+            for (int d = 0; d < TRMV_DPAD; ++d) V[d] = L.u.c.vtab[r][d];
+#pragma unroll
+            for (int d = 0; d < TRMV_DPAD; ++d) R[d] = has_row ? (V[d] > R[d] ? V[d] : R[d]) : V[d];
+            has_row = true;
+            uint32_t w = 0, bpos = 0, bdc = 0;
+            int64_t bsc = 0, bts = 0;
+            for (uint32_t j = 0; j < cnt; ++j) {
+              const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
+              const uint32_t d2 = a.new_s.m_dc[base + j];
+              if (t2 > pick8(V, d2)) {
+                if (w != j) {
+                  a.new_s.m_score[base + w] = s2;
+                  a.new_s.m_ts[base + w] = t2;
+                  a.new_s.m_dc[base + w] = (uint8_t)d2;
+                }
+                if (w == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
+                  bsc = s2;
+                  bdc = d2;
+                  bts = t2;
+                  bpos = w;
+                }
+                ++w;
+              }
+            }
+            moved |= w != cnt;
+            cnt = w;
+            L.u.c.rgs[r] = bsc;
+            L.u.c.rgt[r] = bts;
+            L.u.c.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
+          }
+        }
+        L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
+        if (has_row) {
+          for (int d = 0; d < D; ++d) a.new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
+          f |= Q_ROWV;
+        }
+        if (moved) f |= Q_WALK;
+        L.pf[wp] = f;
+      }
+      wave_lds_sync();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next chunk's replays read these stores
+      RPROF(5);
+
+      // ---- P4. the Observed half, in stream order (recompute_observed/5
+      // :301-334; rmv/3 :267-298)
+      const uint32_t kdr = L.u.c.ckd[lane], crr = L.u.c.cres[lane];
+      const int64_t keyr = mkkey(sc, id);
+      const bool ladd = lane < n && (kdr & 3u) < 2 && !(crr & R_DOM);
+      const uint32_t rl = lane < (uint32_t)RCHR ? lane : 0u;
+      const int64_t rgs = L.u.c.rgs[rl], rgt = L.u.c.rgt[rl];
+      const uint32_t rgdv = L.u.c.rgd[rl];
+      const int64_t vt0 = L.u.c.vtab[lane >> 3][lane & 7], vt1 = L.u.c.vtab[8 + (lane >> 3)][lane & 7];
+      // Per (player, run) segment of the sorted order -- a run = the adds
+      // between two rmvs -- two segmented scans over its non-dominated adds:
+      // gb_sets:largest (Score, DcId, Ts), which brings the player's largest
+      // up to date at the run's end (catch_up), and the cmp/2-largest (Score,
+      // Ts; the first of equals), which is Obs[Id] after the run whenever the
+      // player is in Observed then and had a relevant add (the
+      // state after a run of adds is the top K players by (largest Score,
+      // Id), whatever the order of the run's adds across players).
+      bool cu_ok;
+      int64_t cu_s, cu_t, cm_s, cm_t;
+      uint32_t cu_d, cu_pos, cu_run, cm_d, cm_pos;
+      {
+        const uint32_t scres = L.u.c.cres[so];
+        const bool sadd = sv && (skd & 3u) < 2 && !(scres & R_DOM);
+        const uint32_t srun = sv ? (uint32_t)__builtin_popcountll(rm & ((1ull << so) - 1)) : 0xFFu;
+        const uint32_t seg = (sp << 8) | srun;
+        const uint32_t pseg = shfl32(seg, lane ? (int)lane - 1 : 0);
+        bool ok = sadd, hf = lane == 0 || pseg != seg;
+        int64_t vs = ssc, vt = sts, ws = ssc, wt = sts;
+        uint32_t vd = sdc | ((scres >> 16) << 8), wd = vd;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int src = (int)lane >= d ? (int)lane - d : (int)lane;
+          const bool yok = shfl32(ok ? 1u : 0u, src) != 0;
+          const int64_t ys = shfl64(vs, src), yt = shfl64(vt, src);
+          const uint32_t yd = shfl32(vd, src);
+          const int64_t zs = shfl64(ws, src), zt = shfl64(wt, src);
+          const uint32_t zd = shfl32(wd, src);
+          const bool yhf = shfl32(hf ? 1u : 0u, src) != 0;
+          if ((int)lane >= d && !hf) {
+            if (yok) {
+              if (!ok || gb_gt(ys, yd & 0xFFu, yt, vs, vd & 0xFFu, vt)) {
+                vs = ys;
+                vt = yt;
+                vd = yd;
+              }
+              if (!ok || !(ws > zs || (ws == zs && wt > zt))) {  // the earlier one wins ties
+                ws = zs;
+                wt = zt;
+                wd = zd;
+              }
+              ok = true;
+            }
+            hf = yhf;
+          }
+        }
+        const uint32_t nseg = shfl32(seg, lane < 63 ? (int)lane + 1 : (int)lane);
+        const bool last = sv && (lane == 63 || nseg != seg);
+        cu_ok = last && ok;
+        cu_s = vs;
+        cu_t = vt;
+        cu_d = vd & 0xFFu;
+        cu_pos = vd >> 8;
+        cu_run = srun;
+        cm_s = ws;
+        cm_t = wt;
+        cm_d = wd & 0xFFu;
+        cm_pos = wd >> 8;
+      }
+      const uint32_t cu_p = sp;
+      const int64_t cm_k = mkkey(cm_s, sid);
+      wave_lds_sync();  // the chunk region is free from here on: merge staging
+      int64_t* stk = reinterpret_cast<int64_t*>(&L.u);
+      int64_t* stt = stk + 128;
+      uint32_t* stp = reinterpret_cast<uint32_t*>(stk + 256);
+      auto catch_up = [&](uint32_t run) {
+        if (cu_ok && cu_run == run) {  // one lane per player
+          const uint32_t f = L.pf[cu_p];
+          const int64_t cs = L.msc[cu_p], ct = L.gts[cu_p];
+          const uint32_t cd = L.gdc[cu_p];
+          if (!(f & Q_HASM) || gb_gt(cu_s, cu_d, cu_t, cs, cd, ct)) {
+            L.msc[cu_p] = (int32_t)cu_s;
+            L.gts[cu_p] = cu_t;
+            L.gdc[cu_p] = (uint8_t)cu_d;
+            L.gpos[cu_p] = (uint16_t)cu_pos;
+            if (!(f & Q_HASM)) atomicOr(&L.pf[cu_p], Q_HASM);
+          }
+        }
+        wave_lds_sync();
+      };
+      // A run's effect on Observed in one merge: the players whose run can
+      // change it (an Observed player whose cmp-largest beats Obs[Id]; any
+      // other whose key beats Min -- state at the run's start, where L.msc /
+      // L.ots are exact), their old entries out, their cmp-largest in, the
+      // smallest dropped to K.
+      auto run_merge = [&](uint32_t run) {
+        const bool seg_r = cu_ok && cu_run == run;
+        uint32_t f = 0;
+        int64_t ms = 0, ot = 0;
+        if (seg_r) {
+          f = L.pf[cu_p];
+          ms = L.msc[cu_p];
+          ot = L.ots[cu_p];
+        }
+        const bool inobs = (f & Q_OBS) != 0;
+        const int64_t mk = rl64(ob.key[0], 0);
+        const bool rel = seg_r && (inobs ? (cm_s > ms || (cm_s == ms && cm_t > ot)) : (ob.n < K || cm_k > mk));
+        const uint64_t relm = ballot(rel);
+        RCOUNT(11, __builtin_popcountll(relm));
+        RCOUNT(13, 1);
+        if (!relm) return;
+        bool rem0 = false, rem1 = false;
+        for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries
+          const uint32_t xp = rl32(cu_p, (int)__builtin_ctzll(t));
+          rem0 |= (ob.pl[0] & 0xFFFFu) == xp;
+          rem1 |= (ob.pl[1] & 0xFFFFu) == xp;
+        }
+        const bool v0 = lane < ob.n && !rem0, v1 = 64u + lane < ob.n && !rem1;
+        uint32_t cb0 = 0, cb1 = 0, cbc = 0, abc = 0;
+        for (uint64_t t = relm; t; t &= t - 1) {
+          const int x = (int)__builtin_ctzll(t);
+          const int64_t kx = rl64(cm_k, x);
+          cb0 += (v0 && kx < ob.key[0]) ? 1u : 0u;
+          cb1 += (v1 && kx < ob.key[1]) ? 1u : 0u;
+          cbc += (rel && kx < cm_k) ? 1u : 0u;
+          const uint32_t ab = (uint32_t)__builtin_popcountll(ballot(v0 && ob.key[0] < kx)) +
+                              (uint32_t)__builtin_popcountll(ballot(v1 && ob.key[1] < kx));
+          abc = (int)lane == x ? ab : abc;
+        }
+        const uint64_t rm0 = ballot(rem0 && lane < ob.n), rm1 = ballot(rem1 && 64u + lane < ob.n);
+        const uint32_t nrem = (uint32_t)__builtin_popcountll(rm0) + (uint32_t)__builtin_popcountll(rm1);
+        const uint32_t m = (uint32_t)__builtin_popcountll(relm);
+        const uint32_t T = ob.n - nrem + m, drop = T > K ? T - K : 0u;
+        const int32_t i0 = (int32_t)(lane - mbcnt(rm0) + cb0) - (int32_t)drop;
+        const int32_t i1 = (int32_t)(64u + lane - (uint32_t)__builtin_popcountll(rm0) - mbcnt(rm1) + cb1) - (int32_t)drop;
+        const int32_t ic = (int32_t)(abc + cbc) - (int32_t)drop;
+        if (v0) {
+          if (i0 >= 0) {
+            stk[i0] = ob.key[0];
+            stt[i0] = ob.ts[0];
+            stp[i0] = ob.pl[0];
+          } else {
+            atomicAnd(&L.pf[ob.pl[0] & 0xFFFFu], ~Q_OBS);  // evicted (:325-331)
+          }
+        }
+        if (v1) {
+          if (i1 >= 0) {
+            stk[i1] = ob.key[1];
+            stt[i1] = ob.ts[1];
+            stp[i1] = ob.pl[1];
+          } else {
+            atomicAnd(&L.pf[ob.pl[1] & 0xFFFFu], ~Q_OBS);
+          }
+        }
+        if (rel) {
+          if (ic >= 0) {  // Obs[Id] := its cmp-largest (:303-331)
+            stk[ic] = cm_k;
+            stt[ic] = cm_t;
+            stp[ic] = cu_p | (cm_d << 16);
+            if (!inobs) atomicOr(&L.pf[cu_p], Q_OBS);
+            L.ots[cu_p] = cm_t;
+            L.odc[cu_p] = (uint8_t)cm_d;
+            L.opos[cu_p] = (uint16_t)cm_pos;
+          } else if (inobs) {
+            atomicAnd(&L.pf[cu_p], ~Q_OBS);
+          }
+        }
+        wave_lds_sync();
+        ob.n = T - drop;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const uint32_t i = 64u * t + lane;
+          const uint32_t ii = i < ob.n ? i : 0u;
+          const int64_t kk = stk[ii], tt = stt[ii];
+          const uint32_t pp = stp[ii];
+          ob.key[t] = i < ob.n ? kk : INT64_MAX;
+          ob.ts[t] = i < ob.n ? tt : 0;
+          ob.pl[t] = i < ob.n ? pp : RNONE;
+        }
+        wave_lds_sync();
+      };
+      RPROF(6);
+      for (uint32_t j = 0;;) {
+        const uint64_t nxr = j < 64 ? rm & (~0ull << j) : 0ull;
+        const uint32_t hi = nxr ? (uint32_t)__builtin_ctzll(nxr) : n;
+        const uint32_t run = (uint32_t)__builtin_popcountll(rm & (hi >= 64 ? ~0ull : ((1ull << hi) - 1)));
+        run_merge(run);
+        RPROF(7);
+        if (hi >= n) break;
+        // ---- the rmv at hi: the run's largest elements, then Masked[Id]
+        // after the filter (:255-266), then Observed (:267-298)
+        catch_up(run);
+        const uint32_t kd = rl32(kdr, (int)hi);
+        const uint32_t X = kd >> 8;
+        const uint32_t r = rl32(crr, (int)hi);
+        const uint32_t g = rl32(rgdv, (int)r);
+        if (lane == 0) {
+          if (g & 1u) {
+            L.msc[X] = (int32_t)rl64(rgs, (int)r);
+            L.gts[X] = rl64(rgt, (int)r);
+            L.gdc[X] = (uint8_t)((g >> 8) & 7u);
+            L.gpos[X] = (uint16_t)(g >> 16);
+            atomicOr(&L.pf[X], Q_HASM);
+          } else {
+            atomicAnd(&L.pf[X], ~Q_HASM);
+          }
+        }
+        const uint32_t ix = ob_find(ob, X);
+        if (ix != RNONE) {  // impacts Observed?  VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
+          const uint32_t odc = ob_get32(ob.pl, ix) >> 16;
+          const int vl = (int)(((r & 7u) << 3) | odc);
+          const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
+          if ((r < 8 ? va : vb) >= ob_get64(ob.ts, ix)) {
+            if (lane == 0) atomicAnd(&L.pf[X], ~Q_OBS);
+            wave_lds_sync();
+            int64_t wk = 0;
+            RCOUNT(15, 1);
+            const uint32_t w = r_promote(L, pid, np, wk);
+            if (w == RNONE) {  // (:283-289): Obs[Id] dropped, Min of the rest
+              ob_remove(ob, ix);
+            } else {  // promote the largest (:290-295)
+              const int64_t gt = ufl64(L.gts[w]);
+              const uint32_t gd = ufl(L.gdc[w]), gp = ufl(L.gpos[w]);
+              ob_replace(ob, ix, wk, gt, w | (gd << 16));
+              if (lane == 0) {
+                atomicOr(&L.pf[w], Q_OBS);
+                L.ots[w] = gt;
+                L.odc[w] = (uint8_t)gd;
+                L.opos[w] = (uint16_t)gp;
+                r_emit(a, L, op0, op0 + c0 + hi, CCRDT_TRMV_ADD, key_id(wk), key_score(wk), gd, gt, nullptr);
+              }
+            }
+          }
+        }
+        wave_lds_sync();
+        RPROF(8);
+        j = hi + 1;
+      }
+      catch_up((uint32_t)__builtin_popcountll(rm & (n >= 64 ? ~0ull : ((1ull << n) - 1))));
+      wave_lds_sync();
+      c0 += n;
+    }
+
+    // ---- P5. player records: Observed first (sorted), then the others in
+    // player order; positions of compacted slabs; Vc; meta
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t i = 64u * t + lane;
+      if (i < ob.n) L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
+    }
+    wave_lds_sync();
+    uint32_t rest = ob.n, mcount = 0;
+#pragma unroll
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t p = 64u * u + lane;
+      const bool act = p < np;
+      const uint32_t f = act ? L.pf[p] : 0u;
+      const bool ino = act && (f & Q_OBS);
+      const uint64_t m = ballot(act && !ino);
+      const uint32_t ni = ino ? (uint32_t)L.u.f.nidx[p] : rest + mbcnt(m);
+      rest += (uint32_t)__builtin_popcountll(m);
+      if (act) {
+        uint32_t opos = L.opos[p], gpos = L.gpos[p];
+        const uint32_t ns = L.nslab[p], cnt = ns >> 16;
+        if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
+          const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
+          const int64_t msv = L.msc[p], otv = L.ots[p], gtv = L.gts[p];
+          const uint32_t od = L.odc[p], gd = L.gdc[p];
+          for (uint32_t j = 0; j < cnt; ++j) {
+            const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
+            const uint32_t d2 = a.new_s.m_dc[base + j];
+            if (s2 == msv && t2 == otv && d2 == od) opos = j;
+            if (s2 == msv && t2 == gtv && d2 == gd) gpos = j;
+          }
+        }
+        const uint64_t pq = (uint64_t)nm.p_off + ni;
+        a.new_s.pl_id[pq] = pid[u];
+        a.new_s.pl_slab[pq] = ns;
+        a.new_s.pl_info[pq] = (ino ? (opos & 0xFFFFu) : NONE16) | ((uint32_t)L.prow[p] << 16);
+        a.new_s.pl_gb[pq] = (uint16_t)(cnt > 1 ? gpos : 0u);
+        mcount += cnt;
+      }
+    }
+    uint32_t mtotal;
+    (void)wave_excl_scan_dpp(mcount, mtotal);
+    if (lane < (uint32_t)D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+    if (lane == 0) {
+      KeyMeta out = nm;
+      out.np = np;
+      out.nm = mtotal;
+      out.nr = nr;
+      out.nobs = ob.n;
+      out.minq = ob.n ? 0u : NONE32;
+      a.new_s.meta[key] = out;
+      a.ex_cnt[key] = L.nex;
+    }
+    RPROF(9);
+  }
+  return R_DONE;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void trmv_resident_kernel(TrmvApplyArgs a) {
+  __shared__ RLds L;
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
+    const int r = trmv_resident_key(a, key, L);
+    if (r == R_NEXT && lane_id() == 0) {
+      const uint32_t pos = atomicAdd(&a.status[0], 1u);
+      a.ovf_list[pos] = key;
+    }
+    wave_lds_sync();
+  }
+}
+
+int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
+  if (grid_keys == 0) return CCRDT_OK;
+  const uint64_t blocks = std::min<uint64_t>(grid_keys, 65536);
+  hipLaunchKernelGGL(trmv_resident_kernel, dim3((unsigned)blocks), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+}  // namespace ccrdt
+
+#ifdef TRMV_PROF
+extern "C" int ccrdt_debug_resident_prof(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_resident_prof), 16 * 8) != hipSuccess) return 4;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_resident_prof), z, sizeof(z)) != hipSuccess) return 4;
+  }
+  return 0;
+}
+#endif

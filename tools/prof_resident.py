@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Phase shares of topk_rmv tier R (trmv_resident.hip) on steady-state batches
+(diagnostic build, -DTRMV_PROF):
+    make -C antidote_ccrdt_amd/csrc OUT=../lib/libccrdt_prof.so OBJDIR=../../build/objprof EXTRA=-DTRMV_PROF
+    CCRDT_LIB=antidote_ccrdt_amd/lib/libccrdt_prof.so python tools/prof_resident.py
+Batch 1 of the bench stream on fresh keys, then batches 2.. onto them."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from antidote_ccrdt_amd import _lib  # noqa: E402
+from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv  # noqa: E402
+
+NAMES = ["P1 old players + sorted Obs", "P2 resolve + layout", "P3 bulk copy",
+         "C load/validate/clocks/dups", "C sort + appends", "C replays", "P4 scan + prefilter",
+         "P4 relevant adds", "P4 rmvs + promotions", "P5 records (+ last catch-up)"]
+n_ops = int(os.environ.get("N_OPS", 100_000_000))
+nk = 1 << 20
+eng = TopkRmvEngine(nk, 100, 8)
+try:
+    f = _lib.lib.ccrdt_debug_resident_prof
+    f.argtypes = [C.c_void_p, C.c_int]
+except AttributeError:
+    f = None
+buf = (C.c_ulonglong * 16)()
+for i in range(int(os.environ.get("BATCHES", 3))):
+    b = gen_trmv(n_ops, nk, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64,
+                 seed=0xCC0DE + 2 + 7919 * i, clock0=i * n_ops)
+    db = DeviceTrmvBatch(b)
+    del b
+    if f:
+        f(buf, 1)
+    eng.apply_device(db)
+    eng.sync()
+    db.close()
+    print(f"batch {i + 1}: chain {eng.last_kernel_ms():.2f} ms, tier R {eng.tier_ms(3):.2f} ms, "
+          f"tier S {eng.tier_ms(1):.2f} ms", flush=True)
+    if not f or i == 0:
+        continue
+    f(buf, 1)
+    tot = sum(buf[j] for j in range(len(NAMES))) or 1
+    for j, n in enumerate(NAMES):
+        print(f"  {n:30s} {buf[j] / tot * 100:6.1f} %   {buf[j] / (nk / 64):9.0f} cyc/key")
+    per = nk / 64
+    print(f"  per key: relevant adds {buf[11] / per:.1f} of {buf[12] / per:.1f} non-dominated adds, "
+          f"runs {buf[13] / per:.1f}, Observed changes {buf[14] / per:.1f}, impacting rmvs {buf[15] / per:.1f}")
