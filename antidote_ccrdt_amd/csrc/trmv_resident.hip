@@ -159,7 +159,6 @@ __device__ __forceinline__ uint32_t rhash(int64_t id) {
 
 struct alignas(16) RLds {
   int64_t gts[RP];     // gb_sets:largest(Masked[Id]): Ts
-  int64_t ots[RP];     // Obs[Id]: Ts (players in Observed)
   int32_t msc[RP];     // largest Score of Masked[Id] (= Obs[Id]'s Score in Observed, or below it mid-run)
   uint32_t pf[RP];     // flags
   uint32_t oslab[RP];  // old slab: offset | count << 16
@@ -190,6 +189,7 @@ struct alignas(16) RLds {
       uint32_t mark[RCH];
     } c;
     struct {  // P5
+      int64_t ots[RP];    // Obs[Id]'s Ts by player
       uint16_t nidx[RP];  // a player's index in the new record order
     } f;
   } u;
@@ -415,7 +415,6 @@ __device__ __forceinline__ bool r_resolve(RLds& L, int64_t id, bool v, uint32_t&
     L.pf[p] = 0u;
     L.msc[p] = 0;
     L.gts[p] = 0;
-    L.ots[p] = 0;
     L.opos[p] = (uint16_t)NONE16;
     L.gpos[p] = 0;
     L.odc[p] = 0;
@@ -523,7 +522,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         wide |= !fits32(pid[u]) || !fits32(os) || !fits32(gs);
         L.msc[p] = (int32_t)gs;
         L.gts[p] = gt;
-        L.ots[p] = ot;
         L.pf[p] = (ho ? Q_OBS : 0u) | (cnt ? Q_HASM : 0u) | ((info[t] >> 16) != NONE16 ? Q_ROWV : 0u);
         L.odc[p] = (uint8_t)od;
         L.gdc[p] = (uint8_t)gd;
@@ -604,7 +602,8 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           if (here) {
             const uint32_t p = 64u * u + src;
             ob.key[t] = mkkey(L.msc[p], vi);  // Obs[Id]'s Score = the largest (I1)
-            ob.ts[t] = L.ots[p];
+            // Obs[Id]'s Ts from the old pool (its slab position is L.opos)
+            ob.ts[t] = a.old_s.m_ts[(uint64_t)om.m_off + (L.oslab[p] & 0xFFFFu) + L.opos[p]];
             ob.pl[t] = p | ((uint32_t)L.odc[p] << 16);
           }
         }
@@ -951,22 +950,35 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             has_row = true;
             uint32_t w = 0, bpos = 0, bdc = 0;
             int64_t bsc = 0, bts = 0;
-            for (uint32_t j = 0; j < cnt; ++j) {
-              const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
-              const uint32_t d2 = a.new_s.m_dc[base + j];
-              if (t2 > pick8(V, d2)) {
-                if (w != j) {
-                  a.new_s.m_score[base + w] = s2;
-                  a.new_s.m_ts[base + w] = t2;
-                  a.new_s.m_dc[base + w] = (uint8_t)d2;
+            // the slab in blocks of 4 elements, each block's loads issued
+            // together (the compaction only writes positions already read)
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
+              int64_t s4[4], t4[4];
+              uint32_t d4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t j = j0 + e < cnt ? j0 + e : j0;
+                s4[e] = a.new_s.m_score[base + j];
+                t4[e] = a.new_s.m_ts[base + j];
+                d4[e] = a.new_s.m_dc[base + j];
+              }
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t j = j0 + e;
+                if (j < cnt && t4[e] > pick8(V, d4[e])) {
+                  if (w != j) {
+                    a.new_s.m_score[base + w] = s4[e];
+                    a.new_s.m_ts[base + w] = t4[e];
+                    a.new_s.m_dc[base + w] = (uint8_t)d4[e];
+                  }
+                  if (w == 0 || gb_gt(s4[e], d4[e], t4[e], bsc, bdc, bts)) {
+                    bsc = s4[e];
+                    bdc = d4[e];
+                    bts = t4[e];
+                    bpos = w;
+                  }
+                  ++w;
                 }
-                if (w == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
-                  bsc = s2;
-                  bdc = d2;
-                  bts = t2;
-                  bpos = w;
-                }
-                ++w;
               }
             }
             moved |= w != cnt;
@@ -1080,7 +1092,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       // A run's effect on Observed in one merge: the players whose run can
       // change it (an Observed player whose cmp-largest beats Obs[Id]; any
       // other whose key beats Min -- state at the run's start, where L.msc /
-      // L.ots are exact), their old entries out, their cmp-largest in, the
+      // L.msc is exact), their old entries out, their cmp-largest in, the
       // smallest dropped to K.
       auto run_merge = [&](uint32_t run) {
         const bool seg_r = cu_ok && cu_run == run;
@@ -1089,9 +1101,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (seg_r) {
           f = L.pf[cu_p];
           ms = L.msc[cu_p];
-          ot = L.ots[cu_p];
         }
         const bool inobs = (f & Q_OBS) != 0;
+        for (uint64_t t = ballot(seg_r && inobs); t; t &= t - 1) {  // Obs[Id]'s Ts: from the array
+          const int x = (int)__builtin_ctzll(t);
+          const int64_t tx = ob_get64(ob.ts, ob_find(ob, rl32(cu_p, x)));
+          ot = (int)lane == x ? tx : ot;
+        }
         const int64_t mk = rl64(ob.key[0], 0);
         const bool rel = seg_r && (inobs ? (cm_s > ms || (cm_s == ms && cm_t > ot)) : (ob.n < K || cm_k > mk));
         const uint64_t relm = ballot(rel);
@@ -1147,7 +1163,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             stt[ic] = cm_t;
             stp[ic] = cu_p | (cm_d << 16);
             if (!inobs) atomicOr(&L.pf[cu_p], Q_OBS);
-            L.ots[cu_p] = cm_t;
             L.odc[cu_p] = (uint8_t)cm_d;
             L.opos[cu_p] = (uint16_t)cm_pos;
           } else if (inobs) {
@@ -1213,7 +1228,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
               ob_replace(ob, ix, wk, gt, w | (gd << 16));
               if (lane == 0) {
                 atomicOr(&L.pf[w], Q_OBS);
-                L.ots[w] = gt;
                 L.odc[w] = (uint8_t)gd;
                 L.opos[w] = (uint16_t)gp;
                 r_emit(a, L, op0, op0 + c0 + hi, CCRDT_TRMV_ADD, key_id(wk), key_score(wk), gd, gt, nullptr);
@@ -1235,7 +1249,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t i = 64u * t + lane;
-      if (i < ob.n) L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
+      if (i < ob.n) {
+        L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
+        L.u.f.ots[ob.pl[t] & 0xFFFFu] = ob.ts[t];
+      }
     }
     wave_lds_sync();
     uint32_t rest = ob.n, mcount = 0;
@@ -1253,7 +1270,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const uint32_t ns = L.nslab[p], cnt = ns >> 16;
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
-          const int64_t msv = L.msc[p], otv = L.ots[p], gtv = L.gts[p];
+          const int64_t msv = L.msc[p], otv = ino ? L.u.f.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.odc[p], gd = L.gdc[p];
           for (uint32_t j = 0; j < cnt; ++j) {
             const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
@@ -1290,7 +1307,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void trmv_resident_kernel(TrmvApplyArgs a) {
+// (TRMV_R_WAVES: build knob, the minimum waves per SIMD the register
+// allocation must allow)
+#ifndef TRMV_R_WAVES
+#define TRMV_R_WAVES 3
+#endif
+__global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApplyArgs a) {
   __shared__ RLds L;
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
