@@ -29,6 +29,9 @@ int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
+int trmv_launch_steady_hbm(const TrmvApplyArgs& a, uint32_t waves, void* scratch, hipStream_t st);
+uint64_t trmv_steady_hbm_bytes(bool ranked);
+uint32_t trmv_steady_hbm_players();
 int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
                            hipStream_t st);
 int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
@@ -36,13 +39,16 @@ int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, con
                             int64_t cap, uint32_t* count, hipStream_t st);
 
 // Tiers of the apply chain: 0 = trmv_wave (tier 0), 1 / 2 = trmv_steady with
-// up to 256 / 1024 players per key (tier S), 3 = trmv_resident (tier R).  A
-// batch runs one chain: onto fresh keys 0 -> 1 -> 2, onto resident keys
-// 3 -> 1 -> 2 (tier R needs K <= 128; else 1 -> 2).  Tier 2 is always last:
-// the keys it hands on are over the per-key capacity (CCRDT_EKEYCAP).
-static constexpr int TRMV_N_TIERS = 4;
-static constexpr int TRMV_TIER_LAST = 2;
-static constexpr uint32_t TRMV_MAX_PLAYERS = 1024u;  // players per key (tier S, last class)
+// up to 256 / 1024 players per key (tier S, LDS), 3 = trmv_resident (tier R),
+// 4 = trmv_steady's HBM class (up to trmv_steady_hbm_players() players).  A
+// batch queues one chain: onto fresh keys 0 -> 1 -> 2, onto resident keys
+// 3 -> 1 -> 2 (tier R needs K <= 128; else 1 -> 2); only when tier 2 handed
+// keys on does the host launch tier 4 on them, after the chain's status read.
+// Tier 4 is last: the keys it hands on are over the per-key capacity
+// (CCRDT_EKEYCAP, ccrdt_engine_handed_on(e, 4)).
+static constexpr int TRMV_N_TIERS = 5;
+static constexpr int TRMV_TIER_LAST = 4;
+static constexpr uint32_t TRMV_HBM_WAVES = 128;  // workgroups (scratch slots) of tier 4
 static constexpr int TRMV_STATUS_WORDS = 2 + 2 * TRMV_N_TIERS;  // [0,2) scan, [2+2t, 4+2t) tier t
 static constexpr uint32_t TRMV_LATER_GRID = 4096;  // keys the grids of the later tiers cover
 
@@ -424,13 +430,41 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     E.trmv_tier_ms[t] = ms;
     E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
-  // Keys over the per-key capacity (the last tier's hand-ons) keep their old
-  // state; every other key commits.
-  const uint32_t n_over = nk ? hs[2 + 2 * TRMV_TIER_LAST] : 0u;
+  // Keys past the 1024-player class: tier 4 (HBM scratch), on the host-known
+  // list tier 2 handed on.
+  const uint32_t n_big = nk ? hs[2 + 2 * 2] : 0u;
+  if (n_big) {
+    const uint32_t waves = std::min<uint32_t>(n_big, TRMV_HBM_WAVES);
+    CCRDT_TRY(E.hbm_scratch.ensure((uint64_t)TRMV_HBM_WAVES * trmv_steady_hbm_bytes(E.k <= 128)));
+    a.key_list = E.tier_ovf[2].as<uint32_t>();
+    a.n_list = n_big;
+    a.n_list_dev = nullptr;
+    a.ovf_list = E.tier_ovf[4].as<uint32_t>();
+    a.status = status + 2 + 2 * 4;
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    CCRDT_TRY(trmv_launch_steady_hbm(a, waves, E.hbm_scratch.p, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    const uint32_t e4 = hs[3 + 2 * 4];
+    if (e4) {
+      set_error("trmv_apply: invalid op in batch (tier 4)");
+      return (e4 & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(e4 & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
+                 ? CCRDT_ERANGE
+                 : CCRDT_EINVAL;
+    }
+    float ms = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[ev - 2], E.evt[ev - 1]));
+    E.trmv_tier_ms[4] = ms;
+  }
+  E.trmv_overflow_keys[4] = n_big ? hs[2 + 2 * 4] : 0u;
+  // Keys over the per-key capacity (tier 4's hand-ons) keep their old state;
+  // every other key commits.
+  const uint32_t n_over = E.trmv_overflow_keys[4];
   if (n_over) {
     a.key_list = E.tier_ovf[TRMV_TIER_LAST].as<uint32_t>();
     a.n_list = 0;
-    a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;
+    a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;  // (trmv_keep_kernel reads the count here)
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>(n_over, TRMV_LATER_GRID), E.stream));
   }
   float kernel_ms = 0.f;
@@ -444,9 +478,9 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   E.last_kernel_ms = kernel_ms;
   if (n_over) {
     set_error("trmv_apply: " + std::to_string(n_over) +
-              " key(s) would exceed the per-key capacity (1024 players, 65535 Masked "
-              "elements, 65534 Removals rows): they keep their previous state, the other "
-              "keys committed; ccrdt_engine_handed_on(e, 2) lists them");
+              " key(s) would exceed the per-key capacity (" + std::to_string(trmv_steady_hbm_players()) +
+              " players, 65535 Masked elements, 65534 Removals rows): they keep their previous "
+              "state, the other keys committed; ccrdt_engine_handed_on(e, 4) lists them");
     return CCRDT_EKEYCAP;
   }
   return CCRDT_OK;
@@ -841,8 +875,8 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     std::sort(ids.begin(), ids.end());
     ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
     const uint64_t nmk = in->m_ptr[k + 1] - in->m_ptr[k], nrk = in->r_ptr[k + 1] - in->r_ptr[k];
-    if (ids.size() > TRMV_MAX_PLAYERS || nmk > TRMV_SEG_MAX || nrk >= NONE16) {
-      set_error("trmv_import: key exceeds per-key capacity (1024 players, 65535 Masked elements)");
+    if (ids.size() > trmv_steady_hbm_players() || nmk > TRMV_SEG_MAX || nrk >= NONE16) {
+      set_error("trmv_import: key exceeds per-key capacity (players, 65535 Masked elements, 65534 Removals rows)");
       return CCRDT_ENOMEM;
     }
     auto pidx = [&](int64_t id) -> uint32_t {

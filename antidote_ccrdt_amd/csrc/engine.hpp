@@ -65,7 +65,8 @@ struct ccrdt_engine {
   ccrdt::TrmvBufs trmv[2];
   int cur = 0;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
-  ccrdt::DevBuf tier_ovf[4];    // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf tier_ovf[5];    // keys each topk_rmv tier handed on (last batch)
+  ccrdt::DevBuf hbm_scratch;    // tier 4's per-wave working sets
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;
   uint64_t trmv_tot[2][3] = {};  // per side: bound on (players, pool, rows) held

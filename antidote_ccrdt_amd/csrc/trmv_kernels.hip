@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64) void trmv_downstream_kernel(TrmvDownArgs a) {
 // ops, so the old state fits), closing the holes between Masked slabs, and
 // clears the key's extras.  A fresh engine's previous state is empty.
 __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
-  const uint32_t n = *a.n_list_dev;
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   const int lane = lane_id();
   const int D = a.n_dc;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {

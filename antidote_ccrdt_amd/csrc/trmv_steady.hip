@@ -149,6 +149,23 @@ struct alignas(16) SLds {
   uint32_t nob;                          // K1: old Observed entries gathered
 };
 
+// The HBM class (PCAP > 1024) keeps SLds in a per-wave global scratch
+// instead of LDS.  A wave's lanes hand values to each other through it, and
+// atomics execute in L2 while plain loads may hit this CU's L1: every sync
+// point waits for the wave's stores and invalidates the L1 (agent acquire),
+// so the next loads see what every lane wrote.  Slow, and only for keys past
+// the LDS classes.
+constexpr int PCAP_HBM = 16384;
+template <int PCAP, bool RK>
+__device__ __forceinline__ void lsync(const SLds<PCAP, RK>&) {
+  if constexpr (PCAP > 1024) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
+  wave_lds_sync();
+}
+
 template <int PCAP>
 __device__ __forceinline__ uint32_t shash(int64_t id) {
   constexpr int B = Log2<2 * PCAP>::v;
@@ -259,13 +276,19 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP, RK>& L, int64_t id, bool v,
   constexpr int HS = SLds<PCAP, RK>::HS;
   const int lane = lane_id();
   L.u.k.claim[lane] = id;
-  wave_lds_sync();
+  lsync(L);
   uint32_t h = shash<PCAP>(id);
   bool resolved = !v, claimed = false;
   int follow = -1;
   p = 0;
   constexpr uint32_t HNONE = HSlot<PCAP>::NONE, HCLAIM = HSlot<PCAP>::CLAIM;
+  uint32_t rounds = 0;
+  (void)rounds;
   while (ballot(!resolved)) {
+    if constexpr (PCAP > 1024) {  // HBM class: fresh slot reads each round, and a bound
+      lsync(L);
+      if (++rounds > 4u * HS) return false;
+    }
     if (!resolved) {
       const uint32_t s = L.hs[h];
       if (s == HNONE) {
@@ -289,7 +312,7 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP, RK>& L, int64_t id, bool v,
       }
     }
   }
-  wave_lds_sync();
+  lsync(L);
   const uint64_t cm = ballot(claimed);
   const uint32_t nn = np + (uint32_t)__builtin_popcountll(cm);
   if (nn > (uint32_t)PCAP) return false;
@@ -308,7 +331,7 @@ __device__ __forceinline__ bool s_resolve(SLds<PCAP, RK>& L, int64_t id, bool v,
   const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
   if (follow >= 0) p = fp;
   np = nn;
-  wave_lds_sync();
+  lsync(L);
   return true;
 }
 
@@ -317,7 +340,7 @@ __device__ __forceinline__ uint32_t s_lookup(const SLds<PCAP, RK>& L, int64_t id
   constexpr int HS = SLds<PCAP, RK>::HS;
   uint32_t h = shash<PCAP>(id), p = (uint32_t)PCAP;
   if (v) {
-    for (;;) {
+    for (uint32_t probe = 0; probe < (uint32_t)HS; ++probe) {
       const uint32_t s = L.hs[h];
       if (s == HSlot<PCAP>::NONE) break;  // cannot happen: K2 resolved every Id
       if (L.pid[s] == id) {
@@ -514,7 +537,7 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP, RK>& L, uint32
   }
   if (v0 && pos0 < 0) atomicAnd(&L.opd[o.p[0]], ~F_OBS);  // evicted (:325-331)
   if (v1 && pos1 < 0) atomicAnd(&L.opd[o.p[1]], ~F_OBS);
-  wave_lds_sync();
+  lsync(L);
   o.n = tot - (uint32_t)m;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -528,7 +551,7 @@ __device__ __forceinline__ int32_t ot_merge(ObsTab& o, SLds<PCAP, RK>& L, uint32
     o.ts[t] = ok ? tv : 0;
     o.p[t] = ok ? pv : (uint32_t)PCAP;
   }
-  wave_lds_sync();
+  lsync(L);
   ot_set_min(o);
   return ins ? posi : -1;
 }
@@ -556,7 +579,7 @@ __device__ __forceinline__ void s_catch_up(SLds<PCAP, RK>& L, uint32_t lo, uint3
       atomicOr(&L.opd[p], F_HASM);
     }
   }
-  wave_lds_sync();
+  lsync(L);
 }
 
 // One key.  Writes nothing to the new side before its last early return
@@ -597,7 +620,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     if constexpr (RANKED) L.ork[PCAP] = 0u;
     else L.osc[PCAP] = L.ots[PCAP] = 0;
   }
-  wave_lds_sync();
+  lsync(L);
 
   // ---- K1. old players: four slots per round, each round's HBM loads
   // issued together (records, then the Obs[Id] / largest elements they name)
@@ -662,7 +685,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     }
   }
   span = wave_max_u32_dpp(span);
-  wave_lds_sync();
+  lsync(L);
   SPROF(0);
 
   // ---- K2. the player of every op, ops per player, players with a rmv
@@ -679,7 +702,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       if (kind == 2 || kind == 3) atomicOr(&L.opd[p], F_RMV);
     }
   }
-  wave_lds_sync();
+  lsync(L);
   // new Removals rows, new slab offsets (old count + ops: the new segment)
   uint32_t nr = om.nr, mtot = 0;
   for (uint32_t b = 0; b < np; b += 64) {
@@ -699,7 +722,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     mtot += tot;
   }
   if (nr >= NONE16 || mtot > TRMV_SEG_MAX) return S_NEXT;  // over the per-key capacity
-  wave_lds_sync();
+  lsync(L);
   SPROF(1);
 
   // ---- K3. old slabs (except replayed players') and old Removals rows
@@ -723,17 +746,21 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         nts = a.old_s.m_ts[src];
         ndc = a.old_s.m_dc[src];
       }
+      // The owner of a position is the player whose slab starts last at or
+      // before it.  Slabs are not in player order (tier R writes players in
+      // Observed order), so every player marks its slab start if it falls in
+      // the window; (position, player) pairs, max-scanned by position.
       L.u.c.mark[lane] = 0u;
-      wave_lds_sync();
-      for (uint32_t j0 = (uint32_t)(prev + 1);; j0 += 64) {  // slabs starting in the window
+      lsync(L);
+      for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
         const uint32_t j = j0 + lane;
-        const uint32_t off = j < om.np ? (L.oslab[j] & 0xFFFFu) : S_NONE;
-        if (off >= q0 && off < q0 + 64) atomicMax(&L.u.c.mark[off - q0], j + 1);
-        const uint32_t last = rl32(off, 63);
-        if (!(j0 + 64 < om.np && last < q0 + 64)) break;
+        const uint32_t sl = j < om.np ? L.oslab[j] : 0u;
+        const uint32_t off = sl & 0xFFFFu;
+        if ((sl >> 16) && off >= q0 && off < q0 + 64) L.u.c.mark[off - q0] = j + 1;
       }
-      wave_lds_sync();
-      const uint32_t own = wave_incl_max_dpp(L.u.c.mark[lane]);
+      lsync(L);
+      const uint32_t mk = L.u.c.mark[lane];
+      const uint32_t own = wave_incl_max_dpp(mk ? (((uint32_t)lane + 1) << 16) | mk : 0u) & 0xFFFFu;
       const int32_t o = own ? (int32_t)own - 1 : prev;
       prev = (int32_t)rl32((uint32_t)o, 63);
       if (q < span && o >= 0) {
@@ -746,7 +773,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
           a.new_s.m_dc[dst] = (uint8_t)dc;
         }
       }
-      wave_lds_sync();
+      lsync(L);
     }
   }
   for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
@@ -792,7 +819,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       rk[0] += key_lt(js, ji, es[0], ei[0]) ? 1u : 0u;
       rk[1] += key_lt(js, ji, es[1], ei[1]) ? 1u : 0u;
     }
-    wave_lds_sync();
+    lsync(L);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if ((uint32_t)(t * 64 + lane) < c) {
@@ -803,7 +830,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         L.ork[ep[t]] = (uint8_t)rk[t];
       }
     }
-    wave_lds_sync();
+    lsync(L);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t k = (uint32_t)(t * 64 + lane);
@@ -816,7 +843,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     }
     ob.n = c;
     ot_set_min(ob);
-    wave_lds_sync();
+    lsync(L);
   }
   for (uint32_t c0 = 0; c0 < nops;) {
     uint32_t n = nops - c0 < (uint32_t)S_CH ? nops - c0 : (uint32_t)S_CH;
@@ -851,7 +878,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     // the rmvs' clocks (8 lanes per row)
     const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
     if (isr) L.u.c.crow[rk] = (uint32_t)ts;
-    wave_lds_sync();
+    lsync(L);
     for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7;
       if (r < nrm) {
@@ -892,13 +919,13 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       const bool taint_src = perm32(taint ? 1u : 0u, src) != 0;  // back to stream lanes
       dupc = add && (ts <= vcs || taint_src);
     }
-    wave_lds_sync();
+    lsync(L);
     if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
     L.u.c.csc[lane] = sc;
     L.u.c.cts[lane] = ts;
     L.u.c.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)PCAP << 8);
     L.u.c.cres[lane] = isr ? rk : 0u;
-    wave_lds_sync();
+    lsync(L);
 
     SPROF(4);
     // ---- ops in (player, stream) order
@@ -946,7 +973,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       L.u.c.cres[so] = R_DOM;
       s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
     }
-    wave_lds_sync();
+    lsync(L);
     if (sv && !walk && lane + 1 == (int)shi) {
       const uint32_t ns = L.nslab[sp];
       L.nslab[sp] = ns + ((uint32_t)__builtin_popcountll(nd & segm) << 16);
@@ -960,7 +987,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       L.u.c.cws[k] = (uint8_t)lane;
       L.u.c.cwe[k] = (uint8_t)shi;
     }
-    wave_lds_sync();
+    lsync(L);
     if ((uint32_t)lane < (uint32_t)__builtin_popcountll(wm)) {
       const uint32_t wp = L.u.c.cwp[lane], ws = L.u.c.cws[lane], we = L.u.c.cwe[lane];
       uint32_t f = L.opd[wp];
@@ -1054,7 +1081,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       if (moved) f |= F_WALK;
       L.opd[wp] = f;
     }
-    wave_lds_sync();
+    lsync(L);
     // the next chunk's replays read this chunk's stores
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     SPROF(6);
@@ -1121,7 +1148,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         const bool inr = ladd && (uint32_t)lane >= j && (uint32_t)lane < hi;
         bool rel = inr;
         if (RANKED) {
-          wave_lds_sync();
+          lsync(L);
           const uint32_t pq = inr ? (kdr >> 8) : (uint32_t)PCAP;
           const uint32_t f = L.opd[pq];
           const uint32_t rq = L.ork[pq];  // meaningful with F_OBS
@@ -1144,7 +1171,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
             }
             const bool mine = ((relm >> lane) & 1ull) && !later;
             relm &= ~ballot(mine);
-            wave_lds_sync();
+            lsync(L);
             const uint32_t qq = mine ? q : (uint32_t)PCAP;
             const uint32_t f = L.opd[qq];
             const uint32_t rq = L.ork[qq];  // meaningful with F_OBS
@@ -1163,7 +1190,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
             } else if (up) {
               atomicAnd(&L.opd[q], ~F_OBS);
             }
-            wave_lds_sync();
+            lsync(L);
           }
         }
         while (!RANKED && relm) {
@@ -1213,7 +1240,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
               }
             }
             if (lane == 0) L.opd[q] = (L.opd[q] & F_HASM) | (f & ~F_HASM);
-            wave_lds_sync();
+            lsync(L);
             if (need_min) s_min<PCAP, RANKED>(L, np, mn);
           }
         }
@@ -1237,7 +1264,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
           atomicAnd(&L.opd[q], ~F_HASM);
         }
       }
-      wave_lds_sync();
+      lsync(L);
       SPROF(10);
       // impacts Observed?  VcRmv[ObsDc] >= Obs[Id].Ts (:267-272)
       uint32_t ix = S_NONE;
@@ -1278,21 +1305,21 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
           L.opd[w] = (L.opd[w] & 0xFFu) | F_OBS | (gd & 0xFFFFFF00u);
         }
         if (RANKED) {  // Obs[Id] dropped and the promoted entry placed in one step
-          wave_lds_sync();
+          lsync(L);
           (void)ot_merge<PCAP, RANKED>(ob, L, K, lane == 0, ix, lane == 0, gs, wid, gt, w);
         } else {
           ++nobs;
-          wave_lds_sync();
+          lsync(L);
           s_min<PCAP, RANKED>(L, np, mn);
         }
         if (lane == 0)
           s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + jr, CCRDT_TRMV_ADD, wid, gs, (gd >> 8) & 0xFFu, gt, nullptr);
       }
-      wave_lds_sync();
+      lsync(L);
       SPROF(12);
     }
     s_catch_up<PCAP, RANKED>(L, last, n, kdr, nxt, rok, rsc, rts, rd);
-    wave_lds_sync();
+    lsync(L);
     c0 += n;
     SPROF(7);
   }
@@ -1376,7 +1403,7 @@ __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a
       const uint32_t pos = atomicAdd(&a.status[0], 1u);
       a.ovf_list[pos] = key;
     }
-    wave_lds_sync();
+    lsync(L);
   }
 }
 
@@ -1399,6 +1426,43 @@ int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipS
     else
       hipLaunchKernelGGL((trmv_steady_kernel<1024, 1, false>), dim3((unsigned)blocks), dim3(64), 0, st, a);
   }
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// The HBM class: up to PCAP_HBM players per key, SLds in a per-wave global
+// scratch (`scratch` holds gridDim.x of them), one wave per workgroup.  Run
+// on the keys the 1024-player class handed on.
+template <bool RANKED>
+__global__ __launch_bounds__(64) void trmv_steady_hbm_kernel(TrmvApplyArgs a, SLds<PCAP_HBM, RANKED>* scratch) {
+  SLds<PCAP_HBM, RANKED>& L = scratch[blockIdx.x];
+  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
+    const int r = trmv_steady_key<PCAP_HBM, RANKED>(a, key, L);
+    if (r == S_NEXT && lane_id() == 0) {
+      const uint32_t pos = atomicAdd(&a.status[0], 1u);
+      a.ovf_list[pos] = key;
+    }
+    lsync(L);
+  }
+}
+
+uint64_t trmv_steady_hbm_bytes(bool ranked) {
+  return ranked ? sizeof(SLds<PCAP_HBM, true>) : sizeof(SLds<PCAP_HBM, false>);
+}
+uint32_t trmv_steady_hbm_players() { return (uint32_t)PCAP_HBM; }
+
+// `waves` workgroups, each with its scratch slot in `scratch` (waves *
+// trmv_steady_hbm_bytes(K <= 128)).
+int trmv_launch_steady_hbm(const TrmvApplyArgs& a, uint32_t waves, void* scratch, hipStream_t st) {
+  if (waves == 0) return CCRDT_OK;
+  if (a.k <= 128)
+    hipLaunchKernelGGL((trmv_steady_hbm_kernel<true>), dim3(waves), dim3(64), 0, st, a,
+                       reinterpret_cast<SLds<PCAP_HBM, true>*>(scratch));
+  else
+    hipLaunchKernelGGL((trmv_steady_hbm_kernel<false>), dim3(waves), dim3(64), 0, st, a,
+                       reinterpret_cast<SLds<PCAP_HBM, false>*>(scratch));
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -16,6 +16,11 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib, ptr
 
+# The last tier of the topk_rmv chain (the HBM class): its hand-ons are the
+# keys over the per-key capacity (include/ccrdt.h CCRDT_EKEYCAP).
+TRMV_TIER_LAST = 4
+TRMV_MAX_PLAYERS = 16384
+
 
 def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
@@ -290,7 +295,7 @@ class TopkRmvEngine(_Engine):
         try:
             check(rc, where)
         except _lib.KeyCapacityError as err:
-            err.keys, err.extra = self.handed_on(2), extra
+            err.keys, err.extra = self.handed_on(TRMV_TIER_LAST), extra
             raise
 
     def extra_count(self) -> int:

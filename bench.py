@@ -252,8 +252,9 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    # 0 = tier 0, 1 / 2 = tier S (up to 256 / 1024 players per key)
-    tiers = (0, 1, 2)
+    # 0 = tier 0, 1 / 2 = tier S (up to 256 / 1024 players per key), 3 = tier R
+    # (resident keys; the first tier of a batch onto resident state)
+    tiers = (0, 1, 2, 3)
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
 
@@ -267,11 +268,20 @@ def main():
         eng.apply_device(db)
         eng.sync()
         rows = []
+
+        def state_bytes(ks):
+            # the resident layout (trmv_kernels.hpp): per player Id 8 B + info 4 +
+            # slab 4 + largest 2, per Masked element 17 B, per Removals row 8*D,
+            # per key 32 B meta + 8*D Vc
+            return int((ks["np"].astype(np.int64) * 18 + ks["nm"].astype(np.int64) * 17 +
+                        ks["nr"].astype(np.int64) * 8 * D).sum()) + n_local_keys * (32 + 8 * D)
+        ks_prev = eng.key_sizes()
         for i in range(1, args.steady_batches + 1):
             bi = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6,
                           rmv_pm=100, lag_max=64, seed=seed + 7919 * i, clock0=i * args.n_ops)
             if sharded:
                 bi = route(bi, my_keys).batch
+            op_b = int(np.where(bi.kind >= 2, 9 + 8 * D, 26).astype(np.int64).sum())
             dbi = DeviceTrmvBatch(bi)
             del bi
             eng.sync()
@@ -281,19 +291,38 @@ def main():
             eng.sync()
             ms = (time.perf_counter() - ts0) * 1e3
             dbi.close()
+            ks_new = eng.key_sizes()
+            # bytes the batch must move in this layout: its ops, the old state
+            # read, the new state written, the extra effects
+            moved = op_b + state_bytes(ks_prev) + state_bytes(ks_new) + 32 * eng.extra_count()
+            ks_prev = ks_new
+            tr_ms = eng.tier_ms(3)
             n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
             rows.append({"batch": i + 1, "ms": round(ms, 3),
                          "ops_per_s": n_step / (ms * 1e-3),
                          "apply_chain_ms": round(eng.last_kernel_ms(), 3),
                          "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in tiers},
                          "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers},
+                         "bytes_moved": moved,
+                         "tier_r_GBs": moved / (tr_ms * 1e-3) / 1e9 if tr_ms > 0 else None,
                          "state_after": dict(zip(("observed", "masked", "removal_rows"),
                                                  eng.sizes()))})
         mean_ms = sum(r["ms"] for r in rows) / len(rows)
         n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
+        tr = [r["kernel_ms_by_tier"][3] for r in rows]
+        mv = [r["bytes_moved"] for r in rows]
+        ach = (sum(mv) / len(mv)) / ((sum(tr) / len(tr)) * 1e-3) / 1e9 if sum(tr) > 0 else None
         steady = {"what": "batches 2..n of the bench stream onto the resident keys (no reset), "
                           "one apply_device each, wall time around it (this rank)",
                   "ops_per_s_mean": n_step / (mean_ms * 1e-3), "ms_mean": mean_ms,
+                  "roofline": {"bound": "hbm", "kernel": "trmv_resident_kernel (tier R)",
+                               "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS if ach else None,
+                               "algorithmic_bytes_per_launch": sum(mv) / len(mv),
+                               "kernel_ms": sum(tr) / len(tr),
+                               "bytes": "ops (add 26 B, rmv 9 + 8*D B) + old state read + new state "
+                                        "written (player 18 B, Masked element 17 B, Removals row 8*D B, "
+                                        "key 32 + 8*D B) + 32 B per extra effect"},
                   "batches": rows}
 
     cpu = cpu_mt = None

@@ -43,11 +43,12 @@ extern "C" {
 #define CCRDT_EDEVICE 4 /* HIP / RCCL failure */
 #define CCRDT_ENOSYS 5  /* operation not supported for this type */
 #define CCRDT_EKEYCAP 6 /* topk_rmv: the batch COMMITTED except for the keys
-                           that would exceed the per-key capacity (1024
-                           players, 65535 Masked elements, 65534 Removals
-                           rows); those keep their previous state, produce no
-                           extras, and are listed by ccrdt_engine_handed_on(e,
-                           2).  Their ops go to the host (Erlang) path. */
+                           that would exceed the per-key capacity
+                           (CCRDT_TRMV_MAX_PLAYERS players, 65535 Masked
+                           elements, 65534 Removals rows); those keep their
+                           previous state, produce no extras, and are listed
+                           by ccrdt_engine_handed_on(e, 4).  Their ops go to
+                           the host (Erlang) path. */
 
 /* Registry: antidote_ccrdt:?CCRDTS (src/antidote_ccrdt.erl:28-35). */
 #define CCRDT_AVERAGE 0
@@ -64,8 +65,10 @@ extern "C" {
 #define CCRDT_TRMV_RMV_R 3
 #define CCRDT_NOOP 255 /* downstream result `noop` / "no extra effect" */
 
-/* Per-key capacity of the register-resident topk_rmv apply kernel. */
+/* topk_rmv limits: DCs per engine; players per key (the HBM class of tier S,
+ * tier 4 below, is the last one). */
 #define CCRDT_TRMV_MAX_DC 8
+#define CCRDT_TRMV_MAX_PLAYERS 16384
 
 typedef struct ccrdt_engine ccrdt_engine;
 
@@ -103,12 +106,15 @@ int ccrdt_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
 int ccrdt_device_synchronize(void);
 
 /* Duration (HIP events on the engine stream) of the apply kernel launches of
- * the last batch (all register classes) — the dominant kernel whose roofline
- * bench.py reports. */
+ * the last batch (every tier of the chain) — what bench.py reports. */
 int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms);
-/* Keys handed on by tier `t` of the last topk_rmv batch: t = 0 / 1 are the
- * per-player-parallel kernels (LDS / HBM slabs), t = 2,4,8,16 the register
- * classes of the sequential kernel. */
+/* topk_rmv tiers: 0 = trmv_wave (fresh keys, one wave per
+ * key), 1 / 2 = trmv_steady with up to 256 / 1024 players per key in LDS,
+ * 3 = trmv_resident (resident keys, K <= 128, Observed in registers),
+ * 4 = trmv_steady's HBM class (up to CCRDT_TRMV_MAX_PLAYERS players, working
+ * set in device scratch).  Chains: fresh 0 -> 1 -> 2, resident 3 -> 1 -> 2;
+ * tier 4 runs on tier 2's hand-ons.  Keys handed on by tier `t` in the last
+ * batch: */
 int ccrdt_engine_overflow_keys(ccrdt_engine* e, int t, int64_t* n);
 /* Kernel time (HIP events) of tier `t` in the last topk_rmv batch. */
 int ccrdt_engine_tier_ms(ccrdt_engine* e, int t, float* ms);

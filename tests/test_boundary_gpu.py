@@ -1,6 +1,6 @@
 """The C-ABI's state-boundary entry points on the GPU:
 
-* topk_rmv per-key capacity: a key that would exceed 1024
+* topk_rmv per-key capacity: a key that would exceed 16384
   players or 65535 Masked elements is left out of the batch with
   CCRDT_EKEYCAP -- it keeps its previous state and produces no extras -- while
   every other key commits, bit-exact against the oracle run on the batch
@@ -18,7 +18,7 @@ import pytest
 
 import oracle as orc
 from antidote_ccrdt_amd import _lib
-from antidote_ccrdt_amd.engine import TopkRmvEngine, TrmvBatch, TrmvExtra, gen_trmv
+from antidote_ccrdt_amd.engine import TRMV_MAX_PLAYERS, TopkRmvEngine, TrmvBatch, TrmvExtra, gen_trmv
 from antidote_ccrdt_amd.types import WordcountEngine, WordDocumentCountEngine
 
 pytestmark = pytest.mark.gpu
@@ -71,7 +71,7 @@ def _capacity_case(eng, o, b, key, ids, scores, dcs, tss):
 
 
 @pytest.mark.parametrize("fresh", [True, False])
-def test_key_over_1024_players_left_out(gpu, fresh):
+def test_key_over_max_players_left_out(gpu, fresh):
     nk = 64
     eng, o = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
     clock = 0
@@ -80,13 +80,24 @@ def test_key_over_1024_players_left_out(gpu, fresh):
         xe, xo = eng.apply(b), o.apply(b, 4, want_extra=True)
         assert not orc.trmv_mismatches(eng.export(), xe, o.export(), xo)
         clock = 20000
+    # 1500 distinct players on key 7: past the LDS classes, the HBM class
+    # (tier 4) applies it with the rest of the batch
     b = gen_trmv(20000, nk, D, n_players=300, seed=92, clock0=clock)
-    n = 1500  # 1500 distinct players on key 7
-    _capacity_case(eng, o, b, 7, np.arange(10**6, 10**6 + n), np.arange(n) * 3 + 5,
+    n = 1500
+    b = _splice_key(b, 7, np.arange(10**6, 10**6 + n), np.arange(n) * 3 + 5, np.arange(n) % D,
+                    clock + 1 + np.arange(n))
+    xe, xo = eng.apply(b), o.apply(b, 4, want_extra=True)
+    assert eng.overflow_keys(2) == 1 and eng.overflow_keys(4) == 0
+    assert not orc.trmv_mismatches(eng.export(), xe, o.export(), xo)
+    # MAX_PLAYERS + 100 distinct players on key 9: left out with EKEYCAP
+    clock += 20000 + n
+    b = gen_trmv(20000, nk, D, n_players=300, seed=94, clock0=clock)
+    n = TRMV_MAX_PLAYERS + 100
+    _capacity_case(eng, o, b, 9, np.arange(2 * 10**6, 2 * 10**6 + n), np.arange(n) * 3 + 5,
                    np.arange(n) % D, clock + 1 + np.arange(n))
     # the engine keeps going: the next batch (without ops on key 7) is exact
     b = gen_trmv(20000, nk, D, n_players=300, seed=93, clock0=clock + 40000)
-    b, _ = _without_key(b, 7)
+    b, _ = _without_key(b, 9)
     xe, xo = eng.apply(b), o.apply(b, 4, want_extra=True)
     assert not orc.trmv_mismatches(eng.export(), xe, o.export(), xo)
 

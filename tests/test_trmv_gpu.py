@@ -200,3 +200,52 @@ def test_empty_batch_and_reset(gpu):
     orac = orc.TrmvOracle(nk, 100, D)
     xe, xo = eng.apply(b), orac.apply(b)
     _compare(eng, orac, b, D, xe, xo)
+
+
+def _stream_batches(eng, orac, nk, D, K, plan, seed):
+    """Batches of one stream (clocks rising) with per-batch (n_ops,
+    n_players, score_max), compared with the oracle after every batch."""
+    clock = 0
+    for i, (n, npl, smax) in enumerate(plan):
+        b = gen_trmv(n, nk, D, npl, smax, 120, 16, 20, 10, seed=seed + i, clock0=clock)
+        clock += n + 1
+        xe, xo = eng.apply(b), orac.apply(b)
+        _compare(eng, orac, b, D, xe, xo)
+
+
+def test_resident_key_outgrows_tier_r(gpu):
+    """Keys that tier R wrote (players in sorted-Observed order, slabs not in
+    player order) grow past its 256 players: tier S takes them from there."""
+    nk, D, K = 6, 8, 20
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    plan = [(2400, 180, 1000)] * 3 + [(6000, 700, 1000)] * 3 + [(2400, 200, 1000)] * 2
+    _stream_batches(eng, orac, nk, D, K, plan, seed=901)
+
+
+def test_resident_key_wide_values(gpu):
+    """A batch with Scores past 32 bits sends resident keys from tier R to
+    tier S; the next narrow batch returns them to tier R (which then sorts
+    Observed itself, tier S having written the players)."""
+    nk, D, K = 40, 4, 10
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    plan = [(4000, 30, 500), (4000, 30, 500), (4000, 30, 2**40), (4000, 30, 500), (4000, 30, 500)]
+    _stream_batches(eng, orac, nk, D, K, plan, seed=77)
+
+
+@pytest.mark.parametrize("K", [50, 200])
+def test_key_grows_past_1024_players(gpu, K):
+    """One key grows to more than 5000 players over a stream (tier 2 hands it
+    on, tier 4 -- the HBM class -- applies it), bit-exact against the oracle,
+    no CCRDT_EKEYCAP; a second, small key rides along on the low tiers."""
+    nk, D = 2, 4
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    clock, most = 0, 0
+    for i, (n, npl) in enumerate([(2000, 1500), (9000, 7000), (9000, 7000), (3000, 7000)]):
+        b = gen_trmv(n, nk, D, npl, 10**6, 20, 16, 20, 10, seed=1200 + i, clock0=clock)
+        clock += n + 1
+        xe, xo = eng.apply(b), orac.apply(b)
+        _compare(eng, orac, b, D, xe, xo)
+        assert eng.overflow_keys(4) == 0
+        st = eng.export()
+        most = max(most, max(len({e[0] for e in st.key_state(k)["masked"]}) for k in range(nk)))
+    assert most >= 5000, most
