@@ -243,20 +243,37 @@ def main():
     t0_ms = eng.tier_ms(0)
     kernel_ms = t0_ms
     achieved = alg_bytes_t0 / (t0_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = steady_traffic = None
     if os.path.exists(args.pmc):
         try:
             with open(args.pmc) as f:
                 pm = json.load(f)
             if world == 1 and pm.get("n_ops") == args.n_ops and pm.get("n_keys") == args.n_keys:
                 traffic = pm.get("hbm_bytes_per_launch")
+                steady_traffic = (pm.get("steady") or {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic = None
+            traffic = steady_traffic = None
     # 0 = tier 0, 1 / 2 = tier S (up to 256 / 1024 players per key), 3 = tier R
-    # (resident keys; the first tier of a batch onto resident state)
-    tiers = (0, 1, 2, 3)
+    # (resident keys; the first tier of a batch onto resident state), 4 = the
+    # HBM class of tier S (keys past 1024 players)
+    tiers = (0, 1, 2, 3, 4)
+
     overflow = {c: eng.overflow_keys(c) for c in tiers}
     tier_ms = {c: round(eng.tier_ms(c), 4) for c in tiers}
+
+    # Host entry (reported in detail, never `value`): ccrdt_trmv_apply from
+    # host arrays -- the batch crosses PCIe to the device, the extras come back.
+    eng.reset()
+    eng.sync()
+    th = time.perf_counter()
+    eng.apply(b, want_extra=True)
+    eng.sync()
+    th = time.perf_counter() - th
+    host_entry = {"what": "ccrdt_trmv_apply on host arrays (H2D of the batch + apply chain + D2H of "
+                          "the extra effects), one batch, wall time",
+                  "ops_per_s": b.n_ops / th, "ms": th * 1e3,
+                  "batch_bytes": int(sum(getattr(b, f).nbytes for f in
+                                         ("key_ptr", "kind", "id", "score", "dc", "ts", "rmv_vc")))}
 
     # Steady state (reported beside the headline, never as `value`): the
     # same keys keep their state and receive the next batches of the stream
@@ -319,6 +336,7 @@ def main():
                                "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS if ach else None,
                                "algorithmic_bytes_per_launch": sum(mv) / len(mv),
+                               "traffic": steady_traffic,
                                "kernel_ms": sum(tr) / len(tr),
                                "bytes": "ops (add 26 B, rmv 9 + 8*D B) + old state read + new state "
                                         "written (player 18 B, Masked element 17 B, Removals row 8*D B, "
@@ -408,6 +426,7 @@ def main():
                                 "achieved_GBs": alg_bytes / (chain_ms * 1e-3) / 1e9},
                 "extra_effects": n_extra,
                 "cpu_baseline_threads": cpu_mt,
+                "host_entry": host_entry,
                 "steady_state": steady,
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,

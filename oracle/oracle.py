@@ -15,11 +15,13 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liboracle.so")
+# CCRDT_ORACLE_LIB selects another build of the oracle (the ASan/UBSan one of
+# `make -C oracle asan`, tools/asan_cpu_suite.sh); default: the -O3 build.
+LIB = os.environ.get("CCRDT_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 
 
 def build() -> str:
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, os.path.relpath(LIB, HERE)], check=True)
     return LIB
 
 

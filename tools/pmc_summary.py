@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--kernel", default="")
     ap.add_argument("--bench-json", help="write bench.py's roofline.traffic source here")
     ap.add_argument("--dominant", default="trmv_wave_kernel<true>")
+    ap.add_argument("--steady", default="trmv_resident_kernel",
+                    help="the steady-state leg's kernel (bench.py detail.steady_state.roofline)")
     ap.add_argument("--n-ops", type=int, default=100_000_000)
     ap.add_argument("--n-keys", type=int, default=1 << 20)
     a = ap.parse_args()
@@ -63,8 +65,12 @@ def main():
         dom = [k for k in out if a.dominant in k]
         if len(dom) != 1 or "hbm_bytes" not in out[dom[0]]:
             raise SystemExit(f"dominant kernel {a.dominant!r} not found with FETCH/WRITE counters")
+        st = [k for k in out if a.steady and a.steady in k and "hbm_bytes" in out[k]]
+        steady = ({"kernel": st[0], "hbm_bytes_per_launch": out[st[0]]["hbm_bytes"],
+                   "fetch_kib": out[st[0]]["FETCH_SIZE"], "write_kib": out[st[0]]["WRITE_SIZE"]}
+                  if len(st) == 1 else None)
         with open(a.bench_json, "w") as f:
-            json.dump({"n_ops": a.n_ops, "n_keys": a.n_keys, "kernel": dom[0],
+            json.dump({"n_ops": a.n_ops, "n_keys": a.n_keys, "kernel": dom[0], "steady": steady,
                        "hbm_bytes_per_launch": out[dom[0]]["hbm_bytes"],
                        "fetch_kib": out[dom[0]]["FETCH_SIZE"], "write_kib": out[dom[0]]["WRITE_SIZE"],
                        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 counts half "
