@@ -74,6 +74,9 @@ constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
 constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
+#ifndef TRMV_AHEAD2
+#define TRMV_AHEAD2 1  // FRESH: ops loaded two keys ahead, clocks one key ahead
+#endif
 #ifndef TRMV_KPW
 #define TRMV_KPW 8
 #endif
@@ -266,7 +269,8 @@ enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
 template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
                                               WaveLds<FRESH>& L, bool has_next, const ChunkHdr& hdr,
-                                              uint32_t nj, KeyIn& nxt) {
+                                              uint32_t nj, KeyIn& nxt, bool has_next2, KeyIn& nxt2,
+                                              bool& issued) {
   // opaque per key: lane-derived addresses are formed where they are used
   // instead of being hoisted out of the key loop into VGPR pairs that live
   // (and spill) across every key
@@ -469,7 +473,18 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // retires them, so the next key never waits on (and its vmcnt never
   // counts) this key's stores.  (Non-FRESH keys keep more registers live
   // through step 4: their next key's loads go out at step 5.)
+#if TRMV_AHEAD2
+  // FRESH, two keys ahead: the next key's ops landed during this key's
+  // predecessor; its removal clocks and the ops of the key after it go out
+  // now, a whole key before they are consumed
+  if (FRESH) {
+    if (has_next) wave_load_rows(a, L, nxt);
+    if (has_next2) wave_load_key(a, hdr, nj + 1, nxt2);
+    issued = true;
+  }
+#else
   if (FRESH && has_next) wave_load_key(a, hdr, nj, nxt);
+#endif
 
   PROF_MARK(2);
   // ---- 4. player of every op, Vc, op elements in player order
@@ -733,10 +748,14 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
   // The next key's ops are retired before this key's first store, so the
   // next key never waits on (and its vmcnt never counts) these stores.
+#if !TRMV_AHEAD2
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   // the next key's clock loads go out before this key's first store: a
   // load's data waits for every older vector-memory op, stores included
   if (FRESH && has_next) wave_load_rows(a, L, nxt);
+#else
+  if (!FRESH) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
   PROF_MARK(7);
   uint32_t best_q = NONE32;                      // Min candidate of this lane
   int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
@@ -1092,28 +1111,39 @@ __global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_k
     const uint32_t cn = c0 + W_KPW < n ? W_KPW : n - c0;
     ChunkHdr hdr;
     wave_load_chunk(a, c0, cn, hdr);
-    KeyIn cur;
+    KeyIn cur, nxt;
     wave_load_key(a, hdr, 0, cur);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the ops are in
     wave_load_rows(a, L, cur);
+    const bool ahead2 = TRMV_AHEAD2 && FRESH;
+    if (ahead2 && cn > 1) wave_load_key(a, hdr, 1, nxt);
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
-      const bool has_next = j + 1 < cn;
-      KeyIn nxt;
-      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
+      const bool has_next = j + 1 < cn, has_next2 = j + 2 < cn;
+      KeyIn nxt2;
+      bool issued = false;
+      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt, has_next2, nxt2, issued);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&a.status[0], 1u);
           a.ovf_list[pos] = key;
         }
-        if (has_next) wave_load_key(a, hdr, j + 1, nxt);
-        // retire these loads here, as the common path does before its
-        // stores: otherwise every key would wait on the previous key's stores
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        if (has_next) wave_load_rows(a, L, nxt);
+        if (ahead2) {
+          if (!issued) {
+            if (has_next) wave_load_rows(a, L, nxt);
+            if (has_next2) wave_load_key(a, hdr, j + 2, nxt2);
+          }
+        } else {
+          if (has_next) wave_load_key(a, hdr, j + 1, nxt);
+          // retire these loads here, as the common path does before its
+          // stores: otherwise every key would wait on the previous key's stores
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+          if (has_next) wave_load_rows(a, L, nxt);
+        }
       }
       wave_lds_sync();  // LDS is reused by the wave's next key
       cur = nxt;
+      if (ahead2) nxt = nxt2;
     }
   }
 }
