@@ -77,6 +77,22 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #ifndef TRMV_AHEAD2
 #define TRMV_AHEAD2 1  // FRESH: ops loaded two keys ahead, clocks one key ahead
 #endif
+#ifndef TRMV_NT
+#define TRMV_NT 0  // FRESH output (pool, player records) stored non-temporal
+#endif
+#if TRMV_NT
+#define ST_OUT(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define ST_OUT(p, v) (*(p) = (v))
+#endif
+#ifndef TRMV_NTL
+#define TRMV_NTL 0  // ops (read once) loaded non-temporal
+#endif
+#if TRMV_NTL
+#define LD_IN(p) __builtin_nontemporal_load(p)
+#else
+#define LD_IN(p) (*(p))
+#endif
 #ifndef TRMV_KPW
 #define TRMV_KPW 8
 #endif
@@ -105,24 +121,35 @@ struct alignas(16) WaveLds {
   uint32_t rsrc[W_RCAP];                 // rmv_vc row of each rmv op of the key being prefetched
   uint16_t ekd[W_ECAP + 8];              // kind | dc << 2 | player << 8
   uint8_t hp[W_HCAP];                    // hash slot -> player
-  uint8_t pslot[W_PCAP + 8];             // player -> hash slot
   uint8_t sorted[W_ECAP + 8];            // op index (stream position) of every op element
   uint8_t slab[W_ECAP];                  // working Masked slabs (element indices)
   uint8_t fin[NS_ * (W_ECAP + 8)];       // final pool: element of every output position
-  uint8_t pstart[W_PCAP + 8];            // first position of each player's ops
-  uint8_t pobs[W_PCAP + 8];              // Obs[Id] of each player (element), NONE8 = none
-  uint8_t pgb[W_PCAP + 8];               // gb_sets:largest(Masked[Id]) (element; slab-relative
-                                         // + slab start for replayed players)
-  uint8_t pflag[W_PCAP + 8];             // 1 = player replayed op by op
-  uint8_t pcntf[W_PCAP + 8];             // replayed player: final |Masked[Id]|
+  // Per-player bytes, packed four to a word so a pass over players reads
+  // them with one LDS load each (byte stores still write single fields):
+  //  pa: pstart (first position of the player's ops) | plr (FRESH: 1 +
+  //      position of its last rmv, 0 = none) | pflag (1 = replayed op by op)
+  //      | pcntf (replayed player: final |Masked[Id]|)
+  //  pb: pobs (Obs[Id], an element; NONE8 = none) | prow (its clock row =
+  //      Removals[Id], or NONE8) | pgb (gb_sets:largest(Masked[Id]): element;
+  //      slab-relative + slab start for replayed players) | pslot (hash slot)
+  uint32_t pa[W_PCAP + 8];
+  uint32_t pb[W_PCAP + 8];
   uint8_t pmoff[NS_ * (W_PCAP + 8)];     // replayed player: its working slab in `slab`
-  uint8_t prow[W_PCAP + 8];              // the player's clock row (Removals[Id]) or NONE8
-  uint8_t plr[W_PCAP + 8];               // FRESH: 1 + position of the player's last rmv, 0 = none
   uint8_t peb[NS_ * (W_PCAP + 8)];       // old player: first element of its old slab
   uint8_t cpl[W_PCAP + 8];               // replayed players, packed
   uint8_t rl[W_RCAP + 8];                // clock row of each output Removals row
   uint32_t nex;                          // extra effects emitted by the key
+  __device__ __forceinline__ uint8_t& fa(uint32_t p, int b) { return reinterpret_cast<uint8_t*>(pa)[4 * p + b]; }
+  __device__ __forceinline__ uint8_t& fb(uint32_t p, int b) { return reinterpret_cast<uint8_t*>(pb)[4 * p + b]; }
 };
+#define PSTART(p) L.fa((p), 0)
+#define PLR(p) L.fa((p), 1)
+#define PFLAG(p) L.fa((p), 2)
+#define PCNTF(p) L.fa((p), 3)
+#define POBS(p) L.fb((p), 0)
+#define PROW(p) L.fb((p), 1)
+#define PGB(p) L.fb((p), 2)
+#define PSLOT(p) L.fb((p), 3)
 
 __device__ __forceinline__ uint32_t whash(int64_t id) {
   const uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
@@ -220,11 +247,11 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
   for (int s = 0; s < 2; ++s) {
     const uint32_t l = s * 64 + lane;
     const bool v = l < in.nops;
-    in.id[s] = v ? idp[l] : 0;
-    in.sc[s] = v ? scp[l] : 0;
-    in.ts[s] = v ? tsp[l] : 0;
-    in.kind[s] = v ? (uint32_t)kp[l] : 0u;
-    in.dc[s] = v ? (uint32_t)dp[l] : 0u;
+    in.id[s] = v ? LD_IN(idp + l) : 0;
+    in.sc[s] = v ? LD_IN(scp + l) : 0;
+    in.ts[s] = v ? LD_IN(tsp + l) : 0;
+    in.kind[s] = v ? (uint32_t)LD_IN(kp + l) : 0u;
+    in.dc[s] = v ? (uint32_t)LD_IN(dp + l) : 0u;
   }
 }
 
@@ -330,11 +357,14 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   reinterpret_cast<uint32_t*>(L.hp)[lane] = 0xFFFFFFFFu;  // 256 B
   L.pcnt2[lane] = 0u;
-  if (lane < W_PCAP / 4) reinterpret_cast<uint32_t*>(L.pflag)[lane] = 0u;
-  if (FRESH && lane < (W_PCAP + 8) / 4) {  // step 5's per-player results
-    reinterpret_cast<uint32_t*>(L.pobs)[lane] = 0xFFFFFFFFu;
-    reinterpret_cast<uint32_t*>(L.prow)[lane] = 0xFFFFFFFFu;
-    reinterpret_cast<uint32_t*>(L.plr)[lane] = 0u;
+  // pflag, plr = 0; pobs, prow = NONE8 (the sink entries included)
+  L.pa[lane] = 0u;
+  L.pa[64 + lane] = 0u;
+  L.pb[lane] = 0xFFFFFFFFu;
+  L.pb[64 + lane] = 0xFFFFFFFFu;
+  if (lane < 8) {
+    L.pa[128 + lane] = 0u;
+    L.pb[128 + lane] = 0xFFFFFFFFu;
   }
   if (lane < TRMV_DPAD)
     L.vc[lane] = (!FRESH && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
@@ -432,7 +462,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t p = s * 64 + lane;
       if (p < om.np) {
         L.hp[hs[2 + s]] = (uint8_t)p;
-        L.pslot[p] = (uint8_t)hs[2 + s];
+        PSLOT(p) = (uint8_t)hs[2 + s];
         // every player with Masked elements must be in Observed (P <= K states)
         bad |= ((pslab[s] >> 16) != 0) != ((pinfo[s] & 0xFFFFu) != NONE16);
       }
@@ -462,10 +492,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
                          ((n2 ? i2 : ((hp4 >> 16) & 0xFFu)) << 16) |
                          ((n3 ? i3 : (hp4 >> 24)) << 24);
     reinterpret_cast<uint32_t*>(L.hp)[lane] = nhp;
-    if (n0) L.pslot[i0] = (uint8_t)(lane * 4 + 0);
-    if (n1) L.pslot[i1] = (uint8_t)(lane * 4 + 1);
-    if (n2) L.pslot[i2] = (uint8_t)(lane * 4 + 2);
-    if (n3) L.pslot[i3] = (uint8_t)(lane * 4 + 3);
+    if (n0) PSLOT(i0) = (uint8_t)(lane * 4 + 0);
+    if (n1) PSLOT(i1) = (uint8_t)(lane * 4 + 1);
+    if (n2) PSLOT(i2) = (uint8_t)(lane * 4 + 2);
+    if (n3) PSLOT(i3) = (uint8_t)(lane * 4 + 3);
   }
   wave_lds_sync();
   // the next key's op loads go out here, after the last early return: they
@@ -494,7 +524,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const uint32_t p = xv[s] ? (uint32_t)L.hp[hs[s]] : PSINK;
     xp[s] = p;
     if (xa[s]) atomicMax(&L.vc[xdc[s]], (unsigned long long)xts[s]);  // vc_update (:233)
-    if (!FRESH && xr[s]) L.pflag[p] = 1;                              // a rmv: replayed
+    if (!FRESH && xr[s]) PFLAG(p) = 1;                              // a rmv: replayed
     const uint32_t sh = 16 * (p & 1);
     xrank[s] = 0;
     if (xv[s]) xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
@@ -507,14 +537,14 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const uint32_t c1 = (uint32_t)(64 + lane) < np ? pcnt_of(L, 64 + lane) : 0u;
     const uint32_t st0 = wave_excl_scan_dpp(c0, tot0);
     const uint32_t st1 = wave_excl_scan_dpp(c1, tot1);
-    L.pstart[lane] = (uint8_t)st0;
-    L.pstart[64 + lane] = (uint8_t)(tot0 + st1);
+    PSTART(lane) = (uint8_t)st0;
+    PSTART(64 + lane) = (uint8_t)(tot0 + st1);
   }
   wave_lds_sync();
   uint32_t xq[2], xst[2], xc[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    xst[s] = L.pstart[xp[s]];
+    xst[s] = PSTART(xp[s]);
     xc[s] = pcnt_of(L, xp[s]);
     xq[s] = xv[s] ? xst[s] + xrank[s] : ESINK;
     if (xv[s]) {
@@ -539,7 +569,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll 1
       for (int s = 0; s < 2; ++s) {
         const uint32_t p = s * 64 + lane;
-        const uint32_t c = p < np ? pcnt_of(L, p) : 0u, st = p < np ? L.pstart[p] : 0u;
+        const uint32_t c = p < np ? pcnt_of(L, p) : 0u, st = p < np ? PSTART(p) : 0u;
         for (uint32_t x = 1; x < c; ++x) {
           const uint32_t v = L.sorted[st + x];
           const int64_t vs = L.esc[st + x], vt = L.ets[st + x];
@@ -579,7 +609,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       ebase += tot;
       if (p < om.np) {
         L.peb[p] = (uint8_t)eb;
-        L.pflag[p] = 1;  // old state: replayed
+        PFLAG(p) = 1;  // old state: replayed
       }
       for (uint32_t j = 0; j < oc; ++j) {
         const uint32_t go = (pslab[s] & 0xFFFFu) + j;
@@ -602,7 +632,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     uint32_t me[2], cl[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      simple[s] = xa[s] && !L.pflag[xp[s]];
+      simple[s] = xa[s] && !PFLAG(xp[s]);
       me[s] = xq[s] - xst[s];
       cl[s] = simple[s] ? xc[s] : 0u;
     }
@@ -623,9 +653,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (risk[s]) L.pflag[xp[s]] = 1;
-      if (simple[s] && !beaten[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
-      if (simple[s] && !gbeaten[s]) L.pgb[xp[s]] = (uint8_t)xq[s];
+      if (risk[s]) PFLAG(xp[s]) = 1;
+      if (simple[s] && !beaten[s]) POBS(xp[s]) = (uint8_t)xq[s];
+      if (simple[s] && !gbeaten[s]) PGB(xp[s]) = (uint8_t)xq[s];
     }
     wave_lds_sync();
   } else {
@@ -643,10 +673,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bool single = xv[s] && xc[s] == 1;
-        if (single && xa[s]) L.pobs[xp[s]] = (uint8_t)xq[s];
+        if (single && xa[s]) POBS(xp[s]) = (uint8_t)xq[s];
         if (single && xr[s]) {
-          L.prow[xp[s]] = (uint8_t)xsc[s];
-          L.plr[xp[s]] = (uint8_t)(xq[s] + 1);
+          PROW(xp[s]) = (uint8_t)xsc[s];
+          PLR(xp[s]) = (uint8_t)(xq[s] + 1);
         }
       }
       const bool mu0 = xv[0] && xc[0] > 1, mu1 = xv[1] && xc[1] > 1;
@@ -668,7 +698,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t p = act ? (kd >> 8) : PSINK;
       const bool ya = act && (kd & 2u) == 0, yr = act && (kd & 2u) != 0;
       const uint32_t adc = ya ? ((kd >> 2) & 7u) : 0u;
-      const uint32_t st = L.pstart[p], c = act ? pcnt_of(L, p) : 0u;
+      const uint32_t st = PSTART(p), c = act ? pcnt_of(L, p) : 0u;
       const uint32_t me = q - st;
       bool fb = false, beaten = false, risk = false, seen = false, first = true;
       bool gbeaten = false, gtie = false;  // gb_sets:largest of the segment (by Score; a tie replays)
@@ -706,11 +736,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
       // equal Scores in the last segment: gb_sets order goes on to DcId and
       // Ts, which the replay settles
-      if (act && (fb || risk || (ya && !seen && gtie))) L.pflag[p] = 1;
-      if (ya && !seen && !beaten) L.pobs[p] = (uint8_t)q;
-      if (ya && !seen && !gbeaten) L.pgb[p] = (uint8_t)q;  // largest of the last segment (by Score)
-      if (yr && first) L.prow[p] = (uint8_t)sm;  // a rmv's "score" is its clock row
-      if (yr && !seen) L.plr[p] = (uint8_t)(q + 1);
+      if (act && (fb || risk || (ya && !seen && gtie))) PFLAG(p) = 1;
+      if (ya && !seen && !beaten) POBS(p) = (uint8_t)q;
+      if (ya && !seen && !gbeaten) PGB(p) = (uint8_t)q;  // largest of the last segment (by Score)
+      if (yr && first) PROW(p) = (uint8_t)sm;  // a rmv's "score" is its clock row
+      if (yr && !seen) PLR(p) = (uint8_t)(q + 1);
       if (act) mrg[k] = (uint8_t)(yr && !first);
       any_merge |= ballot(yr && !first) != 0;
     }
@@ -723,8 +753,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const uint32_t k = b + lane;
         const uint32_t q = k < mn && mrg[k] ? (uint32_t)cq[k] : ESINK;
         const uint32_t p = q != ESINK ? (uint32_t)(L.ekd[q] >> 8) : PSINK;
-        if (q != ESINK && !L.pflag[p]) {
-          unsigned long long* dst = reinterpret_cast<unsigned long long*>(L.rows[L.prow[p]]);
+        if (q != ESINK && !PFLAG(p)) {
+          unsigned long long* dst = reinterpret_cast<unsigned long long*>(L.rows[PROW(p)]);
           const int64_t* src = L.rows[(uint32_t)L.esc[q]];
           for (int d = 0; d < D; ++d) atomicMax(dst + d, (unsigned long long)src[d]);
         }
@@ -737,8 +767,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // ---- 5b. replayed players, one lane per player, op by op
   uint32_t ncx;
   {
-    const bool c0 = (uint32_t)lane < np && L.pflag[lane];
-    const bool c1 = (uint32_t)(64 + lane) < np && L.pflag[64 + lane];
+    const bool c0 = (uint32_t)lane < np && PFLAG(lane);
+    const bool c1 = (uint32_t)(64 + lane) < np && PFLAG(64 + lane);
     const uint64_t m0 = ballot(c0), m1 = ballot(c1);
     const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
     ncx = n0 + (uint32_t)__builtin_popcountll(m1);
@@ -778,9 +808,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const int64_t sc = L.esc[qq], ts = L.ets[qq];
       const uint32_t kd = L.ekd[qq];
       if (q < nops) {
-        (a.new_s.m_score + nmeta.m_off)[q] = sc;
-        (a.new_s.m_ts + nmeta.m_off)[q] = ts;
-        (a.new_s.m_dc + nmeta.m_off)[q] = (uint8_t)((kd >> 2) & 7u);
+        ST_OUT((a.new_s.m_score + nmeta.m_off) + (q), sc);
+        ST_OUT((a.new_s.m_ts + nmeta.m_off) + (q), ts);
+        ST_OUT((a.new_s.m_dc + nmeta.m_off) + (q), (uint8_t)((kd >> 2) & 7u));
       }
     }
   }
@@ -797,7 +827,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       eb = L.peb[p];
     }
     const uint32_t c = act ? pcnt_of(L, p) : 0u;
-    const uint32_t st = act ? L.pstart[p] : 0u;
+    const uint32_t st = act ? PSTART(p) : 0u;
     uint32_t tot;
     const uint32_t moff = mbase + wave_excl_scan_dpp(c + ocnt, tot);  // slab capacity
     mbase += tot;
@@ -820,7 +850,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
       if (ri != NONE16) prow = ri;
     }
-    const int64_t id = act ? (int64_t)L.htab[L.pslot[p]] : 0;
+    const int64_t id = act ? (int64_t)L.htab[PSLOT(p)] : 0;
     for (uint32_t x = 0; x < c; ++x) {
       const uint32_t e = st + x;  // op element (player order)
       const uint32_t kd = L.ekd[e];
@@ -903,9 +933,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const uint32_t e2 = L.slab[moff + j];
         const int64_t s2 = L.esc[e2], t2 = L.ets[e2];
         const uint32_t d2 = (L.ekd[e2] >> 2) & 7u;
-        (a.new_s.m_score + nmeta.m_off)[st + j] = s2;
-        (a.new_s.m_ts + nmeta.m_off)[st + j] = t2;
-        (a.new_s.m_dc + nmeta.m_off)[st + j] = (uint8_t)d2;
+        ST_OUT((a.new_s.m_score + nmeta.m_off) + (st + j), s2);
+        ST_OUT((a.new_s.m_ts + nmeta.m_off) + (st + j), t2);
+        ST_OUT((a.new_s.m_dc + nmeta.m_off) + (st + j), (uint8_t)d2);
         opos = e2 == o ? j : opos;
         // gb_sets:largest so far (re-read from LDS: no registers held across)
         const uint32_t eb = L.slab[moff + gj];
@@ -914,17 +944,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         if (s2 > bs || (s2 == bs && (d2 > bd || (d2 == bd && t2 > bt)))) gj = j;
       }
       if (act) {
-        L.pobs[p] = (uint8_t)(o == NONE8 ? NONE8 : st + opos);
-        L.pgb[p] = (uint8_t)(st + gj);
-        L.pcntf[p] = (uint8_t)cnt;
-        L.prow[p] = (uint8_t)prow;
+        POBS(p) = (uint8_t)(o == NONE8 ? NONE8 : st + opos);
+        PGB(p) = (uint8_t)(st + gj);
+        PCNTF(p) = (uint8_t)cnt;
+        PROW(p) = (uint8_t)prow;
       }
       min_cand(act && o != NONE8, osc, id, p);
     } else if (act) {
-      L.pobs[p] = (uint8_t)o;
-      L.pcntf[p] = (uint8_t)cnt;
+      POBS(p) = (uint8_t)o;
+      PCNTF(p) = (uint8_t)cnt;
       L.pmoff[p] = (uint8_t)moff;
-      L.prow[p] = (uint8_t)prow;
+      PROW(p) = (uint8_t)prow;
     }
   }
   wave_lds_sync();
@@ -944,26 +974,27 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t p = s * 64 + lane;
       const bool act = p < np;
       const uint32_t pp = act ? p : (uint32_t)PSINK;
-      const uint32_t st = L.pstart[pp], c = pcnt_of(L, pp), lrp = L.plr[pp];
-      const bool replayed = L.pflag[pp] != 0;
+      const uint32_t wa = L.pa[pp], wb = L.pb[pp];  // (packed fields: WaveLds)
+      const uint32_t st = wa & 0xFFu, c = pcnt_of(L, pp), lrp = (wa >> 8) & 0xFFu;
+      const bool replayed = ((wa >> 16) & 0xFFu) != 0;
       const uint32_t off = (replayed || lrp == 0) ? st : lrp;
-      const uint32_t cnt = act ? (replayed ? (uint32_t)L.pcntf[pp] : st + c - off) : 0u;
-      const uint32_t o = act ? (uint32_t)L.pobs[pp] : NONE8;
-      const uint32_t prow = act ? (uint32_t)L.prow[pp] : NONE8;
+      const uint32_t cnt = act ? (replayed ? (wa >> 24) : st + c - off) : 0u;
+      const uint32_t o = act ? (wb & 0xFFu) : NONE8;
+      const uint32_t prow = act ? ((wb >> 8) & 0xFFu) : NONE8;
       const uint64_t rm = ballot(prow != NONE8);
       const uint32_t rix = rbase + mbcnt(rm);
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      const int64_t id = (int64_t)L.htab[L.pslot[pp]];
+      const int64_t id = (int64_t)L.htab[wb >> 24];
       // gb_sets:largest of the slab: step 5 (a decided player: its last
       // segment, strictly rising Ts, so no two elements tie) or 5b (replayed)
-      const uint32_t gb = (replayed || cnt > 1) ? (uint32_t)L.pgb[pp] - off : 0u;
+      const uint32_t gb = (replayed || cnt > 1) ? ((wb >> 16) & 0xFFu) - off : 0u;
       if (act) {
-        (a.new_s.pl_id + nmeta.p_off)[p] = id;
-        (a.new_s.pl_slab + nmeta.p_off)[p] = off | (cnt << 16);
-        if (cnt > 1) (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)gb;  // readers take 0 for cnt <= 1
-        (a.new_s.pl_info + nmeta.p_off)[p] = (o == NONE8 ? NONE16 : o - off) |
-                                             ((prow != NONE8 ? rix : NONE16) << 16);
+        ST_OUT((a.new_s.pl_id + nmeta.p_off) + (p), id);
+        ST_OUT((a.new_s.pl_slab + nmeta.p_off) + (p), off | (cnt << 16));
+        if (cnt > 1) ST_OUT((a.new_s.pl_gb + nmeta.p_off) + (p), (uint16_t)gb);  // readers take 0 for cnt <= 1
+        ST_OUT(a.new_s.pl_info + nmeta.p_off + p, (o == NONE8 ? NONE16 : o - off) |
+                                             ((prow != NONE8 ? rix : NONE16) << 16));
       }
       csum += cnt;
       nobs += (uint32_t)__builtin_popcountll(ballot(o != NONE8));
@@ -981,18 +1012,18 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t p = s * 64 + lane;
       act[s] = p < np;
       const uint32_t pp = act[s] ? p : PSINK;
-      cx[s] = act[s] && L.pflag[pp];
+      cx[s] = act[s] && PFLAG(pp);
       const uint32_t c = pcnt_of(L, pp);
-      st[s] = L.pstart[pp];
-      po[s] = act[s] ? L.pobs[pp] : NONE8;
-      cnt[s] = act[s] ? (cx[s] ? (uint32_t)L.pcntf[pp] : c) : 0u;  // simple: every add is in Masked[Id]
-      prow[s] = cx[s] ? L.prow[pp] : NONE8;
+      st[s] = PSTART(pp);
+      po[s] = act[s] ? POBS(pp) : NONE8;
+      cnt[s] = act[s] ? (cx[s] ? (uint32_t)PCNTF(pp) : c) : 0u;  // simple: every add is in Masked[Id]
+      prow[s] = cx[s] ? PROW(pp) : NONE8;
       moff[s] = cx[s] ? L.pmoff[pp] : 0u;
       uint32_t ftot;
       goff[s] = fbase + wave_excl_scan_dpp(cnt[s], ftot);
       fbase += ftot;
       opos[s] = (act[s] && !cx[s]) ? po[s] - st[s] : NONE16;
-      gbj[s] = (act[s] && !cx[s]) ? (uint32_t)L.pgb[pp] - st[s] : 0u;
+      gbj[s] = (act[s] && !cx[s]) ? (uint32_t)PGB(pp) - st[s] : 0u;
       gbd[s] = 0u;
       gbs[s] = gbt[s] = 0;
     }
@@ -1024,7 +1055,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t rix = rbase + mbcnt(rm);
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow[s] != NONE8) L.rl[rix] = (uint8_t)prow[s];
-      const int64_t id = (int64_t)L.htab[L.pslot[act[s] ? p : PSINK]];
+      const int64_t id = (int64_t)L.htab[PSLOT(act[s] ? p : PSINK)];
       if (act[s]) {
         (a.new_s.pl_id + nmeta.p_off)[p] = id;
         (a.new_s.pl_info + nmeta.p_off)[p] = (po[s] == NONE8 ? NONE16 : opos[s]) |
@@ -1069,7 +1100,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const uint32_t p = s * 64 + lane;
         const uint32_t o = po[s];
         const int64_t sc = L.esc[o != NONE8 ? o : (uint32_t)ESINK];
-        const int64_t id = (int64_t)L.htab[L.pslot[o != NONE8 ? p : (uint32_t)PSINK]];
+        const int64_t id = (int64_t)L.htab[PSLOT(o != NONE8 ? p : (uint32_t)PSINK)];
         min_cand(o != NONE8, sc, id, p);
       }
     }
