@@ -96,8 +96,9 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #ifndef TRMV_KPW
 #define TRMV_KPW 8
 #endif
-constexpr int W_KPW = TRMV_KPW;  // consecutive keys per wave chunk (a multiple of 8, <= 64)
-constexpr int W_MD = W_KPW / 8;  // metadata registers of a chunk header
+constexpr int W_KPW = TRMV_KPW;  // consecutive keys per wave chunk (1..64)
+constexpr int W_MD = (W_KPW + 7) / 8;  // metadata registers of a chunk header
+static_assert(W_KPW >= 1 && W_KPW <= 64, "TRMV_KPW: 1..64 keys per wave chunk");
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
 constexpr uint32_t NONE8 = 0xFFu;
 // Sink entries: a lane with nothing to read reads the extra entry of the
