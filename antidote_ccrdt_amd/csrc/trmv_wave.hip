@@ -152,6 +152,25 @@ struct alignas(16) WaveLds {
 #define PGB(p) L.fb((p), 2)
 #define PSLOT(p) L.fb((p), 3)
 
+// The kernel's arguments re-read from the kernarg segment at the point of use
+// (scalar loads), through a pointer the compiler cannot see through: the
+// pointers a key's later phases use are not held in SGPRs across the key
+// (where they spill to VGPR lanes and come back by v_readlane) -- TRMV_KARGS.
+typedef const __attribute__((address_space(4))) TrmvApplyArgs* KArgPtr;
+__device__ __forceinline__ KArgPtr kargs() {
+  KArgPtr p = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+#ifndef TRMV_KARGS
+#define TRMV_KARGS 1
+#endif
+#if TRMV_KARGS
+#define KA kargs()
+#else
+#define KA (&a)
+#endif
+
 __device__ __forceinline__ uint32_t whash(int64_t id) {
   const uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
   return (uint32_t)(x >> 56);  // 8 bits = W_HCAP slots
@@ -176,9 +195,9 @@ __device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, W& L, uint64_t
   r.id = id;
   r.score = sc;
   r.ts = ts;
-  a.ex[op0 + pos] = r;
+  KA->ex[op0 + pos] = r;
   if (kind == CCRDT_TRMV_RMV)
-    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
+    for (int d = 0; d < a.n_dc; ++d) KA->ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
 }
 
 // What a key needs before anything else: bounds, new-side metadata, its ops,
@@ -239,11 +258,11 @@ __device__ __forceinline__ void wave_load_key(const TrmvApplyArgs& a, const Chun
   }
   // wave-uniform bases + 32-bit lane offsets (saddr addressing, no 64-bit
   // per-lane address arithmetic)
-  const int64_t* idp = a.id + in.op0;
-  const int64_t* scp = a.score + in.op0;
-  const int64_t* tsp = a.ts + in.op0;
-  const uint8_t* kp = a.kind + in.op0;
-  const uint8_t* dp = a.dc + in.op0;
+  const int64_t* idp = KA->id + in.op0;
+  const int64_t* scp = KA->score + in.op0;
+  const int64_t* tsp = KA->ts + in.op0;
+  const uint8_t* kp = KA->kind + in.op0;
+  const uint8_t* dp = KA->dc + in.op0;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t l = s * 64 + lane;
@@ -285,7 +304,7 @@ __device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, W& L, Key
   for (int s = 0; s < W_RCAP / 8; ++s) {
     const uint32_t k = s * 8 + (lane >> 3);
     const uint32_t row = k < n ? L.rsrc[k] : 0u;
-    in.rv[s] = a.rmv_vc[(uint64_t)row * a.n_dc + d];
+    in.rv[s] = KA->rmv_vc[(uint64_t)row * a.n_dc + d];
   }
   wave_lds_sync();  // rsrc is rewritten for the next key
 }
@@ -391,7 +410,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     err |= (xr[s] && (xts[s] < 0 || xts[s] >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
   }
   if (ballot(err != 0)) {
-    if (err) atomicOr(&a.status[1], err);
+    if (err) atomicOr(&KA->status[1], err);
     return W_REJECT;  // the host rejects the batch
   }
   const uint64_t rb0 = ballot(xr[0]), rb1 = ballot(xr[1]);
@@ -452,7 +471,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (r < nrmv) L.rows[om.nr + r][d] = v;
   }
   if (ballot(err != 0)) {
-    if (err) atomicOr(&a.status[1], err);
+    if (err) atomicOr(&KA->status[1], err);
     return W_REJECT;
   }
   PROF_MARK(9);
@@ -809,9 +828,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const int64_t sc = L.esc[qq], ts = L.ets[qq];
       const uint32_t kd = L.ekd[qq];
       if (q < nops) {
-        ST_OUT((a.new_s.m_score + nmeta.m_off) + (q), sc);
-        ST_OUT((a.new_s.m_ts + nmeta.m_off) + (q), ts);
-        ST_OUT((a.new_s.m_dc + nmeta.m_off) + (q), (uint8_t)((kd >> 2) & 7u));
+        ST_OUT((KA->new_s.m_score + nmeta.m_off) + (q), sc);
+        ST_OUT((KA->new_s.m_ts + nmeta.m_off) + (q), ts);
+        ST_OUT((KA->new_s.m_dc + nmeta.m_off) + (q), (uint8_t)((kd >> 2) & 7u));
       }
     }
   }
@@ -934,9 +953,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         const uint32_t e2 = L.slab[moff + j];
         const int64_t s2 = L.esc[e2], t2 = L.ets[e2];
         const uint32_t d2 = (L.ekd[e2] >> 2) & 7u;
-        ST_OUT((a.new_s.m_score + nmeta.m_off) + (st + j), s2);
-        ST_OUT((a.new_s.m_ts + nmeta.m_off) + (st + j), t2);
-        ST_OUT((a.new_s.m_dc + nmeta.m_off) + (st + j), (uint8_t)d2);
+        ST_OUT((KA->new_s.m_score + nmeta.m_off) + (st + j), s2);
+        ST_OUT((KA->new_s.m_ts + nmeta.m_off) + (st + j), t2);
+        ST_OUT((KA->new_s.m_dc + nmeta.m_off) + (st + j), (uint8_t)d2);
         opos = e2 == o ? j : opos;
         // gb_sets:largest so far (re-read from LDS: no registers held across)
         const uint32_t eb = L.slab[moff + gj];
@@ -991,10 +1010,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       // segment, strictly rising Ts, so no two elements tie) or 5b (replayed)
       const uint32_t gb = (replayed || cnt > 1) ? ((wb >> 16) & 0xFFu) - off : 0u;
       if (act) {
-        ST_OUT((a.new_s.pl_id + nmeta.p_off) + (p), id);
-        ST_OUT((a.new_s.pl_slab + nmeta.p_off) + (p), off | (cnt << 16));
-        if (cnt > 1) ST_OUT((a.new_s.pl_gb + nmeta.p_off) + (p), (uint16_t)gb);  // readers take 0 for cnt <= 1
-        ST_OUT(a.new_s.pl_info + nmeta.p_off + p, (o == NONE8 ? NONE16 : o - off) |
+        ST_OUT((KA->new_s.pl_id + nmeta.p_off) + (p), id);
+        ST_OUT((KA->new_s.pl_slab + nmeta.p_off) + (p), off | (cnt << 16));
+        if (cnt > 1) ST_OUT((KA->new_s.pl_gb + nmeta.p_off) + (p), (uint16_t)gb);  // readers take 0 for cnt <= 1
+        ST_OUT(KA->new_s.pl_info + nmeta.p_off + p, (o == NONE8 ? NONE16 : o - off) |
                                              ((prow != NONE8 ? rix : NONE16) << 16));
       }
       csum += cnt;
@@ -1058,11 +1077,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       if (prow[s] != NONE8) L.rl[rix] = (uint8_t)prow[s];
       const int64_t id = (int64_t)L.htab[PSLOT(act[s] ? p : PSINK)];
       if (act[s]) {
-        (a.new_s.pl_id + nmeta.p_off)[p] = id;
-        (a.new_s.pl_info + nmeta.p_off)[p] = (po[s] == NONE8 ? NONE16 : opos[s]) |
+        (KA->new_s.pl_id + nmeta.p_off)[p] = id;
+        (KA->new_s.pl_info + nmeta.p_off)[p] = (po[s] == NONE8 ? NONE16 : opos[s]) |
                                              ((prow[s] != NONE8 ? rix : NONE16) << 16);
-        (a.new_s.pl_slab + nmeta.p_off)[p] = goff[s] | (cnt[s] << 16);
-        (a.new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)(cnt[s] ? gbj[s] : 0u);
+        (KA->new_s.pl_slab + nmeta.p_off)[p] = goff[s] | (cnt[s] << 16);
+        (KA->new_s.pl_gb + nmeta.p_off)[p] = (uint16_t)(cnt[s] ? gbj[s] : 0u);
       }
       nobs += (uint32_t)__builtin_popcountll(ballot(act[s] && po[s] != NONE8));
     }
@@ -1078,9 +1097,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     const int64_t sc = L.esc[e], ts = L.ets[e];
     const uint8_t dc = (uint8_t)((L.ekd[e] >> 2) & 7u);
     if (q < fbase) {
-      (a.new_s.m_score + nmeta.m_off)[q] = sc;
-      (a.new_s.m_ts + nmeta.m_off)[q] = ts;
-      (a.new_s.m_dc + nmeta.m_off)[q] = dc;
+      (KA->new_s.m_score + nmeta.m_off)[q] = sc;
+      (KA->new_s.m_ts + nmeta.m_off)[q] = ts;
+      (KA->new_s.m_dc + nmeta.m_off)[q] = dc;
     }
   }
   }  // !FRESH
@@ -1089,9 +1108,9 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   for (uint32_t r0 = 0; r0 < rbase; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
     const int64_t v = L.rows[L.rl[r < rbase ? r : 0u]][d];
-    if (r < rbase && (int)d < D) (a.new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
+    if (r < rbase && (int)d < D) (KA->new_s.r_vc + (uint64_t)nmeta.r_off * D)[r * D + d] = v;
   }
-  if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+  if (lane < D) KA->new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   PROF_MARK(11);
   // Min = min_observed(Observed) by (Score, Id) — Ids are distinct (:398-406)
   {
@@ -1122,8 +1141,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     out.nr = rbase;
     out.nobs = nobs;
     out.minq = best_q;
-    a.new_s.meta[key] = out;
-    a.ex_cnt[key] = L.nex;
+    KA->new_s.meta[key] = out;
+    KA->ex_cnt[key] = L.nex;
   }
   PROF_MARK(5);
   return W_DONE;
@@ -1157,8 +1176,8 @@ __global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_k
       const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt, has_next2, nxt2, issued);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
-          const uint32_t pos = atomicAdd(&a.status[0], 1u);
-          a.ovf_list[pos] = key;
+          const uint32_t pos = atomicAdd(&KA->status[0], 1u);
+          KA->ovf_list[pos] = key;
         }
         if (ahead2) {
           if (!issued) {
