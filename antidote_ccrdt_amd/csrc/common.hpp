@@ -153,6 +153,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan_dpp(uint32_t v, uint32_t& tot
   total = rl32(inc, 63);
   return inc - v;
 }
+// A kernel's FIRST parameter (a struct of type T, at kernarg offset 0) read
+// from the kernarg segment through a pointer the compiler cannot see
+// through, so each use is a scalar load at the point of use instead of a
+// value held in SGPRs across the kernel (where it spills to VGPR lanes and
+// returns by v_readlane).  Only in kernels whose first parameter is a T.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* kernarg_as() {
+  const __attribute__((address_space(4))) T* p =
+      (const __attribute__((address_space(4))) T*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // Orders one wavefront's LDS accesses across lanes without a workgroup
 // barrier.  The LDS executes (and returns) a wave's DS instructions in issue
 // order, so a later DS instruction of the wave sees every earlier one's

@@ -100,6 +100,12 @@ struct TrmvApplyArgs {
   uint8_t* op_pl;    // [n_ops] tier R scratch: each op's player index in its key
 };
 
+// The kernel's TrmvApplyArgs re-read at the point of use (kernarg_as,
+// common.hpp): valid in kernels whose FIRST parameter is the TrmvApplyArgs.
+__device__ __forceinline__ const __attribute__((address_space(4))) TrmvApplyArgs* trmv_kargs() {
+  return kernarg_as<TrmvApplyArgs>();
+}
+
 // New-side metadata of key k before its tier writes it.  A fresh batch's
 // segments hold exactly the key's ops (capacity = ops for players, pool and
 // rows), so their offsets are the key's op offset and the capacity scan is

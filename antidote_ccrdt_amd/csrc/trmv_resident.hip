@@ -70,6 +70,15 @@ namespace ccrdt {
 
 namespace {
 
+#ifndef TRMV_KARGS
+#define TRMV_KARGS 1
+#endif
+#if TRMV_KARGS
+#define KA trmv_kargs()  // (trmv_kernels.hpp)
+#else
+#define KA (&a)
+#endif
+
 constexpr int RP = 256;        // players per key
 constexpr int RSL = RP / 64;   // player slots per lane
 constexpr int RCH = 64;        // ops per chunk
@@ -349,9 +358,9 @@ __device__ __forceinline__ void r_emit(const TrmvApplyArgs& a, RLds& L, uint64_t
   r.id = id;
   r.score = sc;
   r.ts = ts;
-  a.ex[op0 + pos] = r;
+  KA->ex[op0 + pos] = r;
   if (vc)
-    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = pick8(*vc, (uint32_t)d);
+    for (int d = 0; d < KA->n_dc; ++d) KA->ex_vc[(op0 + pos) * KA->n_dc + d] = pick8(*vc, (uint32_t)d);
 }
 
 // P2: the player of each lane's Id; new Ids claimed and numbered np, np+1,
@@ -461,22 +470,22 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
 // it from the old side (whatever this one wrote of it is rewritten).
 __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) {
   const uint32_t lane = (uint32_t)lane_id();
-  const int D = a.n_dc;
+  const int D = KA->n_dc;
 #ifdef TRMV_PROF
   unsigned long long prof_t;
   RPROF_STAMP(prof_t);
 #endif
-  const uint64_t op0 = a.key_ptr[key];
-  const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
-  const KeyMeta nm = a.new_s.meta[key];
-  const KeyMeta om = a.old_s.meta[key];
+  const uint64_t op0 = KA->key_ptr[key];
+  const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
+  const KeyMeta nm = KA->new_s.meta[key];
+  const KeyMeta om = KA->old_s.meta[key];
   // (per-player op counts are 16-bit here)
   if (om.np > (uint32_t)RP || om.nobs > 128u || nops > 0xFFFFu) return R_NEXT;
-  const uint32_t K = a.k;
+  const uint32_t K = KA->k;
 
   for (uint32_t i = lane; i < (uint32_t)RP; i += 64) reinterpret_cast<uint32_t*>(L.u.r.hs)[i] = 0xFFFFFFFFu;
   if (lane <= (uint32_t)TRMV_DPAD)
-    L.vc[lane] = lane < (uint32_t)D ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+    L.vc[lane] = lane < (uint32_t)D ? (unsigned long long)KA->old_s.vc[(uint64_t)key * D + lane] : 0ull;
   if (lane == 0) L.nex = 0u;
   wave_lds_sync();
 
@@ -496,10 +505,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint32_t p = 64u * (2 * h + t) + lane;
       const bool v = p < om.np;
       const uint64_t pp = (uint64_t)om.p_off + (v ? p : 0u);
-      pid[2 * h + t] = v ? a.old_s.pl_id[pp] : 0;
-      info[t] = v ? a.old_s.pl_info[pp] : RNONE;
-      slab[t] = v ? a.old_s.pl_slab[pp] : 0u;
-      gb[t] = (v && (slab[t] >> 16) > 1) ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
+      pid[2 * h + t] = v ? KA->old_s.pl_id[pp] : 0;
+      info[t] = v ? KA->old_s.pl_info[pp] : RNONE;
+      slab[t] = v ? KA->old_s.pl_slab[pp] : 0u;
+      gb[t] = (v && (slab[t] >> 16) > 1) ? (uint32_t)KA->old_s.pl_gb[pp] : 0u;
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -508,12 +517,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint32_t off = slab[t] & 0xFFFFu, cnt = slab[t] >> 16, obx = info[t] & 0xFFFFu;
       const uint64_t g0 = (uint64_t)om.m_off + off;
       const bool ho = obx != NONE16, hg = cnt != 0;
-      const int64_t os = ho ? a.old_s.m_score[g0 + obx] : 0;
-      const int64_t ot = ho ? a.old_s.m_ts[g0 + obx] : 0;
-      const uint32_t od = ho ? (uint32_t)a.old_s.m_dc[g0 + obx] : 0u;
-      const int64_t gs = hg ? a.old_s.m_score[g0 + gb[t]] : 0;
-      const int64_t gt = hg ? a.old_s.m_ts[g0 + gb[t]] : 0;
-      const uint32_t gd = hg ? (uint32_t)a.old_s.m_dc[g0 + gb[t]] : 0u;
+      const int64_t os = ho ? KA->old_s.m_score[g0 + obx] : 0;
+      const int64_t ot = ho ? KA->old_s.m_ts[g0 + obx] : 0;
+      const uint32_t od = ho ? (uint32_t)KA->old_s.m_dc[g0 + obx] : 0u;
+      const int64_t gs = hg ? KA->old_s.m_score[g0 + gb[t]] : 0;
+      const int64_t gt = hg ? KA->old_s.m_ts[g0 + gb[t]] : 0;
+      const uint32_t gd = hg ? (uint32_t)KA->old_s.m_dc[g0 + gb[t]] : 0u;
       if (h == 0) {
         k01[t] = mkkey(os, pid[u]);
         t01[t] = ot;
@@ -603,7 +612,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             const uint32_t p = 64u * u + src;
             ob.key[t] = mkkey(L.msc[p], vi);  // Obs[Id]'s Score = the largest (I1)
             // Obs[Id]'s Ts from the old pool (its slab position is L.opos)
-            ob.ts[t] = a.old_s.m_ts[(uint64_t)om.m_off + (L.oslab[p] & 0xFFFFu) + L.opos[p]];
+            ob.ts[t] = KA->old_s.m_ts[(uint64_t)om.m_off + (L.oslab[p] & 0xFFFFu) + L.opos[p]];
             ob.pl[t] = p | ((uint32_t)L.odc[p] << 16);
           }
         }
@@ -620,13 +629,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
       const uint32_t l = c0 + lane;
       const bool v = l < nops;
-      const int64_t id = v ? a.id[op0 + l] : 0;
-      const uint32_t kind = v ? (uint32_t)a.kind[op0 + l] : 0u;
+      const int64_t id = v ? KA->id[op0 + l] : 0;
+      const uint32_t kind = v ? (uint32_t)KA->kind[op0 + l] : 0u;
       if (ballot(v && !fits32(id))) return R_NEXT;  // a wide Id: tier S
       uint32_t p;
       if (!r_resolve(L, id, v, np, p)) return R_NEXT;
       if (v) {
-        a.op_pl[op0 + l] = (uint8_t)p;
+        KA->op_pl[op0 + l] = (uint8_t)p;
         atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
         if (kind == 2 || kind == 3) atomicOr(&L.pf[p], Q_RMV);
       }
@@ -684,9 +693,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       int64_t nsc = 0, nts = 0;
       uint32_t ndc = 0;
       if (lane < span) {
-        nsc = a.old_s.m_score[(uint64_t)om.m_off + lane];
-        nts = a.old_s.m_ts[(uint64_t)om.m_off + lane];
-        ndc = a.old_s.m_dc[(uint64_t)om.m_off + lane];
+        nsc = KA->old_s.m_score[(uint64_t)om.m_off + lane];
+        nts = KA->old_s.m_ts[(uint64_t)om.m_off + lane];
+        ndc = KA->old_s.m_dc[(uint64_t)om.m_off + lane];
       }
       for (uint32_t q0 = 0; q0 < span; q0 += 64) {
         const uint32_t q = q0 + lane;
@@ -694,9 +703,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const uint32_t dc = ndc;
         if (q + 64 < span) {
           const uint64_t src = (uint64_t)om.m_off + q + 64;
-          nsc = a.old_s.m_score[src];
-          nts = a.old_s.m_ts[src];
-          ndc = a.old_s.m_dc[src];
+          nsc = KA->old_s.m_score[src];
+          nts = KA->old_s.m_ts[src];
+          ndc = KA->old_s.m_dc[src];
         }
         // the owner of a position is the player whose slab starts last at or
         // before it (slabs are not in player order: tier R writes players in
@@ -742,9 +751,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           if (q < off + cnt) {
             wide |= !fits32(sc);
             const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
-            a.new_s.m_score[dst] = sc;
-            a.new_s.m_ts[dst] = ts;
-            a.new_s.m_dc[dst] = (uint8_t)dc;
+            KA->new_s.m_score[dst] = sc;
+            KA->new_s.m_ts[dst] = ts;
+            KA->new_s.m_dc[dst] = (uint8_t)dc;
           }
         }
         wave_lds_sync();
@@ -754,7 +763,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
       if (r < om.nr && (int)d < D)
-        a.new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
+        KA->new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = KA->old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
     RPROF(2);
@@ -764,12 +773,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       uint32_t n = nops - c0 < (uint32_t)RCH ? nops - c0 : (uint32_t)RCH;
       bool v = lane < n;
       const uint64_t gi = op0 + c0 + lane;
-      const uint32_t kind = v ? (uint32_t)a.kind[gi] : 0u;
-      const int64_t id = v ? a.id[gi] : 0;
-      const int64_t sc = v ? a.score[gi] : 0;
-      const int64_t ts = v ? a.ts[gi] : 0;
-      const uint32_t dc = v ? (uint32_t)a.dc[gi] : 0u;
-      const uint32_t p = v ? (uint32_t)a.op_pl[gi] : (uint32_t)RP;
+      const uint32_t kind = v ? (uint32_t)KA->kind[gi] : 0u;
+      const int64_t id = v ? KA->id[gi] : 0;
+      const int64_t sc = v ? KA->score[gi] : 0;
+      const int64_t ts = v ? KA->ts[gi] : 0;
+      const uint32_t dc = v ? (uint32_t)KA->dc[gi] : 0u;
+      const uint32_t p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
       bool isr = v && (kind == 2 || kind == 3);
       uint64_t rm = ballot(isr);
       if (__builtin_popcountll(rm) > RCHR) {  // cut before the chunk's 17th rmv
@@ -785,9 +794,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
       err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
       err |= (add && ts < 1) ? TRMV_ERR_TS : 0u;
-      err |= (isr && (ts < 0 || ts >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
+      err |= (isr && (ts < 0 || ts >= KA->n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
       if (ballot(err != 0)) {
-        if (err) atomicOr(&a.status[1], err);
+        if (err) atomicOr(&KA->status[1], err);
         return R_REJECT;
       }
       if (ballot(v && (!fits32(id) || (add && !fits32(sc))))) return R_NEXT;  // wide values: tier S
@@ -797,13 +806,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
         const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
         if (r < nrm) {
-          const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
+          const int64_t x = (int)d < D ? KA->rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
           err |= x < 0 ? TRMV_ERR_VC : 0u;
           L.u.c.vtab[r][d] = x;
         }
       }
       if (ballot(err != 0)) {
-        if (err) atomicOr(&a.status[1], err);
+        if (err) atomicOr(&KA->status[1], err);
         return R_REJECT;
       }
       // Elements that may already be in Masked[Id] (:240-246): every element
@@ -867,7 +876,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       uint32_t orw = NONE16;
       if (sv && !walk && (pf0 & Q_ROWV)) {
         orw = L.prow[sp];
-        dom = a.new_s.r_vc[((uint64_t)nm.r_off + orw) * D + sdc] >= sts;
+        dom = KA->new_s.r_vc[((uint64_t)nm.r_off + orw) * D + sdc] >= sts;
       }
       const bool app = sv && !walk && !dom;
       const uint64_t nd = ballot(app);
@@ -875,14 +884,14 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const uint32_t ns = L.nslab[sp];
         const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << lane) - 1));
         const uint64_t dst = (uint64_t)nm.m_off + (ns & 0xFFFFu) + pos;
-        a.new_s.m_score[dst] = ssc;
-        a.new_s.m_ts[dst] = sts;
-        a.new_s.m_dc[dst] = (uint8_t)sdc;
+        KA->new_s.m_score[dst] = ssc;
+        KA->new_s.m_ts[dst] = sts;
+        KA->new_s.m_dc[dst] = (uint8_t)sdc;
         L.u.c.cres[so] = pos << 16;
       }
       if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
         Row8 rv = (Row8)(0);
-        for (int d = 0; d < D; ++d) rv[d] = a.new_s.r_vc[((uint64_t)nm.r_off + orw) * D + d];
+        for (int d = 0; d < D; ++d) rv[d] = KA->new_s.r_vc[((uint64_t)nm.r_off + orw) * D + d];
         L.u.c.cres[so] = R_DOM;
         r_emit(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, sid, 0, 0, 0, &rv);
       }
@@ -911,7 +920,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         Row8 R = (Row8)(0);
         const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
         if (has_row)
-          for (int d = 0; d < D; ++d) R[d] = a.new_s.r_vc[rbase + d];
+          for (int d = 0; d < D; ++d) R[d] = KA->new_s.r_vc[rbase + d];
         const int64_t wid = L.u.c.cid[ws];
         bool moved = false;
         for (uint32_t x = ws; x < we; ++x) {
@@ -928,16 +937,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             uint32_t pos = RNONE;
             if ((kd >> 5) & 1u)  // set semantics: the element may be there
               for (uint32_t j = 0; j < cnt; ++j)
-                if (a.new_s.m_ts[base + j] == ets && a.new_s.m_dc[base + j] == edc &&
-                    a.new_s.m_score[base + j] == esc) {
+                if (KA->new_s.m_ts[base + j] == ets && KA->new_s.m_dc[base + j] == edc &&
+                    KA->new_s.m_score[base + j] == esc) {
                   pos = j;
                   break;
                 }
             if (pos == RNONE) {
               pos = cnt++;
-              a.new_s.m_score[base + pos] = esc;
-              a.new_s.m_ts[base + pos] = ets;
-              a.new_s.m_dc[base + pos] = (uint8_t)edc;
+              KA->new_s.m_score[base + pos] = esc;
+              KA->new_s.m_ts[base + pos] = ets;
+              KA->new_s.m_dc[base + pos] = (uint8_t)edc;
             }
             L.u.c.cres[o] = pos << 16;
           } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
@@ -958,18 +967,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
-                s4[e] = a.new_s.m_score[base + j];
-                t4[e] = a.new_s.m_ts[base + j];
-                d4[e] = a.new_s.m_dc[base + j];
+                s4[e] = KA->new_s.m_score[base + j];
+                t4[e] = KA->new_s.m_ts[base + j];
+                d4[e] = KA->new_s.m_dc[base + j];
               }
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e;
                 if (j < cnt && t4[e] > pick8(V, d4[e])) {
                   if (w != j) {
-                    a.new_s.m_score[base + w] = s4[e];
-                    a.new_s.m_ts[base + w] = t4[e];
-                    a.new_s.m_dc[base + w] = (uint8_t)d4[e];
+                    KA->new_s.m_score[base + w] = s4[e];
+                    KA->new_s.m_ts[base + w] = t4[e];
+                    KA->new_s.m_dc[base + w] = (uint8_t)d4[e];
                   }
                   if (w == 0 || gb_gt(s4[e], d4[e], t4[e], bsc, bdc, bts)) {
                     bsc = s4[e];
@@ -990,7 +999,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         }
         L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
         if (has_row) {
-          for (int d = 0; d < D; ++d) a.new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
+          for (int d = 0; d < D; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
           f |= Q_ROWV;
         }
         if (moved) f |= Q_WALK;
@@ -1273,23 +1282,23 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const int64_t msv = L.msc[p], otv = ino ? L.u.f.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.odc[p], gd = L.gdc[p];
           for (uint32_t j = 0; j < cnt; ++j) {
-            const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
-            const uint32_t d2 = a.new_s.m_dc[base + j];
+            const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
+            const uint32_t d2 = KA->new_s.m_dc[base + j];
             if (s2 == msv && t2 == otv && d2 == od) opos = j;
             if (s2 == msv && t2 == gtv && d2 == gd) gpos = j;
           }
         }
         const uint64_t pq = (uint64_t)nm.p_off + ni;
-        a.new_s.pl_id[pq] = pid[u];
-        a.new_s.pl_slab[pq] = ns;
-        a.new_s.pl_info[pq] = (ino ? (opos & 0xFFFFu) : NONE16) | ((uint32_t)L.prow[p] << 16);
-        a.new_s.pl_gb[pq] = (uint16_t)(cnt > 1 ? gpos : 0u);
+        KA->new_s.pl_id[pq] = pid[u];
+        KA->new_s.pl_slab[pq] = ns;
+        KA->new_s.pl_info[pq] = (ino ? (opos & 0xFFFFu) : NONE16) | ((uint32_t)L.prow[p] << 16);
+        KA->new_s.pl_gb[pq] = (uint16_t)(cnt > 1 ? gpos : 0u);
         mcount += cnt;
       }
     }
     uint32_t mtotal;
     (void)wave_excl_scan_dpp(mcount, mtotal);
-    if (lane < (uint32_t)D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+    if (lane < (uint32_t)D) KA->new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
     if (lane == 0) {
       KeyMeta out = nm;
       out.np = np;
@@ -1297,8 +1306,8 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       out.nr = nr;
       out.nobs = ob.n;
       out.minq = ob.n ? 0u : NONE32;
-      a.new_s.meta[key] = out;
-      a.ex_cnt[key] = L.nex;
+      KA->new_s.meta[key] = out;
+      KA->ex_cnt[key] = L.nex;
     }
     RPROF(9);
   }

@@ -71,6 +71,15 @@ namespace ccrdt {
 
 namespace {
 
+#ifndef TRMV_KARGS
+#define TRMV_KARGS 1
+#endif
+#if TRMV_KARGS
+#define KA trmv_kargs()  // (trmv_kernels.hpp)
+#else
+#define KA (&a)
+#endif
+
 constexpr int S_CH = 64;    // ops per chunk
 constexpr int S_CHR = 16;   // rmvs per chunk (rows of the clock table)
 constexpr uint32_t S_NONE = 0xFFFFFFFFu;
@@ -264,9 +273,9 @@ __device__ __forceinline__ void s_emit(const TrmvApplyArgs& a, SLds<PCAP, RK>& L
   r.id = id;
   r.score = sc;
   r.ts = ts;
-  a.ex[op0 + pos] = r;
+  KA->ex[op0 + pos] = r;
   if (vc)
-    for (int d = 0; d < a.n_dc; ++d) a.ex_vc[(op0 + pos) * a.n_dc + d] = pick8(*vc, (uint32_t)d);
+    for (int d = 0; d < KA->n_dc; ++d) KA->ex_vc[(op0 + pos) * KA->n_dc + d] = pick8(*vc, (uint32_t)d);
 }
 
 // Player of each lane's Id (v lanes); new Ids are claimed and numbered
@@ -588,27 +597,27 @@ template <int PCAP, bool RANKED>
 __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, RANKED>& L) {
   constexpr int HS = SLds<PCAP, RANKED>::HS;
   const int lane = lane_id();
-  const int D = a.n_dc;
+  const int D = KA->n_dc;
 #ifdef TRMV_PROF
   unsigned long long prof_t;
   SPROF_STAMP(prof_t);
 #endif
-  const uint64_t op0 = a.key_ptr[key];
-  const uint32_t nops = (uint32_t)(a.key_ptr[key + 1] - op0);
+  const uint64_t op0 = KA->key_ptr[key];
+  const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
   const KeyMeta nm = trmv_new_meta(a, key);
   KeyMeta om;
-  if (a.fresh) {
+  if (KA->fresh) {
     om.p_off = om.m_off = om.r_off = 0;
     om.np = om.nm = om.nr = om.nobs = 0;
     om.minq = NONE32;
   } else {
-    om = a.old_s.meta[key];
+    om = KA->old_s.meta[key];
   }
   if (om.np > (uint32_t)PCAP) return S_NEXT;
 
   for (int i = lane; i < HS; i += 64) L.hs[i] = (typename HSlot<PCAP>::T)HSlot<PCAP>::NONE;
   if (lane <= TRMV_DPAD)
-    L.vc[lane] = (!a.fresh && lane < D) ? (unsigned long long)a.old_s.vc[(uint64_t)key * D + lane] : 0ull;
+    L.vc[lane] = (!KA->fresh && lane < D) ? (unsigned long long)KA->old_s.vc[(uint64_t)key * D + lane] : 0ull;
   if (lane == 0) {
     L.nex = 0u;
     L.nob = 0u;
@@ -633,10 +642,10 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       const uint32_t p = b0 + 64 * u + lane;
       const uint64_t pp = (uint64_t)om.p_off + (p < om.np ? p : 0u);
       const bool v = p < om.np;
-      id[u] = v ? a.old_s.pl_id[pp] : 0;
-      info[u] = v ? a.old_s.pl_info[pp] : NONE32;
-      slab[u] = v ? a.old_s.pl_slab[pp] : 0u;
-      gb[u] = (v && (slab[u] >> 16) > 1) ? (uint32_t)a.old_s.pl_gb[pp] : 0u;
+      id[u] = v ? KA->old_s.pl_id[pp] : 0;
+      info[u] = v ? KA->old_s.pl_info[pp] : NONE32;
+      slab[u] = v ? KA->old_s.pl_slab[pp] : 0u;
+      gb[u] = (v && (slab[u] >> 16) > 1) ? (uint32_t)KA->old_s.pl_gb[pp] : 0u;
     }
     int64_t os[4], ot[4], gs[4], gt[4];
     uint32_t od[4], gd[4];
@@ -645,12 +654,12 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
       const uint64_t g0 = (uint64_t)om.m_off + off;
       const bool ho = obx != NONE16, hg = cnt != 0;
-      os[u] = ho ? a.old_s.m_score[g0 + obx] : 0;
-      ot[u] = ho ? a.old_s.m_ts[g0 + obx] : 0;
-      od[u] = ho ? (uint32_t)a.old_s.m_dc[g0 + obx] : 0u;
-      gs[u] = hg ? a.old_s.m_score[g0 + gb[u]] : 0;
-      gt[u] = hg ? a.old_s.m_ts[g0 + gb[u]] : 0;
-      gd[u] = hg ? (uint32_t)a.old_s.m_dc[g0 + gb[u]] : 0u;
+      os[u] = ho ? KA->old_s.m_score[g0 + obx] : 0;
+      ot[u] = ho ? KA->old_s.m_ts[g0 + obx] : 0;
+      od[u] = ho ? (uint32_t)KA->old_s.m_dc[g0 + obx] : 0u;
+      gs[u] = hg ? KA->old_s.m_score[g0 + gb[u]] : 0;
+      gt[u] = hg ? KA->old_s.m_ts[g0 + gb[u]] : 0;
+      gd[u] = hg ? (uint32_t)KA->old_s.m_dc[g0 + gb[u]] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -693,8 +702,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
     const uint32_t l = c0 + lane;
     const bool v = l < nops;
-    const int64_t id = v ? a.id[op0 + l] : 0;
-    const uint32_t kind = v ? (uint32_t)a.kind[op0 + l] : 0u;
+    const int64_t id = v ? KA->id[op0 + l] : 0;
+    const uint32_t kind = v ? (uint32_t)KA->kind[op0 + l] : 0u;
     uint32_t p;
     if (!s_resolve<PCAP, RANKED>(L, id, v, np, p)) return S_NEXT;
     if (v) {
@@ -726,15 +735,15 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   SPROF(1);
 
   // ---- K3. old slabs (except replayed players') and old Removals rows
-  if (!a.fresh && span) {
+  if (!KA->fresh && span) {
     int32_t prev = -1;  // owner of the position before the window
     // the next window's elements load while this one is placed
     int64_t nsc = 0, nts = 0;
     uint32_t ndc = 0;
     if ((uint32_t)lane < span) {
-      nsc = a.old_s.m_score[(uint64_t)om.m_off + lane];
-      nts = a.old_s.m_ts[(uint64_t)om.m_off + lane];
-      ndc = a.old_s.m_dc[(uint64_t)om.m_off + lane];
+      nsc = KA->old_s.m_score[(uint64_t)om.m_off + lane];
+      nts = KA->old_s.m_ts[(uint64_t)om.m_off + lane];
+      ndc = KA->old_s.m_dc[(uint64_t)om.m_off + lane];
     }
     for (uint32_t q0 = 0; q0 < span; q0 += 64) {
       const uint32_t q = q0 + lane;
@@ -742,9 +751,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       const uint32_t dc = ndc;
       if (q + 64 < span) {
         const uint64_t src = (uint64_t)om.m_off + q + 64;
-        nsc = a.old_s.m_score[src];
-        nts = a.old_s.m_ts[src];
-        ndc = a.old_s.m_dc[src];
+        nsc = KA->old_s.m_score[src];
+        nts = KA->old_s.m_ts[src];
+        ndc = KA->old_s.m_dc[src];
       }
       // The owner of a position is the player whose slab starts last at or
       // before it.  Slabs are not in player order (tier R writes players in
@@ -768,9 +777,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
         if (q < off + cnt && !(L.opd[o] & F_RMV)) {
           const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
-          a.new_s.m_score[dst] = sc;
-          a.new_s.m_ts[dst] = ts;
-          a.new_s.m_dc[dst] = (uint8_t)dc;
+          KA->new_s.m_score[dst] = sc;
+          KA->new_s.m_ts[dst] = ts;
+          KA->new_s.m_dc[dst] = (uint8_t)dc;
         }
       }
       lsync(L);
@@ -779,14 +788,14 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
     const uint32_t r = r0 + (lane >> 3), d = lane & 7;
     if (r < om.nr && (int)d < D)
-      a.new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = a.old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
+      KA->new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = KA->old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
   }
   // the replays read rows written here: retire the stores first
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   SPROF(2);
 
   // ---- K4. chunks of the key's ops
-  const uint32_t K = a.k;
+  const uint32_t K = KA->k;
   SMin mn;  // !RANKED: Min and |Observed|
   uint32_t nobs = om.nobs;
   ObsTab ob;  // RANKED: Observed in registers
@@ -849,11 +858,11 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     uint32_t n = nops - c0 < (uint32_t)S_CH ? nops - c0 : (uint32_t)S_CH;
     bool v = (uint32_t)lane < n;
     const uint64_t gi = op0 + c0 + lane;
-    const uint32_t kind = v ? (uint32_t)a.kind[gi] : 0u;
-    const int64_t id = v ? a.id[gi] : 0;
-    const int64_t sc = v ? a.score[gi] : 0;
-    const int64_t ts = v ? a.ts[gi] : 0;
-    const uint32_t dc = v ? (uint32_t)a.dc[gi] : 0u;
+    const uint32_t kind = v ? (uint32_t)KA->kind[gi] : 0u;
+    const int64_t id = v ? KA->id[gi] : 0;
+    const int64_t sc = v ? KA->score[gi] : 0;
+    const int64_t ts = v ? KA->ts[gi] : 0;
+    const uint32_t dc = v ? (uint32_t)KA->dc[gi] : 0u;
     bool isr = v && (kind == 2 || kind == 3);
     uint64_t rm = ballot(isr);
     if (__builtin_popcountll(rm) > S_CHR) {  // cut before the chunk's 17th rmv
@@ -869,9 +878,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
     err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
     err |= (add && ts < 1) ? TRMV_ERR_TS : 0u;
-    err |= (isr && (ts < 0 || ts >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
+    err |= (isr && (ts < 0 || ts >= KA->n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
     if (ballot(err != 0)) {
-      if (err) atomicOr(&a.status[1], err);
+      if (err) atomicOr(&KA->status[1], err);
       return S_REJECT;
     }
     const uint32_t p = s_lookup<PCAP, RANKED>(L, id, v);
@@ -882,13 +891,13 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7;
       if (r < nrm) {
-        const int64_t x = (int)d < D ? a.rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
+        const int64_t x = (int)d < D ? KA->rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
         err |= x < 0 ? TRMV_ERR_VC : 0u;
         L.u.c.vtab[r][d] = x;
       }
     }
     if (ballot(err != 0)) {
-      if (err) atomicOr(&a.status[1], err);
+      if (err) atomicOr(&KA->status[1], err);
       return S_REJECT;
     }
     SPROF(3);
@@ -954,7 +963,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     uint32_t orw = NONE16;
     if (sv && !walk && (pf & F_ROWV)) {
       orw = L.orow[sp] >> 16;
-      dom = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + sdc] >= sts;
+      dom = KA->old_s.r_vc[((uint64_t)om.r_off + orw) * D + sdc] >= sts;
     }
     const bool app = sv && !walk && !dom;
     const uint64_t nd = ballot(app);
@@ -962,14 +971,14 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       const uint32_t ns = L.nslab[sp];
       const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << lane) - 1));
       const uint64_t dst = (uint64_t)nm.m_off + (ns & 0xFFFFu) + pos;
-      a.new_s.m_score[dst] = ssc;
-      a.new_s.m_ts[dst] = sts;
-      a.new_s.m_dc[dst] = (uint8_t)sdc;
+      KA->new_s.m_score[dst] = ssc;
+      KA->new_s.m_ts[dst] = sts;
+      KA->new_s.m_dc[dst] = (uint8_t)sdc;
       L.u.c.cres[so] = pos << 16;
     }
     if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
       Row8 rv = (Row8)(0);
-      for (int d = 0; d < D; ++d) rv[d] = a.old_s.r_vc[((uint64_t)om.r_off + orw) * D + d];
+      for (int d = 0; d < D; ++d) rv[d] = KA->old_s.r_vc[((uint64_t)om.r_off + orw) * D + d];
       L.u.c.cres[so] = R_DOM;
       s_emit<PCAP, RANKED>(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, L.pid[sp], 0, 0, 0, &rv);
     }
@@ -999,9 +1008,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         const uint32_t os = L.oslab[wp];
         const uint64_t g0 = (uint64_t)om.m_off + (os & 0xFFFFu);
         for (uint32_t j = 0; j < (os >> 16); ++j) {
-          a.new_s.m_score[base + j] = a.old_s.m_score[g0 + j];
-          a.new_s.m_ts[base + j] = a.old_s.m_ts[g0 + j];
-          a.new_s.m_dc[base + j] = a.old_s.m_dc[g0 + j];
+          KA->new_s.m_score[base + j] = KA->old_s.m_score[g0 + j];
+          KA->new_s.m_ts[base + j] = KA->old_s.m_ts[g0 + j];
+          KA->new_s.m_dc[base + j] = KA->old_s.m_dc[g0 + j];
         }
         f |= F_MAT;
       }
@@ -1009,7 +1018,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       Row8 R = (Row8)(0);
       const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
       if (has_row)
-        for (int d = 0; d < D; ++d) R[d] = a.new_s.r_vc[rbase + d];
+        for (int d = 0; d < D; ++d) R[d] = KA->new_s.r_vc[rbase + d];
       const int64_t wid = L.pid[wp];
       bool moved = false;
       for (uint32_t x = ws; x < we; ++x) {
@@ -1026,16 +1035,16 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
           uint32_t pos = S_NONE;
           if ((kd >> 5) & 1u)  // set semantics: the element may be there
             for (uint32_t j = 0; j < cnt; ++j)
-              if (a.new_s.m_ts[base + j] == ets && a.new_s.m_dc[base + j] == edc &&
-                  a.new_s.m_score[base + j] == esc) {
+              if (KA->new_s.m_ts[base + j] == ets && KA->new_s.m_dc[base + j] == edc &&
+                  KA->new_s.m_score[base + j] == esc) {
                 pos = j;
                 break;
               }
           if (pos == S_NONE) {
             pos = cnt++;
-            a.new_s.m_score[base + pos] = esc;
-            a.new_s.m_ts[base + pos] = ets;
-            a.new_s.m_dc[base + pos] = (uint8_t)edc;
+            KA->new_s.m_score[base + pos] = esc;
+            KA->new_s.m_ts[base + pos] = ets;
+            KA->new_s.m_dc[base + pos] = (uint8_t)edc;
           }
           L.u.c.cres[o] = pos << 16;
         } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
@@ -1049,13 +1058,13 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
           uint32_t w = 0, bpos = 0, bdc = 0;
           int64_t bsc = 0, bts = 0;
           for (uint32_t j = 0; j < cnt; ++j) {
-            const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
-            const uint32_t d2 = a.new_s.m_dc[base + j];
+            const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
+            const uint32_t d2 = KA->new_s.m_dc[base + j];
             if (t2 > pick8(V, d2)) {
               if (w != j) {
-                a.new_s.m_score[base + w] = s2;
-                a.new_s.m_ts[base + w] = t2;
-                a.new_s.m_dc[base + w] = (uint8_t)d2;
+                KA->new_s.m_score[base + w] = s2;
+                KA->new_s.m_ts[base + w] = t2;
+                KA->new_s.m_dc[base + w] = (uint8_t)d2;
               }
               if (w == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
                 bsc = s2;
@@ -1075,7 +1084,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
       }
       L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
       if (has_row) {
-        for (int d = 0; d < D; ++d) a.new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
+        for (int d = 0; d < D; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
         f |= F_ROWV;
       }
       if (moved) f |= F_WALK;
@@ -1350,8 +1359,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         uint32_t opos = NONE16, bpos = 0, bdc = 0;
         int64_t bsc = 0, bts = 0;
         for (uint32_t j = 0; j < cnt; ++j) {
-          const int64_t s2 = a.new_s.m_score[base + j], t2 = a.new_s.m_ts[base + j];
-          const uint32_t d2 = a.new_s.m_dc[base + j];
+          const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
+          const uint32_t d2 = KA->new_s.m_dc[base + j];
           if (s2 == os && t2 == ot && d2 == od) opos = j;
           if (j == 0 || gb_gt(s2, d2, t2, bsc, bdc, bts)) {
             bsc = s2;
@@ -1364,16 +1373,16 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
         g = (bdc << 8) | (bpos << 16);
       }
       const uint64_t pp = (uint64_t)nm.p_off + p;
-      a.new_s.pl_id[pp] = L.pid[p];
-      a.new_s.pl_slab[pp] = ns;
-      a.new_s.pl_info[pp] = ((f & F_OBS) ? (f >> 16) : NONE16) | (L.orow[p] & 0xFFFF0000u);
-      a.new_s.pl_gb[pp] = (uint16_t)(cnt ? (g >> 16) : 0u);
+      KA->new_s.pl_id[pp] = L.pid[p];
+      KA->new_s.pl_slab[pp] = ns;
+      KA->new_s.pl_info[pp] = ((f & F_OBS) ? (f >> 16) : NONE16) | (L.orow[p] & 0xFFFF0000u);
+      KA->new_s.pl_gb[pp] = (uint16_t)(cnt ? (g >> 16) : 0u);
       mcount += cnt;
     }
   }
   uint32_t mtotal;
   (void)wave_excl_scan_dpp(mcount, mtotal);
-  if (lane < D) a.new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
+  if (lane < D) KA->new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
   if (lane == 0) {
     KeyMeta out = nm;
     out.np = np;
@@ -1381,8 +1390,8 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     out.nr = nr;
     out.nobs = nobs;
     out.minq = mn.p;
-    a.new_s.meta[key] = out;
-    a.ex_cnt[key] = L.nex;
+    KA->new_s.meta[key] = out;
+    KA->ex_cnt[key] = L.nex;
   }
   SPROF(8);
   return S_DONE;

@@ -152,21 +152,11 @@ struct alignas(16) WaveLds {
 #define PGB(p) L.fb((p), 2)
 #define PSLOT(p) L.fb((p), 3)
 
-// The kernel's arguments re-read from the kernarg segment at the point of use
-// (scalar loads), through a pointer the compiler cannot see through: the
-// pointers a key's later phases use are not held in SGPRs across the key
-// (where they spill to VGPR lanes and come back by v_readlane) -- TRMV_KARGS.
-typedef const __attribute__((address_space(4))) TrmvApplyArgs* KArgPtr;
-__device__ __forceinline__ KArgPtr kargs() {
-  KArgPtr p = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
-}
 #ifndef TRMV_KARGS
 #define TRMV_KARGS 1
 #endif
 #if TRMV_KARGS
-#define KA kargs()
+#define KA trmv_kargs()
 #else
 #define KA (&a)
 #endif
@@ -197,7 +187,7 @@ __device__ __forceinline__ void wave_emit(const TrmvApplyArgs& a, W& L, uint64_t
   r.ts = ts;
   KA->ex[op0 + pos] = r;
   if (kind == CCRDT_TRMV_RMV)
-    for (int d = 0; d < a.n_dc; ++d) KA->ex_vc[(op0 + pos) * a.n_dc + d] = L.rows[row][d];
+    for (int d = 0; d < KA->n_dc; ++d) KA->ex_vc[(op0 + pos) * KA->n_dc + d] = L.rows[row][d];
 }
 
 // What a key needs before anything else: bounds, new-side metadata, its ops,
@@ -225,17 +215,17 @@ __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t
                                                 ChunkHdr& h) {
   const int lane = lane_id();
   const uint32_t j = (uint32_t)lane < n ? (uint32_t)lane : 0u;
-  h.key = a.key_list ? a.key_list[c0 + j] : c0 + j;
-  h.lo = a.key_ptr[h.key];
-  h.hi = a.key_ptr[h.key + 1];
+  h.key = KA->key_list ? KA->key_list[c0 + j] : c0 + j;
+  h.lo = KA->key_ptr[h.key];
+  h.hi = KA->key_ptr[h.key + 1];
 #pragma unroll
   for (int i = 0; i < W_MD; ++i) {
     const uint32_t m = 8 * i + (lane >> 3);
     const uint32_t jm = m < n ? m : 0u;
-    const uint32_t km = a.key_list ? a.key_list[c0 + jm] : c0 + jm;
-    if (a.fresh) {  // trmv_new_meta: offsets = the key's op offset, counts 0, Min nil
+    const uint32_t km = KA->key_list ? KA->key_list[c0 + jm] : c0 + jm;
+    if (KA->fresh) {  // trmv_new_meta: offsets = the key's op offset, counts 0, Min nil
       const uint32_t d = lane & 7;
-      h.meta[i] = d < 3 ? (uint32_t)a.key_ptr[km] : (d == 7 ? NONE32 : 0u);
+      h.meta[i] = d < 3 ? (uint32_t)KA->key_ptr[km] : (d == 7 ? NONE32 : 0u);
     } else {
       h.meta[i] = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
     }
@@ -291,20 +281,20 @@ __device__ __forceinline__ void wave_load_rows(const TrmvApplyArgs& a, W& L, Key
   const uint64_t b0 = ballot(r[0]), b1 = ballot(r[1]);
   const uint32_t n0 = (uint32_t)__builtin_popcountll(b0);
   const uint32_t n = n0 + (uint32_t)__builtin_popcountll(b1);
-  if (n == 0 || a.n_rmv_rows <= 0) return;
+  if (n == 0 || KA->n_rmv_rows <= 0) return;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const uint32_t k = s ? n0 + mbcnt(b1) : mbcnt(b0);
     if (r[s] && k < (uint32_t)W_RCAP)
-      L.rsrc[k] = (in.ts[s] >= 0 && in.ts[s] < a.n_rmv_rows) ? (uint32_t)in.ts[s] : 0u;
+      L.rsrc[k] = (in.ts[s] >= 0 && in.ts[s] < KA->n_rmv_rows) ? (uint32_t)in.ts[s] : 0u;
   }
   wave_lds_sync();
-  const uint32_t d = (lane & 7) < a.n_dc ? (lane & 7) : 0u;
+  const uint32_t d = (lane & 7) < KA->n_dc ? (lane & 7) : 0u;
 #pragma unroll
   for (int s = 0; s < W_RCAP / 8; ++s) {
     const uint32_t k = s * 8 + (lane >> 3);
     const uint32_t row = k < n ? L.rsrc[k] : 0u;
-    in.rv[s] = KA->rmv_vc[(uint64_t)row * a.n_dc + d];
+    in.rv[s] = KA->rmv_vc[(uint64_t)row * KA->n_dc + d];
   }
   wave_lds_sync();  // rsrc is rewritten for the next key
 }
@@ -323,7 +313,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // (and spill) across every key
   int lane = lane_id();
   asm volatile("" : "+v"(lane));
-  const int D = a.n_dc;
+  const int D = KA->n_dc;
 #ifdef TRMV_PROF
   unsigned long long prof_t;
   PROF_STAMP(prof_t);
@@ -344,7 +334,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   } else {
     om = a.old_s.meta[key];
   }
-  const uint32_t pmax = a.k < (uint32_t)W_PCAP ? a.k : (uint32_t)W_PCAP;
+  const uint32_t pmax = KA->k < (uint32_t)W_PCAP ? KA->k : (uint32_t)W_PCAP;
   if (nops > (uint32_t)W_ECAP || om.np > pmax || om.nm + nops > (uint32_t)W_ECAP ||
       om.nr > (uint32_t)W_RCAP)
     return W_NEXT_TIER;
@@ -407,7 +397,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     err |= (xv[s] && xkind[s] > 3) ? TRMV_ERR_KIND : 0u;
     err |= (xa[s] && (int)xdc[s] >= D) ? TRMV_ERR_DC : 0u;
     err |= (xa[s] && xts[s] < 1) ? TRMV_ERR_TS : 0u;
-    err |= (xr[s] && (xts[s] < 0 || xts[s] >= a.n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
+    err |= (xr[s] && (xts[s] < 0 || xts[s] >= KA->n_rmv_rows)) ? TRMV_ERR_ROW : 0u;
   }
   if (ballot(err != 0)) {
     if (err) atomicOr(&KA->status[1], err);
