@@ -166,27 +166,29 @@ __device__ __forceinline__ uint32_t rhash(int64_t id) {
   return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> (64 - 9));  // 512 slots
 }
 
+// One key's LDS: 10,064 bytes (16 per CU).  Ids and Scores are 32-bit in
+// this class; Obs[Id]'s DcId lives in the sorted Observed array (Obs.pl).
 struct alignas(16) RLds {
   int64_t gts[RP];     // gb_sets:largest(Masked[Id]): Ts
   int32_t msc[RP];     // largest Score of Masked[Id] (= Obs[Id]'s Score in Observed, or below it mid-run)
-  uint32_t pf[RP];     // flags
-  uint32_t oslab[RP];  // old slab: offset | count << 16
   uint32_t nslab[RP];  // new slab: offset | current count << 16
   uint16_t prow[RP];   // Removals row (new side), NONE16
   uint16_t opos[RP];   // Obs[Id]'s position in the new slab
   uint16_t gpos[RP];   // the largest's position in the new slab
-  uint8_t odc[RP];     // Obs[Id]: DcId
+  uint8_t pf[RP];      // flags (atomics: pf_or / pf_and on the containing word)
   uint8_t gdc[RP];     // the largest: DcId
   union {
-    struct {  // P1 / P2
+    struct {  // P1 / P2 (P3: hs..nops hold the start map; oslab stays)
       uint16_t hs[2 * RP];
-      int64_t pid[RP];
-      int64_t claim[64];
+      int32_t pid[RP];
+      int32_t claim[64];
       uint16_t nops[RP];
+      uint32_t oslab[RP];  // old slab: offset | count << 16
     } r;
     struct {  // chunks
-      int64_t csc[RCH], cts[RCH];
-      int64_t cid[RCH];    // Ids, (player, stream) order
+      int32_t csc[RCH];
+      int64_t cts[RCH];
+      int32_t cid[RCH];    // Ids, (player, stream) order
       uint32_t ckd[RCH];   // kind | dc << 2 | dup candidate << 5 | player << 8
       uint32_t cres[RCH];  // add: R_DOM | slab position << 16; rmv: its rank in the chunk
       int64_t vtab[RCHR][TRMV_DPAD];
@@ -195,16 +197,23 @@ struct alignas(16) RLds {
       uint32_t rgd[RCHR];            // non-empty | dc << 8 | position << 16
       uint16_t cwp[RCH];
       uint8_t cws[RCH], cwe[RCH], csrt[RCH];
-      uint32_t mark[RCH];
     } c;
     struct {  // P5
       int64_t ots[RP];    // Obs[Id]'s Ts by player
       uint16_t nidx[RP];  // a player's index in the new record order
+      uint8_t odc[RP];    // Obs[Id]'s DcId by player
     } f;
   } u;
   unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
   uint32_t nex;
 };
+
+__device__ __forceinline__ void pf_or(RLds& L, uint32_t p, uint32_t m) {
+  atomicOr(reinterpret_cast<uint32_t*>(&L.pf[p & ~3u]), m << (8u * (p & 3u)));
+}
+__device__ __forceinline__ void pf_and(RLds& L, uint32_t p, uint32_t m) {  // clears m
+  atomicAnd(reinterpret_cast<uint32_t*>(&L.pf[p & ~3u]), ~(m << (8u * (p & 3u))));
+}
 
 // --------------------------------------------------- the sorted Observed
 // Entry r = lane r % 64 of slot r / 64, ascending by key = (Score, Id);
@@ -363,6 +372,22 @@ __device__ __forceinline__ void r_emit(const TrmvApplyArgs& a, RLds& L, uint64_t
     for (int d = 0; d < KA->n_dc; ++d) KA->ex_vc[(op0 + pos) * KA->n_dc + d] = pick8(*vc, (uint32_t)d);
 }
 
+// A dominated add's {rmv, {Id, Removals[Id]}} with the row read from memory.
+__device__ __forceinline__ void r_emit_row(const TrmvApplyArgs& a, RLds& L, uint64_t op0, uint64_t op, int64_t id,
+                                           const int64_t* row) {
+  const uint32_t pos = atomicAdd(&L.nex, 1u);
+  TrmvExtraRec r;
+  r.op = (uint32_t)op;
+  r.kind = CCRDT_TRMV_RMV;
+  r.dc = 0;
+  r.pad = 0;
+  r.id = id;
+  r.score = 0;
+  r.ts = 0;
+  KA->ex[op0 + pos] = r;
+  for (int d = 0; d < KA->n_dc; ++d) KA->ex_vc[(op0 + pos) * KA->n_dc + d] = row[d];
+}
+
 // P2: the player of each lane's Id; new Ids claimed and numbered np, np+1,
 // ... in lane order.  False if the key outgrows RP players.
 __device__ __forceinline__ bool r_resolve(RLds& L, int64_t id, bool v, uint32_t& np, uint32_t& p) {
@@ -419,14 +444,13 @@ __device__ __forceinline__ bool r_resolve(RLds& L, int64_t id, bool v, uint32_t&
     L.u.r.pid[p] = id;
     L.u.r.hs[h] = (uint16_t)p;
     L.u.r.nops[p] = 0;
-    L.oslab[p] = 0u;
+    L.u.r.oslab[p] = 0u;
     L.prow[p] = (uint16_t)NONE16;
     L.pf[p] = 0u;
     L.msc[p] = 0;
     L.gts[p] = 0;
     L.opos[p] = (uint16_t)NONE16;
     L.gpos[p] = 0;
-    L.odc[p] = 0;
     L.gdc[p] = 0;
   }
   const uint32_t fp = shfl32(p, follow >= 0 ? follow : lane);
@@ -496,6 +520,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
   int64_t pid[RSL];
   uint32_t span = 0, inobs = 0;  // inobs: bit u = player of slot u in Observed
   int64_t k01[2], t01[2];        // slots 0-1: Obs[Id]'s key and Ts
+  uint32_t odr[RSL];             // Obs[Id]'s DcId by slot
   bool wide = false;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -527,16 +552,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         k01[t] = mkkey(os, pid[u]);
         t01[t] = ot;
       }
+      odr[u] = od;
       if (p < om.np) {
         wide |= !fits32(pid[u]) || !fits32(os) || !fits32(gs);
         L.msc[p] = (int32_t)gs;
         L.gts[p] = gt;
         L.pf[p] = (ho ? Q_OBS : 0u) | (cnt ? Q_HASM : 0u) | ((info[t] >> 16) != NONE16 ? Q_ROWV : 0u);
-        L.odc[p] = (uint8_t)od;
         L.gdc[p] = (uint8_t)gd;
         L.opos[p] = (uint16_t)obx;
         L.gpos[p] = (uint16_t)gb[t];
-        L.oslab[p] = slab[t];
+        L.u.r.oslab[p] = slab[t];
         L.prow[p] = (uint16_t)(info[t] >> 16);
         L.u.r.pid[p] = pid[u];
         L.u.r.nops[p] = 0;
@@ -584,7 +609,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       for (int t = 0; t < 2; ++t) {
         ob.key[t] = k01[t];
         ob.ts[t] = t01[t];
-        ob.pl[t] = (64u * t + lane) | ((uint32_t)L.odc[64u * t + lane] << 16);
+        ob.pl[t] = (64u * t + lane) | (odr[t] << 16);
       }
     } else {
       // the r-th Observed player in player order is pulled by entry r; then sort
@@ -608,12 +633,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const bool here = r >= base[u] && r < base[u + 1];
           const uint32_t src = here ? kth_bit(mk[u], r - base[u]) : lane;
           const int64_t vi = shfl64(pid[u], (int)src);
+          const uint32_t vd = shfl32(odr[u], (int)src);
           if (here) {
             const uint32_t p = 64u * u + src;
             ob.key[t] = mkkey(L.msc[p], vi);  // Obs[Id]'s Score = the largest (I1)
             // Obs[Id]'s Ts from the old pool (its slab position is L.opos)
-            ob.ts[t] = KA->old_s.m_ts[(uint64_t)om.m_off + (L.oslab[p] & 0xFFFFu) + L.opos[p]];
-            ob.pl[t] = p | ((uint32_t)L.odc[p] << 16);
+            ob.ts[t] = KA->old_s.m_ts[(uint64_t)om.m_off + (L.u.r.oslab[p] & 0xFFFFu) + L.opos[p]];
+            ob.pl[t] = p | (vd << 16);
           }
         }
       }
@@ -637,7 +663,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       if (v) {
         KA->op_pl[op0 + l] = (uint8_t)p;
         atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
-        if (kind == 2 || kind == 3) atomicOr(&L.pf[p], Q_RMV);
+        if (kind == 2 || kind == 3) pf_or(L, p, Q_RMV);
       }
     }
     wave_lds_sync();
@@ -659,7 +685,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint64_t m = ballot(newrow);
       if (newrow) L.prow[p] = (uint16_t)(nr + mbcnt(m));
       nr += (uint32_t)__builtin_popcountll(m);
-      const uint32_t ocnt = act ? (L.oslab[q] >> 16) : 0u;
+      const uint32_t ocnt = act ? (L.u.r.oslab[q] >> 16) : 0u;
       const uint32_t cap = act ? ocnt + L.u.r.nops[q] : 0u;
       uint32_t tot;
       const uint32_t ex = wave_excl_scan_dpp(cap, tot);
@@ -673,7 +699,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     // ---- P3. old slabs and old Removals rows -> the new side
     // (start map: u16 per pool position of the span, player + 1 at each slab
     // start, in the P1/P2 union, which is free from here on)
-    constexpr uint32_t SMAP = (uint32_t)(sizeof(L.u.r) / 2);
+    constexpr uint32_t SMAP = (uint32_t)(offsetof(decltype(L.u.r), oslab) / 2);  // oslab stays
     uint16_t* smap16 = reinterpret_cast<uint16_t*>(&L.u.r);
     const bool smap = span <= SMAP;
     if (span && smap) {
@@ -682,7 +708,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #pragma unroll
       for (int u = 0; u < RSL; ++u) {
         const uint32_t p = 64u * u + lane;
-        const uint32_t sl = p < om.np ? L.oslab[p] : 0u;
+        const uint32_t sl = p < om.np ? L.u.r.oslab[p] : 0u;
         if (sl >> 16) smap16[sl & 0xFFFFu] = (uint16_t)(p + 1);
       }
       wave_lds_sync();
@@ -715,16 +741,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (smap) {
           st = q < span ? (uint32_t)smap16[q] : 0u;
         } else {
-          L.u.c.mark[lane] = 0u;
+          uint32_t* const mark = reinterpret_cast<uint32_t*>(smap16);  // (the map is unused here)
+          mark[lane] = 0u;
           wave_lds_sync();
           for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
             const uint32_t j = j0 + lane;
-            const uint32_t sl = j < om.np ? L.oslab[j] : 0u;
+            const uint32_t sl = j < om.np ? L.u.r.oslab[j] : 0u;
             const uint32_t off = sl & 0xFFFFu;
-            if ((sl >> 16) && off >= q0 && off < q0 + 64) L.u.c.mark[off - q0] = j + 1;
+            if ((sl >> 16) && off >= q0 && off < q0 + 64) mark[off - q0] = j + 1;
           }
           wave_lds_sync();
-          st = L.u.c.mark[lane];
+          st = mark[lane];
         }
         uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
         {  // inclusive max-scan (DPP): the last start at or before the lane
@@ -746,7 +773,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const int32_t o = own ? (int32_t)own - 1 : prev;
         prev = (int32_t)rl32((uint32_t)o, 63);
         if (q < span && o >= 0) {
-          const uint32_t sl = L.oslab[o];
+          const uint32_t sl = L.u.r.oslab[o];
           const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
           if (q < off + cnt) {
             wide |= !fits32(sc);
@@ -842,7 +869,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       }
       wave_lds_sync();
       if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
-      if (dupc) atomicOr(&L.pf[p], Q_DUP);
+      if (dupc) pf_or(L, p, Q_DUP);
       L.u.c.csc[lane] = sc;
       L.u.c.cts[lane] = ts;
       L.u.c.ckd[lane] = v ? (kind | (dc << 2) | ((dupc ? 1u : 0u) << 5) | (p << 8)) : ((uint32_t)RP << 8);
@@ -890,10 +917,8 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         L.u.c.cres[so] = pos << 16;
       }
       if (dom) {  // {rmv, {Id, Removals[Id]}} (:236-237)
-        Row8 rv = (Row8)(0);
-        for (int d = 0; d < D; ++d) rv[d] = KA->new_s.r_vc[((uint64_t)nm.r_off + orw) * D + d];
         L.u.c.cres[so] = R_DOM;
-        r_emit(a, L, op0, op0 + c0 + so, CCRDT_TRMV_RMV, sid, 0, 0, 0, &rv);
+        r_emit_row(a, L, op0, op0 + c0 + so, sid, KA->new_s.r_vc + ((uint64_t)nm.r_off + orw) * D);
       }
       wave_lds_sync();
       if (sv && !walk && lane + 1 == shi) {
@@ -951,11 +976,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             L.u.c.cres[o] = pos << 16;
           } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
             const uint32_t r = L.u.c.cres[o];
-            Row8 V;
+            const int64_t* V = L.u.c.vtab[r];  // (read from LDS where used: no second row in registers)
 #pragma unroll
-            for (int d = 0; d < TRMV_DPAD; ++d) V[d] = L.u.c.vtab[r][d];
-#pragma unroll
-            for (int d = 0; d < TRMV_DPAD; ++d) R[d] = has_row ? (V[d] > R[d] ? V[d] : R[d]) : V[d];
+            for (int d = 0; d < TRMV_DPAD; ++d) {
+              const int64_t v = V[d];
+              R[d] = has_row ? (v > R[d] ? v : R[d]) : v;
+            }
             has_row = true;
             uint32_t w = 0, bpos = 0, bdc = 0;
             int64_t bsc = 0, bts = 0;
@@ -974,7 +1000,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e;
-                if (j < cnt && t4[e] > pick8(V, d4[e])) {
+                if (j < cnt && t4[e] > V[d4[e]]) {
                   if (w != j) {
                     KA->new_s.m_score[base + w] = s4[e];
                     KA->new_s.m_ts[base + w] = t4[e];
@@ -1093,7 +1119,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             L.gts[cu_p] = cu_t;
             L.gdc[cu_p] = (uint8_t)cu_d;
             L.gpos[cu_p] = (uint16_t)cu_pos;
-            if (!(f & Q_HASM)) atomicOr(&L.pf[cu_p], Q_HASM);
+            if (!(f & Q_HASM)) pf_or(L, cu_p, Q_HASM);
           }
         }
         wave_lds_sync();
@@ -1154,7 +1180,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             stt[i0] = ob.ts[0];
             stp[i0] = ob.pl[0];
           } else {
-            atomicAnd(&L.pf[ob.pl[0] & 0xFFFFu], ~Q_OBS);  // evicted (:325-331)
+            pf_and(L, ob.pl[0] & 0xFFFFu, Q_OBS);  // evicted (:325-331)
           }
         }
         if (v1) {
@@ -1163,7 +1189,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             stt[i1] = ob.ts[1];
             stp[i1] = ob.pl[1];
           } else {
-            atomicAnd(&L.pf[ob.pl[1] & 0xFFFFu], ~Q_OBS);
+            pf_and(L, ob.pl[1] & 0xFFFFu, Q_OBS);
           }
         }
         if (rel) {
@@ -1171,11 +1197,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             stk[ic] = cm_k;
             stt[ic] = cm_t;
             stp[ic] = cu_p | (cm_d << 16);
-            if (!inobs) atomicOr(&L.pf[cu_p], Q_OBS);
-            L.odc[cu_p] = (uint8_t)cm_d;
+            if (!inobs) pf_or(L, cu_p, Q_OBS);
             L.opos[cu_p] = (uint16_t)cm_pos;
           } else if (inobs) {
-            atomicAnd(&L.pf[cu_p], ~Q_OBS);
+            pf_and(L, cu_p, Q_OBS);
           }
         }
         wave_lds_sync();
@@ -1213,9 +1238,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             L.gts[X] = rl64(rgt, (int)r);
             L.gdc[X] = (uint8_t)((g >> 8) & 7u);
             L.gpos[X] = (uint16_t)(g >> 16);
-            atomicOr(&L.pf[X], Q_HASM);
+            pf_or(L, X, Q_HASM);
           } else {
-            atomicAnd(&L.pf[X], ~Q_HASM);
+            pf_and(L, X, Q_HASM);
           }
         }
         const uint32_t ix = ob_find(ob, X);
@@ -1224,7 +1249,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const int vl = (int)(((r & 7u) << 3) | odc);
           const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
           if ((r < 8 ? va : vb) >= ob_get64(ob.ts, ix)) {
-            if (lane == 0) atomicAnd(&L.pf[X], ~Q_OBS);
+            if (lane == 0) pf_and(L, X, Q_OBS);
             wave_lds_sync();
             int64_t wk = 0;
             RCOUNT(15, 1);
@@ -1236,8 +1261,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
               const uint32_t gd = ufl(L.gdc[w]), gp = ufl(L.gpos[w]);
               ob_replace(ob, ix, wk, gt, w | (gd << 16));
               if (lane == 0) {
-                atomicOr(&L.pf[w], Q_OBS);
-                L.odc[w] = (uint8_t)gd;
+                pf_or(L, w, Q_OBS);
                 L.opos[w] = (uint16_t)gp;
                 r_emit(a, L, op0, op0 + c0 + hi, CCRDT_TRMV_ADD, key_id(wk), key_score(wk), gd, gt, nullptr);
               }
@@ -1261,6 +1285,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       if (i < ob.n) {
         L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
         L.u.f.ots[ob.pl[t] & 0xFFFFu] = ob.ts[t];
+        L.u.f.odc[ob.pl[t] & 0xFFFFu] = (uint8_t)(ob.pl[t] >> 16);
       }
     }
     wave_lds_sync();
@@ -1280,7 +1305,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
           const int64_t msv = L.msc[p], otv = ino ? L.u.f.ots[p] : 0, gtv = L.gts[p];
-          const uint32_t od = L.odc[p], gd = L.gdc[p];
+          const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
           for (uint32_t j = 0; j < cnt; ++j) {
             const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
             const uint32_t d2 = KA->new_s.m_dc[base + j];
@@ -1317,14 +1342,19 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 }  // namespace
 
 // (TRMV_R_WAVES: build knob, the minimum waves per SIMD the register
-// allocation must allow)
+// allocation must allow; TRMV_R_WG: keys (waves) per workgroup)
 #ifndef TRMV_R_WAVES
 #define TRMV_R_WAVES 3
 #endif
-__global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApplyArgs a) {
-  __shared__ RLds L;
+#ifndef TRMV_R_WG
+#define TRMV_R_WG 2
+#endif
+__global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApplyArgs a) {
+  __shared__ RLds lds[TRMV_R_WG];
+  const uint32_t wv = ufl(threadIdx.x >> 6);
+  RLds& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
-  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+  for (uint32_t w = blockIdx.x * TRMV_R_WG + wv; w < n; w += gridDim.x * TRMV_R_WG) {
     const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
     const int r = trmv_resident_key(a, key, L);
     if (r == R_NEXT && lane_id() == 0) {
@@ -1337,8 +1367,8 @@ __global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApp
 
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
-  const uint64_t blocks = std::min<uint64_t>(grid_keys, 65536);
-  hipLaunchKernelGGL(trmv_resident_kernel, dim3((unsigned)blocks), dim3(64), 0, st, a);
+  const uint64_t blocks = std::min<uint64_t>((grid_keys + TRMV_R_WG - 1) / TRMV_R_WG, 65536 / TRMV_R_WG);
+  hipLaunchKernelGGL(trmv_resident_kernel, dim3((unsigned)blocks), dim3(64 * TRMV_R_WG), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
