@@ -75,7 +75,7 @@ constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
 constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #ifndef TRMV_AHEAD2
-#define TRMV_AHEAD2 1  // FRESH: ops loaded two keys ahead, clocks one key ahead
+#define TRMV_AHEAD2 0  // FRESH: ops loaded two keys ahead, clocks one key ahead (measured: 1% slower since the kernel-argument re-read)
 #endif
 #ifndef TRMV_NT
 #define TRMV_NT 0  // FRESH output (pool, player records) stored non-temporal
