@@ -42,6 +42,14 @@ struct DevBuf {
     bytes = b;
     return CCRDT_OK;
   }
+  // Growth with headroom for state that grows batch after batch (the
+  // resident topk_rmv sides): a buffer that must grow is re-allocated at
+  // twice the request, so a steady stream re-allocates every few batches
+  // instead of at each (a re-allocation of GBs costs milliseconds).
+  int ensure_grow(uint64_t need) {
+    if (need <= bytes && p) return CCRDT_OK;
+    return ensure(p ? 2 * need : need);
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;

@@ -193,6 +193,7 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   e->release_all();
+  ccrdt::stage_release(*e);
   if (e->h_status) (void)hipHostFree(e->h_status);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -334,14 +335,14 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   }
   auto grow = [&](TrmvBufs& b) -> int {
     CCRDT_TRY(b.meta.ensure(nk * sizeof(KeyMeta)));
-    CCRDT_TRY(b.pl_id.ensure(tot[0] * 8));
-    CCRDT_TRY(b.pl_info.ensure(tot[0] * 4));
-    CCRDT_TRY(b.pl_slab.ensure(tot[0] * 4));
-    CCRDT_TRY(b.pl_gb.ensure(tot[0] * 2));
-    CCRDT_TRY(b.m_score.ensure(tot[1] * 8));
-    CCRDT_TRY(b.m_ts.ensure(tot[1] * 8));
-    CCRDT_TRY(b.m_dc.ensure(tot[1]));
-    CCRDT_TRY(b.r_vc.ensure(tot[2] * 8 * D));
+    CCRDT_TRY(b.pl_id.ensure_grow(tot[0] * 8));
+    CCRDT_TRY(b.pl_info.ensure_grow(tot[0] * 4));
+    CCRDT_TRY(b.pl_slab.ensure_grow(tot[0] * 4));
+    CCRDT_TRY(b.pl_gb.ensure_grow(tot[0] * 2));
+    CCRDT_TRY(b.m_score.ensure_grow(tot[1] * 8));
+    CCRDT_TRY(b.m_ts.ensure_grow(tot[1] * 8));
+    CCRDT_TRY(b.m_dc.ensure_grow(tot[1]));
+    CCRDT_TRY(b.r_vc.ensure_grow(tot[2] * 8 * D));
     CCRDT_TRY(b.vc.ensure(nk * 8 * D));
     return CCRDT_OK;
   };
@@ -520,34 +521,45 @@ int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n) {
 int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* x) {
   CCRDT_TRY(check_trmv(e));
   if (!x) return CCRDT_EINVAL;
-  const uint64_t n_ops = e->last_n_ops, nk = (uint64_t)e->n_keys;
-  const int D = e->n_dc;
-  if (x->kind)
-    for (uint64_t i = 0; i < n_ops; ++i) x->kind[i] = CCRDT_NOOP;
-  if (!n_ops || !nk) return CCRDT_OK;
-  CCRDT_HIP(hipStreamSynchronize(e->stream));
-  std::vector<uint32_t> cnt(nk);
-  std::vector<uint64_t> kp(nk + 1);
-  std::vector<TrmvExtraRec> rec(n_ops);
-  std::vector<int64_t> vc(n_ops * D);
-  CCRDT_HIP(hipMemcpy(cnt.data(), e->ex_cnt.p, nk * 4, hipMemcpyDeviceToHost));
-  CCRDT_HIP(hipMemcpy(kp.data(), e->ex_key_ptr.p, (nk + 1) * 8, hipMemcpyDeviceToHost));
-  CCRDT_HIP(hipMemcpy(rec.data(), e->ex.p, n_ops * sizeof(TrmvExtraRec), hipMemcpyDeviceToHost));
-  CCRDT_HIP(hipMemcpy(vc.data(), e->ex_vc.p, n_ops * 8 * D, hipMemcpyDeviceToHost));
-  for (uint64_t k = 0; k < nk; ++k) {
-    for (uint32_t j = 0; j < cnt[k]; ++j) {
-      const uint64_t pos = kp[k] + j;
-      const TrmvExtraRec& r = rec[pos];
-      const uint64_t op = r.op;
-      if (op >= n_ops) continue;
-      if (x->kind) x->kind[op] = r.kind;
-      if (x->id) x->id[op] = r.id;
-      if (x->score) x->score[op] = r.score;
-      if (x->dc) x->dc[op] = r.dc;
-      if (x->ts) x->ts[op] = r.ts;
-      if (x->vc && r.kind == CCRDT_TRMV_RMV)
-        for (int d = 0; d < D; ++d) x->vc[op * D + d] = vc[pos * D + d];
-    }
+  Engine& E = *e;
+  const uint64_t n_ops = E.last_n_ops, nk = (uint64_t)E.n_keys;
+  const int D = E.n_dc;
+  if (x->kind && n_ops) memset(x->kind, CCRDT_NOOP, n_ops);
+  if (!n_ops || !nk || !E.ex_cnt.p) return CCRDT_OK;
+  // The extras are packed on the device into rows [op, kind, id, score, dc,
+  // ts, vc...] (the exchange's pack kernel) and only those rows cross PCIe:
+  // a batch's extras are a few per million ops, its op-indexed extra
+  // buffers are n_ops records.
+  const uint64_t w = 6 + (uint64_t)D;
+  uint64_t cap = std::max<uint64_t>(E.st_out_vc.bytes / (w * 8), 4096);
+  uint32_t cnt = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    CCRDT_TRY(E.st_out_vc.ensure(cap * w * 8));
+    CCRDT_TRY(E.st_out_kind.ensure(4));
+    CCRDT_TRY(trmv_launch_pack_extras(E.ex_key_ptr.as<uint64_t>(), E.ex_cnt.as<uint32_t>(),
+                                      E.ex.as<TrmvExtraRec>(), E.ex_vc.as<int64_t>(), nk, D,
+                                      E.st_out_vc.as<int64_t>(), (int64_t)cap,
+                                      E.st_out_kind.as<uint32_t>(), E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.st_out_kind.p, 4, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    memcpy(&cnt, E.h_status, 4);
+    if (cnt <= cap) break;
+    cap = cnt;  // (a second pass packs them all)
+  }
+  if (!cnt) return CCRDT_OK;
+  std::vector<int64_t> rows((size_t)cnt * w);
+  CCRDT_HIP(hipMemcpy(rows.data(), E.st_out_vc.p, rows.size() * 8, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < cnt; ++i) {
+    const int64_t* r = &rows[i * w];
+    const uint64_t op = (uint64_t)r[0];
+    if (op >= n_ops) continue;
+    if (x->kind) x->kind[op] = (uint8_t)r[1];
+    if (x->id) x->id[op] = r[2];
+    if (x->score) x->score[op] = r[3];
+    if (x->dc) x->dc[op] = (uint8_t)r[4];
+    if (x->ts) x->ts[op] = r[5];
+    if (x->vc && r[1] == CCRDT_TRMV_RMV)
+      for (int d = 0; d < D; ++d) x->vc[op * D + d] = r[6 + d];
   }
   return CCRDT_OK;
 }
@@ -579,16 +591,16 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   CCRDT_TRY(E.st_dc.ensure(n));
   CCRDT_TRY(E.st_ts.ensure(n * 8));
   CCRDT_TRY(E.st_rvc.ensure(nr * D * 8));
-  CCRDT_HIP(hipMemcpyAsync(E.st_kp.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyHostToDevice, E.stream));
+  // (pageable caller memory: through the pinned staging slots, staging.cpp)
+  CCRDT_TRY(h2d_staged(E, E.st_kp.p, ops->key_ptr, (nk + 1) * 8));
   if (n) {
-    CCRDT_HIP(hipMemcpyAsync(E.st_kind.p, ops->kind, n, hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.st_id.p, ops->id, n * 8, hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.st_score.p, ops->score, n * 8, hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.st_dc.p, ops->dc, n, hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.st_ts.p, ops->ts, n * 8, hipMemcpyHostToDevice, E.stream));
+    CCRDT_TRY(h2d_staged(E, E.st_kind.p, ops->kind, n));
+    CCRDT_TRY(h2d_staged(E, E.st_id.p, ops->id, n * 8));
+    CCRDT_TRY(h2d_staged(E, E.st_score.p, ops->score, n * 8));
+    CCRDT_TRY(h2d_staged(E, E.st_dc.p, ops->dc, n));
+    CCRDT_TRY(h2d_staged(E, E.st_ts.p, ops->ts, n * 8));
   }
-  if (nr)
-    CCRDT_HIP(hipMemcpyAsync(E.st_rvc.p, ops->rmv_vc, nr * D * 8, hipMemcpyHostToDevice, E.stream));
+  if (nr) CCRDT_TRY(h2d_staged(E, E.st_rvc.p, ops->rmv_vc, nr * D * 8));
   ccrdt_trmv_ops d = *ops;
   d.key_ptr = E.st_kp.as<uint64_t>();
   d.kind = E.st_kind.as<uint8_t>();

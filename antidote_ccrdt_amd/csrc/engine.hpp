@@ -74,6 +74,9 @@ struct ccrdt_engine {
   std::map<int, float> trmv_tier_ms;
   // host-API staging
   ccrdt::DevBuf st_kp, st_kind, st_id, st_score, st_dc, st_ts, st_rvc, st_out_kind, st_out_vc;
+  void* pin[8] = {};           // pinned upload slots (staging.cpp), allocated on first use
+  hipEvent_t pin_ev[8] = {};   // each slot's last DMA
+  int pin_n = 0;
 
   // other types
   ccrdt::TypeBufs tb;
@@ -88,4 +91,8 @@ struct ccrdt_engine {
 
 namespace ccrdt {
 using Engine = ccrdt_engine;
+// Host -> device copy of pageable caller memory through the engine's pinned
+// staging slots, parallel host threads (staging.cpp); queued on E.stream.
+int h2d_staged(Engine& E, void* dst, const void* src, uint64_t bytes);
+void stage_release(Engine& E);
 }

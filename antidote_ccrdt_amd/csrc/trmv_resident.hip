@@ -166,10 +166,11 @@ __device__ __forceinline__ uint32_t rhash(int64_t id) {
   return (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> (64 - 9));  // 512 slots
 }
 
-// One key's LDS: 10,064 bytes (16 per CU).  Ids and Scores are 32-bit in
+// One key's LDS: 12,112 bytes (6 two-key workgroups per CU).  Ids and Scores are 32-bit in
 // this class; Obs[Id]'s DcId lives in the sorted Observed array (Obs.pl).
 struct alignas(16) RLds {
   int64_t gts[RP];     // gb_sets:largest(Masked[Id]): Ts
+  int64_t ots[RP];     // Obs[Id]'s Ts (valid while the player is in Observed)
   int32_t msc[RP];     // largest Score of Masked[Id] (= Obs[Id]'s Score in Observed, or below it mid-run)
   uint32_t nslab[RP];  // new slab: offset | current count << 16
   uint16_t prow[RP];   // Removals row (new side), NONE16
@@ -199,7 +200,6 @@ struct alignas(16) RLds {
       uint8_t cws[RCH], cwe[RCH], csrt[RCH];
     } c;
     struct {  // P5
-      int64_t ots[RP];    // Obs[Id]'s Ts by player
       uint16_t nidx[RP];  // a player's index in the new record order
       uint8_t odc[RP];    // Obs[Id]'s DcId by player
     } f;
@@ -647,6 +647,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     }
   }
   ob_clear_tail(ob);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    if (64u * t + lane < ob.n) L.ots[ob.pl[t] & 0xFFFFu] = ob.ts[t];
   wave_lds_sync();
   RPROF(0);
   {
@@ -1136,13 +1139,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (seg_r) {
           f = L.pf[cu_p];
           ms = L.msc[cu_p];
+          ot = L.ots[cu_p];  // (meaningful when in Observed)
         }
         const bool inobs = (f & Q_OBS) != 0;
-        for (uint64_t t = ballot(seg_r && inobs); t; t &= t - 1) {  // Obs[Id]'s Ts: from the array
-          const int x = (int)__builtin_ctzll(t);
-          const int64_t tx = ob_get64(ob.ts, ob_find(ob, rl32(cu_p, x)));
-          ot = (int)lane == x ? tx : ot;
-        }
         const int64_t mk = rl64(ob.key[0], 0);
         const bool rel = seg_r && (inobs ? (cm_s > ms || (cm_s == ms && cm_t > ot)) : (ob.n < K || cm_k > mk));
         const uint64_t relm = ballot(rel);
@@ -1199,6 +1198,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             stp[ic] = cu_p | (cm_d << 16);
             if (!inobs) pf_or(L, cu_p, Q_OBS);
             L.opos[cu_p] = (uint16_t)cm_pos;
+            L.ots[cu_p] = cm_t;
           } else if (inobs) {
             pf_and(L, cu_p, Q_OBS);
           }
@@ -1263,6 +1263,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
               if (lane == 0) {
                 pf_or(L, w, Q_OBS);
                 L.opos[w] = (uint16_t)gp;
+                L.ots[w] = gt;
                 r_emit(a, L, op0, op0 + c0 + hi, CCRDT_TRMV_ADD, key_id(wk), key_score(wk), gd, gt, nullptr);
               }
             }
@@ -1284,7 +1285,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint32_t i = 64u * t + lane;
       if (i < ob.n) {
         L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
-        L.u.f.ots[ob.pl[t] & 0xFFFFu] = ob.ts[t];
         L.u.f.odc[ob.pl[t] & 0xFFFFu] = (uint8_t)(ob.pl[t] >> 16);
       }
     }
@@ -1304,7 +1304,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const uint32_t ns = L.nslab[p], cnt = ns >> 16;
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
-          const int64_t msv = L.msc[p], otv = ino ? L.u.f.ots[p] : 0, gtv = L.gts[p];
+          const int64_t msv = L.msc[p], otv = ino ? L.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
           for (uint32_t j = 0; j < cnt; ++j) {
             const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];

@@ -263,14 +263,21 @@ def main():
 
     # Host entry (reported in detail, never `value`): ccrdt_trmv_apply from
     # host arrays -- the batch crosses PCIe to the device, the extras come back.
-    eng.reset()
-    eng.sync()
-    th = time.perf_counter()
-    eng.apply(b, want_extra=True)
-    eng.sync()
-    th = time.perf_counter() - th
-    host_entry = {"what": "ccrdt_trmv_apply on host arrays (H2D of the batch + apply chain + D2H of "
-                          "the extra effects), one batch, wall time",
+    # The first call sizes the staging buffers (device copies of the batch,
+    # pinned upload slots): it is a warm-up; the second is timed.
+    ths = []
+    for _ in range(2):
+        eng.reset()
+        eng.sync()
+        th = time.perf_counter()
+        eng.apply(b, want_extra=True)
+        eng.sync()
+        ths.append(time.perf_counter() - th)
+    th = ths[-1]
+    host_entry = {"what": "ccrdt_trmv_apply on host arrays (pageable numpy; H2D of the batch through "
+                          "the pinned staging slots + apply chain + D2H of the extra effects), the "
+                          "second of two calls (the first sizes the buffers), wall time",
+                  "first_call_ms": ths[0] * 1e3,
                   "ops_per_s": b.n_ops / th, "ms": th * 1e3,
                   "batch_bytes": int(sum(getattr(b, f).nbytes for f in
                                          ("key_ptr", "kind", "id", "score", "dc", "ts", "rmv_vc")))}
