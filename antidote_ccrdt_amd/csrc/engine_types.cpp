@@ -54,10 +54,11 @@ static int copy_buf(DevBuf& dst, const DevBuf& src, hipStream_t st) {
   return CCRDT_OK;
 }
 
-static int h2d(DevBuf& d, const void* src, uint64_t bytes, hipStream_t st) {
+// (host memory of the caller: large copies go through the engine's pinned
+// staging slots, staging.cpp)
+static int h2d(Engine& E, DevBuf& d, const void* src, uint64_t bytes) {
   CCRDT_TRY(d.ensure(bytes));
-  if (bytes) CCRDT_HIP(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
-  return CCRDT_OK;
+  return h2d_staged(E, d.p, src, bytes);
 }
 
 template <class T>
@@ -234,8 +235,8 @@ static int hbm_regions(ccrdt_engine* e, const uint32_t* list, uint64_t n, const 
     cap[w] = (uint32_t)c;
     t += c;
   }
-  CCRDT_TRY(h2d(T.hb_off, off.data(), n * 8, e->stream));
-  CCRDT_TRY(h2d(T.hb_cap, cap.data(), n * 4, e->stream));
+  CCRDT_TRY(h2d(*e, T.hb_off, off.data(), n * 8));
+  CCRDT_TRY(h2d(*e, T.hb_cap, cap.data(), n * 4));
   *total = t;
   return CCRDT_OK;
 }
@@ -292,9 +293,9 @@ int ccrdt_avg_apply(ccrdt_engine* e, const ccrdt_avg_ops* ops) {
   const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
   CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
   TypeBufs& T = e->tb;
-  CCRDT_TRY(h2d(T.kp, ops->key_ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[0], ops->value, n * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[1], ops->n, n * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.kp, ops->key_ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[0], ops->value, n * 8));
+  CCRDT_TRY(h2d(*e, T.stage[1], ops->n, n * 8));
   ccrdt_avg_ops d{ops->n_ops, T.kp.as<uint64_t>(), T.stage[0].as<int64_t>(), T.stage[1].as<int64_t>()};
   return ccrdt_avg_apply_device(e, &d);
 }
@@ -318,8 +319,8 @@ int ccrdt_avg_import(ccrdt_engine* e, const int64_t* sum, const int64_t* num) {
   if (!sum || !num) return CCRDT_EINVAL;
   const uint64_t nk = (uint64_t)e->n_keys;
   TypeBufs& T = e->tb;
-  CCRDT_TRY(h2d(T.avg_sum[T.tcur], sum, nk * 8, e->stream));
-  CCRDT_TRY(h2d(T.avg_num[T.tcur], num, nk * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.avg_sum[T.tcur], sum, nk * 8));
+  CCRDT_TRY(h2d(*e, T.avg_num[T.tcur], num, nk * 8));
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   e->fresh = false;
   return CCRDT_OK;
@@ -421,9 +422,9 @@ int ccrdt_topk_apply(ccrdt_engine* e, const ccrdt_topk_ops* ops) {
   const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
   CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
   TypeBufs& T = e->tb;
-  CCRDT_TRY(h2d(T.kp, ops->key_ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[0], ops->id, n * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[1], ops->score, n * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.kp, ops->key_ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[0], ops->id, n * 8));
+  CCRDT_TRY(h2d(*e, T.stage[1], ops->score, n * 8));
   ccrdt_topk_ops d{ops->n_ops, T.kp.as<uint64_t>(), T.stage[0].as<int64_t>(), T.stage[1].as<int64_t>()};
   return ccrdt_topk_apply_device(e, &d);
 }
@@ -547,10 +548,10 @@ int ccrdt_topk_import(ccrdt_engine* e, const uint64_t* ptr, const int64_t* id, c
     }
   }
   const int c = T.tcur;
-  CCRDT_TRY(h2d(T.tk_off[c], ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.tk_cnt[c], cnt.data(), nk * 4, e->stream));
-  CCRDT_TRY(h2d(T.tk_id[c], id, ptr[nk] * 8, e->stream));
-  CCRDT_TRY(h2d(T.tk_score[c], score, ptr[nk] * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.tk_off[c], ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.tk_cnt[c], cnt.data(), nk * 4));
+  CCRDT_TRY(h2d(*e, T.tk_id[c], id, ptr[nk] * 8));
+  CCRDT_TRY(h2d(*e, T.tk_score[c], score, ptr[nk] * 8));
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   e->fresh = false;
   return CCRDT_OK;
@@ -733,24 +734,37 @@ int ccrdt_lb_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, u
 
 int ccrdt_lb_fetch_extra(ccrdt_engine* e, ccrdt_lb_extra* x) {
   CCRDT_TRY(check_type(e, CCRDT_LEADERBOARD));
+  if (!x) return CCRDT_EINVAL;
   const uint64_t nk = (uint64_t)e->n_keys, n = e->last_n_ops;
-  if (x->kind)
-    for (uint64_t i = 0; i < n; ++i) x->kind[i] = CCRDT_NOOP;
-  if (!n || !nk) return CCRDT_OK;
-  std::vector<uint32_t> cnt;
-  std::vector<uint64_t> kp;
-  std::vector<LbExtraRec> rec;
-  CCRDT_TRY(d2h(cnt, e->tb.ex_cnt, nk, e->stream));
-  CCRDT_TRY(d2h(kp, e->tb.kp, nk + 1, e->stream));
-  CCRDT_TRY(d2h(rec, e->tb.ex, n, e->stream));
-  for (uint64_t k = 0; k < nk; ++k)
-    for (uint32_t j = 0; j < cnt[k]; ++j) {
-      const LbExtraRec& r = rec[kp[k] + j];
-      if (r.op >= n) continue;
-      if (x->kind) x->kind[r.op] = CCRDT_LB_ADD;
-      if (x->id) x->id[r.op] = r.id;
-      if (x->score) x->score[r.op] = r.score;
-    }
+  if (x->kind && n) memset(x->kind, CCRDT_NOOP, n);
+  if (!n || !nk || !e->tb.ex_cnt.p) return CCRDT_OK;
+  // packed on the device ([key, op, id, score] rows, the replication
+  // exchange's pack kernel); only those rows cross PCIe
+  TypeBufs& T = e->tb;
+  uint64_t cap = std::max<uint64_t>(T.stage[7].bytes / 32, 4096);
+  uint32_t cnt = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    CCRDT_TRY(T.stage[7].ensure(cap * 32));
+    CCRDT_TRY(T.status.ensure(64));
+    CCRDT_TRY(lb_launch_pack_extras(T.kp.as<uint64_t>(), T.ex_cnt.as<uint32_t>(), T.ex.as<LbExtraRec>(), nk,
+                                    T.stage[7].as<int64_t>(), (int64_t)cap, T.status.as<uint32_t>() + 8,
+                                    e->stream));
+    CCRDT_HIP(hipMemcpyAsync(e->h_status, T.status.as<uint32_t>() + 8, 4, hipMemcpyDeviceToHost, e->stream));
+    CCRDT_HIP(hipStreamSynchronize(e->stream));
+    memcpy(&cnt, e->h_status, 4);
+    if (cnt <= cap) break;
+    cap = cnt;
+  }
+  std::vector<int64_t> rows;
+  CCRDT_TRY(d2h(rows, T.stage[7], (uint64_t)cnt * 4, e->stream));
+  for (uint64_t i = 0; i < cnt; ++i) {
+    const int64_t* r = &rows[i * 4];
+    const uint64_t op = (uint64_t)r[1];
+    if (op >= n) continue;
+    if (x->kind) x->kind[op] = CCRDT_LB_ADD;
+    if (x->id) x->id[op] = r[2];
+    if (x->score) x->score[op] = r[3];
+  }
   return CCRDT_OK;
 }
 
@@ -760,10 +774,10 @@ int ccrdt_lb_apply(ccrdt_engine* e, const ccrdt_lb_ops* ops, ccrdt_lb_extra* ext
   const uint64_t nk = (uint64_t)e->n_keys, n = (uint64_t)ops->n_ops;
   CCRDT_TRY(check_csr(ops->key_ptr, nk, n));
   TypeBufs& T = e->tb;
-  CCRDT_TRY(h2d(T.stage[0], ops->key_ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[1], ops->kind, n, e->stream));
-  CCRDT_TRY(h2d(T.stage[2], ops->id, n * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[3], ops->score, n * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.stage[0], ops->key_ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[1], ops->kind, n));
+  CCRDT_TRY(h2d(*e, T.stage[2], ops->id, n * 8));
+  CCRDT_TRY(h2d(*e, T.stage[3], ops->score, n * 8));
   ccrdt_lb_ops d{ops->n_ops, T.stage[0].as<uint64_t>(), T.stage[1].as<uint8_t>(), T.stage[2].as<int64_t>(),
                  T.stage[3].as<int64_t>()};
   CCRDT_TRY(ccrdt_lb_apply_device(e, &d));
@@ -932,10 +946,10 @@ int ccrdt_lb_import(ccrdt_engine* e, const ccrdt_lb_state* in) {
   }
   TypeBufs& T = e->tb;
   const int c = T.tcur;
-  CCRDT_TRY(h2d(T.lb_meta[c], meta.data(), nk * sizeof(LbMeta), e->stream));
-  CCRDT_TRY(h2d(T.lb_id[c], id.data(), id.size() * 8, e->stream));
-  CCRDT_TRY(h2d(T.lb_score[c], score.data(), score.size() * 8, e->stream));
-  CCRDT_TRY(h2d(T.lb_st[c], st.data(), st.size(), e->stream));
+  CCRDT_TRY(h2d(*e, T.lb_meta[c], meta.data(), nk * sizeof(LbMeta)));
+  CCRDT_TRY(h2d(*e, T.lb_id[c], id.data(), id.size() * 8));
+  CCRDT_TRY(h2d(*e, T.lb_score[c], score.data(), score.size() * 8));
+  CCRDT_TRY(h2d(*e, T.lb_st[c], st.data(), st.size()));
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   e->fresh = false;
   return CCRDT_OK;
@@ -988,10 +1002,10 @@ int ccrdt_lb_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const u
     }
   TypeBufs& T = e->tb;
   const uint64_t un = (uint64_t)n;
-  CCRDT_TRY(h2d(T.stage[0], key, un * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[1], op, un, e->stream));
-  CCRDT_TRY(h2d(T.stage[2], id, un * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[3], score, un * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.stage[0], key, un * 8));
+  CCRDT_TRY(h2d(*e, T.stage[1], op, un));
+  CCRDT_TRY(h2d(*e, T.stage[2], id, un * 8));
+  CCRDT_TRY(h2d(*e, T.stage[3], score, un * 8));
   CCRDT_TRY(T.stage[4].ensure(un));
   const int c = T.tcur;
   for (DevBuf* d : {&T.lb_meta[c], &T.lb_id[c], &T.lb_score[c], &T.lb_st[c]}) CCRDT_TRY(d->ensure(8));
@@ -1094,7 +1108,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   tptr[0] = 0;
   for (uint64_t d = 0; d < nd; ++d)
     tptr[d + 1] = tptr[d] + ((doff[d + 1] - doff[d]) / WC_TILE + WC_TPW) / WC_TPW;
-  CCRDT_TRY(h2d(T.stage[4], tptr.data(), (nd + 1) * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.stage[4], tptr.data(), (nd + 1) * 8));
   if (nd > 0xFFFFFFFFull) {
     set_error("wc_apply: more than 2^32 documents in one batch");
     return CCRDT_EINVAL;
@@ -1102,7 +1116,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   std::vector<uint32_t> cdoc(tptr[nd] + 1, 0u);  // chunk -> document (lives until the batch is done)
   for (uint64_t d = 0; d < nd; ++d)
     for (uint64_t c = tptr[d]; c < tptr[d + 1]; ++c) cdoc[c] = (uint32_t)d;
-  CCRDT_TRY(h2d(T.stage[5], cdoc.data(), cdoc.size() * 4, e->stream));
+  CCRDT_TRY(h2d(*e, T.stage[5], cdoc.data(), cdoc.size() * 4));
   // worddocumentcount: groups of 4 chunks of one document (one workgroup each)
   std::vector<uint64_t> gptr(nd + 1, 0);
   std::vector<uint32_t> gdoc;
@@ -1111,8 +1125,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     gdoc.resize(gptr[nd] + 1, 0u);
     for (uint64_t d = 0; d < nd; ++d)
       for (uint64_t g = gptr[d]; g < gptr[d + 1]; ++g) gdoc[g] = (uint32_t)d;
-    CCRDT_TRY(h2d(T.stage[6], gptr.data(), (nd + 1) * 8, e->stream));
-    CCRDT_TRY(h2d(T.stage[7], gdoc.data(), gdoc.size() * 4, e->stream));
+    CCRDT_TRY(h2d(*e, T.stage[6], gptr.data(), (nd + 1) * 8));
+    CCRDT_TRY(h2d(*e, T.stage[7], gdoc.data(), gdoc.size() * 4));
   }
   std::vector<uint64_t> top;
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
@@ -1225,7 +1239,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       // the state is unchanged: the new table side is dropped, the arena
       // top goes back to the words it held
       const uint64_t back[2] = {arena_used, words_old};
-      CCRDT_TRY(h2d(T.arena_top, back, 16, e->stream));
+      CCRDT_TRY(h2d(*e, T.arena_top, back, 16));
       CCRDT_HIP(hipStreamSynchronize(e->stream));
       if ((st[1] & 1) && !reseeded) {
         // two distinct words met on one 64-bit hash: the collision depends on
@@ -1257,9 +1271,9 @@ int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     return CCRDT_EINVAL;
   }
   TypeBufs& T = e->tb;
-  CCRDT_TRY(h2d(T.kp, docs->key_ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[2], docs->doc_off, (nd + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[3], docs->bytes, docs->n_bytes, e->stream));
+  CCRDT_TRY(h2d(*e, T.kp, docs->key_ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[2], docs->doc_off, (nd + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[3], docs->bytes, docs->n_bytes));
   CCRDT_TRY(T.stage[3].ensure(8));
   ccrdt_wc_docs d{docs->n_docs, T.kp.as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[3].as<uint8_t>(),
                   docs->n_bytes};
@@ -1299,11 +1313,11 @@ static int wc_merge_words(ccrdt_engine* e, int64_t n_words, const uint64_t* key_
   }
   TypeBufs& T = e->tb;
   // words -> device: keys, offsets, bytes, counts
-  CCRDT_TRY(h2d(T.kp, key_ptr, (nk + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[2], word_off, (nw + 1) * 8, e->stream));
-  CCRDT_TRY(h2d(T.stage[3], bytes, nb, e->stream));
+  CCRDT_TRY(h2d(*e, T.kp, key_ptr, (nk + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[2], word_off, (nw + 1) * 8));
+  CCRDT_TRY(h2d(*e, T.stage[3], bytes, nb));
   CCRDT_TRY(T.stage[3].ensure(8));
-  CCRDT_TRY(h2d(T.stage[1], count, nw * 8, e->stream));
+  CCRDT_TRY(h2d(*e, T.stage[1], count, nw * 8));
   CCRDT_TRY(T.stage[0].ensure(nw * 8 + 8));
   CCRDT_TRY(wc_launch_doc_key(T.kp.as<uint64_t>(), nk, nw, T.stage[0].as<uint64_t>(), e->stream));
   return wc_merge_core(e, nw, T.stage[0].as<uint64_t>(), T.stage[2].as<uint64_t>(), T.stage[1].as<int64_t>(),
