@@ -501,15 +501,24 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #endif
   const uint64_t op0 = KA->key_ptr[key];
   const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
-  const KeyMeta nm = KA->new_s.meta[key];
-  const KeyMeta om = KA->old_s.meta[key];
+  // (a fresh batch: the keys tier 0 handed on, with no old state)
+  const bool fresh = KA->fresh != 0;
+  const KeyMeta nm = trmv_new_meta(a, key);
+  KeyMeta om;
+  if (fresh) {
+    om.p_off = om.m_off = om.r_off = 0;
+    om.np = om.nm = om.nr = om.nobs = 0;
+    om.minq = NONE32;
+  } else {
+    om = KA->old_s.meta[key];
+  }
   // (per-player op counts are 16-bit here)
   if (om.np > (uint32_t)RP || om.nobs > 128u || nops > 0xFFFFu) return R_NEXT;
   const uint32_t K = KA->k;
 
   for (uint32_t i = lane; i < (uint32_t)RP; i += 64) reinterpret_cast<uint32_t*>(L.u.r.hs)[i] = 0xFFFFFFFFu;
   if (lane <= (uint32_t)TRMV_DPAD)
-    L.vc[lane] = lane < (uint32_t)D ? (unsigned long long)KA->old_s.vc[(uint64_t)key * D + lane] : 0ull;
+    L.vc[lane] = (!fresh && lane < (uint32_t)D) ? (unsigned long long)KA->old_s.vc[(uint64_t)key * D + lane] : 0ull;
   if (lane == 0) L.nex = 0u;
   wave_lds_sync();
 
