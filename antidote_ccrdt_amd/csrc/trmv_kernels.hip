@@ -23,15 +23,29 @@ constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 4;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
+// Ops of kind 2/3 (rmv: the only ones that can add a Removals row) in
+// [o0, o1): bit 1 of each kind byte, eight bytes per load.  A kind above 3
+// counts too (the batch is rejected anyway).
+__device__ __forceinline__ uint64_t rmv_ops(const uint8_t* kind, uint64_t o0, uint64_t o1) {
+  uint64_t n = 0, i = o0;
+  for (; i < o1 && (reinterpret_cast<uintptr_t>(kind + i) & 7); ++i) n += (kind[i] >> 1) & 1u;
+  for (; i + 8 <= o1; i += 8) {
+    const uint64_t x = *reinterpret_cast<const uint64_t*>(kind + i);
+    n += (uint64_t)__builtin_popcountll((x >> 1) & 0x0101010101010101ull);
+  }
+  for (; i < o1; ++i) n += (kind[i] >> 1) & 1u;
+  return n;
+}
+
 __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint64_t c[3]) {
-  const uint64_t nops = a.key_ptr[k + 1] - a.key_ptr[k];
+  const uint64_t o0 = a.key_ptr[k], nops = a.key_ptr[k + 1] - o0;
   if (a.fresh) {
     c[0] = c[1] = c[2] = nops;
   } else {
     const KeyMeta m = a.old_s.meta[k];
     c[0] = m.np + nops;
     c[1] = m.nm + nops;
-    c[2] = m.nr + nops;
+    c[2] = m.nr + rmv_ops(a.kind, o0, o0 + nops);  // (rows: rmv ops only)
   }
   // No per-key limit here: a segment is address space only.  The tiers check
   // the key's real layout against the u16 slab offsets (TRMV_SEG_MAX) and hand
