@@ -20,10 +20,22 @@ from collections import defaultdict
 def load(prof_dir):
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> dispatch -> value
     meta = {}
-    for f in glob.glob(os.path.join(prof_dir, "*", "*_counter_collection.csv")):
+    files = glob.glob(os.path.join(prof_dir, "*", "*_counter_collection.csv"))
+    # A kernel launched over grids of different sizes (tier R: the whole key
+    # space on a resident batch, a few hundred hand-ons on a fresh one) is
+    # averaged per grid size: the largest grid keeps the kernel's name, the
+    # others are listed as "name [grid N]".
+    gmax = defaultdict(int)
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                gmax[r["Kernel_Name"]] = max(gmax[r["Kernel_Name"]], int(r["Grid_Size"]))
+    for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 k, c, d = r["Kernel_Name"], r["Counter_Name"], (f, r["Dispatch_Id"])
+                if int(r["Grid_Size"]) != gmax[k]:
+                    k = f"{k} [grid {r['Grid_Size']}]"
                 per[k][c][d] += float(r["Counter_Value"])
                 meta[k] = {"vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
                            "lds": int(r["LDS_Block_Size"]), "wg": int(r["Workgroup_Size"])}
@@ -62,10 +74,10 @@ def main():
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
     if a.bench_json:
-        dom = [k for k in out if a.dominant in k]
+        dom = [k for k in out if a.dominant in k and "[grid" not in k]
         if len(dom) != 1 or "hbm_bytes" not in out[dom[0]]:
             raise SystemExit(f"dominant kernel {a.dominant!r} not found with FETCH/WRITE counters")
-        st = [k for k in out if a.steady and a.steady in k and "hbm_bytes" in out[k]]
+        st = [k for k in out if a.steady and a.steady in k and "[grid" not in k and "hbm_bytes" in out[k]]
         steady = ({"kernel": st[0], "hbm_bytes_per_launch": out[st[0]]["hbm_bytes"],
                    "fetch_kib": out[st[0]]["FETCH_SIZE"], "write_kib": out[st[0]]["WRITE_SIZE"]}
                   if len(st) == 1 else None)
