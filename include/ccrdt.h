@@ -112,7 +112,8 @@ int ccrdt_engine_last_kernel_ms(ccrdt_engine* e, float* ms);
  * key), 1 / 2 = trmv_steady with up to 256 / 1024 players per key in LDS,
  * 3 = trmv_resident (resident keys, K <= 128, Observed in registers),
  * 4 = trmv_steady's HBM class (up to CCRDT_TRMV_MAX_PLAYERS players, working
- * set in device scratch).  Chains: fresh 0 -> 1 -> 2, resident 3 -> 1 -> 2;
+ * set in device scratch).  Chains: fresh 0 -> 3 -> 1 -> 2 (K <= 128),
+ * resident 3 -> 1 -> 2;
  * tier 4 runs on tier 2's hand-ons.  Keys handed on by tier `t` in the last
  * batch: */
 int ccrdt_engine_overflow_keys(ccrdt_engine* e, int t, int64_t* n);
