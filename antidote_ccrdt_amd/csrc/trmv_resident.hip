@@ -957,7 +957,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         Row8 R = (Row8)(0);
         const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
         if (has_row)
-          for (int d = 0; d < D; ++d) R[d] = KA->new_s.r_vc[rbase + d];
+          for (int d = 0, dn = KA->n_dc; d < dn; ++d) R[d] = KA->new_s.r_vc[rbase + d];  // (n_dc re-read here: no per-d masks held across the key)
         const int64_t wid = L.u.c.cid[ws];
         bool moved = false;
         for (uint32_t x = ws; x < we; ++x) {
@@ -1037,7 +1037,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         }
         L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
         if (has_row) {
-          for (int d = 0; d < D; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
+          for (int d = 0, dn = KA->n_dc; d < dn; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
           f |= Q_ROWV;
         }
         if (moved) f |= Q_WALK;
