@@ -1076,16 +1076,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         bool ok = sadd, hf = lane == 0 || pseg != seg;
         int64_t vs = ssc, vt = sts, ws = ssc, wt = sts;
         uint32_t vd = sdc | ((scres >> 16) << 8), wd = vd;
+        int sl = (int)lane;
+        asm volatile("" : "+v"(sl));  // the (lane >= d) masks are made here, not held across keys
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-          const int src = (int)lane >= d ? (int)lane - d : (int)lane;
+          const int src = sl >= d ? sl - d : sl;
           const bool yok = shfl32(ok ? 1u : 0u, src) != 0;
           const int64_t ys = shfl64(vs, src), yt = shfl64(vt, src);
           const uint32_t yd = shfl32(vd, src);
           const int64_t zs = shfl64(ws, src), zt = shfl64(wt, src);
           const uint32_t zd = shfl32(wd, src);
           const bool yhf = shfl32(hf ? 1u : 0u, src) != 0;
-          if ((int)lane >= d && !hf) {
+          if (sl >= d && !hf) {
             if (yok) {
               if (!ok || gb_gt(ys, yd & 0xFFu, yt, vs, vd & 0xFFu, vt)) {
                 vs = ys;
@@ -1364,11 +1366,11 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
   RLds& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x * TRMV_R_WG + wv; w < n; w += gridDim.x * TRMV_R_WG) {
-    const uint32_t key = ufl(a.key_list ? a.key_list[w] : w);
+    const uint32_t key = ufl(KA->key_list ? KA->key_list[w] : w);
     const int r = trmv_resident_key(a, key, L);
     if (r == R_NEXT && lane_id() == 0) {
-      const uint32_t pos = atomicAdd(&a.status[0], 1u);
-      a.ovf_list[pos] = key;
+      const uint32_t pos = atomicAdd(&KA->status[0], 1u);
+      KA->ovf_list[pos] = key;
     }
     wave_lds_sync();
   }
