@@ -62,10 +62,14 @@ int h2d_staged(Engine& E, void* dst, const void* src, uint64_t bytes) {
       for (uint64_t c = (uint64_t)t; c < n_chunks; c += (uint64_t)T) {
         const uint64_t off = c * STAGE_CHUNK;
         const uint64_t len = std::min<uint64_t>(STAGE_CHUNK, bytes - off);
-        if (hipEventSynchronize(E.pin_ev[t]) != hipSuccess ||
-            (memcpy(E.pin[t], static_cast<const char*>(src) + off, len),
-             hipMemcpyAsync(static_cast<char*>(dst) + off, E.pin[t], len, hipMemcpyHostToDevice,
-                            E.stream) != hipSuccess) ||
+        // the slot's previous DMA must have read it before it is refilled
+        if (hipEventSynchronize(E.pin_ev[t]) != hipSuccess) {
+          rc[t] = CCRDT_EDEVICE;
+          return;
+        }
+        memcpy(E.pin[t], static_cast<const char*>(src) + off, len);
+        if (hipMemcpyAsync(static_cast<char*>(dst) + off, E.pin[t], len, hipMemcpyHostToDevice, E.stream) !=
+                hipSuccess ||
             hipEventRecord(E.pin_ev[t], E.stream) != hipSuccess) {
           rc[t] = CCRDT_EDEVICE;
           return;
