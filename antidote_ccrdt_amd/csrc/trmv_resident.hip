@@ -1044,7 +1044,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         L.pf[wp] = f;
       }
       wave_lds_sync();
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next chunk's replays read these stores
+      // vmcnt(0): the next chunk's replays read these stores.  After the last
+      // chunk nothing reads them before P5, which waits there: the Observed
+      // half runs while they drain.
+      if (c0 + n < nops) __builtin_amdgcn_s_waitcnt(0x0F70);
       RPROF(5);
 
       // ---- P4. the Observed half, in stream order (recompute_observed/5
@@ -1290,7 +1293,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     }
 
     // ---- P5. player records: Observed first (sorted), then the others in
-    // player order; positions of compacted slabs; Vc; meta
+    // player order; positions of compacted slabs; Vc; meta.  (The re-find of
+    // a compacted slab reads the last chunk's stores: they must have landed.)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t i = 64u * t + lane;
