@@ -1124,7 +1124,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const int64_t cm_k = mkkey(cm_s, sid);
       wave_lds_sync();  // the chunk region is free from here on: merge staging
       int64_t* stk = reinterpret_cast<int64_t*>(&L.u);
-      int64_t* stt = stk + 128;
       uint32_t* stp = reinterpret_cast<uint32_t*>(stk + 256);
       auto catch_up = [&](uint32_t run) {
         if (cu_ok && cu_run == run) {  // one lane per player
@@ -1190,7 +1189,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (v0) {
           if (i0 >= 0) {
             stk[i0] = ob.key[0];
-            stt[i0] = ob.ts[0];
             stp[i0] = ob.pl[0];
           } else {
             pf_and(L, ob.pl[0] & 0xFFFFu, Q_OBS);  // evicted (:325-331)
@@ -1199,7 +1197,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (v1) {
           if (i1 >= 0) {
             stk[i1] = ob.key[1];
-            stt[i1] = ob.ts[1];
             stp[i1] = ob.pl[1];
           } else {
             pf_and(L, ob.pl[1] & 0xFFFFu, Q_OBS);
@@ -1208,7 +1205,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         if (rel) {
           if (ic >= 0) {  // Obs[Id] := its cmp-largest (:303-331)
             stk[ic] = cm_k;
-            stt[ic] = cm_t;
             stp[ic] = cu_p | (cm_d << 16);
             if (!inobs) pf_or(L, cu_p, Q_OBS);
             L.opos[cu_p] = (uint16_t)cm_pos;
@@ -1223,8 +1219,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         for (int t = 0; t < 2; ++t) {
           const uint32_t i = 64u * t + lane;
           const uint32_t ii = i < ob.n ? i : 0u;
-          const int64_t kk = stk[ii], tt = stt[ii];
+          const int64_t kk = stk[ii];
           const uint32_t pp = stp[ii];
+          const int64_t tt = L.ots[i < ob.n ? (pp & 0xFFFFu) : 0u];  // (Obs[Id]'s Ts: kept per player)
           ob.key[t] = i < ob.n ? kk : INT64_MAX;
           ob.ts[t] = i < ob.n ? tt : 0;
           ob.pl[t] = i < ob.n ? pp : RNONE;
