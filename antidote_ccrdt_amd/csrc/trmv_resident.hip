@@ -1053,8 +1053,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       // ---- P4. the Observed half, in stream order (recompute_observed/5
       // :301-334; rmv/3 :267-298)
       const uint32_t kdr = L.u.c.ckd[lane], crr = L.u.c.cres[lane];
-      const int64_t keyr = mkkey(sc, id);
-      const bool ladd = lane < n && (kdr & 3u) < 2 && !(crr & R_DOM);
       const uint32_t rl = lane < (uint32_t)RCHR ? lane : 0u;
       const int64_t rgs = L.u.c.rgs[rl], rgt = L.u.c.rgt[rl];
       const uint32_t rgdv = L.u.c.rgd[rl];
