@@ -84,7 +84,9 @@ def route(batch: TrmvBatch, keys: np.ndarray) -> Shard:
 def _apply_keycap(engine, batch, host_keys: set, key_ids=None):
     """engine.apply(batch, want_extra=True), with CCRDT_EKEYCAP turned into a
     record: the batch committed for every key but the listed ones, whose
-    extras are in err.extra; their (global) ids join host_keys."""
+    extras are in err.extra; their (global) ids join host_keys.  The caller
+    finishes its collectives and then raises for every rank
+    (raise_host_keys), so no rank leaves a collective sequence early."""
     from ._lib import KeyCapacityError
     try:
         return engine.apply(batch, want_extra=True)
@@ -94,6 +96,49 @@ def _apply_keycap(engine, batch, host_keys: set, key_ids=None):
             keys = np.asarray(key_ids, np.int64)[keys]
         host_keys.update(int(k) for k in keys)
         return err.extra
+
+
+def _drop_keys(batch: TrmvBatch, drop: np.ndarray) -> TrmvBatch:
+    """The batch without the ops of the (local) keys in `drop` (their key
+    ranges left empty; rmv clock rows renumbered)."""
+    kp = np.asarray(batch.key_ptr, np.int64)
+    keep = np.ones(batch.n_ops, bool)
+    for k in drop:
+        keep[kp[k]:kp[k + 1]] = False
+    lens = np.diff(kp)
+    lens[drop] = 0
+    nkp = np.zeros_like(kp)
+    np.cumsum(lens, out=nkp[1:])
+    kind = batch.kind[keep]
+    ts = np.array(batch.ts[keep], np.int64)
+    rm = kind >= 2
+    rows = ts[rm]
+    ts[rm] = np.arange(rows.shape[0], dtype=np.int64)
+    return TrmvBatch(nkp.astype(np.uint64), kind, batch.id[keep], batch.score[keep], batch.dc[keep], ts,
+                     np.ascontiguousarray(batch.rmv_vc[rows], dtype=np.int64))
+
+
+def raise_host_keys(mine, extra=None, coll=None) -> None:
+    """Collective check after a step's exchanges: every rank's host-path keys
+    (CCRDT_EKEYCAP: the batch committed for every other key) are gathered,
+    and when any rank has one, EVERY rank raises KeyCapacityError with the
+    same sorted global ids in .keys and its step result in .extra.  Keys
+    past the engine's per-key capacity are the host path's from then on
+    (INTEGRATION.md): the drivers leave their ops out of later batches."""
+    import torch
+
+    from ._lib import EKEYCAP, KeyCapacityError
+    mine = np.array(sorted(int(k) for k in mine), np.int64)
+    if coll is not None and coll.world > 1:
+        parts = coll.all_gather_v(torch.from_numpy(mine))
+        allk = np.unique(np.concatenate([p.cpu().numpy() for p in parts])) if parts else mine
+    else:
+        allk = mine
+    if allk.shape[0]:
+        err = KeyCapacityError(EKEYCAP, "trmv step",
+                               f"{allk.shape[0]} key(s) over the per-key capacity went to the host path")
+        err.keys, err.extra = allk, extra
+        raise err
 
 
 def _dist():
@@ -159,57 +204,230 @@ def all_reduce_max(v: np.ndarray) -> np.ndarray:
     return t.cpu().numpy()
 
 
+class TrmvShardExchange:
+    """The two per-batch exchange steps of a key-sharded topk_rmv rank
+    (topk_rmv.erl:236,294 for the extras, :378-386 for the Vc
+    merge) -- the ONE implementation that bench.py --gpus N times and the
+    tests check.
+
+    A rank's pack is one int64 buffer on its device, [count | Vc | rows]:
+    word 0 holds the extra-effect count (low 32 bits) and the rank's number
+    of host-path keys (high 32 bits), then the rank's elementwise-max Vc,
+    then the effect rows (global op, kind, id, score, dc, ts, vc[n_dc]).  A
+    step is one fixed-size all-gather of [head | first FAST rows] -- the Vc
+    max is taken from the gathered copies, so the Vc all-reduce rides the
+    same collective -- and, only when some rank has more than FAST effects,
+    a second (variable) gather of the rest.  `coll` is a TorchCollective
+    (RCCL on device tensors over xGMI; gloo staged through the host) or an
+    in-process stand-in; None means one rank.  The pack is filled from the
+    HIP engine on the device (fill_from_engine: extras packed by a kernel,
+    local op indices mapped to global ones by a gather on the device) or
+    from host rows (fill_from_rows: engines that only have a host apply,
+    e.g. the oracle the CPU tests inject)."""
+
+    FAST = 256
+
+    def __init__(self, n_dc: int, coll=None, device=None, rows_cap: int = 1 << 20):
+        import torch
+        self.torch, self.n_dc, self.coll = torch, n_dc, coll
+        self.w = EXTRA_COLS + n_dc
+        self.head = 1 + n_dc
+        self.rows_cap = rows_cap
+        self.dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
+        self.pack = torch.zeros(self.head + rows_cap * self.w, dtype=torch.int64, device=self.dev)
+        self.count = 0  # this rank's effects in the pack (host-known only after run())
+        self.op_map = None
+
+    def _rows(self):
+        return self.pack[self.head:].view(self.rows_cap, self.w)
+
+    def fill_from_engine(self, engine, op_index=None, n_host_keys: int = 0) -> None:
+        """The engine's last batch: its extras (ccrdt_trmv_extras_device) and
+        its shard Vc (ccrdt_trmv_replica_vc_device), packed on the device.
+        op_index: device int64 tensor, local op index -> global (None: the
+        same)."""
+        p = self.pack.data_ptr()
+        engine.extras_device(p + 8 * self.head, self.rows_cap, p)
+        engine.replica_vc_device(p + 8)
+        engine.sync()
+        # (the count word's high half: host-path keys; the kernel wrote the low half)
+        self.pack[0] = (self.pack[0] & 0xFFFFFFFF) | (int(n_host_keys) << 32)
+        self.op_map = op_index
+        if op_index is not None and op_index.shape[0]:
+            # rows past the count are stale; mapping them is harmless
+            c0 = self._rows()[:self.FAST, 0]
+            c0.copy_(op_index[c0.clamp(0, op_index.shape[0] - 1)])
+
+    def fill_from_rows(self, rows: np.ndarray, vc: np.ndarray, n_host_keys: int = 0) -> None:
+        """Host extras rows (global op index first) and the shard Vc."""
+        m = int(rows.shape[0])
+        if m > self.rows_cap:
+            raise RuntimeError(f"trmv exchange: {m} extra effects > {self.rows_cap} rows")
+        h = np.zeros(self.head + m * self.w, np.int64)
+        h[0] = m | (int(n_host_keys) << 32)
+        h[1:self.head] = vc
+        h[self.head:] = np.ascontiguousarray(rows, np.int64).reshape(-1)
+        self.pack[:h.shape[0]] = self.torch.from_numpy(h).to(self.dev)
+        self.op_map = None
+
+    def run(self):
+        """The exchange: returns (every rank's extras as an int64 tensor
+        [M, 6 + n_dc] in global stream order -- identical on every rank --,
+        the replica Vc (elementwise max over the ranks), total host-path
+        keys over the ranks)."""
+        torch = self.torch
+        L = self.head + self.FAST * self.w
+        mine = self.pack[:L]
+        if self.coll is not None and self.coll.world > 1:
+            parts = self.coll.all_gather(mine)
+        else:
+            parts = [mine]
+        allp = torch.stack([q.to(self.dev) for q in parts])
+        cnt = allp[:, 0] & 0xFFFFFFFF
+        host = allp[:, 0] >> 32
+        vc = allp[:, 1:self.head].max(0).values
+        hv = torch.cat([cnt, host.sum().view(1), mine[:1] & 0xFFFFFFFF]).cpu().tolist()
+        counts, n_host, self.count = [int(c) for c in hv[:-2]], int(hv[-2]), int(hv[-1])
+        if max(counts) > self.rows_cap:
+            raise RuntimeError(f"trmv exchange: {max(counts)} extra effects > {self.rows_cap} rows")
+        heads = [allp[r, self.head:].view(self.FAST, self.w)[:min(c, self.FAST)] for r, c in enumerate(counts)]
+        if max(counts) > self.FAST:  # rare: the rest of the rows in a second gather
+            rest = self._rows()[self.FAST:max(self.count, self.FAST)]
+            if self.op_map is not None and rest.shape[0]:
+                rest[:, 0] = self.op_map[rest[:, 0].clamp(0, self.op_map.shape[0] - 1)]
+            if self.coll is not None and self.coll.world > 1:
+                tails = [t.to(self.dev) for t in self.coll.all_gather_v(rest.contiguous())]
+            else:
+                tails = [rest]
+            parts_rows = [torch.cat([h, t]) for h, t in zip(heads, tails)]
+        else:
+            parts_rows = heads
+        rows = torch.cat(parts_rows) if parts_rows else self._rows()[:0]
+        if rows.shape[0]:
+            rows = rows[torch.argsort(rows[:, 0], stable=True)]
+        return rows, vc, n_host
+
+
 class ShardedTopkRmv:
-    """This rank's shard of an n_keys topk_rmv keyspace."""
+    """This rank's shard of an n_keys topk_rmv keyspace.  A step is the
+    shard's apply (no data-path communication) and then the exchange
+    (TrmvShardExchange).  Keys over the engine's per-key capacity
+    (CCRDT_EKEYCAP: the batch committed for every other key) become host-path
+    keys: after the exchange every rank raises KeyCapacityError listing them
+    (raise_host_keys), and later batches leave their ops out of the engine."""
 
     def __init__(self, n_keys: int, k: int = 100, n_dc: int = 8, rank: int | None = None,
-                 world: int | None = None, engine_factory=None, device: int = 0):
+                 world: int | None = None, engine_factory=None, device: int = 0, coll=None):
         dist = _dist()
         self.rank = rank if rank is not None else (dist.get_rank() if dist else 0)
         self.world = world if world is not None else (dist.get_world_size() if dist else 1)
         self.n_keys, self.k, self.n_dc = n_keys, k, n_dc
         self.keys = owned_keys(n_keys, self.world, self.rank)
+        self.on_device = engine_factory is None
         if engine_factory is None:
             from .engine import TopkRmvEngine
 
             def engine_factory(nk, kk, d):
                 return TopkRmvEngine(nk, kk, d, device=device)
         self.engine = engine_factory(len(self.keys), k, n_dc)
-        self.host_keys: set[int] = set()
+        self.host_keys: set[int] = set()   # global ids
+        if coll is None and dist is not None and self.world > 1:
+            coll = TorchCollective(dist)
+        self.coll = coll
+        self.xchg = TrmvShardExchange(n_dc, coll, device if self.on_device else None)
+
+    def route(self, batch: TrmvBatch) -> Shard:
+        """This rank's sub-batch of a global batch (host-path keys' ops left out)."""
+        sh = route(batch, self.keys)
+        if self.host_keys:
+            drop = np.nonzero(np.isin(self.keys, np.array(sorted(self.host_keys), np.int64)))[0]
+            kp = np.asarray(sh.batch.key_ptr, np.int64)
+            keep = np.ones(sh.batch.n_ops, bool)
+            for k in drop:
+                keep[kp[k]:kp[k + 1]] = False
+            sh = Shard(sh.keys, _drop_keys(sh.batch, drop), sh.op_index[keep])
+        return sh
 
     def apply(self, batch: TrmvBatch) -> np.ndarray:
-        """update/2 over this rank's keys of a global batch; returns the
-        rank's extra effects as packed rows (global op index first).  Keys
-        over the engine's per-key capacity (CCRDT_EKEYCAP: the batch
-        committed for every other key) are recorded, as global ids, in
-        `host_keys` for the host path, and the rank goes on with the
-        collectives like the others."""
-        sh = route(batch, self.keys)
+        """update/2 over this rank's keys of a global batch on the engine's
+        host entry; returns the rank's extra effects as packed rows (global
+        op index first).  Over-capacity keys join host_keys."""
+        sh = self.route(batch)
         x = _apply_keycap(self.engine, sh.batch, self.host_keys, self.keys)
         if isinstance(x, dict):
             x = TrmvExtra(**x)
         return pack_extras(x, sh.op_index)
 
-    def host_keys_all(self) -> np.ndarray:
-        """Every rank's host-path keys (CCRDT_EKEYCAP), all-gathered: the same
-        sorted global ids on every rank."""
-        mine = np.array(sorted(self.host_keys), np.int64).reshape(-1, 1)
-        return np.unique(all_gather_rows(mine)[:, 0]) if self.world > 1 else mine[:, 0]
+    def apply_device(self, db, op_index=None) -> int:
+        """update/2 over a device-resident sub-batch (DeviceTrmvBatch, CSR over
+        this rank's keys); its extras and the shard Vc go into the exchange
+        pack on the device.  op_index: device int64 tensor, local op -> global
+        op.  Returns the number of keys handed to the host path."""
+        from ._lib import KeyCapacityError
+        n_new = 0
+        try:
+            self.engine.apply_device(db)
+        except KeyCapacityError as err:
+            ks = np.asarray(err.keys if err.keys is not None else [], np.int64)
+            self.host_keys.update(int(self.keys[k]) for k in ks)
+            n_new = int(ks.shape[0])
+        self.xchg.fill_from_engine(self.engine, op_index, n_new)
+        return n_new
 
-    def exchange_extras(self, rows: np.ndarray) -> np.ndarray:
-        """Every rank's extras, in stream order (identical on all ranks)."""
-        allr = all_gather_rows(rows)
-        return allr[np.argsort(allr[:, 0], kind="stable")] if allr.shape[0] else allr
-
-    def replica_vc(self) -> np.ndarray:
-        """Elementwise max of every key's Vc over the whole keyspace."""
+    def _local_vc(self) -> np.ndarray:
         st = self.engine.export()
         vc = st["vc"] if isinstance(st, dict) else st.vc
-        local = vc.max(axis=0) if vc.shape[0] else np.zeros(self.n_dc, np.int64)
-        return all_reduce_max(local)
+        return vc.max(axis=0) if vc.shape[0] else np.zeros(self.n_dc, np.int64)
+
+    def step(self, batch: TrmvBatch):
+        """One batch: apply this rank's keys, then the exchange.  Returns
+        (every rank's extras as int64 rows in global stream order, the
+        replica Vc), numpy, identical on every rank."""
+        sh = self.route(batch)
+        n0 = len(self.host_keys)
+        if self.on_device:
+            import torch
+
+            from .engine import DeviceTrmvBatch
+            db = DeviceTrmvBatch(sh.batch)
+            try:
+                self.apply_device(db, torch.from_numpy(sh.op_index).to(self.xchg.dev))
+            finally:
+                db.close()
+        else:
+            rows = pack_extras(TrmvExtra(**_as_dict(_apply_keycap(self.engine, sh.batch, self.host_keys,
+                                                                  self.keys))), sh.op_index)
+            self.xchg.fill_from_rows(rows, self._local_vc(), len(self.host_keys) - n0)
+        rows, vc, n_host = self.xchg.run()
+        out = (rows.cpu().numpy(), vc.cpu().numpy())
+        if n_host:  # (the same on every rank: the sum over the gathered headers)
+            raise_host_keys(self.host_keys, out, self.coll)
+        return out
+
+    def exchange_extras(self, rows: np.ndarray) -> np.ndarray:
+        """Every rank's extras from host rows, in stream order (identical on
+        all ranks); the shard Vc rides along (replica_vc())."""
+        self.xchg.fill_from_rows(rows, self._local_vc())
+        r, vc, _ = self.xchg.run()
+        self._vc = vc.cpu().numpy()
+        return r.cpu().numpy()
+
+    def replica_vc(self) -> np.ndarray:
+        """Elementwise max of every key's Vc over the whole keyspace (from the
+        last exchange when there was one)."""
+        v = getattr(self, "_vc", None)
+        if v is not None:
+            return v
+        return all_reduce_max(self._local_vc())
 
     def export(self):
         return self.engine.export()
+
+
+def _as_dict(x):
+    if isinstance(x, dict):
+        return x
+    return {f: getattr(x, f) for f in x.__dataclass_fields__}
 
 
 def all_reduce_sum(v: int) -> int:
@@ -241,6 +459,7 @@ class _TrmvCodec:
     n_keys: int
     n_dc: int
     host_keys: set = field(default_factory=set)
+    reported: set = field(default_factory=set)
     COLS = 8
 
     def rows_of_batch(self, b: TrmvBatch) -> np.ndarray:
@@ -342,14 +561,30 @@ class _Replica:
 
     def step(self, batch, max_rounds: int = 64) -> int:
         """One replication step over torch.distributed (all_gather_rows);
-        returns the number of delivery rounds."""
+        returns the number of delivery rounds.  A topk_rmv replica whose engine
+        handed keys to the host path (CCRDT_EKEYCAP) raises KeyCapacityError
+        on every rank once the step has quiesced (raise_host_keys)."""
         out = self.originate(batch)
         for rounds in range(max_rounds):
             allr = all_gather_rows(out)
             if not allr.shape[0]:
+                self.check_host_keys(rounds)
                 return rounds
             out = self.deliver(allr)
         raise RuntimeError("replication did not quiesce")
+
+    def check_host_keys(self, result=None, local: bool = False) -> None:
+        """Collective (unless `local`: replicas held by one process): raise on
+        every rank when any rank's codec handed keys to the host path since
+        the last report."""
+        hk = getattr(self.codec, "host_keys", None)
+        if hk is None:
+            return
+        new = hk - self.codec.reported
+        dist = None if local else _dist()
+        coll = TorchCollective(dist) if dist is not None and self.world > 1 else None
+        self.codec.reported |= new
+        raise_host_keys(new, result, coll)
 
     def export(self):
         return self.engine.export()
@@ -390,6 +625,13 @@ def replicate_local(replicas, batches, max_rounds: int = 64) -> int:
     for rounds in range(max_rounds):
         allr = np.concatenate(outs)
         if not allr.shape[0]:
+            new = set()
+            for r in replicas:  # (every replica's report, then one raise)
+                hk = getattr(r.codec, "host_keys", None)
+                if hk is not None:
+                    new |= hk - r.codec.reported
+                    r.codec.reported |= hk
+            raise_host_keys(new, rounds)
             return rounds
         outs = [r.deliver(allr) for r in replicas]
     raise RuntimeError("replication did not quiesce")
@@ -539,6 +781,15 @@ class TorchCollective:
 
     def _wire(self, t):
         return t.cpu() if self.staged else t
+
+    def all_gather(self, t):
+        """Rank r's t (the same shape on every rank) -> [t of rank 0, ..., t of
+        rank W-1]: one collective."""
+        import torch
+        w = self._wire(t.contiguous())
+        outs = [torch.empty_like(w) for _ in range(self.world)]
+        self.dist.all_gather(outs, w)
+        return [o.to(t.device) for o in outs]
 
     def all_gather_v(self, t):
         """Rank r's t (variable first dimension) -> [t of rank 0, ..., t of rank W-1]."""

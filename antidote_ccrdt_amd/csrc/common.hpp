@@ -46,9 +46,20 @@ struct DevBuf {
   // resident topk_rmv sides): a buffer that must grow is re-allocated at
   // twice the request, so a steady stream re-allocates every few batches
   // instead of at each (a re-allocation of GBs costs milliseconds).
+  // When the doubled size does not fit on the device, the exact need is tried.
   int ensure_grow(uint64_t need) {
     if (need <= bytes && p) return CCRDT_OK;
-    return ensure(p ? 2 * need : need);
+    if (!p) return ensure(need);
+    CCRDT_HIP(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, 2 * need) == hipSuccess) {
+      bytes = 2 * need;
+      return CCRDT_OK;
+    }
+    p = nullptr;
+    (void)hipGetLastError();  // (the failed allocation's error is not sticky)
+    return ensure(need);
   }
   void release() {
     if (p) (void)hipFree(p);

@@ -86,7 +86,7 @@ void ccrdt_engine::release_all() {
     b.vc.release();
   }
   for (DevBuf& d : tier_ovf) d.release();
-  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &st_kp,
+  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl, &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
   release_types();
@@ -474,8 +474,10 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;  // (trmv_keep_kernel reads the count here)
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>(n_over, TRMV_LATER_GRID), E.stream));
   }
+  // the sum of the tiers' own intervals (tier 4 starts after a host round
+  // trip, whose gap is not kernel time)
   float kernel_ms = 0.f;
-  if (nk && ev > 1) CCRDT_HIP(hipEventElapsedTime(&kernel_ms, E.evt[0], E.evt[ev - 1]));
+  for (const auto& tm : E.trmv_tier_ms) kernel_ms += tm.second;
   CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
                            E.stream));
   for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];

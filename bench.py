@@ -5,13 +5,14 @@ One step = one pass of the hot path (antidote_ccrdt_topk_rmv update/2 for
 every effect of the batch, src/antidote_ccrdt_topk_rmv.erl:140-148) over one
 batch of synthetic input: 100M effect ops (90% add / 10% rmv, 8-DC vector
 clocks) CSR-grouped over 2^20 keys (BASELINE configs[2]), applied to fresh
-keys (new(100)), with the ops already resident in HBM.  With N ranks the same
-global keyspace is hash-sharded, owner(key) = splitmix64(key) mod N
-(antidote_ccrdt_amd/cluster.py): every rank generates the global stream, keeps
-its keys' ops (stream order kept), and a step is its apply plus the batch's
-two exchange steps (extras all-gather, replica-Vc max all-reduce).  Total work
-is fixed, so scaling is strong.  --weak gives every rank its own 2^20-key /
-100M-op stream instead (per-GPU work fixed, weak scaling).
+keys (new(100)), with the ops already resident in HBM.  Keys are independent
+CRDT objects, so N ranks hash-shard a keyspace of N x 2^20 keys: every rank
+applies its own 2^20 keys' 100M-op batch (per-GPU work fixed: weak scaling,
+no data-path collective) and a step adds the batch's two exchange steps
+(extras all-gather, replica-Vc max, one collective: cluster.TrmvShardExchange,
+the code path the tests check).  --strong instead hash-shards ONE global
+2^20-key stream over the ranks, owner(key) = splitmix64(key) mod N (every
+rank generates it and keeps its keys' ops in stream order): total work fixed.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -45,85 +46,31 @@ def parse():
     ap.add_argument("--steady-batches", type=int, default=4,
                     help="steady-state leg: batches 2..n+1 of the same stream applied onto the "
                          "resident keys after batch 1 (0 = skip)")
+    ap.add_argument("--cpu-steady-keys", type=int, default=1 << 16,
+                    help="keys of every steady batch the steady-state CPU baseline replays (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "trmv_pmc.json"))
-    ap.add_argument("--weak", action="store_true",
-                    help="N > 1: every rank its own 2^20-key stream (weak scaling) instead of a "
-                         "shard of the global keyspace")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: the ranks shard ONE global 2^20-key stream (strong scaling) instead "
+                         "of each applying its own 2^20 keys (weak scaling, the default)")
     ap.add_argument("--dist-backend", default=None,
                     help="N > 1: nccl (RCCL, default on GPUs) or gloo (host-staged; tests)")
     return ap.parse_args()
 
 
-class Exchange:
-    """The two per-batch exchange steps of the key-sharded cluster (SURVEY
-    §8(e), cluster.py): the shard's extra effects are packed on the device and
-    all-gathered (every replica ends with the same effect list), and the
-    shard's elementwise-max Vc is MAX-reduced.  Both ride ONE all-gather of a
-    packed buffer [count | Vc | the first FAST effect rows] (the Vc max is
-    taken from the gathered copies), so a step pays one collective and one
-    host sync; a rank with more than FAST effects triggers a second gather of
-    the full rows.  nccl = RCCL on device tensors; gloo (tests on a one-GPU
-    box) stages through the host."""
+def sample_keys(b, m: int):
+    """The first m keys of a batch (their ops in stream order, rmv clock rows
+    renumbered), as a new TrmvBatch: the CPU baselines' bounded sample."""
+    import numpy as np
 
-    ROWS_CAP = 1 << 20  # extra effects per rank and batch (the bench stream makes ~46)
-    FAST = 256          # effect rows that ride the first gather
-
-    def __init__(self, eng, n_dc, world, backend, device, dist):
-        import numpy as np
-        import torch
-        from antidote_ccrdt_amd.engine import DeviceArray
-        self.eng, self.world, self.dist, self.np, self.torch = eng, world, dist, np, torch
-        self.w = 6 + n_dc
-        self.d = n_dc
-        self.head = 1 + n_dc  # int64 words before the rows: count (low 32 bits), Vc
-        n = self.head + self.ROWS_CAP * self.w
-        self.on_dev = backend == "nccl"
-        if self.on_dev:
-            self.pack = torch.zeros(n, dtype=torch.int64, device=torch.device("cuda", device))
-            base = self.pack.data_ptr()
-        else:
-            self.d_pack = DeviceArray(np.zeros(n, np.int64))
-            base = self.d_pack.p
-            self.h_head = np.zeros(self.head + self.FAST * self.w, np.int64)
-        self.p_cnt, self.p_vc, self.p_rows = base, base + 8, base + 8 * self.head
-        self.n_gathered = 0
-        self.replica_vc = None
-
-    def _d2h(self, host, dptr, nbytes):
-        from antidote_ccrdt_amd import _lib
-        _lib.check(_lib.lib.ccrdt_memcpy_d2h(_lib.ptr(host), dptr, nbytes), "d2h")
-
-    def run(self):
-        torch, dist = self.torch, self.dist
-        self.eng.extras_device(self.p_rows, self.ROWS_CAP, self.p_cnt)
-        self.eng.replica_vc_device(self.p_vc)
-        self.eng.sync()
-        L = self.head + self.FAST * self.w
-        if self.on_dev:
-            mine = self.pack[:L]
-        else:
-            self._d2h(self.h_head, self.p_cnt, self.h_head.nbytes)
-            mine = torch.from_numpy(self.h_head)
-        outs = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(outs, mine)
-        allp = torch.stack(outs)
-        cnts = allp[:, 0] & 0xFFFFFFFF
-        m, tot = (int(v) for v in torch.stack([cnts.max(), cnts.sum()]).tolist())
-        self.replica_vc = allp[:, 1:1 + self.d].max(0).values
-        if m > self.ROWS_CAP:
-            raise RuntimeError(f"bench exchange: {m} extra effects > {self.ROWS_CAP} rows")
-        if m > self.FAST:  # rare: the full rows in a second gather
-            if self.on_dev:
-                rows = self.pack[self.head:self.head + m * self.w]
-            else:
-                h = self.np.zeros(m * self.w, self.np.int64)
-                self._d2h(h, self.p_rows, h.nbytes)
-                rows = torch.from_numpy(h)
-            outs = [torch.empty_like(rows) for _ in range(self.world)]
-            dist.all_gather(outs, rows)
-            if self.on_dev:  # the next step's extras overwrite the rows this gather reads
-                torch.cuda.current_stream().synchronize()
-        self.n_gathered = tot
+    from antidote_ccrdt_amd.engine import TrmvBatch
+    n_s = int(b.key_ptr[m])
+    kind = np.array(b.kind[:n_s])
+    ts = np.array(b.ts[:n_s], np.int64)
+    rm = kind >= 2
+    rows = ts[rm]
+    ts[rm] = np.arange(rows.shape[0], dtype=np.int64)
+    return TrmvBatch(np.array(b.key_ptr[:m + 1]), kind, np.array(b.id[:n_s]), np.array(b.score[:n_s]),
+                     np.array(b.dc[:n_s]), ts, np.ascontiguousarray(b.rmv_vc[rows]))
 
 
 def cpu_share() -> int:
@@ -176,27 +123,40 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    sharded = world > 1 and not args.weak
+    sharded = world > 1 and args.strong
     seed = 0xCC0DE + 2 + (0 if sharded else 1_000_003 * rank)
     t_gen = time.perf_counter()
     b = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6, rmv_pm=100,
                  lag_max=64, seed=seed)
     n_local_keys = args.n_keys
-    if sharded:  # this rank's shard of the global keyspace (cluster.py)
-        from antidote_ccrdt_amd.cluster import owned_keys, route
-        my_keys = owned_keys(args.n_keys, world, rank)
-        b = route(b, my_keys).batch
-        n_local_keys = int(my_keys.shape[0])
+    shard = op_index = None
+    if world > 1:
+        # this rank's shard (cluster.ShardedTopkRmv: the tested multi-GPU code
+        # path, its exchange TrmvShardExchange); weak (default): every rank its
+        # own 2^20 keys and stream, the same apply + exchange
+        from antidote_ccrdt_amd.cluster import ShardedTopkRmv, TorchCollective
+        coll = TorchCollective(dist)
+        if sharded:
+            shard = ShardedTopkRmv(args.n_keys, args.k, args.n_dc, device=device, coll=coll)
+            sh = shard.route(b)
+            b = sh.batch
+            op_index = torch.from_numpy(sh.op_index).to(shard.xchg.dev)
+        else:
+            shard = ShardedTopkRmv(args.n_keys, args.k, args.n_dc, rank=0, world=1, device=device, coll=coll)
+        n_local_keys = len(shard.keys)
     t_gen = time.perf_counter() - t_gen
     db = DeviceTrmvBatch(b)
-    eng = TopkRmvEngine(n_local_keys, args.k, args.n_dc, device=device)
-    xchg = Exchange(eng, args.n_dc, world, backend, device, dist) if world > 1 else None
+    eng = shard.engine if shard is not None else TopkRmvEngine(n_local_keys, args.k, args.n_dc, device=device)
+    xres = {}
 
     def step():
-        eng.reset()            # every key back to new(K): O(1), no traffic
-        eng.apply_device(db)   # scan -> apply kernel(s) -> status
-        if xchg is not None:   # the batch's two exchange steps
-            xchg.run()
+        eng.reset()              # every key back to new(K): O(1), no traffic
+        if shard is None:
+            eng.apply_device(db)  # scan -> apply kernel(s) -> status
+        else:                    # the apply, then the batch's two exchange steps
+            shard.apply_device(db, op_index)
+            rows, vc, _ = shard.xchg.run()
+            xres.update(rows=rows, vc=vc)
 
     for _ in range(args.warmup):
         step()
@@ -300,11 +260,16 @@ def main():
             return int((ks["np"].astype(np.int64) * 18 + ks["nm"].astype(np.int64) * 17 +
                         ks["nr"].astype(np.int64) * 8 * D).sum()) + n_local_keys * (32 + 8 * D)
         ks_prev = eng.key_sizes()
+        # the steady CPU baseline's sample: the same first keys of every batch
+        cpu_m = min(args.cpu_steady_keys, n_local_keys) if (rank == 0 and world == 1) else 0
+        cpu_samples = [sample_keys(b, cpu_m)] if cpu_m else []
         for i in range(1, args.steady_batches + 1):
             bi = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6,
                           rmv_pm=100, lag_max=64, seed=seed + 7919 * i, clock0=i * args.n_ops)
             if sharded:
-                bi = route(bi, my_keys).batch
+                bi = shard.route(bi).batch
+            if cpu_m:
+                cpu_samples.append(sample_keys(bi, cpu_m))
             op_b = int(np.where(bi.kind >= 2, 9 + 8 * D, 26).astype(np.int64).sum())
             dbi = DeviceTrmvBatch(bi)
             del bi
@@ -349,6 +314,36 @@ def main():
                                         "written (player 18 B, Masked element 17 B, Removals row 8*D B, "
                                         "key 32 + 8*D B) + 32 B per extra effect"},
                   "batches": rows}
+        if cpu_samples:
+            # the oracle on the same keys' batches 2..n onto its own resident
+            # state (batch 1 applied untimed): the CPU side of the path Antidote
+            # drives, 1 thread and every CPU of the process's share
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as orc
+            nt = cpu_share()
+            res = {}
+            for name, thr in (("1_thread", 1), ("all_cores", nt)):
+                o = orc.TrmvOracle(cpu_m, args.k, args.n_dc)
+                o.apply(cpu_samples[0], thr, want_extra=True)
+                n_s, tc = 0, 0.0
+                for sb in cpu_samples[1:]:
+                    t1 = time.perf_counter()
+                    o.apply(sb, thr, want_extra=True)
+                    tc += time.perf_counter() - t1
+                    n_s += sb.n_ops
+                res[name] = {"value": n_s / tc, "unit": "ops/s", "cores": thr, "kind": "port"}
+                del o
+            gpu_rate = steady["ops_per_s_mean"]
+            kern_rate = n_step / (steady["roofline"]["kernel_ms"] * 1e-3)
+            steady["cpu_baseline"] = {
+                **res,
+                "sample": f"first {cpu_m} keys of every steady batch ({sum(x.n_ops for x in cpu_samples[1:])} "
+                          f"effect ops over batches 2..{args.steady_batches + 1}, batch 1 applied untimed), "
+                          f"C++ -O3 restatement (oracle/ccrdt_oracle.hpp) on {cpu_model()}; CPU restatement, "
+                          f"not BEAM",
+                "gpu_over_cpu_wall": {k: gpu_rate / v["value"] for k, v in res.items()},
+                "gpu_kernel_over_cpu": {k: kern_rate / v["value"] for k, v in res.items()}}
+            del cpu_samples
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_sample_keys > 0:  # reported at N=1 only
@@ -357,11 +352,8 @@ def main():
 
         import oracle as orc
         m = min(args.cpu_sample_keys, args.n_keys)
-        n_s = int(b.key_ptr[m])
-        kind = b.kind[:n_s]
-        n_r = int(np.count_nonzero(kind >= 2))
-        sb = TrmvBatch(b.key_ptr[:m + 1].copy(), kind, b.id[:n_s], b.score[:n_s], b.dc[:n_s],
-                       b.ts[:n_s], b.rmv_vc[:n_r])
+        sb = sample_keys(b, m)
+        n_s = sb.n_ops
         o = orc.TrmvOracle(m, args.k, args.n_dc)
         tc = time.perf_counter()
         o.apply(sb, 1, want_extra=True)
@@ -438,10 +430,12 @@ def main():
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),
-                "exchange": (None if xchg is None else
-                             {"backend": backend, "extras_all_gathered": xchg.n_gathered,
-                              "replica_vc": [int(v) for v in xchg.replica_vc.cpu().tolist()],
-                              "in_step": "one all_gather of [count | Vc | first 256 effect rows] (Vc max taken from the gathered copies; a second gather only past 256 rows)"}),
+                "exchange": (None if shard is None else
+                             {"backend": backend, "extras_all_gathered": int(xres["rows"].shape[0]),
+                              "replica_vc": [int(v) for v in xres["vc"].cpu().tolist()],
+                              "in_step": "cluster.TrmvShardExchange.run: one all_gather of [count | Vc | "
+                                         "first 256 effect rows] (Vc max taken from the gathered copies; a "
+                                         "second gather only past 256 rows), extras sorted by global op"}),
             },
         }
         print(json.dumps(out), flush=True)

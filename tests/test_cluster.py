@@ -143,3 +143,187 @@ def test_sharded_engines_on_gpu(gpu):
             assert _key_view(stv, j) == _key_view(st_full, g)
     ex = np.concatenate(ex_all)
     assert np.array_equal(ex[np.argsort(ex[:, 0])], ex_full)
+
+
+# ------------------------------------------- the step path (apply + exchange)
+def _step_worker(rank, world, port, errf):
+    """ShardedTopkRmv.step over gloo with oracle engines: the exchange
+    (TrmvShardExchange.run, the code bench.py --gpus N times) gives every
+    rank the single-replica extras in stream order and the replica Vc."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = _batch()
+        st_full, ex_full = _full_oracle(b)
+        s = ShardedTopkRmv(N_KEYS, K, D, engine_factory=lambda nk, kk, d: orc.TrmvOracle(nk, kk, d))
+        s.xchg.FAST = 8  # (the second, variable gather too: more than 8 effects per rank)
+        rows, vc = s.step(b)
+        assert np.array_equal(rows, ex_full), "gathered extras differ from the single-replica stream"
+        assert np.array_equal(vc, st_full["vc"].max(axis=0))
+        st = s.export()
+        for j, g in enumerate(s.keys):
+            assert _key_view(st, j) == _key_view(st_full, g)
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_step_gloo(world, tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_step_worker, args=(world, _free_port(), errf), nprocs=world, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+class _CapOracle:
+    """The oracle as a shard engine whose per-key capacity is `cap` ops in one
+    batch: a key past it keeps its state and is reported as the engine's
+    CCRDT_EKEYCAP does (KeyCapacityError, .keys local, .extra the batch's
+    extras for every other key)."""
+
+    def __init__(self, nk, kk, d, cap):
+        self.o, self.nk, self.cap = orc.TrmvOracle(nk, kk, d), nk, cap
+
+    def apply(self, b, want_extra=True):
+        kp = np.asarray(b.key_ptr, np.int64)
+        over = np.nonzero(np.diff(kp) > self.cap)[0]
+        if not over.shape[0]:
+            return self.o.apply(b, 1, want_extra=True)
+        from antidote_ccrdt_amd.cluster import _drop_keys
+        sub = _drop_keys(b, over)
+        x = self.o.apply(sub, 1, want_extra=True)
+        keep = np.ones(b.n_ops, bool)
+        for k in over:
+            keep[kp[k]:kp[k + 1]] = False
+        full = {f: np.zeros((b.n_ops,) + np.asarray(v).shape[1:], np.asarray(v).dtype) for f, v in x.items()}
+        full["kind"][:] = 255
+        for f in full:
+            full[f][keep] = x[f]
+        err = _lib.KeyCapacityError(_lib.EKEYCAP, "cap", "over")
+        err.keys, err.extra = over, full
+        raise err
+
+    def export(self):
+        return self.o.export()
+
+
+def _cap_worker(rank, world, port, errf):
+    """A key over the engine's capacity on one rank: every rank raises
+    KeyCapacityError with the same global ids after the exchange (no rank
+    left inside a collective), the committed extras of every other key are
+    exchanged, and the next batch leaves the host key's ops out."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = _batch()
+        lens = np.diff(np.asarray(b.key_ptr, np.int64))
+        cap = int(lens.max()) - 1  # the longest key(s) over
+        big = np.nonzero(lens > cap)[0]
+        s = ShardedTopkRmv(N_KEYS, K, D, engine_factory=lambda nk, kk, d: _CapOracle(nk, kk, d, cap))
+        try:
+            s.step(b)
+            raise AssertionError("no KeyCapacityError")
+        except _lib.KeyCapacityError as err:
+            assert list(err.keys) == list(big), err.keys
+            rows, vc = err.extra
+        # the reference without that key's ops
+        from antidote_ccrdt_amd.cluster import _drop_keys
+        o = orc.TrmvOracle(N_KEYS, K, D)
+        sub = _drop_keys(b, big)
+        xo = o.apply(sub, 1, want_extra=True)
+        keep = np.ones(b.n_ops, bool)
+        for k in big:
+            keep[int(b.key_ptr[k]):int(b.key_ptr[k + 1])] = False
+        want = pack_extras(TrmvExtra(**xo), np.nonzero(keep)[0])
+        assert np.array_equal(rows, want)
+        # next batch: the host key's ops stay out of the engine, no new raise
+        b2 = gen_trmv(N_OPS // 4, N_KEYS, D, n_players=12, score_max=50, rmv_pm=150, lag_max=16,
+                      seed=0xC2, clock0=10 ** 7)
+        s.step(b2)
+        o.apply(_drop_keys(b2, big), 1, want_extra=True)
+        st, sto = s.export(), o.export()
+        for j, g in enumerate(s.keys):
+            assert _key_view(st, j) == _key_view(sto, g)
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_keycap_gloo(tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_cap_worker, args=(2, _free_port(), errf), nprocs=2, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+# --------------------------------------- HIP engines, one process per rank
+GN_KEYS, GN_OPS = 1 << 16, 3_000_000
+
+
+def _gpu_batch(i):
+    return gen_trmv(GN_OPS, GN_KEYS, D, n_players=160, score_max=10**6, rmv_pm=100, lag_max=64,
+                    seed=0xCC0DE + 40 + i, clock0=i * GN_OPS)
+
+
+def _gpu_step_worker(rank, world, port, errf):
+    """Two ranks, each a ShardedTopkRmv over its HIP engine (device path:
+    apply_device + TrmvShardExchange packed on the GPU, gloo staging the
+    collective through the host), two batches (fresh keys, then resident
+    ones): every rank's shard equals one oracle over the whole keyspace, and
+    the gathered extras and replica Vc equal the oracle's."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = ShardedTopkRmv(GN_KEYS, 100, D, device=0)
+        assert s.on_device and s.coll.staged
+        o = orc.TrmvOracle(GN_KEYS, 100, D)
+        for i in range(2):
+            b = _gpu_batch(i)
+            rows, vc = s.step(b)
+            xo = o.apply(b, 16, want_extra=True)
+            want = pack_extras(TrmvExtra(**xo), np.arange(b.n_ops, dtype=np.int64))
+            assert np.array_equal(rows, want), (i, rows.shape, want.shape)
+            sto = o.export()
+            assert np.array_equal(vc, sto["vc"].max(axis=0))
+            st = s.export()
+            stv = {f: getattr(st, f) for f in st.__dataclass_fields__}
+            for j, g in enumerate(s.keys):
+                assert _key_view(stv, j) == _key_view(sto, g), (i, g)
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_step_two_processes_gpu(gpu, tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_gpu_step_worker, args=(2, _free_port(), errf), nprocs=2, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+def test_replicated_keycap_raises_after_quiescence():
+    """Replication mode: a replica whose engine hands a key to the host path
+    finishes the step (every round delivered), then the step raises
+    KeyCapacityError with that key; the next step does not raise again."""
+    from antidote_ccrdt_amd.cluster import ReplicatedTopkRmv, replicate_local
+    W, NK = 2, 200
+    bs = [gen_trmv(6000, NK, D, n_players=12, score_max=50, rmv_pm=150, lag_max=16, seed=0xD0 + r)
+          for r in range(W)]
+    cap = int(max(np.diff(np.asarray(b.key_ptr, np.int64)).max() for b in bs))  # no key over alone ...
+    reps = [ReplicatedTopkRmv(NK, K, D, rank=r, world=W, engine=_CapOracle(NK, K, D, cap)) for r in range(W)]
+    with pytest.raises(_lib.KeyCapacityError) as ei:  # ... but the delivered rows push some past it
+        replicate_local(reps, bs)
+    assert len(ei.value.keys) > 0
+    b2 = [gen_trmv(200, NK, D, n_players=12, score_max=50, seed=0xE0 + r, clock0=10 ** 6) for r in range(W)]
+    replicate_local(reps, b2)
