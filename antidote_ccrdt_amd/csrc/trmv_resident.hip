@@ -43,7 +43,7 @@
 // Diagnostic build only (-DTRMV_PROF): per-phase s_memtime stamps summed over
 // a sample of keys; read with ccrdt_debug_resident_prof().
 #ifdef TRMV_PROF
-__device__ unsigned long long g_resident_prof[16];
+__device__ unsigned long long g_resident_prof[32];
 #define RPROF_STAMP(v)                                                        \
   do {                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                        \
@@ -1156,9 +1156,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const int64_t mk = rl64(ob.key[0], 0);
         const bool rel = seg_r && (inobs ? (cm_s > ms || (cm_s == ms && cm_t > ot)) : (ob.n < K || cm_k > mk));
         const uint64_t relm = ballot(rel);
-        RCOUNT(11, __builtin_popcountll(relm));
-        RCOUNT(13, 1);
+        RCOUNT(27, __builtin_popcountll(relm));
+        RCOUNT(29, 1);
         if (!relm) return;
+        RPROF(16);
         bool rem0 = false, rem1 = false;
         for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries
           const uint32_t xp = rl32(cu_p, (int)__builtin_ctzll(t));
@@ -1177,6 +1178,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
                               (uint32_t)__builtin_popcountll(ballot(v1 && ob.key[1] < kx));
           abc = (int)lane == x ? ab : abc;
         }
+        RPROF(17);
         const uint64_t rm0 = ballot(rem0 && lane < ob.n), rm1 = ballot(rem1 && 64u + lane < ob.n);
         const uint32_t nrem = (uint32_t)__builtin_popcountll(rm0) + (uint32_t)__builtin_popcountll(rm1);
         const uint32_t m = (uint32_t)__builtin_popcountll(relm);
@@ -1212,6 +1214,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           }
         }
         wave_lds_sync();
+        RPROF(18);
         ob.n = T - drop;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -1237,6 +1240,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         // ---- the rmv at hi: the run's largest elements, then Masked[Id]
         // after the filter (:255-266), then Observed (:267-298)
         catch_up(run);
+        RPROF(20);
         const uint32_t kd = rl32(kdr, (int)hi);
         const uint32_t X = kd >> 8;
         const uint32_t r = rl32(crr, (int)hi);
@@ -1261,8 +1265,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             if (lane == 0) pf_and(L, X, Q_OBS);
             wave_lds_sync();
             int64_t wk = 0;
-            RCOUNT(15, 1);
+            RCOUNT(31, 1);
+            RPROF(21);
             const uint32_t w = r_promote(L, pid, np, wk);
+            RPROF(22);
             if (w == RNONE) {  // (:283-289): Obs[Id] dropped, Min of the rest
               ob_remove(ob, ix);
             } else {  // promote the largest (:290-295)
@@ -1387,10 +1393,10 @@ int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t
 }  // namespace ccrdt
 
 #ifdef TRMV_PROF
-extern "C" int ccrdt_debug_resident_prof(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_resident_prof), 16 * 8) != hipSuccess) return 4;
+extern "C" int ccrdt_debug_resident_prof(unsigned long long* out16, int reset) {  // (32 entries)
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_resident_prof), 32 * 8) != hipSuccess) return 4;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_resident_prof), z, sizeof(z)) != hipSuccess) return 4;
   }
   return 0;

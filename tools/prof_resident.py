@@ -13,9 +13,12 @@ sys.path.insert(0, ROOT)
 from antidote_ccrdt_amd import _lib  # noqa: E402
 from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv  # noqa: E402
 
-NAMES = ["P1 old players + sorted Obs", "P2 resolve + layout", "P3 bulk copy",
-         "C load/validate/clocks/dups", "C sort + appends", "C replays", "P4 scan + prefilter",
-         "P4 relevant adds", "P4 rmvs + promotions", "P5 records (+ last catch-up)"]
+NAMES = {0: "P1 old players + sorted Obs", 1: "P2 resolve + layout", 2: "P3 bulk copy",
+         3: "C load/validate/clocks/dups", 4: "C sort + appends", 5: "C replays", 6: "P4 scan + prefilter",
+         16: "P4 merge: prefilter (runs with relevant adds)", 17: "P4 merge: upgrade + rank loops",
+         18: "P4 merge: staging writes", 7: "P4 merge: restage (+ whole merges with none relevant)",
+         20: "P4 rmv: catch-up", 21: "P4 rmv: find + impact test (impacting)", 22: "P4 rmv: promote scan",
+         8: "P4 rmv: shift + emit (+ non-impacting tests)", 9: "P5 records (+ last catch-up)"}
 n_ops = int(os.environ.get("N_OPS", 100_000_000))
 nk = 1 << 20
 eng = TopkRmvEngine(nk, 100, 8)
@@ -24,7 +27,7 @@ try:
     f.argtypes = [C.c_void_p, C.c_int]
 except AttributeError:
     f = None
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 for i in range(int(os.environ.get("BATCHES", 3))):
     b = gen_trmv(n_ops, nk, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64,
                  seed=0xCC0DE + 2 + 7919 * i, clock0=i * n_ops)
@@ -40,9 +43,9 @@ for i in range(int(os.environ.get("BATCHES", 3))):
     if not f or i == 0:
         continue
     f(buf, 1)
-    tot = sum(buf[j] for j in range(len(NAMES))) or 1
-    for j, n in enumerate(NAMES):
+    tot = sum(buf[j] for j in NAMES) or 1
+    for j, n in NAMES.items():
         print(f"  {n:30s} {buf[j] / tot * 100:6.1f} %   {buf[j] / (nk / 64):9.0f} cyc/key")
     per = nk / 64
-    print(f"  per key: relevant adds {buf[11] / per:.1f} of {buf[12] / per:.1f} non-dominated adds, "
-          f"runs {buf[13] / per:.1f}, Observed changes {buf[14] / per:.1f}, impacting rmvs {buf[15] / per:.1f}")
+    print(f"  per key: relevant adds {buf[27] / per:.1f}, runs {buf[29] / per:.1f}, "
+          f"impacting rmvs {buf[31] / per:.1f}")

@@ -2,7 +2,7 @@ import os, sys, time
 sys.path.insert(0, os.getcwd())
 from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv
 nk, n_ops = 1 << 20, 100_000_000
-eng = TopkRmvEngine(nk, 100, 8)
+eng = TopkRmvEngine(nk, 100, 8)  # (CCRDT_LIB selects the build)
 for i in range(4):
     b = gen_trmv(n_ops, nk, 8, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64, seed=0xCC0DE + 2 + 7919 * i, clock0=i * n_ops)
     db = DeviceTrmvBatch(b); del b
