@@ -735,7 +735,24 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   SPROF(1);
 
   // ---- K3. old slabs (except replayed players') and old Removals rows
-  if (!KA->fresh && span) {
+  if (PCAP > 1024 && !KA->fresh && span && om.np > 64) {
+    // The HBM class with many players: one lane per old player copies its
+    // slab (O(np + span); the position windows below would sweep every
+    // player for every 64 positions)
+    for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool act = j < om.np;
+      const uint32_t sl = act ? L.oslab[j] : 0u;
+      const uint32_t cnt = (act && !(L.opd[j] & F_RMV)) ? (sl >> 16) : 0u;
+      const uint64_t src = (uint64_t)om.m_off + (sl & 0xFFFFu);
+      const uint64_t dst = (uint64_t)nm.m_off + (act ? (L.nslab[j] & 0xFFFFu) : 0u);
+      for (uint32_t e = 0; e < cnt; ++e) {
+        KA->new_s.m_score[dst + e] = KA->old_s.m_score[src + e];
+        KA->new_s.m_ts[dst + e] = KA->old_s.m_ts[src + e];
+        KA->new_s.m_dc[dst + e] = KA->old_s.m_dc[src + e];
+      }
+    }
+  } else if (!KA->fresh && span) {
     int32_t prev = -1;  // owner of the position before the window
     // the next window's elements load while this one is placed
     int64_t nsc = 0, nts = 0;

@@ -24,3 +24,7 @@ for spec in default "$@"; do
   grep -E "scan|resident" "$f" | cut -d, -f1-8
   grep "chain ms" "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log"
 done
+cd "$GRAFT_REPO_ROOT"
+if [ -f antidote_ccrdt_amd/lib/libccrdt_prof.so ] && [ -z "$SKIP_PROF" ]; then
+  echo "== tierR phases"; CCRDT_LIB=$GRAFT_REPO_ROOT/antidote_ccrdt_amd/lib/libccrdt_prof.so timeout -k 10 300 python tools/prof_resident.py > gpurun_out/tierR_phases.txt 2>&1; rc=$?; cat gpurun_out/tierR_phases.txt; [ $rc -eq 0 ] || exit $rc
+fi
