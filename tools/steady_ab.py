@@ -1,5 +1,5 @@
 import os, sys, time
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from antidote_ccrdt_amd.engine import DeviceTrmvBatch, TopkRmvEngine, gen_trmv
 nk, n_ops = 1 << 20, 100_000_000
 eng = TopkRmvEngine(nk, 100, 8)  # (CCRDT_LIB selects the build)
