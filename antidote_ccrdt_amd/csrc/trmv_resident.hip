@@ -218,8 +218,9 @@ __device__ __forceinline__ void pf_and(RLds& L, uint32_t p, uint32_t m) {  // cl
 // --------------------------------------------------- the sorted Observed
 // Entry r = lane r % 64 of slot r / 64, ascending by key = (Score, Id);
 // pl = player | Obs[Id]'s DcId << 16; entries >= n hold (INT64_MAX, RNONE).
+// (Obs[Id]'s Ts lives per player in LDS, RLds::ots: an entry is three dwords.)
 struct Obs {
-  int64_t key[2], ts[2];
+  int64_t key[2];
   uint32_t pl[2];
   uint32_t n;
 };
@@ -230,7 +231,6 @@ __device__ __forceinline__ void ob_clear_tail(Obs& o) {
   for (int t = 0; t < 2; ++t)
     if (64u * t + l >= o.n) {
       o.key[t] = INT64_MAX;
-      o.ts[t] = 0;
       o.pl[t] = RNONE;
     }
 }
@@ -242,10 +242,10 @@ __device__ __forceinline__ void ob_shift(Obs& o, uint32_t lo, uint32_t hi) {
   const uint32_t l = (uint32_t)lane_id();
   const bool in0 = DOWN ? (l >= lo && l < hi) : (l >= lo && l <= hi);
   const bool in1 = DOWN ? (64u + l >= lo && 64u + l < hi) : (64u + l >= lo && 64u + l <= hi);
-  uint32_t w0[5] = {lo32(o.key[0]), hi32(o.key[0]), lo32(o.ts[0]), hi32(o.ts[0]), o.pl[0]};
-  uint32_t w1[5] = {lo32(o.key[1]), hi32(o.key[1]), lo32(o.ts[1]), hi32(o.ts[1]), o.pl[1]};
+  uint32_t w0[3] = {lo32(o.key[0]), hi32(o.key[0]), o.pl[0]};
+  uint32_t w1[3] = {lo32(o.key[1]), hi32(o.key[1]), o.pl[1]};
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 3; ++k) {
     uint32_t n0, n1;
     if (DOWN) {
       n0 = wshl1(w0[k], rl32(w1[k], 0));
@@ -258,23 +258,19 @@ __device__ __forceinline__ void ob_shift(Obs& o, uint32_t lo, uint32_t hi) {
     w1[k] = in1 ? n1 : w1[k];
   }
   o.key[0] = mk64(w0[0], w0[1]);
-  o.ts[0] = mk64(w0[2], w0[3]);
-  o.pl[0] = w0[4];
+  o.pl[0] = w0[2];
   o.key[1] = mk64(w1[0], w1[1]);
-  o.ts[1] = mk64(w1[2], w1[3]);
-  o.pl[1] = w1[4];
+  o.pl[1] = w1[2];
 }
 
-__device__ __forceinline__ void ob_put(Obs& o, uint32_t q, int64_t key, int64_t ts, uint32_t pl) {
+__device__ __forceinline__ void ob_put(Obs& o, uint32_t q, int64_t key, uint32_t pl) {
   const uint32_t l = (uint32_t)lane_id();
   if (l == (q & 63u)) {
     if (q < 64u) {
       o.key[0] = key;
-      o.ts[0] = ts;
       o.pl[0] = pl;
     } else {
       o.key[1] = key;
-      o.ts[1] = ts;
       o.pl[1] = pl;
     }
   }
@@ -301,17 +297,17 @@ __device__ __forceinline__ uint32_t ob_get32(const uint32_t f[2], uint32_t i) {
   return i < 64u ? a : b;
 }
 
-// Entry r removed and (key, ts, pl) inserted, in one range shift.
-__device__ __forceinline__ void ob_replace(Obs& o, uint32_t r, int64_t key, int64_t ts, uint32_t pl) {
+// Entry r removed and (key, pl) inserted, in one range shift.
+__device__ __forceinline__ void ob_replace(Obs& o, uint32_t r, int64_t key, uint32_t pl) {
   const uint32_t q = ob_rank(o, key, r);
   if (q >= r) ob_shift<true>(o, r, q);
   else ob_shift<false>(o, q + 1, r);
-  ob_put(o, q, key, ts, pl);
+  ob_put(o, q, key, pl);
 }
-__device__ __forceinline__ void ob_insert(Obs& o, int64_t key, int64_t ts, uint32_t pl) {
+__device__ __forceinline__ void ob_insert(Obs& o, int64_t key, uint32_t pl) {
   const uint32_t q = ob_rank(o, key, RNONE);
   ob_shift<false>(o, q + 1, o.n);
-  ob_put(o, q, key, ts, pl);
+  ob_put(o, q, key, pl);
   ++o.n;
 }
 __device__ __forceinline__ void ob_remove(Obs& o, uint32_t r) {
@@ -330,9 +326,7 @@ __device__ __forceinline__ void ob_sort(Obs& o) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
       if (j == 64) {  // partner = the other slot, same lane (k == 128: ascending)
         if (o.key[1] < o.key[0]) {
-          int64_t t;
-          t = o.key[0]; o.key[0] = o.key[1]; o.key[1] = t;
-          t = o.ts[0]; o.ts[0] = o.ts[1]; o.ts[1] = t;
+          const int64_t t = o.key[0]; o.key[0] = o.key[1]; o.key[1] = t;
           const uint32_t u = o.pl[0]; o.pl[0] = o.pl[1]; o.pl[1] = u;
         }
         continue;
@@ -341,14 +335,13 @@ __device__ __forceinline__ void ob_sort(Obs& o) {
       for (int s = 0; s < 2; ++s) {
         const uint32_t i = 64u * s + l;
         const int src = (int)(l ^ j);
-        const int64_t pk = shfl64(o.key[s], src), pt = shfl64(o.ts[s], src);
+        const int64_t pk = shfl64(o.key[s], src);
         const uint32_t pp = shfl32(o.pl[s], src);
         const bool lower = (i & j) == 0;  // this position is the lower of its pair
         const bool asc = (i & k) == 0;    // this block sorts ascending
         const bool take = (lower == asc) ? pk < o.key[s] : o.key[s] < pk;
         if (take) {
           o.key[s] = pk;
-          o.ts[s] = pt;
           o.pl[s] = pp;
         }
       }
@@ -522,78 +515,92 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
   if (lane == 0) L.nex = 0u;
   wave_lds_sync();
 
-  // ---- P1. old players: records, then the Obs[Id] / largest elements they
-  // name (two halves of two slots: fewer loads in flight at once).
+  // ---- P1. old players: records of all four slots, then the Obs[Id] /
+  // largest elements they name (two rounds of loads in flight), then LDS and
+  // the Id hash (the four slots' probes interleaved).
   // Observed's entries are players 0..nobs-1 when the key was last written
   // by tier R (checked), else gathered and sorted here.
   int64_t pid[RSL];
   uint32_t span = 0, inobs = 0;  // inobs: bit u = player of slot u in Observed
-  int64_t k01[2], t01[2];        // slots 0-1: Obs[Id]'s key and Ts
+  int64_t k01[2];                // slots 0-1: Obs[Id]'s key
   uint32_t odr[RSL];             // Obs[Id]'s DcId by slot
   bool wide = false;
+  {
+    uint32_t info[RSL], slab[RSL], gb[RSL];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint32_t info[2], slab[2], gb[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const uint32_t p = 64u * (2 * h + t) + lane;
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t p = 64u * u + lane;
       const bool v = p < om.np;
       const uint64_t pp = (uint64_t)om.p_off + (v ? p : 0u);
-      pid[2 * h + t] = v ? KA->old_s.pl_id[pp] : 0;
-      info[t] = v ? KA->old_s.pl_info[pp] : RNONE;
-      slab[t] = v ? KA->old_s.pl_slab[pp] : 0u;
-      gb[t] = (v && (slab[t] >> 16) > 1) ? (uint32_t)KA->old_s.pl_gb[pp] : 0u;
+      pid[u] = v ? KA->old_s.pl_id[pp] : 0;
+      info[u] = v ? KA->old_s.pl_info[pp] : RNONE;
+      slab[u] = v ? KA->old_s.pl_slab[pp] : 0u;
+      gb[u] = (v && (slab[u] >> 16) > 1) ? (uint32_t)KA->old_s.pl_gb[pp] : 0u;
     }
+    int64_t os[RSL], ot[RSL], gs[RSL], gt[RSL];
+    uint32_t gd[RSL];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int u = 2 * h + t;
-      const uint32_t p = 64u * u + lane;
-      const uint32_t off = slab[t] & 0xFFFFu, cnt = slab[t] >> 16, obx = info[t] & 0xFFFFu;
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
       const uint64_t g0 = (uint64_t)om.m_off + off;
       const bool ho = obx != NONE16, hg = cnt != 0;
-      const int64_t os = ho ? KA->old_s.m_score[g0 + obx] : 0;
-      const int64_t ot = ho ? KA->old_s.m_ts[g0 + obx] : 0;
-      const uint32_t od = ho ? (uint32_t)KA->old_s.m_dc[g0 + obx] : 0u;
-      const int64_t gs = hg ? KA->old_s.m_score[g0 + gb[t]] : 0;
-      const int64_t gt = hg ? KA->old_s.m_ts[g0 + gb[t]] : 0;
-      const uint32_t gd = hg ? (uint32_t)KA->old_s.m_dc[g0 + gb[t]] : 0u;
-      if (h == 0) {
-        k01[t] = mkkey(os, pid[u]);
-        t01[t] = ot;
-      }
-      odr[u] = od;
+      os[u] = ho ? KA->old_s.m_score[g0 + obx] : 0;
+      ot[u] = ho ? KA->old_s.m_ts[g0 + obx] : 0;
+      odr[u] = ho ? (uint32_t)KA->old_s.m_dc[g0 + obx] : 0u;
+      gs[u] = hg ? KA->old_s.m_score[g0 + gb[u]] : 0;
+      gt[u] = hg ? KA->old_s.m_ts[g0 + gb[u]] : 0;
+      gd[u] = hg ? (uint32_t)KA->old_s.m_dc[g0 + gb[u]] : 0u;
+    }
+    uint32_t hh[RSL];
+    bool pend[RSL];
+#pragma unroll
+    for (int u = 0; u < RSL; ++u) {
+      const uint32_t p = 64u * u + lane;
+      const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
+      const bool ho = obx != NONE16;
+      if (u < 2) k01[u] = mkkey(os[u], pid[u]);
+      pend[u] = p < om.np;
+      hh[u] = rhash(pid[u]);
       if (p < om.np) {
-        wide |= !fits32(pid[u]) || !fits32(os) || !fits32(gs);
-        L.msc[p] = (int32_t)gs;
-        L.gts[p] = gt;
-        L.pf[p] = (ho ? Q_OBS : 0u) | (cnt ? Q_HASM : 0u) | ((info[t] >> 16) != NONE16 ? Q_ROWV : 0u);
-        L.gdc[p] = (uint8_t)gd;
+        wide |= !fits32(pid[u]) || !fits32(os[u]) || !fits32(gs[u]);
+        L.msc[p] = (int32_t)gs[u];
+        L.gts[p] = gt[u];
+        L.ots[p] = ot[u];  // (meaningful for players in Observed)
+        L.pf[p] = (ho ? Q_OBS : 0u) | (cnt ? Q_HASM : 0u) | ((info[u] >> 16) != NONE16 ? Q_ROWV : 0u);
+        L.gdc[p] = (uint8_t)gd[u];
         L.opos[p] = (uint16_t)obx;
-        L.gpos[p] = (uint16_t)gb[t];
-        L.u.r.oslab[p] = slab[t];
-        L.prow[p] = (uint16_t)(info[t] >> 16);
+        L.gpos[p] = (uint16_t)gb[u];
+        L.u.r.oslab[p] = slab[u];
+        L.prow[p] = (uint16_t)(info[u] >> 16);
         L.u.r.pid[p] = pid[u];
         L.u.r.nops[p] = 0;
         span = off + cnt > span ? off + cnt : span;
-        uint32_t hh = rhash(pid[u]);
-        for (;;) {  // insert into the hash (slots of 16 bits: CAS on the word)
-          uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[hh & ~1u]);
-          const uint32_t sh = (hh & 1u) * 16u;
-          uint32_t old = *w;
-          bool done = false;
-          while (((old >> sh) & 0xFFFFu) == RH_NONE) {
-            const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (p << sh));
-            if (prev == old) {
-              done = true;
-              break;
-            }
-            old = prev;
-          }
-          if (done) break;
-          hh = (hh + 1) & (2 * RP - 1);
-        }
       }
       inobs |= (ho ? 1u : 0u) << u;
+    }
+    // the Id hash (16-bit slots: CAS on the containing word); each round
+    // reads every pending slot's word, then claims the free ones
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) any |= pend[u];
+      if (!ballot(any)) break;
+      uint32_t cur[RSL];
+#pragma unroll
+      for (int u = 0; u < RSL; ++u)
+        cur[u] = pend[u] ? *reinterpret_cast<const uint32_t*>(&L.u.r.hs[hh[u] & ~1u]) : 0u;
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        if (!pend[u]) continue;
+        const uint32_t sh = (hh[u] & 1u) * 16u;
+        if (((cur[u] >> sh) & 0xFFFFu) == RH_NONE) {
+          const uint32_t p = 64u * u + lane;
+          uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[hh[u] & ~1u]);
+          if (atomicCAS(w, cur[u], (cur[u] & ~(0xFFFFu << sh)) | (p << sh)) == cur[u]) pend[u] = false;
+        } else {
+          hh[u] = (hh[u] + 1) & (2 * RP - 1);
+        }
+      }
     }
   }
   if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
@@ -617,7 +624,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         ob.key[t] = k01[t];
-        ob.ts[t] = t01[t];
         ob.pl[t] = (64u * t + lane) | (odr[t] << 16);
       }
     } else {
@@ -635,7 +641,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       for (int t = 0; t < 2; ++t) {
         const uint32_t r = 64u * t + lane;
         ob.key[t] = INT64_MAX;
-        ob.ts[t] = 0;
         ob.pl[t] = RNONE;
 #pragma unroll
         for (int u = 0; u < RSL; ++u) {
@@ -646,8 +651,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           if (here) {
             const uint32_t p = 64u * u + src;
             ob.key[t] = mkkey(L.msc[p], vi);  // Obs[Id]'s Score = the largest (I1)
-            // Obs[Id]'s Ts from the old pool (its slab position is L.opos)
-            ob.ts[t] = KA->old_s.m_ts[(uint64_t)om.m_off + (L.u.r.oslab[p] & 0xFFFFu) + L.opos[p]];
             ob.pl[t] = p | (vd << 16);
           }
         }
@@ -656,9 +659,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     }
   }
   ob_clear_tail(ob);
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-    if (64u * t + lane < ob.n) L.ots[ob.pl[t] & 0xFFFFu] = ob.ts[t];
   wave_lds_sync();
   RPROF(0);
   {
@@ -728,74 +728,77 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     bool wide = false;
     if (span) {
       int32_t prev = -1;
-      int64_t nsc = 0, nts = 0;
-      uint32_t ndc = 0;
-      if (lane < span) {
-        nsc = KA->old_s.m_score[(uint64_t)om.m_off + lane];
-        nts = KA->old_s.m_ts[(uint64_t)om.m_off + lane];
-        ndc = KA->old_s.m_dc[(uint64_t)om.m_off + lane];
-      }
-      for (uint32_t q0 = 0; q0 < span; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        const int64_t sc = nsc, ts = nts;
-        const uint32_t dc = ndc;
-        if (q + 64 < span) {
-          const uint64_t src = (uint64_t)om.m_off + q + 64;
-          nsc = KA->old_s.m_score[src];
-          nts = KA->old_s.m_ts[src];
-          ndc = KA->old_s.m_dc[src];
+      // four windows of 64 positions per round: their loads go out together
+      for (uint32_t g0 = 0; g0 < span; g0 += 256) {
+        int64_t wsc[4], wts[4];
+        uint32_t wdc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t q = g0 + 64u * i + lane;
+          const uint64_t src = (uint64_t)om.m_off + (q < span ? q : 0u);
+          wsc[i] = q < span ? KA->old_s.m_score[src] : 0;
+          wts[i] = q < span ? KA->old_s.m_ts[src] : 0;
+          wdc[i] = q < span ? (uint32_t)KA->old_s.m_dc[src] : 0u;
         }
-        // the owner of a position is the player whose slab starts last at or
-        // before it (slabs are not in player order: tier R writes players in
-        // Observed order); starts come from the start map, or for a span past
-        // its size from a sweep of every player
-        uint32_t st = 0;
-        if (smap) {
-          st = q < span ? (uint32_t)smap16[q] : 0u;
-        } else {
-          uint32_t* const mark = reinterpret_cast<uint32_t*>(smap16);  // (the map is unused here)
-          mark[lane] = 0u;
-          wave_lds_sync();
-          for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
-            const uint32_t j = j0 + lane;
-            const uint32_t sl = j < om.np ? L.u.r.oslab[j] : 0u;
-            const uint32_t off = sl & 0xFFFFu;
-            if ((sl >> 16) && off >= q0 && off < q0 + 64) mark[off - q0] = j + 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t q0 = g0 + 64u * i;
+          if (q0 >= span) break;
+          const uint32_t q = q0 + lane;
+          const int64_t sc = wsc[i], ts = wts[i];
+          const uint32_t dc = wdc[i];
+          // the owner of a position is the player whose slab starts last at
+          // or before it (slabs are not in player order: tier R writes
+          // players in Observed order); starts come from the start map, or
+          // for a span past its size from a sweep of every player
+          uint32_t st = 0;
+          if (smap) {
+            st = q < span ? (uint32_t)smap16[q] : 0u;
+          } else {
+            uint32_t* const mark = reinterpret_cast<uint32_t*>(smap16);  // (the map is unused here)
+            mark[lane] = 0u;
+            wave_lds_sync();
+            for (uint32_t j0 = 0; j0 < om.np; j0 += 64) {
+              const uint32_t j = j0 + lane;
+              const uint32_t sl = j < om.np ? L.u.r.oslab[j] : 0u;
+              const uint32_t off = sl & 0xFFFFu;
+              if ((sl >> 16) && off >= q0 && off < q0 + 64) mark[off - q0] = j + 1;
+            }
+            wave_lds_sync();
+            st = mark[lane];
+          }
+          uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
+          {  // inclusive max-scan (DPP): the last start at or before the lane
+            uint32_t o;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x111, 0xf, 0xf, false);
+            own = o > own ? o : own;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x112, 0xf, 0xf, false);
+            own = o > own ? o : own;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x114, 0xf, 0xf, false);
+            own = o > own ? o : own;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x118, 0xf, 0xf, false);
+            own = o > own ? o : own;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x142, 0xa, 0xf, false);
+            own = o > own ? o : own;
+            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x143, 0xc, 0xf, false);
+            own = o > own ? o : own;
+          }
+          own &= 0xFFFFu;
+          const int32_t o = own ? (int32_t)own - 1 : prev;
+          prev = (int32_t)rl32((uint32_t)o, 63);
+          if (q < span && o >= 0) {
+            const uint32_t sl = L.u.r.oslab[o];
+            const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
+            if (q < off + cnt) {
+              wide |= !fits32(sc);
+              const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
+              KA->new_s.m_score[dst] = sc;
+              KA->new_s.m_ts[dst] = ts;
+              KA->new_s.m_dc[dst] = (uint8_t)dc;
+            }
           }
           wave_lds_sync();
-          st = mark[lane];
         }
-        uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
-        {  // inclusive max-scan (DPP): the last start at or before the lane
-          uint32_t o;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x111, 0xf, 0xf, false);
-          own = o > own ? o : own;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x112, 0xf, 0xf, false);
-          own = o > own ? o : own;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x114, 0xf, 0xf, false);
-          own = o > own ? o : own;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x118, 0xf, 0xf, false);
-          own = o > own ? o : own;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x142, 0xa, 0xf, false);
-          own = o > own ? o : own;
-          o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x143, 0xc, 0xf, false);
-          own = o > own ? o : own;
-        }
-        own &= 0xFFFFu;
-        const int32_t o = own ? (int32_t)own - 1 : prev;
-        prev = (int32_t)rl32((uint32_t)o, 63);
-        if (q < span && o >= 0) {
-          const uint32_t sl = L.u.r.oslab[o];
-          const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
-          if (q < off + cnt) {
-            wide |= !fits32(sc);
-            const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
-            KA->new_s.m_score[dst] = sc;
-            KA->new_s.m_ts[dst] = ts;
-            KA->new_s.m_dc[dst] = (uint8_t)dc;
-          }
-        }
-        wave_lds_sync();
       }
     }
     if (ballot(wide)) return R_NEXT;  // a wide Score in Masked: tier S
@@ -1222,9 +1225,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const uint32_t ii = i < ob.n ? i : 0u;
           const int64_t kk = stk[ii];
           const uint32_t pp = stp[ii];
-          const int64_t tt = L.ots[i < ob.n ? (pp & 0xFFFFu) : 0u];  // (Obs[Id]'s Ts: kept per player)
           ob.key[t] = i < ob.n ? kk : INT64_MAX;
-          ob.ts[t] = i < ob.n ? tt : 0;
           ob.pl[t] = i < ob.n ? pp : RNONE;
         }
         wave_lds_sync();
@@ -1261,7 +1262,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const uint32_t odc = ob_get32(ob.pl, ix) >> 16;
           const int vl = (int)(((r & 7u) << 3) | odc);
           const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
-          if ((r < 8 ? va : vb) >= ob_get64(ob.ts, ix)) {
+          if ((r < 8 ? va : vb) >= ufl64(L.ots[X])) {  // (Obs[Id]'s Ts: kept per player)
             if (lane == 0) pf_and(L, X, Q_OBS);
             wave_lds_sync();
             int64_t wk = 0;
@@ -1274,7 +1275,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             } else {  // promote the largest (:290-295)
               const int64_t gt = ufl64(L.gts[w]);
               const uint32_t gd = ufl(L.gdc[w]), gp = ufl(L.gpos[w]);
-              ob_replace(ob, ix, wk, gt, w | (gd << 16));
+              ob_replace(ob, ix, wk, w | (gd << 16));
               if (lane == 0) {
                 pf_or(L, w, Q_OBS);
                 L.opos[w] = (uint16_t)gp;
