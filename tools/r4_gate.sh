@@ -29,5 +29,5 @@ if [ -f antidote_ccrdt_amd/lib/libccrdt_prof.so ] && [ -z "$SKIP_PROF" ]; then
   echo "== tierR phases"; CCRDT_LIB=$GRAFT_REPO_ROOT/antidote_ccrdt_amd/lib/libccrdt_prof.so timeout -k 10 300 python tools/prof_resident.py > gpurun_out/tierR_phases.txt 2>&1; rc=$?; cat gpurun_out/tierR_phases.txt; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "$AB" ]; then
-  echo "== A/B steady"; STEADY=4 NO_TESTS=1 bash tools/ab.sh $AB || exit 1
+  echo "== A/B"; STEADY=${ABSTEADY:-4} NO_TESTS=${ABNOTESTS-1} bash tools/ab.sh $AB || exit 1
 fi
