@@ -10,7 +10,7 @@ step() {  # name, timeout, command...
   echo "== $n"; timeout -k 10 "$t" "$@" > "gpurun_out/$n.log" 2>&1; local rc=$?
   tail -4 "gpurun_out/$n.log"; [ $rc -eq 0 ] || { echo "FAILED $n rc=$rc"; exit $rc; }
 }
-[ -z "$SKIP_TESTS" ] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+[ -z "$SKIP_TESTS" ] && step pytest_gpu 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread
 [ -z "$SKIP_TESTS" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [ -z "$SKIP_BENCH" ] && step bench 600 python bench.py
 [ -z "$SKIP_N2" ] && step bench_n2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo --steady-batches 0 --cpu-sample-keys 0
@@ -19,7 +19,7 @@ for spec in default "$@"; do
   n=${spec%%=*}; l=${spec#*=}
   lib=""; [ "$spec" != default ] && lib="$GRAFT_REPO_ROOT/$l"
   echo "== scan $n"
-  CCRDT_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/kt_$n" -o kt -- python3 "$GRAFT_REPO_ROOT/tools/steady_ab.py" > "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log" 2>&1 || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log"; exit 1; }
+  CCRDT_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/kt_$n" -o kt -- python3 "$GRAFT_REPO_ROOT/tools/steady_ab.py" > "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log" 2>&1 || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log"; exit 1; }
   f=$(find "$GRAFT_REPO_ROOT/gpurun_out/kt_$n" -name '*kernel_stats.csv' | head -1)
   grep -E "scan|resident" "$f" | cut -d, -f1-8
   grep "chain ms" "$GRAFT_REPO_ROOT/gpurun_out/kt_$n.log"
