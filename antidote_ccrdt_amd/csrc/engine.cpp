@@ -23,7 +23,7 @@ namespace ccrdt {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st);
+int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, uint32_t* key_rmv, hipStream_t st);
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
@@ -86,6 +86,8 @@ void ccrdt_engine::release_all() {
     b.vc.release();
   }
   for (DevBuf& d : tier_ovf) d.release();
+  for (DevBuf& d : st_n32) d.release();
+  for (DevBuf& d : st_nbase) d.release();
   for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl, &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -306,7 +308,8 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.trmv[out].meta.ensure(nk * sizeof(KeyMeta)));
   a.new_s = E.trmv_side(out);
   const uint64_t nb = (nk + 1023) / 1024;
-  CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t)));
+  // partials: per-tile sums and totals, then each key's rmv-op count (u32)
+  CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t) + nk * sizeof(uint32_t)));
   // status words: [0..1] scan, [2+2t, 3+2t] tier t (overflow count, errors)
   CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4));
   uint32_t* status = E.status.as<uint32_t>();
@@ -314,7 +317,9 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.status = status;
   // 1) capacities -> segment offsets of the new state (a fresh batch's
   //    offsets are the keys' op offsets: trmv_new_meta, no scan)
-  if (!E.fresh) CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(), E.stream));
+  if (!E.fresh)
+    CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(),
+                               reinterpret_cast<uint32_t*>(E.partials.as<uint64_t>() + nb * 3 + 3), E.stream));
   // Sizes of the new side.  Its totals are sum(old counts + ops per key) <=
   // (old side's totals) + n_ops, known on the host without waiting for the
   // scan; only when that bound outgrows the buffers does the host read the
@@ -601,14 +606,26 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   CCRDT_TRY(E.st_rvc.ensure(nr * D * 8));
   // (pageable caller memory: through the pinned staging slots, staging.cpp)
   CCRDT_TRY(h2d_staged(E, E.st_kp.p, ops->key_ptr, (nk + 1) * 8));
-  if (n) {
+  int up = n ? h2d_trmv_ops(E, n, ops->kind, ops->id, ops->score, ops->dc, ops->ts, E.st_kind.as<uint8_t>(),
+                            E.st_dc.as<uint8_t>(), E.st_id.as<int64_t>(), E.st_score.as<int64_t>(),
+                            E.st_ts.as<int64_t>(), E.st_n32[0], E.st_nbase[2])
+               : CCRDT_OK;
+  if (up != CCRDT_OK && up != CCRDT_ERANGE) return up;
+  if (up == CCRDT_ERANGE) {  // a value leaves int32: column by column
     CCRDT_TRY(h2d_staged(E, E.st_kind.p, ops->kind, n));
-    CCRDT_TRY(h2d_staged(E, E.st_id.p, ops->id, n * 8));
-    CCRDT_TRY(h2d_staged(E, E.st_score.p, ops->score, n * 8));
+    // Ids, Scores and Ts cross as int32 when they fit (Ts relative to a
+    // per-chunk base), widened on the device; else as they are
+    CCRDT_TRY(h2d_staged_i64(E, E.st_id.as<int64_t>(), ops->id, n, nullptr, nullptr, 0, E.st_n32[0], E.st_nbase[0]));
+    CCRDT_TRY(h2d_staged_i64(E, E.st_score.as<int64_t>(), ops->score, n, nullptr, nullptr, 1, E.st_n32[1],
+                             E.st_nbase[1]));
     CCRDT_TRY(h2d_staged(E, E.st_dc.p, ops->dc, n));
-    CCRDT_TRY(h2d_staged(E, E.st_ts.p, ops->ts, n * 8));
+    CCRDT_TRY(h2d_staged_i64(E, E.st_ts.as<int64_t>(), ops->ts, n, ops->kind, E.st_kind.as<uint8_t>(), 2, E.st_n32[2],
+                             E.st_nbase[2]));
   }
-  if (nr) CCRDT_TRY(h2d_staged(E, E.st_rvc.p, ops->rmv_vc, nr * D * 8));
+  // removal clocks as int32 relative to a per-chunk base when they fit
+  if (nr)
+    CCRDT_TRY(h2d_staged_i64(E, E.st_rvc.as<int64_t>(), ops->rmv_vc, nr * D, nullptr, nullptr, 1, E.st_n32[1],
+                             E.st_nbase[1], true));
   ccrdt_trmv_ops d = *ops;
   d.key_ptr = E.st_kp.as<uint64_t>();
   d.kind = E.st_kind.as<uint8_t>();

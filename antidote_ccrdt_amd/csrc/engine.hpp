@@ -74,8 +74,11 @@ struct ccrdt_engine {
   std::map<int, float> trmv_tier_ms;
   // host-API staging
   ccrdt::DevBuf st_kp, st_kind, st_id, st_score, st_dc, st_ts, st_rvc, st_out_kind, st_out_vc;
-  void* pin[8] = {};           // pinned upload slots (staging.cpp), allocated on first use
-  hipEvent_t pin_ev[8] = {};   // each slot's last DMA
+  void* pin[16] = {};          // pinned upload slots (staging.cpp), allocated on first use
+  void* pin_base = nullptr;    // pinned chunk bases of the narrow column uploads (staging.cpp)
+  hipEvent_t pin_bev[3] = {};  // each base region's last DMA
+  ccrdt::DevBuf st_n32[3], st_nbase[3];  // narrow upload scratch: int32 column, chunk bases
+  hipEvent_t pin_ev[16] = {};  // each slot's last DMA
   int pin_n = 0;
 
   // other types
@@ -94,5 +97,11 @@ using Engine = ccrdt_engine;
 // Host -> device copy of pageable caller memory through the engine's pinned
 // staging slots, parallel host threads (staging.cpp); queued on E.stream.
 int h2d_staged(Engine& E, void* dst, const void* src, uint64_t bytes);
+// An int64 column through the staging slots as int32 (staging.cpp).
+int h2d_staged_i64(Engine& E, int64_t* dst, const int64_t* src, uint64_t n, const uint8_t* kind,
+                   const uint8_t* kind_dev, int slot, DevBuf& scratch, DevBuf& dbase, bool based = false);
+int h2d_trmv_ops(Engine& E, uint64_t n, const uint8_t* kind, const int64_t* id, const int64_t* score,
+                 const uint8_t* dc, const int64_t* ts, uint8_t* kind_d, uint8_t* dc_d, int64_t* id_d,
+                 int64_t* score_d, int64_t* ts_d, DevBuf& scratch, DevBuf& dbase);
 void stage_release(Engine& E);
 }

@@ -74,6 +74,46 @@ __global__ __launch_bounds__(256) void trmv_pack_extras_kernel(const uint64_t* k
   }
 }
 
+// The narrow upload's widening (staging.cpp h2d_staged_i64): dst[i] = src[i]
+// + (kind == nullptr || kind[i] < 2 ? base[i / chunk] : 0).
+__global__ __launch_bounds__(256) void widen_i64_kernel(int64_t* dst, const int32_t* src, const int64_t* base,
+                                                        const uint8_t* kind, uint64_t n, uint64_t chunk) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t b = (kind && kind[i] >= 2) ? 0 : base[i / chunk];
+    dst[i] = (int64_t)((uint64_t)(int64_t)src[i] + (uint64_t)b);  // (modulo 2^64, as narrowed)
+  }
+}
+
+int launch_widen_i64(int64_t* dst, const int32_t* src, const int64_t* base, const uint8_t* kind, uint64_t n,
+                     uint64_t chunk, hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(widen_i64_kernel, dim3(blocks), dim3(256), 0, st, dst, src, base, kind, n, chunk);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// The one-pass upload's widening (staging.cpp h2d_trmv_ops): src = [Id | Score
+// | Ts] int32, n each; Ts of adds (kind < 2) plus its chunk's base.
+__global__ __launch_bounds__(256) void widen_ops_kernel(int64_t* id, int64_t* score, int64_t* ts, const int32_t* src,
+                                                        const int64_t* base, const uint8_t* kind, uint64_t n,
+                                                        uint64_t chunk) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    id[i] = (int64_t)src[i];
+    score[i] = (int64_t)src[n + i];
+    ts[i] = (int64_t)((uint64_t)(int64_t)src[2 * n + i] + (uint64_t)(kind[i] < 2 ? base[i / chunk] : 0));
+  }
+}
+
+int launch_widen_ops(int64_t* id, int64_t* score, int64_t* ts, const int32_t* src, const int64_t* base,
+                     const uint8_t* kind, uint64_t n, uint64_t chunk, hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(widen_ops_kernel, dim3(blocks), dim3(256), 0, st, id, score, ts, src, base, kind, n, chunk);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
 int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t* out,
                            hipStream_t st) {
   CCRDT_HIP(hipMemsetAsync(out, 0, (size_t)n_dc * 8, st));

@@ -23,21 +23,60 @@ constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 4;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
-// Ops of kind 2/3 (rmv: the only ones that can add a Removals row) in
-// [o0, o1): bit 1 of each kind byte, eight bytes per load.  A kind above 3
-// counts too (the batch is rejected anyway).
-__device__ __forceinline__ uint64_t rmv_ops(const uint8_t* kind, uint64_t o0, uint64_t o1) {
-  uint64_t n = 0, i = o0;
-  for (; i < o1 && (reinterpret_cast<uintptr_t>(kind + i) & 7); ++i) n += (kind[i] >> 1) & 1u;
-  for (; i + 8 <= o1; i += 8) {
-    const uint64_t x = *reinterpret_cast<const uint64_t*>(kind + i);
-    n += (uint64_t)__builtin_popcountll((x >> 1) & 0x0101010101010101ull);
+// Ops of kind 2/3 (rmv: the only ones that can add a Removals row) of the
+// 64 keys [k0, k0 + 64) -- lane j: key k0 + j; keys past n_keys count 0 --
+// with the wave reading their op range's kind bytes as coalesced aligned
+// 8-byte words (bytes of the first and last word outside the range lie in
+// the same aligned word, hence the same page, and are never counted).  A
+// kind above 3 counts too (the batch is rejected anyway).  P(x) = rmv bytes
+// in [aligned start, x): per 64-word round, each lane's word count, a DPP
+// prefix sum, and each key lane picks the prefix of the word holding its end
+// boundary; the key's count is P(end) - P(start), its start being the
+// previous key's end.
+__device__ __forceinline__ uint32_t wave_rmv_counts(const uint64_t* key_ptr, const uint8_t* kind, uint64_t k0,
+                                                    uint64_t n_keys) {
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint64_t kl = k0 + lane < n_keys ? k0 + lane : n_keys;
+  const uint64_t hi = key_ptr[kl + (k0 + lane < n_keys ? 1 : 0)];  // this key's end (past n_keys: the last end)
+  const uint64_t lo0 = key_ptr[k0 < n_keys ? k0 : n_keys];
+  const uint64_t hi63 = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)hi, 63) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hi >> 32), 63) << 32);
+  if (hi63 <= lo0) return 0u;
+  const uintptr_t ab = reinterpret_cast<uintptr_t>(kind + lo0) & ~(uintptr_t)7;
+  const uint64_t nw = (reinterpret_cast<uintptr_t>(kind + hi63) - ab + 7) / 8;
+  const uint64_t wx = (reinterpret_cast<uintptr_t>(kind + hi) - ab) / 8;  // word of the end boundary
+  const uint32_t bx = (uint32_t)((reinterpret_cast<uintptr_t>(kind + hi) - ab) & 7);
+  uint64_t P = 0, carry = 0;
+  for (uint64_t w0 = 0; w0 < nw; w0 += 64) {
+    const uint64_t w = w0 + lane;
+    const uint64_t v = w < nw ? reinterpret_cast<const uint64_t*>(ab)[w] : 0ull;
+    const uint64_t bits = (v >> 1) & 0x0101010101010101ull;
+    const uint32_t c = (uint32_t)__builtin_popcountll(bits);
+    const uint32_t incl = wave_incl_scan_dpp(c);
+    const uint32_t tot = rl32(incl, 63);
+    // the end boundary's word in this round: its exclusive prefix and its
+    // bytes below the boundary
+    const bool here = wx >= w0 && wx < w0 + 64;
+    const int src = here ? (int)(wx - w0) : (int)lane;
+    const uint32_t ex = shfl32(incl - c, src);
+    const uint64_t wb = (uint64_t)shfl64((int64_t)bits, src);
+    const uint64_t below = bx ? (wb & ((1ull << (8 * bx)) - 1)) : 0ull;
+    if (here) P = carry + ex + (uint32_t)__builtin_popcountll(below);
+    carry += tot;
   }
-  for (; i < o1; ++i) n += (kind[i] >> 1) & 1u;
-  return n;
+  if (wx >= nw) P = carry;
+  // the start boundary of key 0: the bytes of [ab, lo0) are not in the range
+  const uint64_t ps = (uint64_t)shfl64((int64_t)P, lane ? (int)lane - 1 : 0);
+  uint64_t P0 = 0;
+  {
+    const uint32_t b0 = (uint32_t)((reinterpret_cast<uintptr_t>(kind + lo0) - ab) & 7);
+    const uint64_t v0 = *reinterpret_cast<const uint64_t*>(ab);
+    P0 = b0 ? (uint64_t)__builtin_popcountll((v0 >> 1) & 0x0101010101010101ull & ((1ull << (8 * b0)) - 1)) : 0ull;
+  }
+  return (uint32_t)(P - (lane ? ps : P0));
 }
 
-__device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint64_t c[3]) {
+__device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint32_t nrmv, uint64_t c[3]) {
   const uint64_t o0 = a.key_ptr[k], nops = a.key_ptr[k + 1] - o0;
   if (a.fresh) {
     c[0] = c[1] = c[2] = nops;
@@ -45,7 +84,7 @@ __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint
     const KeyMeta m = a.old_s.meta[k];
     c[0] = m.np + nops;
     c[1] = m.nm + nops;
-    c[2] = m.nr + rmv_ops(a.kind, o0, o0 + nops);  // (rows: rmv ops only)
+    c[2] = m.nr + nrmv;  // (rows: rmv ops only)
   }
   // No per-key limit here: a segment is address space only.  The tiers check
   // the key's real layout against the u16 slab offsets (TRMV_SEG_MAX) and hand
@@ -80,14 +119,30 @@ __device__ __forceinline__ void block_scan3(uint64_t v[3], uint64_t total[3]) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_partials(TrmvApplyArgs a, uint64_t* partials) {
+// Pass 1: each key's rmv-op count (every wave counts 256 consecutive keys,
+// 64 at a time, coalesced; key_rmv keeps them for pass 2), then the tile sums.
+__global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_partials(TrmvApplyArgs a, uint64_t* partials,
+                                                                    uint32_t* key_rmv) {
+  __shared__ uint32_t cnt[SCAN_TILE];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * SCAN_TILE;
+  if (!a.fresh) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+      const uint64_t k0 = tile0 + 256u * w + 64u * g;
+      const uint32_t r = k0 < (uint64_t)a.n_keys ? wave_rmv_counts(a.key_ptr, a.kind, k0, (uint64_t)a.n_keys) : 0u;
+      cnt[256u * w + 64u * g + lane] = r;
+      if (k0 + lane < (uint64_t)a.n_keys) key_rmv[k0 + lane] = r;
+    }
+    __syncthreads();
+  }
   uint64_t sum[3] = {0, 0, 0};
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  const uint64_t base = tile0 + (uint64_t)threadIdx.x * SCAN_ITEMS;
   for (int j = 0; j < SCAN_ITEMS; ++j) {
     const uint64_t k = base + j;
     if (k < (uint64_t)a.n_keys) {
       uint64_t c[3];
-      caps_of(a, k, c);
+      caps_of(a, k, a.fresh ? 0u : cnt[threadIdx.x * SCAN_ITEMS + j], c);
       for (int x = 0; x < 3; ++x) sum[x] += c[x];
     }
   }
@@ -118,13 +173,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_tops(uint64_t* partials,
   if (threadIdx.x < 3) partials[nb * 3 + threadIdx.x] = carry[threadIdx.x];
 }
 
-__global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_apply(TrmvApplyArgs a, const uint64_t* partials) {
+__global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_apply(TrmvApplyArgs a, const uint64_t* partials,
+                                                                 const uint32_t* key_rmv) {
   uint64_t c[SCAN_ITEMS][3];
   uint64_t sum[3] = {0, 0, 0};
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   for (int j = 0; j < SCAN_ITEMS; ++j) {
     const uint64_t k = base + j;
-    if (k < (uint64_t)a.n_keys) caps_of(a, k, c[j]);
+    if (k < (uint64_t)a.n_keys) caps_of(a, k, a.fresh ? 0u : key_rmv[k], c[j]);
     else c[j][0] = c[j][1] = c[j][2] = 0;
     for (int x = 0; x < 3; ++x) sum[x] += c[j][x];
   }
@@ -273,12 +329,12 @@ int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st) {
   return CCRDT_OK;
 }
 
-int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, hipStream_t st) {
+int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, uint32_t* key_rmv, hipStream_t st) {
   const uint64_t nb = ((uint64_t)a.n_keys + SCAN_TILE - 1) / SCAN_TILE;
   if (nb == 0) return CCRDT_OK;
-  hipLaunchKernelGGL(trmv_scan_partials, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, st, a, partials);
+  hipLaunchKernelGGL(trmv_scan_partials, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, st, a, partials, key_rmv);
   hipLaunchKernelGGL(trmv_scan_tops, dim3(1), dim3(SCAN_BLOCK), 0, st, partials, nb);
-  hipLaunchKernelGGL(trmv_scan_apply, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, st, a, partials);
+  hipLaunchKernelGGL(trmv_scan_apply, dim3((unsigned)nb), dim3(SCAN_BLOCK), 0, st, a, partials, key_rmv);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

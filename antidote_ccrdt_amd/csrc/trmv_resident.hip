@@ -84,6 +84,15 @@ constexpr int RSL = RP / 64;   // player slots per lane
 constexpr int RCH = 64;        // ops per chunk
 constexpr int RCHR = 16;       // rmvs per chunk (rows of the clock table)
 constexpr uint32_t RNONE = 0xFFFFFFFFu;
+#ifndef TRMV_WARM
+#define TRMV_WARM 1  // the next key's lines are loaded into the caches during P1-P3
+#endif
+#ifndef TRMV_DPPSCAN
+#define TRMV_DPPSCAN 1  // P4's segmented scan on DPP row shifts (0: ds_bpermute shuffles)
+#endif
+#ifndef TRMV_MSEQ
+#define TRMV_MSEQ 0  // merges of up to this many candidates run on the register array (0: off; A/B r04: 8 cost ~1 ms per steady batch)
+#endif
 constexpr uint32_t RH_NONE = 0xFFFFu, RH_CLAIM = 0x8000u;  // hash slots: player | CLAIM|lane | NONE
 enum : int { R_DONE = 0, R_NEXT = 1, R_REJECT = 2 };
 
@@ -94,6 +103,7 @@ constexpr uint32_t Q_ROWV = 4u;  // Removals[Id] exists
 constexpr uint32_t Q_RMV = 8u;   // a rmv of Id in this batch: its slab is replayed by one lane
 constexpr uint32_t Q_WALK = 16u; // a replay compacted the slab: positions restated in P5
 constexpr uint32_t Q_DUP = 32u;  // a possibly duplicated element: replayed too
+constexpr uint32_t Q_UPG = 64u;  // (inside a merge) an Observed player whose entry the run upgrades
 constexpr uint32_t R_DOM = 1u;   // cres: dominated add (:234-237)
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -130,6 +140,45 @@ __device__ __forceinline__ bool gb_gt(int64_t s1, uint32_t d1, int64_t t1, int64
   return s1 > s2 || (s1 == s2 && (d1 > d2 || (d1 == d2 && t1 > t2)));
 }
 
+// One step of P4's segmented scan over the sorted chunk (DPP: row_shr 1, 2,
+// 4, 8 inside rows of 16, then row_bcast 15 and 31 across rows -- the
+// inclusive-scan pattern, valid for any associative operator).  A lane whose
+// source lies outside its row (or whose row the step skips) reads 0: flags
+// 0, no source, the step leaves it as it is.  Per lane: v = the gb_sets-largest
+// (Score, DcId, Ts) of the segment so far, w = its cmp/2-largest (Score, Ts;
+// the earlier of equals); vd = DcId | slab position << 8 | ok << 30 | head << 31.
+template <int C, int RM>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, C, RM, 0xf, false);
+}
+template <int C, int RM>
+__device__ __forceinline__ int64_t dpp0_64(int64_t x) {
+  return (int64_t)(((uint64_t)dpp0<C, RM>((uint32_t)((uint64_t)x >> 32)) << 32) | dpp0<C, RM>((uint32_t)x));
+}
+template <int C, int RM>
+__device__ __forceinline__ void seg_step(int32_t& vs, int64_t& vt, uint32_t& vd, int32_t& ws, int64_t& wt,
+                                         uint32_t& wd) {
+  const uint32_t yd = dpp0<C, RM>(vd), zd = dpp0<C, RM>(wd);
+  const int32_t ys = (int32_t)dpp0<C, RM>((uint32_t)vs), zs = (int32_t)dpp0<C, RM>((uint32_t)ws);
+  const int64_t yt = dpp0_64<C, RM>(vt), zt = dpp0_64<C, RM>(wt);
+  const bool ok = (vd >> 30) & 1u, hf = (vd >> 31) != 0u, yok = (yd >> 30) & 1u, yhf = (yd >> 31) != 0u;
+  if (!hf) {
+    if (yok) {
+      if (!ok || gb_gt(ys, yd & 0xFFu, yt, vs, vd & 0xFFu, vt)) {
+        vs = ys;
+        vt = yt;
+        vd = (vd & 0xC0000000u) | (yd & 0x3FFFFFFFu);
+      }
+      if (!ok || !(ws > zs || (ws == zs && wt > zt))) {  // the earlier one wins ties
+        ws = zs;
+        wt = zt;
+        wd = zd;
+      }
+    }
+    vd = (vd & 0x3FFFFFFFu) | ((ok || yok) ? (1u << 30) : 0u) | (yhf ? (1u << 31) : 0u);
+  }
+}
+
 typedef int64_t Row8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ int64_t pick8(const Row8& v, uint32_t d) {
   int64_t r = v[0];
@@ -149,6 +198,27 @@ __device__ __forceinline__ uint32_t wave_radix_sort(uint32_t kv) {  // by bits [
     kv = perm32(kv, dst);
   }
   return kv;
+}
+
+// One stable counting pass over a 4-bit digit (bits [6 + SHIFT, 10 + SHIFT))
+// of kv (payload: the low 6 bits): the sixteen digit masks by ballot, each
+// lane's destination = the lanes of smaller digits + its rank among its own,
+// one permute.  Two passes sort by 8 bits with two LDS-crossbar round trips
+// (a bit per pass took eight).
+template <int SHIFT>
+__device__ __forceinline__ uint32_t radix16_pass(uint32_t kv) {
+  const uint32_t dg = (kv >> (6 + SHIFT)) & 15u;
+  uint64_t mine = 0;
+  uint32_t base = 0, acc = 0;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const bool me = dg == (uint32_t)d;
+    const uint64_t m = ballot(me);
+    mine = me ? m : mine;
+    base = me ? acc : base;
+    acc += (uint32_t)__builtin_popcountll(m);
+  }
+  return perm32(kv, base + mbcnt(mine));
 }
 
 // Position of the k-th (0-based) set bit of m (k < popcount(m)).
@@ -455,43 +525,67 @@ __device__ __forceinline__ bool r_resolve(RLds& L, int64_t id, bool v, uint32_t&
 
 // Promotion candidate of rmv/3 (:276-281, :291): the player outside Observed
 // with Masked elements whose (largest Score, Id) is largest; RNONE if none.
-// Its key in `wk`.
-__device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[RSL], uint32_t np, int64_t& wk) {
+// Its key in `wk`, its largest element's Ts / DcId / slab position in `wt`,
+// `wd`, `wp` (read with the slots' flags and Scores, one LDS round trip).
+__device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[RSL], uint32_t np, int64_t& wk,
+                                             int64_t& wt, uint32_t& wd, uint32_t& wp) {
   const uint32_t l = (uint32_t)lane_id();
   uint32_t bp = RNONE;
   int64_t best = INT64_MIN;
-  uint32_t f[RSL];
+  uint32_t f[RSL], gd[RSL], gp[RSL];
   int32_t sc[RSL];
+  int64_t gt[RSL];
 #pragma unroll
   for (int u = 0; u < RSL; ++u) {
     const uint32_t p = 64u * u + l;
     f[u] = p < np ? L.pf[p] : 0u;
     sc[u] = L.msc[p];
+    gt[u] = L.gts[p];
+    gd[u] = L.gdc[p];
+    gp[u] = L.gpos[p];
   }
+  int64_t bt = 0;
+  uint32_t bd = 0, bg = 0;
 #pragma unroll
   for (int u = 0; u < RSL; ++u) {
     const int64_t k = mkkey(sc[u], pid[u]);
     if ((f[u] & (Q_OBS | Q_HASM)) == Q_HASM && (bp == RNONE || k > best)) {
       bp = 64u * u + l;
       best = k;
+      bt = gt[u];
+      bd = gd[u];
+      bg = gp[u];
     }
   }
   if (!ballot(bp != RNONE)) return RNONE;
   const int64_t m = wave_max_i64_dpp(bp != RNONE ? best : INT64_MIN);
-  const uint64_t hit = ballot(bp != RNONE && best == m);
+  const int src = (int)__builtin_ctzll(ballot(bp != RNONE && best == m));
   wk = m;
-  return rl32(bp, (int)__builtin_ctzll(hit));
+  wt = rl64(bt, src);
+  wd = rl32(bd, src);
+  wp = rl32(bg, src);
+  return rl32(bp, src);
 }
 
 // One key.  Returns R_NEXT for a key outside the class; the next tier redoes
 // it from the old side (whatever this one wrote of it is rewritten).
-__device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) {
+__device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t nkey, RLds& L) {
   const uint32_t lane = (uint32_t)lane_id();
   const int D = KA->n_dc;
 #ifdef TRMV_PROF
   unsigned long long prof_t;
   RPROF_STAMP(prof_t);
 #endif
+  // the wave's next key: its metadata and op range now (scalar loads), the
+  // lines of its state and ops after P1 (warm_next)
+  const bool warm = TRMV_WARM && nkey != RNONE && !KA->fresh;
+  KeyMeta wmeta;
+  uint64_t wo0 = 0, wo1 = 0;
+  if (warm) {
+    wmeta = KA->old_s.meta[nkey];
+    wo0 = KA->key_ptr[nkey];
+    wo1 = KA->key_ptr[nkey + 1];
+  }
   const uint64_t op0 = KA->key_ptr[key];
   const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
   // (a fresh batch: the keys tier 0 handed on, with no old state)
@@ -527,29 +621,45 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
   bool wide = false;
   {
     uint32_t info[RSL], slab[RSL], gb[RSL];
+    {
+      // (the four arrays' bases once, and pl_gb read whatever the slab's
+      // count: a load conditional on another load's value waited for it, slot
+      // by slot)
+      const int64_t* const pl_id = KA->old_s.pl_id + om.p_off;
+      const uint32_t* const pl_info = KA->old_s.pl_info + om.p_off;
+      const uint32_t* const pl_slab = KA->old_s.pl_slab + om.p_off;
+      const uint16_t* const pl_gb = KA->old_s.pl_gb + om.p_off;
 #pragma unroll
-    for (int u = 0; u < RSL; ++u) {
-      const uint32_t p = 64u * u + lane;
-      const bool v = p < om.np;
-      const uint64_t pp = (uint64_t)om.p_off + (v ? p : 0u);
-      pid[u] = v ? KA->old_s.pl_id[pp] : 0;
-      info[u] = v ? KA->old_s.pl_info[pp] : RNONE;
-      slab[u] = v ? KA->old_s.pl_slab[pp] : 0u;
-      gb[u] = (v && (slab[u] >> 16) > 1) ? (uint32_t)KA->old_s.pl_gb[pp] : 0u;
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        const bool v = p < om.np;
+        const uint32_t pp = v ? p : 0u;
+        pid[u] = v ? pl_id[pp] : 0;
+        info[u] = v ? pl_info[pp] : RNONE;
+        slab[u] = v ? pl_slab[pp] : 0u;
+        gb[u] = v ? (uint32_t)pl_gb[pp] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) gb[u] = (slab[u] >> 16) > 1 ? gb[u] : 0u;  // (readers take 0 below 2)
     }
     int64_t os[RSL], ot[RSL], gs[RSL], gt[RSL];
     uint32_t gd[RSL];
+    {
+      const int64_t* const m_score = KA->old_s.m_score + om.m_off;
+      const int64_t* const m_ts = KA->old_s.m_ts + om.m_off;
+      const uint8_t* const m_dc = KA->old_s.m_dc + om.m_off;
 #pragma unroll
-    for (int u = 0; u < RSL; ++u) {
-      const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
-      const uint64_t g0 = (uint64_t)om.m_off + off;
-      const bool ho = obx != NONE16, hg = cnt != 0;
-      os[u] = ho ? KA->old_s.m_score[g0 + obx] : 0;
-      ot[u] = ho ? KA->old_s.m_ts[g0 + obx] : 0;
-      odr[u] = ho ? (uint32_t)KA->old_s.m_dc[g0 + obx] : 0u;
-      gs[u] = hg ? KA->old_s.m_score[g0 + gb[u]] : 0;
-      gt[u] = hg ? KA->old_s.m_ts[g0 + gb[u]] : 0;
-      gd[u] = hg ? (uint32_t)KA->old_s.m_dc[g0 + gb[u]] : 0u;
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
+        const bool ho = obx != NONE16, hg = cnt != 0;
+        const uint32_t qo = off + (ho ? obx : 0u), qg = off + gb[u];
+        os[u] = ho ? m_score[qo] : 0;
+        ot[u] = ho ? m_ts[qo] : 0;
+        odr[u] = ho ? (uint32_t)m_dc[qo] : 0u;
+        gs[u] = hg ? m_score[qg] : 0;
+        gt[u] = hg ? m_ts[qg] : 0;
+        gd[u] = hg ? (uint32_t)m_dc[qg] : 0u;
+      }
     }
     uint32_t hh[RSL];
     bool pend[RSL];
@@ -604,6 +714,31 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
     }
   }
   if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
+  // Next key's lines into the caches (L2 / Infinity Cache) while this key
+  // works: one load per 128-byte line of its player records, Masked pool,
+  // Removals rows and ops, so the dependent load chains of its P1-P3 and
+  // chunks find their lines there instead of in HBM.  Nothing waits for
+  // these loads until P3's own wait (their values are folded into a fake use
+  // there).
+  uint32_t tch = 0;
+  uint32_t tv[12];
+  if (warm) {
+    const uint32_t np2 = wmeta.np, nm2 = wmeta.nm, nr2 = wmeta.nr;
+    const uint64_t n2 = wo1 - wo0;
+    const void* reg[12] = {KA->old_s.pl_id + wmeta.p_off, KA->old_s.pl_info + wmeta.p_off,
+                           KA->old_s.pl_slab + wmeta.p_off, KA->old_s.pl_gb + wmeta.p_off,
+                           KA->old_s.m_score + wmeta.m_off, KA->old_s.m_ts + wmeta.m_off,
+                           KA->old_s.m_dc + wmeta.m_off, KA->old_s.r_vc + (uint64_t)wmeta.r_off * D,
+                           KA->id + wo0, KA->score + wo0, KA->ts + wo0, KA->kind + wo0};
+    const uint64_t len[12] = {8ull * np2, 4ull * np2, 4ull * np2, 2ull * np2, 8ull * nm2, 8ull * nm2, nm2,
+                              8ull * D * nr2, 8 * n2, 8 * n2, 8 * n2, n2};
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const uintptr_t b = reinterpret_cast<uintptr_t>(reg[i]);
+      const uintptr_t l0 = b >> 7, l1 = (b + len[i] + 127) >> 7;
+      tv[i] = (len[i] && l0 + lane < l1) ? *reinterpret_cast<const uint32_t*>((l0 + lane) << 7) : 0u;
+    }
+  }
   span = wave_max_u32_dpp(span);
   Obs ob;
   ob.n = om.nobs;
@@ -664,18 +799,32 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
   {
     // ---- P2. every op's player; ops per player; rmv players
     uint32_t np = om.np;
-    for (uint32_t c0 = 0; c0 < nops; c0 += 64) {
-      const uint32_t l = c0 + lane;
-      const bool v = l < nops;
-      const int64_t id = v ? KA->id[op0 + l] : 0;
-      const uint32_t kind = v ? (uint32_t)KA->kind[op0 + l] : 0u;
-      if (ballot(v && !fits32(id))) return R_NEXT;  // a wide Id: tier S
-      uint32_t p;
-      if (!r_resolve(L, id, v, np, p)) return R_NEXT;
-      if (v) {
-        KA->op_pl[op0 + l] = (uint8_t)p;
-        atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
-        if (kind == 2 || kind == 3) pf_or(L, p, Q_RMV);
+    // 128 ops per round: both halves' Ids and kinds load together, then each
+    // half is resolved (one 64-lane claim table)
+    for (uint32_t c0 = 0; c0 < nops; c0 += 128) {
+      int64_t idh[2];
+      uint32_t kh[2];
+      bool vh[2], wide = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t l = c0 + 64u * h + lane;
+        vh[h] = l < nops;
+        idh[h] = vh[h] ? KA->id[op0 + l] : 0;
+        kh[h] = vh[h] ? (uint32_t)KA->kind[op0 + l] : 0u;
+        wide |= vh[h] && !fits32(idh[h]);
+      }
+      if (ballot(wide)) return R_NEXT;  // a wide Id: tier S
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (c0 + 64u * h >= nops) break;
+        const uint32_t l = c0 + 64u * h + lane;
+        uint32_t p;
+        if (!r_resolve(L, idh[h], vh[h], np, p)) return R_NEXT;
+        if (vh[h]) {
+          KA->op_pl[op0 + l] = (uint8_t)p;
+          atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
+          if (kh[h] == 2 || kh[h] == 3) pf_or(L, p, Q_RMV);
+        }
       }
     }
     wave_lds_sync();
@@ -808,6 +957,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         KA->new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = KA->old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
+    if (warm) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) tch ^= tv[i];
+      asm volatile("" ::"v"(tch));  // (keeps the warm-up loads)
+    }
     RPROF(2);
 
     // ---- chunks
@@ -864,23 +1018,25 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       bool dupc;
       {
         const int64_t vcs = (int64_t)L.vc[add ? dc : (uint32_t)TRMV_DPAD];
-        const uint32_t kv = wave_radix_sort<4>(((add ? dc : 8u) << 6) | lane);
-        const uint32_t src = kv & 63u, sdc = kv >> 6;
-        const int64_t sts = shfl64(ts, (int)src);
-        const uint32_t lkv = shfl32(kv, lane ? (int)lane - 1 : 0);
-        const int64_t lts = shfl64(sts, lane ? (int)lane - 1 : 0);
-        const bool fall = lane > 0 && sdc < 8u && (lkv >> 6) == sdc && lts >= sts;
-        const uint64_t fm = ballot(fall);
-        bool taint = false;
-        if (fm) {
-          const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-          const uint64_t f = fm & below;
-          const uint32_t hi = f ? 63u - (uint32_t)__builtin_clzll(f) : lane;
-          const uint32_t fkv = shfl32(kv, (int)hi);
-          taint = f != 0 && (fkv >> 6) == sdc;
+        // per dc, the adds of the chunk as a lane mask (lane order = stream
+        // order): a fall is an add whose previous add of its dc has a Ts as
+        // large; every add of that dc from the first fall on is a candidate
+        uint64_t md = 0;
+#pragma unroll
+        for (int d = 0; d < TRMV_DPAD; ++d) {
+          const bool in = add && dc == (uint32_t)d;
+          const uint64_t m = ballot(in);
+          md = in ? m : md;
         }
-        const bool taint_src = perm32(taint ? 1u : 0u, src) != 0;
-        dupc = add && (ts <= vcs || taint_src);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // (lane masks made here, not held across keys)
+        const uint64_t below = ln ? (~0ull >> (64u - ln)) : 0ull;
+        const uint64_t pm = md & below;
+        const int prv = pm ? 63 - (int)__builtin_clzll(pm) : (int)ln;
+        const int64_t pts = shfl64(ts, prv);
+        const uint64_t fm = ballot(add && pm != 0 && pts >= ts);
+        const bool taint = (fm & md & (below | (1ull << ln))) != 0;
+        dupc = add && (ts <= vcs || taint);
       }
       wave_lds_sync();
       if (add) atomicMax(&L.vc[dc], (unsigned long long)ts);  // vc_update (:233)
@@ -894,14 +1050,20 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
 
       // ---- P3c. ops in (player, stream) order: appends of players without
       // a rmv or duplicate candidate (op-parallel), replays of the others
-      const uint32_t kvs = wave_radix_sort<9>(((v ? p : (uint32_t)RP) << 6) | lane);
-      const uint32_t sp = kvs >> 6, so = kvs & 63u;
-      const bool sv = sp < (uint32_t)RP;
+      // (player, stream) order: a stable sort by the 8-bit player, lanes past
+      // the chunk keyed 255 (they follow any real player 255: stable, and
+      // told apart by their source lane)
+      const uint32_t kvs = radix16_pass<4>(radix16_pass<0>(((v ? p : 255u) << 6) | lane));
+      const uint32_t so = kvs & 63u;
+      const bool sv = so < n;
+      const uint32_t sp = sv ? (kvs >> 6) : (uint32_t)RP;
       const uint32_t lkvs = shfl32(kvs, lane ? (int)lane - 1 : 0);
       const bool start = sv && (lane == 0 || (lkvs >> 6) != sp);
       L.u.c.csrt[lane] = (uint8_t)so;
       const uint64_t ss = ballot(start);
-      const uint64_t incl = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+      uint32_t ol = lane;
+      asm volatile("" : "+v"(ol));  // (lane masks made here, not held across keys)
+      const uint64_t incl = ol == 63 ? ~0ull : ((2ull << ol) - 1);
       const uint64_t sb = ss & incl;
       const uint32_t slo = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
       const uint64_t above = ss & ~incl;
@@ -924,7 +1086,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint64_t nd = ballot(app);
       if (app) {
         const uint32_t ns = L.nslab[sp];
-        const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << lane) - 1));
+        const uint32_t pos = (ns >> 16) + (uint32_t)__builtin_popcountll(nd & segm & ((1ull << ol) - 1));
         const uint64_t dst = (uint64_t)nm.m_off + (ns & 0xFFFFu) + pos;
         KA->new_s.m_score[dst] = ssc;
         KA->new_s.m_ts[dst] = sts;
@@ -959,8 +1121,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         bool has_row = (f & Q_ROWV) != 0;
         Row8 R = (Row8)(0);
         const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
-        if (has_row)
-          for (int d = 0, dn = KA->n_dc; d < dn; ++d) R[d] = KA->new_s.r_vc[rbase + d];  // (n_dc re-read here: no per-d masks held across the key)
+        {
+          const int dn = KA->n_dc;  // (re-read here: no per-d masks held across the key)
+#pragma unroll
+          for (int d = 0; d < TRMV_DPAD; ++d) R[d] = (has_row && d < dn) ? KA->new_s.r_vc[rbase + d] : 0;
+        }
         const int64_t wid = L.u.c.cid[ws];
         bool moved = false;
         for (uint32_t x = ws; x < we; ++x) {
@@ -1077,7 +1242,22 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         const uint32_t srun = sv ? (uint32_t)__builtin_popcountll(rm & ((1ull << so) - 1)) : 0xFFu;
         const uint32_t seg = (sp << 8) | srun;
         const uint32_t pseg = shfl32(seg, lane ? (int)lane - 1 : 0);
-        bool ok = sadd, hf = lane == 0 || pseg != seg;
+        const bool hf0 = lane == 0 || pseg != seg;
+#if TRMV_DPPSCAN
+        int32_t vs = (int32_t)ssc, ws = (int32_t)ssc;  // (Scores of adds fit 32 bits here)
+        int64_t vt = sts, wt = sts;
+        uint32_t vd = sdc | ((scres >> 16) << 8) | (sadd ? (1u << 30) : 0u) | (hf0 ? (1u << 31) : 0u);
+        uint32_t wd = sdc | ((scres >> 16) << 8);
+        seg_step<0x111, 0xf>(vs, vt, vd, ws, wt, wd);
+        seg_step<0x112, 0xf>(vs, vt, vd, ws, wt, wd);
+        seg_step<0x114, 0xf>(vs, vt, vd, ws, wt, wd);
+        seg_step<0x118, 0xf>(vs, vt, vd, ws, wt, wd);
+        seg_step<0x142, 0xa>(vs, vt, vd, ws, wt, wd);
+        seg_step<0x143, 0xc>(vs, vt, vd, ws, wt, wd);
+        const bool ok = (vd >> 30) & 1u;
+        vd &= 0x3FFFFFFFu;
+#else
+        bool ok = sadd, hf = hf0;
         int64_t vs = ssc, vt = sts, ws = ssc, wt = sts;
         uint32_t vd = sdc | ((scres >> 16) << 8), wd = vd;
         int sl = (int)lane;
@@ -1108,6 +1288,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
             hf = yhf;
           }
         }
+#endif
         const uint32_t nseg = shfl32(seg, lane < 63 ? (int)lane + 1 : (int)lane);
         const bool last = sv && (lane == 63 || nseg != seg);
         cu_ok = last && ok;
@@ -1124,8 +1305,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
       const uint32_t cu_p = sp;
       const int64_t cm_k = mkkey(cm_s, sid);
       wave_lds_sync();  // the chunk region is free from here on: merge staging
+      // merge staging (K <= 128 entries), the candidate list, its histogram
       int64_t* stk = reinterpret_cast<int64_t*>(&L.u);
-      uint32_t* stp = reinterpret_cast<uint32_t*>(stk + 256);
+      uint32_t* stp = reinterpret_cast<uint32_t*>(stk + 128);
+      int64_t* ck = reinterpret_cast<int64_t*>(stp + 128);
+      uint32_t* hist = reinterpret_cast<uint32_t*>(ck + 64);
+      static_assert(sizeof(L.u) >= 128 * 8 + 128 * 4 + 64 * 8 + 72 * 4, "merge staging in the chunk union");
       auto catch_up = [&](uint32_t run) {
         if (cu_ok && cu_run == run) {  // one lane per player
           const uint32_t f = L.pf[cu_p];
@@ -1163,28 +1348,102 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         RCOUNT(29, 1);
         if (!relm) return;
         RPROF(16);
-        bool rem0 = false, rem1 = false;
-        for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries
-          const uint32_t xp = rl32(cu_p, (int)__builtin_ctzll(t));
-          rem0 |= (ob.pl[0] & 0xFFFFu) == xp;
-          rem1 |= (ob.pl[1] & 0xFFFFu) == xp;
+        const uint32_t m = (uint32_t)__builtin_popcountll(relm);
+        if (m <= (uint32_t)TRMV_MSEQ) {
+          // Few candidates: each one applied to the register array as the
+          // add it stands for (recompute_observed/5, :301-334) -- an upgrade
+          // re-sorts its player's entry, an entry into a full Observed
+          // evicts Min (entry 0) -- one ballot rank and one DPP range shift
+          // each, no LDS round trip.  Any order of the run's candidates
+          // gives the batch merge's result (the state after a
+          // run is the top K by (largest Score, Id)); an upgraded player
+          // whose old entry an earlier candidate evicted enters as a new one.
+          const uint64_t inm = ballot(rel && inobs);
+          for (uint64_t t = relm; t; t &= t - 1) {
+            const int x = (int)__builtin_ctzll(t);
+            const int64_t kx = rl64(cm_k, x);
+            const uint32_t px = rl32(cu_p, x);
+            const uint32_t plx = px | (rl32(cm_d, x) << 16);
+            const uint32_t ix = ((inm >> x) & 1u) ? ob_find(ob, px) : RNONE;
+            bool put = true;
+            if (ix != RNONE) {
+              ob_replace(ob, ix, kx, plx);
+            } else if (ob.n < K) {
+              ob_insert(ob, kx, plx);
+              if ((int)lane == x) pf_or(L, px, Q_OBS);
+            } else if (kx > rl64(ob.key[0], 0)) {
+              const uint32_t ev = rl32(ob.pl[0], 0) & 0xFFFFu;  // evicted (:325-331)
+              if (lane == 0) pf_and(L, ev, Q_OBS);
+              ob_replace(ob, 0, kx, plx);
+              if ((int)lane == x) pf_or(L, px, Q_OBS);
+            } else {
+              put = false;
+            }
+            if (put && (int)lane == x) {  // Obs[Id] := its cmp-largest
+              L.opos[px] = (uint16_t)cm_pos;
+              L.ots[px] = cm_t;
+            }
+          }
+          wave_lds_sync();
+          return;
+        }
+        // The merge's ranks.  Up to three candidates: a ballot pair per
+        // candidate.  More: no loop over the candidates -- their keys are
+        // listed in LDS (upgraded players flagged Q_UPG); every kept entry and
+        // every candidate counts the candidates below it from the list
+        // (broadcast reads); a histogram of the kept entries by that count,
+        // prefix-summed, gives each candidate the kept entries below it:
+        // entry < candidate c  <=>  (candidates below the entry) <= (c's rank
+        // among the candidates), keys being distinct.
+        bool rem0, rem1;
+        uint32_t cb0 = 0, cb1 = 0, cbc = 0, abc = 0;
+        if (m <= 3) {
+          // few candidates: one ballot pair per candidate
+          rem0 = rem1 = false;
+          for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries
+            const uint32_t xp = rl32(cu_p, (int)__builtin_ctzll(t));
+            rem0 |= lane < ob.n && (ob.pl[0] & 0xFFFFu) == xp;
+            rem1 |= 64u + lane < ob.n && (ob.pl[1] & 0xFFFFu) == xp;
+          }
+          const bool v0 = lane < ob.n && !rem0, v1 = 64u + lane < ob.n && !rem1;
+          for (uint64_t t = relm; t; t &= t - 1) {
+            const int x = (int)__builtin_ctzll(t);
+            const int64_t kx = rl64(cm_k, x);
+            cb0 += (v0 && kx < ob.key[0]) ? 1u : 0u;
+            cb1 += (v1 && kx < ob.key[1]) ? 1u : 0u;
+            cbc += (rel && kx < cm_k) ? 1u : 0u;
+            const uint32_t ab = (uint32_t)__builtin_popcountll(ballot(v0 && ob.key[0] < kx)) +
+                                (uint32_t)__builtin_popcountll(ballot(v1 && ob.key[1] < kx));
+            abc = (int)lane == x ? ab : abc;
+          }
+        } else {
+          if (rel) {
+            ck[mbcnt(relm)] = cm_k;
+            if (inobs) pf_or(L, cu_p, Q_UPG);
+          }
+          if (lane <= m) hist[lane] = 0u;
+          wave_lds_sync();
+          rem0 = lane < ob.n && (L.pf[lane < ob.n ? (ob.pl[0] & 0xFFFFu) : 0u] & Q_UPG);
+          rem1 = 64u + lane < ob.n && (L.pf[64u + lane < ob.n ? (ob.pl[1] & 0xFFFFu) : 0u] & Q_UPG);
+#pragma unroll 4
+          for (uint32_t j = 0; j < m; ++j) {
+            const int64_t kj = ck[j];
+            cb0 += kj < ob.key[0] ? 1u : 0u;
+            cb1 += kj < ob.key[1] ? 1u : 0u;
+            cbc += kj < cm_k ? 1u : 0u;
+          }
+          const bool v0 = lane < ob.n && !rem0, v1 = 64u + lane < ob.n && !rem1;
+          if (v0) atomicAdd(&hist[cb0], 1u);
+          if (v1) atomicAdd(&hist[cb1], 1u);
+          wave_lds_sync();
+          const uint32_t hinc = wave_incl_scan_dpp(lane <= m ? hist[lane] : 0u);
+          abc = shfl32(hinc, rel ? (int)cbc : (int)lane);
+          if (rel && inobs) pf_and(L, cu_p, Q_UPG);
         }
         const bool v0 = lane < ob.n && !rem0, v1 = 64u + lane < ob.n && !rem1;
-        uint32_t cb0 = 0, cb1 = 0, cbc = 0, abc = 0;
-        for (uint64_t t = relm; t; t &= t - 1) {
-          const int x = (int)__builtin_ctzll(t);
-          const int64_t kx = rl64(cm_k, x);
-          cb0 += (v0 && kx < ob.key[0]) ? 1u : 0u;
-          cb1 += (v1 && kx < ob.key[1]) ? 1u : 0u;
-          cbc += (rel && kx < cm_k) ? 1u : 0u;
-          const uint32_t ab = (uint32_t)__builtin_popcountll(ballot(v0 && ob.key[0] < kx)) +
-                              (uint32_t)__builtin_popcountll(ballot(v1 && ob.key[1] < kx));
-          abc = (int)lane == x ? ab : abc;
-        }
         RPROF(17);
-        const uint64_t rm0 = ballot(rem0 && lane < ob.n), rm1 = ballot(rem1 && 64u + lane < ob.n);
+        const uint64_t rm0 = ballot(rem0), rm1 = ballot(rem1);
         const uint32_t nrem = (uint32_t)__builtin_popcountll(rm0) + (uint32_t)__builtin_popcountll(rm1);
-        const uint32_t m = (uint32_t)__builtin_popcountll(relm);
         const uint32_t T = ob.n - nrem + m, drop = T > K ? T - K : 0u;
         const int32_t i0 = (int32_t)(lane - mbcnt(rm0) + cb0) - (int32_t)drop;
         const int32_t i1 = (int32_t)(64u + lane - (uint32_t)__builtin_popcountll(rm0) - mbcnt(rm1) + cb1) - (int32_t)drop;
@@ -1231,6 +1490,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         wave_lds_sync();
       };
       RPROF(6);
+      uint32_t nexs = ufl(L.nex);  // (the replays' extras are counted)
       for (uint32_t j = 0;;) {
         const uint64_t nxr = j < 64 ? rm & (~0ull << j) : 0ull;
         const uint32_t hi = nxr ? (uint32_t)__builtin_ctzll(nxr) : n;
@@ -1244,6 +1504,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         RPROF(20);
         const uint32_t kd = rl32(kdr, (int)hi);
         const uint32_t X = kd >> 8;
+        const int64_t xots = L.ots[X];  // Obs[Id]'s Ts (kept per player; read early)
         const uint32_t r = rl32(crr, (int)hi);
         const uint32_t g = rl32(rgdv, (int)r);
         if (lane == 0) {
@@ -1262,25 +1523,35 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
           const uint32_t odc = ob_get32(ob.pl, ix) >> 16;
           const int vl = (int)(((r & 7u) << 3) | odc);
           const int64_t va = rl64(vt0, vl), vb = rl64(vt1, vl);
-          if ((r < 8 ? va : vb) >= ufl64(L.ots[X])) {  // (Obs[Id]'s Ts: kept per player)
+          if ((r < 8 ? va : vb) >= ufl64(xots)) {
             if (lane == 0) pf_and(L, X, Q_OBS);
             wave_lds_sync();
-            int64_t wk = 0;
+            int64_t wk = 0, gt = 0;
+            uint32_t gd = 0, gp = 0;
             RCOUNT(31, 1);
             RPROF(21);
-            const uint32_t w = r_promote(L, pid, np, wk);
+            const uint32_t w = r_promote(L, pid, np, wk, gt, gd, gp);
             RPROF(22);
             if (w == RNONE) {  // (:283-289): Obs[Id] dropped, Min of the rest
               ob_remove(ob, ix);
             } else {  // promote the largest (:290-295)
-              const int64_t gt = ufl64(L.gts[w]);
-              const uint32_t gd = ufl(L.gdc[w]), gp = ufl(L.gpos[w]);
               ob_replace(ob, ix, wk, w | (gd << 16));
+              // the extra effect's slot: P4 emits from one lane at a time, so
+              // the key's count is a wave-uniform register here (nexs)
+              const uint32_t pos = nexs++;
               if (lane == 0) {
                 pf_or(L, w, Q_OBS);
                 L.opos[w] = (uint16_t)gp;
                 L.ots[w] = gt;
-                r_emit(a, L, op0, op0 + c0 + hi, CCRDT_TRMV_ADD, key_id(wk), key_score(wk), gd, gt, nullptr);
+                TrmvExtraRec e;
+                e.op = (uint32_t)(op0 + c0 + hi);
+                e.kind = CCRDT_TRMV_ADD;
+                e.dc = (uint8_t)gd;
+                e.pad = 0;
+                e.id = key_id(wk);
+                e.score = key_score(wk);
+                e.ts = gt;
+                KA->ex[op0 + pos] = e;
               }
             }
           }
@@ -1290,6 +1561,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, RLds& L) 
         j = hi + 1;
       }
       catch_up((uint32_t)__builtin_popcountll(rm & (n >= 64 ? ~0ull : ((1ull << n) - 1))));
+      if (lane == 0) L.nex = nexs;
       wave_lds_sync();
       c0 += n;
     }
@@ -1374,7 +1646,9 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
   for (uint32_t w = blockIdx.x * TRMV_R_WG + wv; w < n; w += gridDim.x * TRMV_R_WG) {
     const uint32_t key = ufl(KA->key_list ? KA->key_list[w] : w);
-    const int r = trmv_resident_key(a, key, L);
+    const uint32_t w2 = w + gridDim.x * TRMV_R_WG;
+    const uint32_t nkey = w2 < n ? ufl(KA->key_list ? KA->key_list[w2] : w2) : RNONE;
+    const int r = trmv_resident_key(a, key, nkey, L);
     if (r == R_NEXT && lane_id() == 0) {
       const uint32_t pos = atomicAdd(&KA->status[0], 1u);
       KA->ovf_list[pos] = key;

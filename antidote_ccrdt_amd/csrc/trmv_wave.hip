@@ -93,6 +93,9 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #else
 #define LD_IN(p) (*(p))
 #endif
+#ifndef TRMV_POOLSKIP
+#define TRMV_POOLSKIP 1  // FRESH pool: only decided players' final slabs written position-parallel
+#endif
 #ifndef TRMV_KPW
 #define TRMV_KPW 8
 #endif
@@ -710,40 +713,48 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t adc = ya ? ((kd >> 2) & 7u) : 0u;
       const uint32_t st = PSTART(p), c = act ? pcnt_of(L, p) : 0u;
       const uint32_t me = q - st;
-      bool fb = false, beaten = false, risk = false, seen = false, first = true;
-      bool gbeaten = false, gtie = false;  // gb_sets:largest of the segment (by Score; a tie replays)
       const uint32_t maxc = wave_max_u32_dpp(c);
       // software-pipelined: position x+1 is read while position x's clock
-      // entry (its address depends on x's element) is in flight
+      // entry (its address depends on x's element) is in flight.  The flags
+      // are wave lane masks combined on the scalar unit: each condition is
+      // one compare (a VALU instruction writing a mask), everything else
+      // SALU (as per-lane bools under short-circuits the compiler made
+      // divergent branches and kept the flags in VGPRs, four VALU
+      // instructions per flag per position)
+      const uint64_t Mya = ballot(ya);
+      uint64_t Mfb = 0, Mbeaten = 0, Mrisk = 0, Mseen = 0, Mfirst = ~0ull, Mgbeaten = 0, Mgtie = 0;
       const uint32_t p0 = c ? st : (uint32_t)ESINK;
       int64_t sxn = L.esc[p0], txn = L.ets[p0];
       uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
         const int64_t sx = sxn, tx = txn;
-        const bool valid = x < c && x != me;
-        const bool isr = valid && (kxn & 2u) != 0;
-        const bool before = x < me;
+        const uint64_t Mvalid = ballot(x < c) & ballot(x != me);
+        const uint64_t Misr = Mvalid & ballot((kxn & 2u) != 0u);
+        const uint64_t Mbefore = ballot(x < me);
         // an add against a rmv of its player: dominated by an earlier one
         // (:234), or kept by the first later one (:255-266) -> replay
-        const bool need = ya && isr && (before || !seen);
+        const uint64_t Mneed = Mya & Misr & (Mbefore | ~Mseen);
+        const bool need = (Mneed >> lane) & 1u;
         const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
         const uint32_t pn = x + 1 < c ? st + x + 1 : (uint32_t)ESINK;
         sxn = L.esc[pn];
         txn = L.ets[pn];
         kxn = L.ekd[pn];
-        fb |= need && (before ? rt >= tm : rt < tm);
-        seen |= isr && !before;
-        first &= !(isr && before);
-        risk = risk && !isr;
-        beaten = beaten && !isr;
-        gbeaten = gbeaten && !isr;
-        gtie = gtie && !isr;
-        const bool both = ya && valid && !isr;
-        risk |= both && before && tx >= tm;
-        beaten |= both && (sx > sm || (sx == sm && (before ? tx >= tm : tx > tm)));
-        gbeaten |= both && sx > sm;
-        gtie |= both && sx == sm;
+        const uint64_t Msgt = ballot(sx > sm), Mseq = ballot(sx == sm);
+        const uint64_t Mtge = ballot(tx >= tm), Mtgt = ballot(tx > tm);
+        const uint64_t Mrge = ballot(rt >= tm);
+        Mfb |= Mneed & ~(Mbefore ^ Mrge);  // before ? rt >= tm : rt < tm
+        Mseen |= Misr & ~Mbefore;
+        Mfirst &= ~(Misr & Mbefore);
+        const uint64_t Mboth = Mya & Mvalid & ~Misr;
+        Mrisk = (Mrisk & ~Misr) | (Mboth & Mbefore & Mtge);
+        Mbeaten = (Mbeaten & ~Misr) | (Mboth & (Msgt | (Mseq & ((Mbefore & Mtge) | (~Mbefore & Mtgt)))));
+        Mgbeaten = (Mgbeaten & ~Misr) | (Mboth & Msgt);
+        Mgtie = (Mgtie & ~Misr) | (Mboth & Mseq);
       }
+      const bool fb = (Mfb >> lane) & 1u, beaten = (Mbeaten >> lane) & 1u, risk = (Mrisk >> lane) & 1u;
+      const bool seen = (Mseen >> lane) & 1u, first = (Mfirst >> lane) & 1u;
+      const bool gbeaten = (Mgbeaten >> lane) & 1u, gtie = (Mgtie >> lane) & 1u;
       // equal Scores in the last segment: gb_sets order goes on to DcId and
       // Ts, which the replay settles
       if (act && (fb || risk || (ya && !seen && gtie))) PFLAG(p) = 1;
@@ -808,16 +819,18 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   if (FRESH) {
     // FRESH: every player's Masked slab lives inside its own op positions
     // [pstart, pstart + ops) of the key's pool segment (|Masked[Id]| <= its
-    // adds), so no pool order has to be built: every op position is written
-    // as its op's element (coalesced); replayed players rewrite their own
-    // ranges below, in program order after these
+    // adds), so no pool order has to be built: the op positions of a decided
+    // player's last segment (its slab) are written as their ops' elements
+    // (coalesced); rmv ops, the adds before a player's last rmv and replayed
+    // players' positions (written below) are skipped
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t q = s * 64 + lane;
       const uint32_t qq = q < nops ? q : (uint32_t)ESINK;
       const int64_t sc = L.esc[qq], ts = L.ets[qq];
       const uint32_t kd = L.ekd[qq];
-      if (q < nops) {
+      const uint32_t wa = L.pa[q < nops ? (kd >> 8) : (uint32_t)PSINK];  // pstart | plr | pflag | pcntf
+      if (q < nops && (!TRMV_POOLSKIP || (((wa >> 16) & 0xFFu) == 0u && q >= ((wa >> 8) & 0xFFu)))) {
         ST_OUT((KA->new_s.m_score + nmeta.m_off) + (q), sc);
         ST_OUT((KA->new_s.m_ts + nmeta.m_off) + (q), ts);
         ST_OUT((KA->new_s.m_dc + nmeta.m_off) + (q), (uint8_t)((kd >> 2) & 7u));
@@ -1115,13 +1128,21 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
     }
     const bool has = best_q != NONE32;
-    if (ballot(has)) {
+    const bool narrow = best_sc == (int64_t)(int32_t)best_sc && best_id == (int64_t)(int32_t)best_id;
+    if (!ballot(has)) {
+      best_q = NONE32;
+    } else if (!ballot(has && !narrow)) {
+      // 32-bit Scores and Ids: (Score, Id) as one signed 64-bit key (the
+      // Id's sign bit flipped so it orders unsigned): one reduction
+      const int64_t k = (int64_t)(((uint64_t)(uint32_t)(int32_t)best_sc << 32) |
+                                  ((uint32_t)(int32_t)best_id ^ 0x80000000u));
+      const int64_t mk = wave_min_i64_dpp(has ? k : INT64_MAX);
+      best_q = rl32(best_q, (int)__builtin_ctzll(ballot(has && k == mk)));
+    } else {
       const int64_t ms = wave_min_i64_dpp(has ? best_sc : INT64_MAX);
       const int64_t mi = wave_min_i64_dpp(has && best_sc == ms ? best_id : INT64_MAX);
       const uint64_t hit = ballot(has && best_sc == ms && best_id == mi);
       best_q = rl32(best_q, (int)__builtin_ctzll(hit));
-    } else {
-      best_q = NONE32;
     }
   }
   if (lane == 0) {

@@ -271,6 +271,13 @@ def main():
             if cpu_m:
                 cpu_samples.append(sample_keys(bi, cpu_m))
             op_b = int(np.where(bi.kind >= 2, 9 + 8 * D, 26).astype(np.int64).sum())
+            # players the batch names (sample: the first keys): the share of
+            # the state a batch needs to touch (steady byte model)
+            tm = min(65536, n_local_keys)
+            tkp = bi.key_ptr[:tm + 1].astype(np.int64)
+            tkey = np.repeat(np.arange(tm, dtype=np.int64), np.diff(tkp))
+            touched = int(np.unique((tkey << 32) | (bi.id[:int(tkp[-1])] & 0xFFFFFFFF)).size)
+            del tkey
             dbi = DeviceTrmvBatch(bi)
             del bi
             eng.sync()
@@ -284,6 +291,14 @@ def main():
             # bytes the batch must move in this layout: its ops, the old state
             # read, the new state written, the extra effects
             moved = op_b + state_bytes(ks_prev) + state_bytes(ks_new) + 32 * eng.extra_count()
+            # needed: the same with only the named players' records, slabs and
+            # Removals rows read and written (an in-place layout), every key's
+            # meta + Vc read and written and its Observed order (2 B per entry)
+            # rewritten
+            t_frac = touched / max(1, int(ks_new["np"][:tm].astype(np.int64).sum()))
+            key_b = n_local_keys * (32 + 8 * D)
+            needed = (op_b + t_frac * (state_bytes(ks_prev) + state_bytes(ks_new) - 2 * key_b) + 2 * key_b +
+                      2 * int(ks_new["nobs"].astype(np.int64).sum()) + 32 * eng.extra_count())
             ks_prev = ks_new
             tr_ms = eng.tier_ms(3)
             n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
@@ -293,6 +308,7 @@ def main():
                          "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in tiers},
                          "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers},
                          "bytes_moved": moved,
+                         "bytes_needed": int(needed), "touched_player_share": round(t_frac, 4),
                          "tier_r_GBs": moved / (tr_ms * 1e-3) / 1e9 if tr_ms > 0 else None,
                          "state_after": dict(zip(("observed", "masked", "removal_rows"),
                                                  eng.sizes()))})
@@ -301,6 +317,8 @@ def main():
         tr = [r["kernel_ms_by_tier"][3] for r in rows]
         mv = [r["bytes_moved"] for r in rows]
         ach = (sum(mv) / len(mv)) / ((sum(tr) / len(tr)) * 1e-3) / 1e9 if sum(tr) > 0 else None
+        nd = [r["bytes_needed"] for r in rows]
+        ach_n = (sum(nd) / len(nd)) / ((sum(tr) / len(tr)) * 1e-3) / 1e9 if sum(tr) > 0 else None
         steady = {"what": "batches 2..n of the bench stream onto the resident keys (no reset), "
                           "one apply_device each, wall time around it (this rank)",
                   "ops_per_s_mean": n_step / (mean_ms * 1e-3), "ms_mean": mean_ms,
@@ -312,7 +330,14 @@ def main():
                                "kernel_ms": sum(tr) / len(tr),
                                "bytes": "ops (add 26 B, rmv 9 + 8*D B) + old state read + new state "
                                         "written (player 18 B, Masked element 17 B, Removals row 8*D B, "
-                                        "key 32 + 8*D B) + 32 B per extra effect"},
+                                        "key 32 + 8*D B) + 32 B per extra effect",
+                               "needed": {"bytes_per_launch": sum(nd) / len(nd), "achieved": ach_n,
+                                          "frac": ach_n / HBM_PEAK_GBS if ach_n else None,
+                                          "bytes": "ops + the players the batch names (their records, "
+                                                   "slabs and Removals rows, old read + new written; share "
+                                                   "from the first 65,536 keys) + every key's meta and Vc "
+                                                   "read and written + 2 B per Observed entry + 32 B per "
+                                                   "extra effect: what an in-place layout would move"}},
                   "batches": rows}
         if cpu_samples:
             # the oracle on the same keys' batches 2..n onto its own resident

@@ -249,3 +249,33 @@ def test_key_grows_past_1024_players(gpu, K):
         st = eng.export()
         most = max(most, max(len({e[0] for e in st.key_state(k)["masked"]}) for k in range(nk)))
     assert most >= 5000, most
+
+
+@pytest.mark.parametrize("shift", ["small", "epoch_us", "wide_id", "wide_score"])
+def test_host_entry_narrow_columns(gpu, shift):
+    """The host entry sends Id / Score / Ts columns over PCIe as int32 when they
+    fit (Ts relative to a per-chunk base, rmv rows as they are) and widens
+    them on the device; a value outside int32 sends its column wide.  Every
+    variant is bit-exact against the oracle on the same stream, two batches
+    (fresh keys, then resident ones)."""
+    from dataclasses import replace
+    nk, D, K = 20000, 8, 100
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    for i in range(2):
+        b = gen_trmv(2_500_000, nk, D, n_players=64, score_max=10**6, rmv_pm=100, lag_max=64,
+                     seed=0x5EED + i, clock0=i * 2_500_000)
+        add = b.kind < 2
+        if shift == "epoch_us":  # microsecond timestamps: wide values, narrow within a chunk
+            ts = b.ts.copy()
+            ts[add] += 1_700_000_000_000_000
+            b = replace(b, ts=ts, rmv_vc=np.where(b.rmv_vc > 0, b.rmv_vc + 1_700_000_000_000_000, 0))
+        elif shift == "wide_id":
+            ids = b.id.copy()
+            ids[b.n_ops // 2] = 1 << 40
+            b = replace(b, id=ids)
+        elif shift == "wide_score":
+            sc = b.score.copy()
+            sc[np.nonzero(add)[0][-1]] = -(1 << 35)
+            b = replace(b, score=sc)
+        xe, xo = eng.apply(b), orac.apply(b)
+        _compare(eng, orac, b, D, xe, xo)
