@@ -7,6 +7,9 @@
 // canonical state image and the device layout.  There is no CPU compute path:
 // if the HIP runtime or the device is missing, calls fail with CCRDT_EDEVICE.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -586,6 +589,14 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   Engine& E = *e;
   const uint64_t nk = (uint64_t)E.n_keys, n = (uint64_t)ops->n_ops;
   const int D = E.n_dc;
+  // CCRDT_STAGE_TRACE=1: host-side phase times of this call on stderr
+  static const bool trace = std::getenv("CCRDT_STAGE_TRACE") != nullptr;
+  double tp[6] = {};
+  int ti = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto mark = [&] {
+    if (trace) tp[ti++] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
   // CSR shape checks (host side; values are validated by the kernel)
   if (ops->key_ptr[0] != 0 || ops->key_ptr[nk] != n) {
     set_error("trmv_apply: key_ptr must start at 0 and end at n_ops");
@@ -605,6 +616,7 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   CCRDT_TRY(E.st_ts.ensure(n * 8));
   CCRDT_TRY(E.st_rvc.ensure(nr * D * 8));
   // (pageable caller memory: through the pinned staging slots, staging.cpp)
+  mark();
   CCRDT_TRY(h2d_staged(E, E.st_kp.p, ops->key_ptr, (nk + 1) * 8));
   int up = n ? h2d_trmv_ops(E, n, ops->kind, ops->id, ops->score, ops->dc, ops->ts, E.st_kind.as<uint8_t>(),
                             E.st_dc.as<uint8_t>(), E.st_id.as<int64_t>(), E.st_score.as<int64_t>(),
@@ -622,6 +634,7 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
     CCRDT_TRY(h2d_staged_i64(E, E.st_ts.as<int64_t>(), ops->ts, n, ops->kind, E.st_kind.as<uint8_t>(), 2, E.st_n32[2],
                              E.st_nbase[2]));
   }
+  mark();
   // removal clocks as int32 relative to a per-chunk base when they fit
   if (nr)
     CCRDT_TRY(h2d_staged_i64(E, E.st_rvc.as<int64_t>(), ops->rmv_vc, nr * D, nullptr, nullptr, 1, E.st_n32[1],
@@ -635,13 +648,20 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   d.ts = E.st_ts.as<int64_t>();
   d.rmv_vc = nr ? E.st_rvc.as<int64_t>() : nullptr;
   d.n_rmv_rows = (int64_t)nr;
+  mark();
   const int rc = ccrdt_trmv_apply_device(e, &d);
+  mark();
   if (rc != CCRDT_OK && rc != CCRDT_EKEYCAP) return rc;
   if (extra) {  // EKEYCAP: the batch committed; its extras are fetched too
     const std::string msg = g_last_error;
     CCRDT_TRY(ccrdt_trmv_fetch_extra(e, extra));
     if (rc != CCRDT_OK) set_error(msg);
   }
+  mark();
+  if (trace)
+    std::fprintf(stderr, "trmv_apply: checks %.2f | key_ptr + ops staged %.2f | rmv clocks staged %.2f | "
+                 "apply (waits the DMAs) %.2f | extras %.2f ms\n", tp[0], tp[1] - tp[0], tp[2] - tp[1],
+                 tp[3] - tp[2], tp[4] - tp[3]);
   return rc;
 }
 

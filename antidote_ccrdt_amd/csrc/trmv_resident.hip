@@ -85,7 +85,10 @@ constexpr int RCH = 64;        // ops per chunk
 constexpr int RCHR = 16;       // rmvs per chunk (rows of the clock table)
 constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
-#define TRMV_WARM 1  // the next key's lines are loaded into the caches during P1-P3
+#define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
+#endif
+#ifndef TRMV_RPF
+#define TRMV_RPF 0  // replays: a rmv-first player's first slab lines touched with its Removals row
 #endif
 #ifndef TRMV_DPPSCAN
 #define TRMV_DPPSCAN 1  // P4's segmented scan on DPP row shifts (0: ds_bpermute shuffles)
@@ -1126,6 +1129,15 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #pragma unroll
           for (int d = 0; d < TRMV_DPAD; ++d) R[d] = (has_row && d < dn) ? KA->new_s.r_vc[rbase + d] : 0;
         }
+#if TRMV_RPF
+        // a player whose first op here is a rmv: its slab's first lines are
+        // touched with the Removals row (into this CU's L1), so the filter's
+        // first block of loads does not go to L2
+        if (cnt != 0 && (L.u.c.ckd[L.u.c.csrt[ws]] & 3u) >= 2) {
+          const int64_t tch = KA->new_s.m_score[base] ^ KA->new_s.m_ts[base] ^ (int64_t)KA->new_s.m_dc[base];
+          asm volatile("" ::"v"(tch));
+        }
+#endif
         const int64_t wid = L.u.c.cid[ws];
         bool moved = false;
         for (uint32_t x = ws; x < we; ++x) {

@@ -94,7 +94,7 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #define LD_IN(p) (*(p))
 #endif
 #ifndef TRMV_POOLSKIP
-#define TRMV_POOLSKIP 1  // FRESH pool: only decided players' final slabs written position-parallel
+#define TRMV_POOLSKIP 0  // FRESH pool: only decided players' final slabs written (A/B r04: tier 0 2.24 -> 2.44 ms)
 #endif
 #ifndef TRMV_KPW
 #define TRMV_KPW 8
