@@ -540,7 +540,7 @@ int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* x) {
   Engine& E = *e;
   const uint64_t n_ops = E.last_n_ops, nk = (uint64_t)E.n_keys;
   const int D = E.n_dc;
-  if (x->kind && n_ops) memset(x->kind, CCRDT_NOOP, n_ops);
+  if (x->kind && n_ops) host_fill(x->kind, CCRDT_NOOP, n_ops);
   if (!n_ops || !nk || !E.ex_cnt.p) return CCRDT_OK;
   // The extras are packed on the device into rows [op, kind, id, score, dc,
   // ts, vc...] (the exchange's pack kernel) and only those rows cross PCIe:

@@ -96,6 +96,7 @@ namespace ccrdt {
 using Engine = ccrdt_engine;
 // Host -> device copy of pageable caller memory through the engine's pinned
 // staging slots, parallel host threads (staging.cpp); queued on E.stream.
+void host_fill(void* dst, int v, uint64_t bytes);
 int h2d_staged(Engine& E, void* dst, const void* src, uint64_t bytes);
 // An int64 column through the staging slots as int32 (staging.cpp).
 int h2d_staged_i64(Engine& E, int64_t* dst, const int64_t* src, uint64_t n, const uint8_t* kind,

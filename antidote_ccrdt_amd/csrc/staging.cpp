@@ -30,8 +30,9 @@ namespace {
 constexpr int STAGE_THREADS = 16;                       // (at most; see stage_threads)
 constexpr uint64_t STAGE_CHUNK = 16ull << 20;          // bytes per slot
 constexpr uint64_t STAGE_DIRECT = 4ull << 20;           // below: one plain copy
-constexpr uint64_t NARROW_CHUNK = STAGE_CHUNK / 4;      // int32 elements per slot
-constexpr uint64_t NARROW_MAX_CHUNKS = 1024;            // (4 Gi elements)
+constexpr uint64_t NARROW_CHUNK = STAGE_CHUNK / 16;     // int32 elements per chunk (a quarter slot: the
+                                                        // threads stay busy to the column's end)
+constexpr uint64_t NARROW_MAX_CHUNKS = 4096;            // (4 Gi elements)
 constexpr uint64_t OPS_CHUNK = 1ull << 20;              // ops per slot in h2d_trmv_ops (14 B each)
 static_assert(OPS_CHUNK * 14 <= STAGE_CHUNK, "an ops chunk fits one slot");
 }  // namespace
@@ -76,6 +77,28 @@ static bool narrow_chunk_plain(const int64_t* src, const uint8_t* kind, int32_t*
     bad |= (uint64_t)((v >> 31) ^ (v >> 63));
   }
   return bad == 0;
+}
+
+// memset on the staging threads (a host output buffer of n_ops bytes: its
+// first touch is page faults, which the threads take in parallel)
+void host_fill(void* dst, int v, uint64_t bytes) {
+  constexpr uint64_t PART = 8ull << 20;
+  const uint64_t parts = (bytes + PART - 1) / PART;
+  const int T = (int)std::min<uint64_t>((uint64_t)stage_threads(), parts);
+  if (T <= 1) {
+    memset(dst, v, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([=] {
+      for (uint64_t c = (uint64_t)t; c < parts; c += (uint64_t)T) {
+        const uint64_t off = c * PART;
+        memset(static_cast<char*>(dst) + off, v, std::min<uint64_t>(PART, bytes - off));
+      }
+    });
+  for (std::thread& x : th) x.join();
 }
 
 static int stage_init(Engine& E) {

@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_C0PRE
+#define TRMV_C0PRE 0  // the first chunk's ops kept in registers from P2
+#endif
 #ifndef TRMV_RPF
 #define TRMV_RPF 0  // replays: a rmv-first player's first slab lines touched with its Removals row
 #endif
@@ -802,6 +805,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   {
     // ---- P2. every op's player; ops per player; rmv players
     uint32_t np = om.np;
+#if TRMV_C0PRE
+    // the first chunk's ops stay in registers from here (its Ids, kinds and
+    // players from this pass; Scores, Ts, DcIds loaded with them), so the
+    // chunk loop's first round does not wait for its loads
+    int64_t c0id = 0, c0sc = 0, c0ts = 0;
+    uint32_t c0kd = 0, c0dc = 0, c0p = (uint32_t)RP;
+#endif
     // 128 ops per round: both halves' Ids and kinds load together, then each
     // half is resolved (one 64-lane claim table)
     for (uint32_t c0 = 0; c0 < nops; c0 += 128) {
@@ -816,6 +826,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         kh[h] = vh[h] ? (uint32_t)KA->kind[op0 + l] : 0u;
         wide |= vh[h] && !fits32(idh[h]);
       }
+#if TRMV_C0PRE
+      if (c0 == 0 && vh[0]) {
+        c0sc = KA->score[op0 + lane];
+        c0ts = KA->ts[op0 + lane];
+        c0dc = KA->dc[op0 + lane];
+      }
+#endif
       if (ballot(wide)) return R_NEXT;  // a wide Id: tier S
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -823,6 +840,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint32_t l = c0 + 64u * h + lane;
         uint32_t p;
         if (!r_resolve(L, idh[h], vh[h], np, p)) return R_NEXT;
+#if TRMV_C0PRE
+        if (c0 == 0 && h == 0) {
+          c0id = idh[0];
+          c0kd = kh[0];
+          c0p = vh[0] ? p : (uint32_t)RP;
+        }
+#endif
         if (vh[h]) {
           KA->op_pl[op0 + l] = (uint8_t)p;
           atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
@@ -972,12 +996,32 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       uint32_t n = nops - c0 < (uint32_t)RCH ? nops - c0 : (uint32_t)RCH;
       bool v = lane < n;
       const uint64_t gi = op0 + c0 + lane;
+#if TRMV_C0PRE
+      uint32_t kind, dc, p;
+      int64_t id, sc, ts;
+      if (c0 == 0) {
+        kind = c0kd;
+        id = c0id;
+        sc = c0sc;
+        ts = c0ts;
+        dc = c0dc;
+        p = c0p;
+      } else {
+        kind = v ? (uint32_t)KA->kind[gi] : 0u;
+        id = v ? KA->id[gi] : 0;
+        sc = v ? KA->score[gi] : 0;
+        ts = v ? KA->ts[gi] : 0;
+        dc = v ? (uint32_t)KA->dc[gi] : 0u;
+        p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
+      }
+#else
       const uint32_t kind = v ? (uint32_t)KA->kind[gi] : 0u;
       const int64_t id = v ? KA->id[gi] : 0;
       const int64_t sc = v ? KA->score[gi] : 0;
       const int64_t ts = v ? KA->ts[gi] : 0;
       const uint32_t dc = v ? (uint32_t)KA->dc[gi] : 0u;
       const uint32_t p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
+#endif
       bool isr = v && (kind == 2 || kind == 3);
       uint64_t rm = ballot(isr);
       if (__builtin_popcountll(rm) > RCHR) {  // cut before the chunk's 17th rmv
