@@ -76,6 +76,33 @@ struct DevBuf {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Bounds-checked loads through a buffer descriptor over [base, base + bytes):
+// a lane whose byte offset lies past the range reads 0 -- no branch around
+// the load, no fault -- so a run of conditional loads issues back to back.
+// The descriptor's inputs are made provably wave-uniform (readfirstlane):
+// the caller's base and size must be the same on every lane.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr uint32_t BOOB = 0x7FFFFFF0u;  // an open-ended range, and the offset that reads past it
+__device__ __forceinline__ int64_t bld64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return (int64_t)(((uint64_t)v[1] << 32) | v[0]);
+}
+__device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b8(r, (int)off, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }

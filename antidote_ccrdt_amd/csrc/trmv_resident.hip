@@ -87,6 +87,12 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_HOISTP
+#define TRMV_HOISTP 1  // the replays' pool column bases read once per replay, not per access
+#endif
+#ifndef TRMV_BUFLD
+#define TRMV_BUFLD 1  // P1's record and element loads through bounds-checked buffer descriptors
+#endif
 #ifndef TRMV_C0PRE
 #define TRMV_C0PRE 0  // the first chunk's ops kept in registers from P2
 #endif
@@ -631,6 +637,24 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       // (the four arrays' bases once, and pl_gb read whatever the slab's
       // count: a load conditional on another load's value waited for it, slot
       // by slot)
+#if TRMV_BUFLD
+      // (bounds-checked buffer loads: the slots past np read 0, every load
+      // of the four slots goes out back to back)
+      const __amdgpu_buffer_rsrc_t rid = bsrc(KA->old_s.pl_id + om.p_off, om.np * 8u);
+      const __amdgpu_buffer_rsrc_t rinfo = bsrc(KA->old_s.pl_info + om.p_off, om.np * 4u);
+      const __amdgpu_buffer_rsrc_t rslab = bsrc(KA->old_s.pl_slab + om.p_off, om.np * 4u);
+      const __amdgpu_buffer_rsrc_t rgb = bsrc(KA->old_s.pl_gb + om.p_off, om.np * 2u);
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        const bool v = p < om.np;
+        pid[u] = bld64(rid, p * 8u);
+        const uint32_t in = bld32(rinfo, p * 4u);
+        info[u] = v ? in : RNONE;
+        slab[u] = bld32(rslab, p * 4u);
+        gb[u] = bld16(rgb, p * 2u);
+      }
+#else
       const int64_t* const pl_id = KA->old_s.pl_id + om.p_off;
       const uint32_t* const pl_info = KA->old_s.pl_info + om.p_off;
       const uint32_t* const pl_slab = KA->old_s.pl_slab + om.p_off;
@@ -645,12 +669,33 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         slab[u] = v ? pl_slab[pp] : 0u;
         gb[u] = v ? (uint32_t)pl_gb[pp] : 0u;
       }
+#endif
 #pragma unroll
       for (int u = 0; u < RSL; ++u) gb[u] = (slab[u] >> 16) > 1 ? gb[u] : 0u;  // (readers take 0 below 2)
     }
     int64_t os[RSL], ot[RSL], gs[RSL], gt[RSL];
     uint32_t gd[RSL];
     {
+#if TRMV_BUFLD
+      // (slabs may leave holes, so a key's pool segment is not [0, nm): the
+      // range is open-ended and only the lanes with nothing to read are sent
+      // past it; the others read exactly what the plain loads read)
+      const __amdgpu_buffer_rsrc_t rsc = bsrc(KA->old_s.m_score + om.m_off, BOOB);
+      const __amdgpu_buffer_rsrc_t rts = bsrc(KA->old_s.m_ts + om.m_off, BOOB);
+      const __amdgpu_buffer_rsrc_t rdc = bsrc(KA->old_s.m_dc + om.m_off, BOOB);
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
+        const bool ho = obx != NONE16, hg = cnt != 0;
+        const uint32_t qo = off + (ho ? obx : 0u), qg = off + gb[u];
+        os[u] = bld64(rsc, ho ? qo * 8u : BOOB);
+        ot[u] = bld64(rts, ho ? qo * 8u : BOOB);
+        odr[u] = bld8(rdc, ho ? qo : BOOB);
+        gs[u] = bld64(rsc, hg ? qg * 8u : BOOB);
+        gt[u] = bld64(rts, hg ? qg * 8u : BOOB);
+        gd[u] = bld8(rdc, hg ? qg : BOOB);
+      }
+#else
       const int64_t* const m_score = KA->old_s.m_score + om.m_off;
       const int64_t* const m_ts = KA->old_s.m_ts + om.m_off;
       const uint8_t* const m_dc = KA->old_s.m_dc + om.m_off;
@@ -666,17 +711,48 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         gt[u] = hg ? m_ts[qg] : 0;
         gd[u] = hg ? (uint32_t)m_dc[qg] : 0u;
       }
+#endif
     }
-    uint32_t hh[RSL];
-    bool pend[RSL];
+    {
+      // the Id hash (16-bit slots: CAS on the containing word) while the
+      // element loads above are in flight; each round reads every pending
+      // slot's word, then claims the free ones
+      uint32_t hh[RSL];
+      bool pend[RSL];
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        pend[u] = 64u * u + lane < om.np;
+        hh[u] = rhash(pid[u]);
+      }
+      for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < RSL; ++u) any |= pend[u];
+        if (!ballot(any)) break;
+        uint32_t cur[RSL];
+#pragma unroll
+        for (int u = 0; u < RSL; ++u)
+          cur[u] = pend[u] ? *reinterpret_cast<const uint32_t*>(&L.u.r.hs[hh[u] & ~1u]) : 0u;
+#pragma unroll
+        for (int u = 0; u < RSL; ++u) {
+          if (!pend[u]) continue;
+          const uint32_t sh = (hh[u] & 1u) * 16u;
+          if (((cur[u] >> sh) & 0xFFFFu) == RH_NONE) {
+            const uint32_t p = 64u * u + lane;
+            uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[hh[u] & ~1u]);
+            if (atomicCAS(w, cur[u], (cur[u] & ~(0xFFFFu << sh)) | (p << sh)) == cur[u]) pend[u] = false;
+          } else {
+            hh[u] = (hh[u] + 1) & (2 * RP - 1);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < RSL; ++u) {
       const uint32_t p = 64u * u + lane;
       const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
       const bool ho = obx != NONE16;
       if (u < 2) k01[u] = mkkey(os[u], pid[u]);
-      pend[u] = p < om.np;
-      hh[u] = rhash(pid[u]);
       if (p < om.np) {
         wide |= !fits32(pid[u]) || !fits32(os[u]) || !fits32(gs[u]);
         L.msc[p] = (int32_t)gs[u];
@@ -693,30 +769,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         span = off + cnt > span ? off + cnt : span;
       }
       inobs |= (ho ? 1u : 0u) << u;
-    }
-    // the Id hash (16-bit slots: CAS on the containing word); each round
-    // reads every pending slot's word, then claims the free ones
-    for (;;) {
-      bool any = false;
-#pragma unroll
-      for (int u = 0; u < RSL; ++u) any |= pend[u];
-      if (!ballot(any)) break;
-      uint32_t cur[RSL];
-#pragma unroll
-      for (int u = 0; u < RSL; ++u)
-        cur[u] = pend[u] ? *reinterpret_cast<const uint32_t*>(&L.u.r.hs[hh[u] & ~1u]) : 0u;
-#pragma unroll
-      for (int u = 0; u < RSL; ++u) {
-        if (!pend[u]) continue;
-        const uint32_t sh = (hh[u] & 1u) * 16u;
-        if (((cur[u] >> sh) & 0xFFFFu) == RH_NONE) {
-          const uint32_t p = 64u * u + lane;
-          uint32_t* w = reinterpret_cast<uint32_t*>(&L.u.r.hs[hh[u] & ~1u]);
-          if (atomicCAS(w, cur[u], (cur[u] & ~(0xFFFFu << sh)) | (p << sh)) == cur[u]) pend[u] = false;
-        } else {
-          hh[u] = (hh[u] + 1) & (2 * RP - 1);
-        }
-      }
     }
   }
   if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
@@ -1159,6 +1211,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
       wave_lds_sync();
       if (lane < (uint32_t)__builtin_popcountll(wm)) {
+#if TRMV_HOISTP
+        // the pool columns' bases read once here: a kernel argument is
+        // re-read at each use (kernarg_as), and inside these loops each
+        // re-read is a scalar load the next global access waits for
+        int64_t* const Msc = KA->new_s.m_score;
+        int64_t* const Mts = KA->new_s.m_ts;
+        uint8_t* const Mdc = KA->new_s.m_dc;
+#else
+#define Msc KA->new_s.m_score
+#define Mts KA->new_s.m_ts
+#define Mdc KA->new_s.m_dc
+#endif
         const uint32_t wp = L.u.c.cwp[lane], ws = L.u.c.cws[lane], we = L.u.c.cwe[lane];
         uint32_t f = L.pf[wp];
         const uint32_t ns = L.nslab[wp];
@@ -1178,7 +1242,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         // touched with the Removals row (into this CU's L1), so the filter's
         // first block of loads does not go to L2
         if (cnt != 0 && (L.u.c.ckd[L.u.c.csrt[ws]] & 3u) >= 2) {
-          const int64_t tch = KA->new_s.m_score[base] ^ KA->new_s.m_ts[base] ^ (int64_t)KA->new_s.m_dc[base];
+          const int64_t tch = Msc[base] ^ Mts[base] ^ (int64_t)Mdc[base];
           asm volatile("" ::"v"(tch));
         }
 #endif
@@ -1198,16 +1262,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             uint32_t pos = RNONE;
             if ((kd >> 5) & 1u)  // set semantics: the element may be there
               for (uint32_t j = 0; j < cnt; ++j)
-                if (KA->new_s.m_ts[base + j] == ets && KA->new_s.m_dc[base + j] == edc &&
-                    KA->new_s.m_score[base + j] == esc) {
+                if (Mts[base + j] == ets && Mdc[base + j] == edc &&
+                    Msc[base + j] == esc) {
                   pos = j;
                   break;
                 }
             if (pos == RNONE) {
               pos = cnt++;
-              KA->new_s.m_score[base + pos] = esc;
-              KA->new_s.m_ts[base + pos] = ets;
-              KA->new_s.m_dc[base + pos] = (uint8_t)edc;
+              Msc[base + pos] = esc;
+              Mts[base + pos] = ets;
+              Mdc[base + pos] = (uint8_t)edc;
             }
             L.u.c.cres[o] = pos << 16;
           } else {  // rmv/3: merge_vc (:254, :369-386), filter Masked[Id] (:255-266)
@@ -1229,18 +1293,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
-                s4[e] = KA->new_s.m_score[base + j];
-                t4[e] = KA->new_s.m_ts[base + j];
-                d4[e] = KA->new_s.m_dc[base + j];
+                s4[e] = Msc[base + j];
+                t4[e] = Mts[base + j];
+                d4[e] = Mdc[base + j];
               }
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e;
                 if (j < cnt && t4[e] > V[d4[e]]) {
                   if (w != j) {
-                    KA->new_s.m_score[base + w] = s4[e];
-                    KA->new_s.m_ts[base + w] = t4[e];
-                    KA->new_s.m_dc[base + w] = (uint8_t)d4[e];
+                    Msc[base + w] = s4[e];
+                    Mts[base + w] = t4[e];
+                    Mdc[base + w] = (uint8_t)d4[e];
                   }
                   if (w == 0 || gb_gt(s4[e], d4[e], t4[e], bsc, bdc, bts)) {
                     bsc = s4[e];
@@ -1259,6 +1323,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             L.u.c.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
           }
         }
+#if !TRMV_HOISTP
+#undef Msc
+#undef Mts
+#undef Mdc
+#endif
         L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
         if (has_row) {
           for (int d = 0, dn = KA->n_dc; d < dn; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);

@@ -268,8 +268,12 @@ class TopkRmvEngine(_Engine):
         return _lib.TrmvOps(b.n_ops, int(b.rmv_vc.shape[0]), ptr(b.key_ptr), ptr(b.kind),
                             ptr(b.id), ptr(b.score), ptr(b.dc), ptr(b.ts), ptr(b.rmv_vc))
 
-    def apply(self, batch: TrmvBatch, want_extra: bool = True) -> TrmvExtra | None:
-        """update/2 for every op of the batch (topk_rmv.erl:140-148)."""
+    def apply(self, batch: TrmvBatch, want_extra: bool = True,
+              out: TrmvExtra | None = None) -> TrmvExtra | None:
+        """update/2 for every op of the batch (topk_rmv.erl:140-148).
+
+        `out`: caller-owned extras arrays of at least n_ops entries (as a NIF
+        would keep them), filled in place and returned; else fresh ones."""
         b = TrmvBatch(*(getattr(batch, f.name) for f in fields(TrmvBatch))).normalized()
         if b.n_keys != self.n_keys:
             raise ValueError("batch key_ptr must have n_keys+1 entries")
@@ -279,9 +283,19 @@ class TopkRmvEngine(_Engine):
         x = cx = None
         if want_extra:
             n = b.n_ops
-            x = TrmvExtra(np.empty(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64),
-                          np.zeros(n, np.uint8), np.zeros(n, np.int64),
-                          np.zeros((n, self.n_dc), np.int64))
+            if out is not None:
+                cols = (out.kind, out.id, out.score, out.dc, out.ts)
+                if (any(c.shape[0] < n or not c.flags.c_contiguous for c in cols) or
+                        out.vc.ndim != 2 or out.vc.shape[0] < n or out.vc.shape[1] != self.n_dc or
+                        not out.vc.flags.c_contiguous or
+                        [c.dtype for c in cols] != [np.uint8, np.int64, np.int64, np.uint8, np.int64] or
+                        out.vc.dtype != np.int64):
+                    raise ValueError("out: TrmvExtra of contiguous columns with >= n_ops entries")
+                x = out
+            else:
+                x = TrmvExtra(np.empty(n, np.uint8), np.zeros(n, np.int64), np.zeros(n, np.int64),
+                              np.zeros(n, np.uint8), np.zeros(n, np.int64),
+                              np.zeros((n, self.n_dc), np.int64))
             cx = C.byref(_lib.TrmvExtra(ptr(x.kind), ptr(x.id), ptr(x.score), ptr(x.dc), ptr(x.ts),
                                         ptr(x.vc)))
         self._checked(lib.ccrdt_trmv_apply(self.h, C.byref(ops), cx), "trmv_apply", x)

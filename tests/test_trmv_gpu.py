@@ -5,7 +5,7 @@ import pytest
 
 import oracle as orc
 from antidote_ccrdt_amd import _lib
-from antidote_ccrdt_amd.engine import TopkRmvEngine, TrmvState, gen_trmv
+from antidote_ccrdt_amd.engine import TopkRmvEngine, TrmvExtra, TrmvState, gen_trmv
 from trmv_helpers import effects_to_batch, extra_term, load, run_fixture, state_key
 
 pytestmark = pytest.mark.gpu
@@ -92,7 +92,11 @@ def test_multi_batch_and_import(gpu, K, npl):
         add = b.kind < 2
         b.ts[add] += i * 10**6
         b.rmv_vc[b.rmv_vc > 0] += i * 10**6
-        xe, xo = eng.apply(b), orac.apply(b)
+        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
+        if i:
+            assert xe is xout
+            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
+        xo = orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
     st = eng.export()
     e2 = TopkRmvEngine(nk, K, D)
@@ -209,7 +213,11 @@ def _stream_batches(eng, orac, nk, D, K, plan, seed):
     for i, (n, npl, smax) in enumerate(plan):
         b = gen_trmv(n, nk, D, npl, smax, 120, 16, 20, 10, seed=seed + i, clock0=clock)
         clock += n + 1
-        xe, xo = eng.apply(b), orac.apply(b)
+        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
+        if i:
+            assert xe is xout
+            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
+        xo = orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
 
 
@@ -243,7 +251,11 @@ def test_key_grows_past_1024_players(gpu, K):
     for i, (n, npl) in enumerate([(2000, 1500), (9000, 7000), (9000, 7000), (3000, 7000)]):
         b = gen_trmv(n, nk, D, npl, 10**6, 20, 16, 20, 10, seed=1200 + i, clock0=clock)
         clock += n + 1
-        xe, xo = eng.apply(b), orac.apply(b)
+        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
+        if i:
+            assert xe is xout
+            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
+        xo = orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
         assert eng.overflow_keys(4) == 0
         st = eng.export()
@@ -261,6 +273,11 @@ def test_host_entry_narrow_columns(gpu, shift):
     from dataclasses import replace
     nk, D, K = 20000, 8, 100
     eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    # the second batch's extras go into caller-owned columns left dirty by
+    # the first one (apply(out=...)): every field the oracle has must be rewritten
+    n_out = 2_600_000
+    xout = TrmvExtra(np.full(n_out, 7, np.uint8), np.full(n_out, -3, np.int64), np.full(n_out, -3, np.int64),
+                     np.full(n_out, 9, np.uint8), np.full(n_out, -3, np.int64), np.full((n_out, D), -3, np.int64))
     for i in range(2):
         b = gen_trmv(2_500_000, nk, D, n_players=64, score_max=10**6, rmv_pm=100, lag_max=64,
                      seed=0x5EED + i, clock0=i * 2_500_000)
@@ -277,5 +294,9 @@ def test_host_entry_narrow_columns(gpu, shift):
             sc = b.score.copy()
             sc[np.nonzero(add)[0][-1]] = -(1 << 35)
             b = replace(b, score=sc)
-        xe, xo = eng.apply(b), orac.apply(b)
+        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
+        if i:
+            assert xe is xout
+            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
+        xo = orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
