@@ -866,6 +866,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #endif
     // 128 ops per round: both halves' Ids and kinds load together, then each
     // half is resolved (one 64-lane claim table)
+#if TRMV_BUFLD
+    // (the key's op columns through bounds-checked descriptors: past nops reads 0)
+    const __amdgpu_buffer_rsrc_t bid = bsrc(KA->id + op0, nops * 8u);
+    const __amdgpu_buffer_rsrc_t bkd = bsrc(KA->kind + op0, nops);
+#endif
     for (uint32_t c0 = 0; c0 < nops; c0 += 128) {
       int64_t idh[2];
       uint32_t kh[2];
@@ -874,8 +879,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       for (int h = 0; h < 2; ++h) {
         const uint32_t l = c0 + 64u * h + lane;
         vh[h] = l < nops;
+#if TRMV_BUFLD
+        idh[h] = bld64(bid, l * 8u);
+        kh[h] = bld8(bkd, l);
+#else
         idh[h] = vh[h] ? KA->id[op0 + l] : 0;
         kh[h] = vh[h] ? (uint32_t)KA->kind[op0 + l] : 0u;
+#endif
         wide |= vh[h] && !fits32(idh[h]);
       }
 #if TRMV_C0PRE
@@ -956,6 +966,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     bool wide = false;
     if (span) {
       int32_t prev = -1;
+#if TRMV_BUFLD
+      // (the old pool through bounds-checked descriptors over the key's span,
+      // the new side's bases read once: the window's loads and stores issue
+      // without a branch or a scalar wait each)
+      const __amdgpu_buffer_rsrc_t qsc = bsrc(KA->old_s.m_score + om.m_off, span * 8u);
+      const __amdgpu_buffer_rsrc_t qts = bsrc(KA->old_s.m_ts + om.m_off, span * 8u);
+      const __amdgpu_buffer_rsrc_t qdc = bsrc(KA->old_s.m_dc + om.m_off, span);
+      int64_t* const Nsc = KA->new_s.m_score + nm.m_off;
+      int64_t* const Nts = KA->new_s.m_ts + nm.m_off;
+      uint8_t* const Ndc = KA->new_s.m_dc + nm.m_off;
+#endif
       // four windows of 64 positions per round: their loads go out together
       for (uint32_t g0 = 0; g0 < span; g0 += 256) {
         int64_t wsc[4], wts[4];
@@ -963,10 +984,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t q = g0 + 64u * i + lane;
+#if TRMV_BUFLD
+          wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
+          wts[i] = bld64(qts, q * 8u);
+          wdc[i] = bld8(qdc, q);
+#else
           const uint64_t src = (uint64_t)om.m_off + (q < span ? q : 0u);
           wsc[i] = q < span ? KA->old_s.m_score[src] : 0;
           wts[i] = q < span ? KA->old_s.m_ts[src] : 0;
           wdc[i] = q < span ? (uint32_t)KA->old_s.m_dc[src] : 0u;
+#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1019,10 +1046,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
             if (q < off + cnt) {
               wide |= !fits32(sc);
+#if TRMV_BUFLD
+              const uint32_t dst = (L.nslab[o] & 0xFFFFu) + (q - off);
+              Nsc[dst] = sc;
+              Nts[dst] = ts;
+              Ndc[dst] = (uint8_t)dc;
+#else
               const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
               KA->new_s.m_score[dst] = sc;
               KA->new_s.m_ts[dst] = ts;
               KA->new_s.m_dc[dst] = (uint8_t)dc;
+#endif
             }
           }
           wave_lds_sync();
@@ -1030,11 +1064,33 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     }
     if (ballot(wide)) return R_NEXT;  // a wide Score in Masked: tier S
+#if TRMV_BUFLD
+    {
+      // old Removals rows, 32 per round: the round's loads, then its stores
+      const __amdgpu_buffer_rsrc_t qr = bsrc(KA->old_s.r_vc + (uint64_t)om.r_off * D, om.nr * (uint32_t)D * 8u);
+      int64_t* const Nr = KA->new_s.r_vc + (uint64_t)nm.r_off * D;
+      const uint32_t d = lane & 7u;
+      for (uint32_t r0 = 0; r0 < om.nr; r0 += 32) {
+        int64_t rv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t r = r0 + 8u * i + (lane >> 3);
+          rv[i] = bld64(qr, (int)d < D ? (r * (uint32_t)D + d) * 8u : BOOB);  // (past nr: 0)
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t r = r0 + 8u * i + (lane >> 3);
+          if (r < om.nr && (int)d < D) Nr[r * (uint32_t)D + d] = rv[i];
+        }
+      }
+    }
+#else
     for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
       const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
       if (r < om.nr && (int)d < D)
         KA->new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = KA->old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
     }
+#endif
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
     if (warm) {
 #pragma unroll
@@ -1066,6 +1122,39 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         dc = v ? (uint32_t)KA->dc[gi] : 0u;
         p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
       }
+#elif TRMV_BUFLD
+      // (bounds-checked loads over the key's ops: no branch around them)
+      uint32_t kind, dc, p;
+      int64_t id, sc, ts;
+      {
+        const uint32_t o = c0 + lane;
+        const uint32_t kb = bld8(bsrc(KA->kind + op0, nops), o);
+        const int64_t ib = bld64(bsrc(KA->id + op0, nops * 8u), o * 8u);
+        const int64_t sb = bld64(bsrc(KA->score + op0, nops * 8u), o * 8u);
+        const int64_t tb = bld64(bsrc(KA->ts + op0, nops * 8u), o * 8u);
+        const uint32_t db = bld8(bsrc(KA->dc + op0, nops), o);
+        const uint32_t pb = bld8(bsrc(KA->op_pl + op0, nops), o);
+        kind = v ? kb : 0u;
+        id = v ? ib : 0;
+        sc = v ? sb : 0;
+        ts = v ? tb : 0;
+        dc = v ? db : 0u;
+        p = v ? pb : (uint32_t)RP;
+      }
+#elif TRMV_HOISTP
+      // (the six columns' bases read together: one scalar wait, not one per load)
+      const uint8_t* const Ck = KA->kind;
+      const int64_t* const Ci = KA->id;
+      const int64_t* const Cs = KA->score;
+      const int64_t* const Ct = KA->ts;
+      const uint8_t* const Cd = KA->dc;
+      const uint8_t* const Cp = KA->op_pl;
+      const uint32_t kind = v ? (uint32_t)Ck[gi] : 0u;
+      const int64_t id = v ? Ci[gi] : 0;
+      const int64_t sc = v ? Cs[gi] : 0;
+      const int64_t ts = v ? Ct[gi] : 0;
+      const uint32_t dc = v ? (uint32_t)Cd[gi] : 0u;
+      const uint32_t p = v ? (uint32_t)Cp[gi] : (uint32_t)RP;
 #else
       const uint32_t kind = v ? (uint32_t)KA->kind[gi] : 0u;
       const int64_t id = v ? KA->id[gi] : 0;

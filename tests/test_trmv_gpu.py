@@ -92,11 +92,7 @@ def test_multi_batch_and_import(gpu, K, npl):
         add = b.kind < 2
         b.ts[add] += i * 10**6
         b.rmv_vc[b.rmv_vc > 0] += i * 10**6
-        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
-        if i:
-            assert xe is xout
-            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
-        xo = orac.apply(b)
+        xe, xo = eng.apply(b), orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
     st = eng.export()
     e2 = TopkRmvEngine(nk, K, D)
@@ -213,11 +209,7 @@ def _stream_batches(eng, orac, nk, D, K, plan, seed):
     for i, (n, npl, smax) in enumerate(plan):
         b = gen_trmv(n, nk, D, npl, smax, 120, 16, 20, 10, seed=seed + i, clock0=clock)
         clock += n + 1
-        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
-        if i:
-            assert xe is xout
-            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
-        xo = orac.apply(b)
+        xe, xo = eng.apply(b), orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
 
 
@@ -251,11 +243,7 @@ def test_key_grows_past_1024_players(gpu, K):
     for i, (n, npl) in enumerate([(2000, 1500), (9000, 7000), (9000, 7000), (3000, 7000)]):
         b = gen_trmv(n, nk, D, npl, 10**6, 20, 16, 20, 10, seed=1200 + i, clock0=clock)
         clock += n + 1
-        xe = eng.apply(b) if i == 0 else eng.apply(b, out=xout)
-        if i:
-            assert xe is xout
-            xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
-        xo = orac.apply(b)
+        xe, xo = eng.apply(b), orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
         assert eng.overflow_keys(4) == 0
         st = eng.export()
