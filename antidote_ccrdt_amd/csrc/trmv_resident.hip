@@ -87,8 +87,14 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_LANELOCAL
+#define TRMV_LANELOCAL 1  // chunks: lane-derived addresses computed per chunk (VGPR pressure)
+#endif
+#ifndef TRMV_DOMPF
+#define TRMV_DOMPF 1  // chunks: a non-replayed add's Removals-row entry loaded before the sort
+#endif
 #ifndef TRMV_HOISTP
-#define TRMV_HOISTP 1  // the replays' pool column bases read once per replay, not per access
+#define TRMV_HOISTP 0  // the replays' pool column bases read once per replay, not per access (A/B r04: spills, slower)
 #endif
 #ifndef TRMV_BUFLD
 #define TRMV_BUFLD 1  // P1's record and element loads through bounds-checked buffer descriptors
@@ -1101,9 +1107,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 
     // ---- chunks
     for (uint32_t c0 = 0; c0 < nops;) {
+#if TRMV_LANELOCAL
+      // this chunk's lane-indexed LDS addresses are made from a lane the
+      // compiler cannot see through, so they are computed here and not held
+      // in VGPRs across the whole kernel
+      uint32_t lane_o = lane;
+      asm volatile("" : "+v"(lane_o));
+      const uint32_t lane = lane_o;
+#endif
       uint32_t n = nops - c0 < (uint32_t)RCH ? nops - c0 : (uint32_t)RCH;
       bool v = lane < n;
-      const uint64_t gi = op0 + c0 + lane;
+      [[maybe_unused]] const uint64_t gi = op0 + c0 + lane;
 #if TRMV_C0PRE
       uint32_t kind, dc, p;
       int64_t id, sc, ts;
@@ -1174,6 +1188,20 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         rm = ballot(isr);
       }
       const bool add = v && kind < 2;
+#if TRMV_DOMPF
+      // the Removals-row entry a non-replayed add is checked against (:234),
+      // loaded here and read after the sort: a player without a rmv in the
+      // batch keeps its row unchanged through the batch's replays
+      int64_t rte;
+      {
+        const uint32_t pq = add ? p : 0u;
+        const uint32_t pfe = L.pf[pq];
+        const bool need = add && (pfe & Q_ROWV) && !(pfe & Q_RMV);
+        const uint32_t orwe = L.prow[pq];
+        rte = bld64(bsrc(KA->new_s.r_vc + (uint64_t)nm.r_off * D, nr * (uint32_t)D * 8u),
+                    need ? (orwe * (uint32_t)D + dc) * 8u : BOOB);
+      }
+#endif
       uint32_t err = 0;
       err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
       err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
@@ -1266,10 +1294,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const bool walk = sv && (pf0 & (Q_RMV | Q_DUP));
       bool dom = false;
       uint32_t orw = NONE16;
+#if TRMV_DOMPF
+      const int64_t rts = shfl64(rte, (int)so);
+      if (sv && !walk && (pf0 & Q_ROWV)) {
+        orw = L.prow[sp];
+        dom = rts >= sts;
+      }
+#else
       if (sv && !walk && (pf0 & Q_ROWV)) {
         orw = L.prow[sp];
         dom = KA->new_s.r_vc[((uint64_t)nm.r_off + orw) * D + sdc] >= sts;
       }
+#endif
       const bool app = sv && !walk && !dom;
       const uint64_t nd = ballot(app);
       if (app) {
