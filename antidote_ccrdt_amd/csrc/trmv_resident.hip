@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_RBUF
+#define TRMV_RBUF 0  // replays: Removals row and slab loads through descriptors
+#endif
 #ifndef TRMV_LANELOCAL
 #define TRMV_LANELOCAL 1  // chunks: lane-derived addresses computed per chunk (VGPR pressure)
 #endif
@@ -1335,6 +1338,14 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         L.u.c.cwe[k] = (uint8_t)shi;
       }
       wave_lds_sync();
+#if TRMV_RBUF
+      // (the replays' Removals rows and pool through bounds-checked
+      // descriptors made once per chunk: no scalar pointer re-read per load)
+      const __amdgpu_buffer_rsrc_t qR = bsrc(KA->new_s.r_vc + (uint64_t)nm.r_off * D, nr * (uint32_t)D * 8u);
+      const __amdgpu_buffer_rsrc_t qS = bsrc(KA->new_s.m_score + nm.m_off, BOOB);
+      const __amdgpu_buffer_rsrc_t qT = bsrc(KA->new_s.m_ts + nm.m_off, BOOB);
+      const __amdgpu_buffer_rsrc_t qD = bsrc(KA->new_s.m_dc + nm.m_off, BOOB);
+#endif
       if (lane < (uint32_t)__builtin_popcountll(wm)) {
 #if TRMV_HOISTP
         // the pool columns' bases read once here: a kernel argument is
@@ -1359,8 +1370,13 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
         {
           const int dn = KA->n_dc;  // (re-read here: no per-d masks held across the key)
+#if TRMV_RBUF
+#pragma unroll
+          for (int d = 0; d < TRMV_DPAD; ++d) R[d] = bld64(qR, (has_row && d < dn) ? (row * (uint32_t)D + d) * 8u : BOOB);
+#else
 #pragma unroll
           for (int d = 0; d < TRMV_DPAD; ++d) R[d] = (has_row && d < dn) ? KA->new_s.r_vc[rbase + d] : 0;
+#endif
         }
 #if TRMV_RPF
         // a player whose first op here is a rmv: its slab's first lines are
@@ -1415,6 +1431,15 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
               int64_t s4[4], t4[4];
               uint32_t d4[4];
+#if TRMV_RBUF
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t q = (ns & 0xFFFFu) + (j0 + e < cnt ? j0 + e : j0);
+                s4[e] = bld64(qS, q * 8u);
+                t4[e] = bld64(qT, q * 8u);
+                d4[e] = bld8(qD, q);
+              }
+#else
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
@@ -1422,6 +1447,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
                 t4[e] = Mts[base + j];
                 d4[e] = Mdc[base + j];
               }
+#endif
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const uint32_t j = j0 + e;
