@@ -1168,10 +1168,33 @@ __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
   const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
   bool ovf = (uint64_t)om.n + (op1 - op0) > (uint64_t)E;
   if (NARROW && !ovf) {  // every Id and Score of the board, old entries included
+    // (bounds-checked loads, four rounds of 64 per trip, both columns: the
+    // loads go out together instead of one round trip per column and round;
+    // past the end they read 0, which fits)
     bool wide = false;
-    for (uint64_t i = op0 + lane_id(); i < op1; i += 64) wide |= !lb_fits32(a.id[i]) || !lb_fits32(a.score[i]);
-    for (uint32_t j = lane_id(); j < om.n; j += 64)
-      wide |= !lb_fits32(a.id_in[om.off + j]) || !lb_fits32(a.score_in[om.off + j]);
+    const uint32_t nops = (uint32_t)(op1 - op0), l = (uint32_t)lane_id();
+    const __amdgpu_buffer_rsrc_t rid = bsrc(a.id + op0, nops * 8u), rsc = bsrc(a.score + op0, nops * 8u);
+    for (uint32_t i0 = 0; i0 < nops; i0 += 256) {
+      int64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        x[2 * u] = bld64(rid, (i0 + 64u * u + l) * 8u);
+        x[2 * u + 1] = bld64(rsc, (i0 + 64u * u + l) * 8u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wide |= !lb_fits32(x[u]);
+    }
+    const __amdgpu_buffer_rsrc_t oid = bsrc(a.id_in + om.off, om.n * 8u), osc = bsrc(a.score_in + om.off, om.n * 8u);
+    for (uint32_t j0 = 0; j0 < om.n; j0 += 256) {
+      int64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        x[2 * u] = bld64(oid, (j0 + 64u * u + l) * 8u);
+        x[2 * u + 1] = bld64(osc, (j0 + 64u * u + l) * 8u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wide |= !lb_fits32(x[u]);
+    }
     ovf = ballot(wide) != 0;
   }
   if (ovf) {
