@@ -164,28 +164,46 @@ __global__ __launch_bounds__(64) void topk_apply_kernel(TopkArgs a) {
     if (act) L.sseq[s] = -(int32_t)j - 2;
   }
   __syncthreads();
+  // (each round's Ids load while the previous round probes the table)
+  int64_t idn = i0 + lane < i1 ? a.op_id[i0 + lane] : 0;
   for (uint64_t b = i0; b < i1; b += 64) {
     const uint64_t i = b + lane;
     const bool act = i < i1;
-    const int64_t id = act ? a.op_id[i] : 0;
+    const int64_t id = idn;
+    idn = i + 64 < i1 ? a.op_id[i + 64] : 0;
     const uint32_t s = tk_slot<HCAP>(L, id, act);
     if (act) atomicMax(&L.sseq[s], (int32_t)(i - i0));
   }
   __syncthreads();
-  // compact surviving entries into the new segment
+  // compact surviving entries into the new segment, four rounds of slots per
+  // trip: the rounds' score loads go out together, then their stores
   const uint64_t off_new = a.off_out[k];
   uint32_t n = 0;
-  for (int b = 0; b < HCAP; b += 64) {
-    const int h = b + lane;
-    const bool used = L.sstate[h] != 0u;
-    const uint64_t m = ballot(used);
-    if (used) {
-      const uint64_t dst = off_new + n + mbcnt(m);
-      const int32_t q = L.sseq[h];
-      a.id_out[dst] = L.sid[h];
-      a.score_out[dst] = q >= 0 ? a.op_score[i0 + q] : a.score_in[off_old + (uint32_t)(-q - 2)];
+  for (int b0 = 0; b0 < HCAP; b0 += 256) {
+    int64_t sc[4], id[4];
+    uint64_t dst[4];
+    bool used[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = b0 + 64 * r + lane;
+      used[r] = (b0 + 64 * r < HCAP) && L.sstate[h < HCAP ? h : 0] != 0u;
+      const uint64_t m = ballot(used[r]);
+      dst[r] = off_new + n + mbcnt(m);
+      n += (uint32_t)__builtin_popcountll(m);
+      sc[r] = 0;
+      id[r] = 0;
+      if (used[r]) {
+        const int32_t q = L.sseq[h];
+        id[r] = L.sid[h];
+        sc[r] = q >= 0 ? a.op_score[i0 + q] : a.score_in[off_old + (uint32_t)(-q - 2)];
+      }
     }
-    n += (uint32_t)__builtin_popcountll(m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (used[r]) {
+        a.id_out[dst[r]] = id[r];
+        a.score_out[dst[r]] = sc[r];
+      }
   }
   if (lane == 0) a.cnt_out[k] = n;
 }
