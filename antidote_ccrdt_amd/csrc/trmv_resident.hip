@@ -1855,6 +1855,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     }
     wave_lds_sync();
+#if TRMV_BUFLD
+    const __amdgpu_buffer_rsrc_t pS = bsrc(KA->new_s.m_score + nm.m_off, BOOB);
+    const __amdgpu_buffer_rsrc_t pT = bsrc(KA->new_s.m_ts + nm.m_off, BOOB);
+    const __amdgpu_buffer_rsrc_t pD = bsrc(KA->new_s.m_dc + nm.m_off, BOOB);
+#endif
     uint32_t rest = ob.n, mcount = 0;
 #pragma unroll
     for (int u = 0; u < RSL; ++u) {
@@ -1869,15 +1874,37 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         uint32_t opos = L.opos[p], gpos = L.gpos[p];
         const uint32_t ns = L.nslab[p], cnt = ns >> 16;
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
-          const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
           const int64_t msv = L.msc[p], otv = ino ? L.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
+#if TRMV_BUFLD
+          // (four elements per trip, their loads together)
+          const uint32_t q0 = ns & 0xFFFFu;
+          for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
+            int64_t s4[4], t4[4];
+            uint32_t d4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t off = j0 + e < cnt ? q0 + j0 + e : BOOB / 8u;
+              s4[e] = bld64(pS, off * 8u);
+              t4[e] = bld64(pT, off * 8u);
+              d4[e] = bld8(pD, j0 + e < cnt ? off : BOOB);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t j = j0 + e;
+              if (j < cnt && s4[e] == msv && t4[e] == otv && d4[e] == od) opos = j;
+              if (j < cnt && s4[e] == msv && t4[e] == gtv && d4[e] == gd) gpos = j;
+            }
+          }
+#else
+          const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
           for (uint32_t j = 0; j < cnt; ++j) {
             const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
             const uint32_t d2 = KA->new_s.m_dc[base + j];
             if (s2 == msv && t2 == otv && d2 == od) opos = j;
             if (s2 == msv && t2 == gtv && d2 == gd) gpos = j;
           }
+#endif
         }
         const uint64_t pq = (uint64_t)nm.p_off + ni;
         KA->new_s.pl_id[pq] = pid[u];
