@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_P5BUF
+#define TRMV_P5BUF 0  // P5: a compacted slab's re-find four elements per trip (A/B r04: slower)
+#endif
 #ifndef TRMV_RBUF
 #define TRMV_RBUF 0  // replays: Removals row and slab loads through descriptors
 #endif
@@ -1855,7 +1858,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     }
     wave_lds_sync();
-#if TRMV_BUFLD
+#if TRMV_P5BUF
     const __amdgpu_buffer_rsrc_t pS = bsrc(KA->new_s.m_score + nm.m_off, BOOB);
     const __amdgpu_buffer_rsrc_t pT = bsrc(KA->new_s.m_ts + nm.m_off, BOOB);
     const __amdgpu_buffer_rsrc_t pD = bsrc(KA->new_s.m_dc + nm.m_off, BOOB);
@@ -1876,7 +1879,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const int64_t msv = L.msc[p], otv = ino ? L.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
-#if TRMV_BUFLD
+#if TRMV_P5BUF
           // (four elements per trip, their loads together)
           const uint32_t q0 = ns & 0xFFFFu;
           for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {

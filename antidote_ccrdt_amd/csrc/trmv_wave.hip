@@ -93,6 +93,10 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #else
 #define LD_IN(p) (*(p))
 #endif
+#ifndef TRMV_EARLY
+#define TRMV_EARLY 0  // FRESH: the next key's ops loaded at the start of the current key (not after its hash)
+#endif
+constexpr bool EARLY = TRMV_EARLY && !TRMV_AHEAD2;
 #ifndef TRMV_POOLSKIP
 #define TRMV_POOLSKIP 0  // FRESH pool: only decided players' final slabs written (A/B r04: tier 0 2.24 -> 2.44 ms)
 #endif
@@ -416,6 +420,25 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     xsc[0] = xr[0] ? (int64_t)(om.nr + r0) : xsc[0];
     xsc[1] = xr[1] ? (int64_t)(om.nr + r1) : xsc[1];
   }
+  if (EARLY && FRESH) {
+    // the rmv clocks first (their loads went out a key ago), then the next
+    // key's op loads, whose latency the hash build and steps 4-5 now hide
+#pragma unroll
+    for (int s = 0; s < W_RCAP / 8; ++s) {
+      const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+      const int64_t v = (int)d < D ? in.rv[s] : 0;
+      err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
+      if (r < nrmv) L.rows[om.nr + r][d] = v;
+    }
+    if (ballot(err != 0)) {
+      if (err) atomicOr(&KA->status[1], err);
+      return W_REJECT;
+    }
+    if (has_next) {
+      wave_load_key(a, hdr, nj, nxt);
+      issued = true;
+    }
+  }
   wave_lds_sync();
   // ---- 3 (set-up). hash slots; an Id equal to the empty marker takes tier 1
   constexpr int NS = FRESH ? 2 : 4;
@@ -456,16 +479,18 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   PROF_MARK(8);
   // write the rmv clocks (their loads were issued with the key's ops)
+  if (!(EARLY && FRESH)) {
 #pragma unroll
-  for (int s = 0; s < W_RCAP / 8; ++s) {
-    const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-    const int64_t v = (int)d < D ? in.rv[s] : 0;
-    err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
-    if (r < nrmv) L.rows[om.nr + r][d] = v;
-  }
-  if (ballot(err != 0)) {
-    if (err) atomicOr(&KA->status[1], err);
-    return W_REJECT;
+    for (int s = 0; s < W_RCAP / 8; ++s) {
+      const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
+      const int64_t v = (int)d < D ? in.rv[s] : 0;
+      err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
+      if (r < nrmv) L.rows[om.nr + r][d] = v;
+    }
+    if (ballot(err != 0)) {
+      if (err) atomicOr(&KA->status[1], err);
+      return W_REJECT;
+    }
   }
   PROF_MARK(9);
   // old players keep their index
@@ -526,7 +551,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     issued = true;
   }
 #else
-  if (FRESH && has_next) wave_load_key(a, hdr, nj, nxt);
+  if (FRESH && !EARLY && has_next) wave_load_key(a, hdr, nj, nxt);
 #endif
 
   PROF_MARK(2);
@@ -1196,7 +1221,7 @@ __global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_k
             if (has_next2) wave_load_key(a, hdr, j + 2, nxt2);
           }
         } else {
-          if (has_next) wave_load_key(a, hdr, j + 1, nxt);
+          if (has_next && !issued) wave_load_key(a, hdr, j + 1, nxt);
           // retire these loads here, as the common path does before its
           // stores: otherwise every key would wait on the previous key's stores
           __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
