@@ -93,6 +93,12 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #else
 #define LD_IN(p) (*(p))
 #endif
+#ifndef TRMV_DIAG_LDS
+// Diagnostic builds only (wrong results, for the LDS bank-conflict counters):
+// 1 = the records pass's gathers (Id slot, Obs element) made lane-linear,
+// 2 = step 5's gathers (elements, clock rows) made lane-linear.
+#define TRMV_DIAG_LDS 0
+#endif
 #ifndef TRMV_EARLY
 #define TRMV_EARLY 0  // FRESH: the next key's ops loaded at the start of the current key (not after its hash)
 #endif
@@ -731,7 +737,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t k = b + lane;
       const bool act = k < mn;
       const uint32_t q = act ? (uint32_t)cq[k] : ESINK;
-      const int64_t sm = L.esc[q], tm = L.ets[q];
+      const uint32_t qd = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : q;  // (diagnostic builds only)
+      const int64_t sm = L.esc[qd], tm = L.ets[qd];
       const uint32_t kd = L.ekd[q];
       const uint32_t p = act ? (kd >> 8) : PSINK;
       const bool ya = act && (kd & 2u) == 0, yr = act && (kd & 2u) != 0;
@@ -749,7 +756,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint64_t Mya = ballot(ya);
       uint64_t Mfb = 0, Mbeaten = 0, Mrisk = 0, Mseen = 0, Mfirst = ~0ull, Mgbeaten = 0, Mgtie = 0;
       const uint32_t p0 = c ? st : (uint32_t)ESINK;
-      int64_t sxn = L.esc[p0], txn = L.ets[p0];
+      const uint32_t p0d = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : p0;
+      int64_t sxn = L.esc[p0d], txn = L.ets[p0d];
       uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
         const int64_t sx = sxn, tx = txn;
@@ -760,10 +768,12 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         // (:234), or kept by the first later one (:255-266) -> replay
         const uint64_t Mneed = Mya & Misr & (Mbefore | ~Mseen);
         const bool need = (Mneed >> lane) & 1u;
-        const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
+        const int64_t rt = TRMV_DIAG_LDS == 2 ? L.rows[(uint32_t)lane >> 3][(uint32_t)lane & 7u]
+                                              : L.rows[need ? (uint32_t)sx : 0u][adc];
         const uint32_t pn = x + 1 < c ? st + x + 1 : (uint32_t)ESINK;
-        sxn = L.esc[pn];
-        txn = L.ets[pn];
+        const uint32_t pnd = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : pn;
+        sxn = L.esc[pnd];
+        txn = L.ets[pnd];
         kxn = L.ekd[pn];
         const uint64_t Msgt = ballot(sx > sm), Mseq = ballot(sx == sm);
         const uint64_t Mtge = ballot(tx >= tm), Mtgt = ballot(tx > tm);
@@ -1033,7 +1043,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t rix = rbase + mbcnt(rm);
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      const int64_t id = (int64_t)L.htab[wb >> 24];
+      const int64_t id = (int64_t)L.htab[TRMV_DIAG_LDS == 1 ? (uint32_t)lane : (wb >> 24)];
       // gb_sets:largest of the slab: step 5 (a decided player: its last
       // segment, strictly rising Ts, so no two elements tie) or 5b (replayed)
       const uint32_t gb = (replayed || cnt > 1) ? ((wb >> 16) & 0xFFu) - off : 0u;
@@ -1046,7 +1056,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
       csum += cnt;
       nobs += (uint32_t)__builtin_popcountll(ballot(o != NONE8));
-      min_cand(!replayed && o != NONE8, L.esc[o != NONE8 ? o : (uint32_t)ESINK], id, p);
+      min_cand(!replayed && o != NONE8, L.esc[TRMV_DIAG_LDS == 1 ? (uint32_t)lane : (o != NONE8 ? o : (uint32_t)ESINK)], id, p);
     }
     (void)wave_excl_scan_dpp(csum, fbase);  // |Masked| of the key
     wave_lds_sync();

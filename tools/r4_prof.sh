@@ -21,6 +21,7 @@ for spec in "${@:-default}"; do
   lib=""; [ "$spec" != default ] && lib="$GRAFT_REPO_ROOT/$l"
   for pass in "write:WRITE_SIZE" "fetch:FETCH_SIZE" "sq2:SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" "sq1:SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
     pn=${pass%%:*}; cs=${pass#*:}
+    case " ${PASSES:-write fetch sq2 sq1} " in *" $pn "*) ;; *) continue ;; esac
     echo "== $n $pn"
     CCRDT_LIB=$lib timeout -k 10 300 rocprofv3 --pmc $cs -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$n/$pn" -o $pn --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" $B > "$GRAFT_REPO_ROOT/gpurun_out/pmc_${n}_$pn.log" 2>&1 || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/pmc_${n}_$pn.log"; exit 1; }
   done
