@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_MBALLOT
+#define TRMV_MBALLOT 3  // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
+#endif
 #ifndef TRMV_P5BUF
 #define TRMV_P5BUF 0  // P5: a compacted slab's re-find four elements per trip (A/B r04: slower)
 #endif
@@ -1676,7 +1679,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         // among the candidates), keys being distinct.
         bool rem0, rem1;
         uint32_t cb0 = 0, cb1 = 0, cbc = 0, abc = 0;
-        if (m <= 3) {
+        if (m <= (uint32_t)TRMV_MBALLOT) {
           // few candidates: one ballot pair per candidate
           rem0 = rem1 = false;
           for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries

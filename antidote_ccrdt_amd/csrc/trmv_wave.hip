@@ -94,9 +94,10 @@ constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
 #define LD_IN(p) (*(p))
 #endif
 #ifndef TRMV_DIAG_LDS
-// Diagnostic builds only (wrong results, for the LDS bank-conflict counters):
-// 1 = the records pass's gathers (Id slot, Obs element) made lane-linear,
-// 2 = step 5's gathers (elements, clock rows) made lane-linear.
+// Diagnostic build only (wrong Ids and Min, for the LDS bank-conflict
+// counters): 1 = the records pass's gathers (Id slot, Obs element) made
+// lane-linear.  (Redirecting step 5's gathers the same way sends garbage
+// into clock-row indices and faulted: not a usable diagnostic.)
 #define TRMV_DIAG_LDS 0
 #endif
 #ifndef TRMV_EARLY
@@ -737,8 +738,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t k = b + lane;
       const bool act = k < mn;
       const uint32_t q = act ? (uint32_t)cq[k] : ESINK;
-      const uint32_t qd = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : q;  // (diagnostic builds only)
-      const int64_t sm = L.esc[qd], tm = L.ets[qd];
+      const int64_t sm = L.esc[q], tm = L.ets[q];
       const uint32_t kd = L.ekd[q];
       const uint32_t p = act ? (kd >> 8) : PSINK;
       const bool ya = act && (kd & 2u) == 0, yr = act && (kd & 2u) != 0;
@@ -756,8 +756,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint64_t Mya = ballot(ya);
       uint64_t Mfb = 0, Mbeaten = 0, Mrisk = 0, Mseen = 0, Mfirst = ~0ull, Mgbeaten = 0, Mgtie = 0;
       const uint32_t p0 = c ? st : (uint32_t)ESINK;
-      const uint32_t p0d = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : p0;
-      int64_t sxn = L.esc[p0d], txn = L.ets[p0d];
+      int64_t sxn = L.esc[p0], txn = L.ets[p0];
       uint32_t kxn = L.ekd[p0];
       for (uint32_t x = 0; x < maxc; ++x) {
         const int64_t sx = sxn, tx = txn;
@@ -768,12 +767,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         // (:234), or kept by the first later one (:255-266) -> replay
         const uint64_t Mneed = Mya & Misr & (Mbefore | ~Mseen);
         const bool need = (Mneed >> lane) & 1u;
-        const int64_t rt = TRMV_DIAG_LDS == 2 ? L.rows[(uint32_t)lane >> 3][(uint32_t)lane & 7u]
-                                              : L.rows[need ? (uint32_t)sx : 0u][adc];
+        const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
         const uint32_t pn = x + 1 < c ? st + x + 1 : (uint32_t)ESINK;
-        const uint32_t pnd = TRMV_DIAG_LDS == 2 ? (uint32_t)lane : pn;
-        sxn = L.esc[pnd];
-        txn = L.ets[pnd];
+        sxn = L.esc[pn];
+        txn = L.ets[pn];
         kxn = L.ekd[pn];
         const uint64_t Msgt = ballot(sx > sm), Mseq = ballot(sx == sm);
         const uint64_t Mtge = ballot(tx >= tm), Mtgt = ballot(tx > tm);
