@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_PROMOTE2
+#define TRMV_PROMOTE2 0  // rmv promotions: the largest element's fields read for each lane's best slot only
+#endif
 #ifndef TRMV_MBALLOT
 #define TRMV_MBALLOT 3  // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
 #endif
@@ -559,6 +562,29 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
   const uint32_t l = (uint32_t)lane_id();
   uint32_t bp = RNONE;
   int64_t best = INT64_MIN;
+#if TRMV_PROMOTE2
+  // flags and Scores of the lane's four slots, then the largest element's
+  // Ts / DcId / position of its best slot only (4 + 3 LDS reads, not 20)
+  uint32_t f[RSL];
+  int32_t sc[RSL];
+#pragma unroll
+  for (int u = 0; u < RSL; ++u) {
+    const uint32_t p = 64u * u + l;
+    f[u] = p < np ? L.pf[p] : 0u;
+    sc[u] = L.msc[p];
+  }
+#pragma unroll
+  for (int u = 0; u < RSL; ++u) {
+    const int64_t k = mkkey(sc[u], pid[u]);
+    if ((f[u] & (Q_OBS | Q_HASM)) == Q_HASM && (bp == RNONE || k > best)) {
+      bp = 64u * u + l;
+      best = k;
+    }
+  }
+  const uint32_t bq = bp != RNONE ? bp : 0u;
+  const int64_t bt = L.gts[bq];
+  const uint32_t bd = L.gdc[bq], bg = L.gpos[bq];
+#else
   uint32_t f[RSL], gd[RSL], gp[RSL];
   int32_t sc[RSL];
   int64_t gt[RSL];
@@ -584,6 +610,7 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
       bg = gp[u];
     }
   }
+#endif
   if (!ballot(bp != RNONE)) return RNONE;
   const int64_t m = wave_max_i64_dpp(bp != RNONE ? best : INT64_MIN);
   const int src = (int)__builtin_ctzll(ballot(bp != RNONE && best == m));
