@@ -88,7 +88,7 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
 #ifndef TRMV_PROMOTE2
-#define TRMV_PROMOTE2 0  // rmv promotions: the largest element's fields read for each lane's best slot only
+#define TRMV_PROMOTE2 1  // rmv promotions: the largest element's fields read for each lane's best slot only
 #endif
 #ifndef TRMV_MBALLOT
 #define TRMV_MBALLOT 3  // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
@@ -674,6 +674,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   uint32_t odr[RSL];             // Obs[Id]'s DcId by slot
   bool wide = false;
   {
+#if TRMV_LANELOCAL > 1
+    uint32_t lane_o = lane;  // (P1's lane-derived addresses made here)
+    asm volatile("" : "+v"(lane_o));
+    const uint32_t lane = lane_o;
+#endif
     uint32_t info[RSL], slab[RSL], gb[RSL];
     {
       // (the four arrays' bases once, and pl_gb read whatever the slab's
@@ -898,6 +903,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   RPROF(0);
   {
     // ---- P2. every op's player; ops per player; rmv players
+#if TRMV_LANELOCAL > 1
+    uint32_t lane_o = lane;  // (P2-P5's lane-derived addresses made here)
+    asm volatile("" : "+v"(lane_o));
+    const uint32_t lane = lane_o;
+#endif
     uint32_t np = om.np;
 #if TRMV_C0PRE
     // the first chunk's ops stay in registers from here (its Ids, kinds and
@@ -1875,6 +1885,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       c0 += n;
     }
 
+#if TRMV_LANELOCAL > 2
+    {
+      uint32_t lane_o = lane;  // (P5's lane-derived addresses made here)
+      asm volatile("" : "+v"(lane_o));
+      const uint32_t lane = lane_o;
+#endif
     // ---- P5. player records: Observed first (sorted), then the others in
     // player order; positions of compacted slabs; Vc; meta.  (The re-find of
     // a compacted slab reads the last chunk's stores: they must have landed.)
@@ -1960,6 +1976,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       KA->new_s.meta[key] = out;
       KA->ex_cnt[key] = L.nex;
     }
+#if TRMV_LANELOCAL > 2
+    }
+#endif
     RPROF(9);
   }
   return R_DONE;
