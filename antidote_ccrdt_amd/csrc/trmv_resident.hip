@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_DUP4
+#define TRMV_DUP4 0  // replays: a duplicate candidate's slab scan four elements per trip
+#endif
 #ifndef TRMV_PROMOTE2
 #define TRMV_PROMOTE2 1  // rmv promotions: the largest element's fields read for each lane's best slot only
 #endif
@@ -1444,6 +1447,26 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
               continue;
             }
             uint32_t pos = RNONE;
+#if TRMV_DUP4
+            if ((kd >> 5) & 1u) {  // set semantics: the element may be there
+              // four elements per trip, their loads together (one round trip
+              // per four elements, not one or three per element)
+              for (uint32_t j0 = 0; j0 < cnt && pos == RNONE; j0 += 4) {
+                int64_t t4[4], s4[4];
+                uint32_t d4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const uint32_t j = j0 + e < cnt ? j0 + e : j0;
+                  t4[e] = Mts[base + j];
+                  s4[e] = Msc[base + j];
+                  d4[e] = Mdc[base + j];
+                }
+#pragma unroll
+                for (int e = 3; e >= 0; --e)
+                  if (j0 + e < cnt && t4[e] == ets && d4[e] == edc && s4[e] == esc) pos = j0 + e;
+              }
+            }
+#else
             if ((kd >> 5) & 1u)  // set semantics: the element may be there
               for (uint32_t j = 0; j < cnt; ++j)
                 if (Mts[base + j] == ets && Mdc[base + j] == edc &&
@@ -1451,6 +1474,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
                   pos = j;
                   break;
                 }
+#endif
             if (pos == RNONE) {
               pos = cnt++;
               Msc[base + pos] = esc;
