@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_CLK2
+#define TRMV_CLK2 0  // chunks: both rounds of clock-row loads issued before either is stored
+#endif
 #ifndef TRMV_DUP4
 #define TRMV_DUP4 0  // replays: a duplicate candidate's slab scan four elements per trip
 #endif
@@ -1264,6 +1267,21 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
       if (isr) L.u.c.crow[rk] = (uint32_t)ts;
       wave_lds_sync();
+#if TRMV_CLK2
+      {
+        // (<= 16 rows: both halves' loads go out before either is stored)
+        static_assert(RCHR <= 16, "two rounds of 8 clock rows");
+        const uint32_t d = lane & 7u, ra = lane >> 3, rb = 8u + (lane >> 3);
+        const bool va = ra < nrm && (int)d < D, vb = rb < nrm && (int)d < D;
+        const uint32_t ca = L.u.c.crow[ra < nrm ? ra : 0u], cb = L.u.c.crow[rb < nrm ? rb : 0u];
+        const int64_t* const rv = KA->rmv_vc;
+        const int64_t xa = va ? rv[(uint64_t)ca * D + d] : 0;
+        const int64_t xb = vb ? rv[(uint64_t)cb * D + d] : 0;
+        err |= (xa < 0 || xb < 0) ? TRMV_ERR_VC : 0u;
+        if (ra < nrm) L.u.c.vtab[ra][d] = xa;
+        if (rb < nrm) L.u.c.vtab[rb][d] = xb;
+      }
+#else
       for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
         const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
         if (r < nrm) {
@@ -1272,6 +1290,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
           L.u.c.vtab[r][d] = x;
         }
       }
+#endif
       if (ballot(err != 0)) {
         if (err) atomicOr(&KA->status[1], err);
         return R_REJECT;
