@@ -88,10 +88,10 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
 #ifndef TRMV_CLK2
-#define TRMV_CLK2 0  // chunks: both rounds of clock-row loads issued before either is stored
+#define TRMV_CLK2 1  // chunks: both rounds of clock-row loads issued before either is stored
 #endif
 #ifndef TRMV_DUP4
-#define TRMV_DUP4 0  // replays: a duplicate candidate's slab scan four elements per trip
+#define TRMV_DUP4 1  // replays: a duplicate candidate's slab scan four elements per trip
 #endif
 #ifndef TRMV_PROMOTE2
 #define TRMV_PROMOTE2 1  // rmv promotions: the largest element's fields read for each lane's best slot only
