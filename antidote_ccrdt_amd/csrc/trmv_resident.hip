@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_P2PRE
+#define TRMV_P2PRE 0  // P2's first 128 op Ids and kinds loaded at the start of P1
+#endif
 #ifndef TRMV_CLK2
 #define TRMV_CLK2 1  // chunks: both rounds of clock-row loads issued before either is stored
 #endif
@@ -669,6 +672,21 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   if (lane == 0) L.nex = 0u;
   wave_lds_sync();
 
+#if TRMV_P2PRE
+  // P2's first round of op Ids and kinds, loaded now: their latency runs
+  // under P1's own load chains instead of after them
+  int64_t pre_id[2];
+  uint32_t pre_kd[2];
+  {
+    const __amdgpu_buffer_rsrc_t bid0 = bsrc(KA->id + op0, nops * 8u);
+    const __amdgpu_buffer_rsrc_t bkd0 = bsrc(KA->kind + op0, nops);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pre_id[h] = bld64(bid0, (64u * h + lane) * 8u);
+      pre_kd[h] = bld8(bkd0, 64u * h + lane);
+    }
+  }
+#endif
   // ---- P1. old players: records of all four slots, then the Obs[Id] /
   // largest elements they name (two rounds of loads in flight), then LDS and
   // the Id hash (the four slots' probes interleaved).
@@ -938,8 +956,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint32_t l = c0 + 64u * h + lane;
         vh[h] = l < nops;
 #if TRMV_BUFLD
-        idh[h] = bld64(bid, l * 8u);
-        kh[h] = bld8(bkd, l);
+#if TRMV_P2PRE
+        if (c0 == 0) {
+          idh[h] = pre_id[h];
+          kh[h] = pre_kd[h];
+        } else
+#endif
+        {
+          idh[h] = bld64(bid, l * 8u);
+          kh[h] = bld8(bkd, l);
+        }
 #else
         idh[h] = vh[h] ? KA->id[op0 + l] : 0;
         kh[h] = vh[h] ? (uint32_t)KA->kind[op0 + l] : 0u;
