@@ -88,7 +88,7 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
 #ifndef TRMV_P2PRE
-#define TRMV_P2PRE 0  // P2's first 128 op Ids and kinds loaded at the start of P1
+#define TRMV_P2PRE 1  // P2's first 128 op Ids and kinds loaded at the start of P1
 #endif
 #ifndef TRMV_CLK2
 #define TRMV_CLK2 1  // chunks: both rounds of clock-row loads issued before either is stored
