@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_P3PRE
+#define TRMV_P3PRE 0  // P3's first window of old pool positions loaded at the start of P2
+#endif
 #ifndef TRMV_P2PRE
 #define TRMV_P2PRE 1  // P2's first 128 op Ids and kinds loaded at the start of P1
 #endif
@@ -933,6 +936,20 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     const uint32_t lane = lane_o;
 #endif
     uint32_t np = om.np;
+#if TRMV_P3PRE && TRMV_BUFLD
+    // P3's first window of old pool positions, loaded now: its latency runs
+    // under P2 (the range is the key's span: past it reads 0)
+    int64_t p3_sc, p3_ts;
+    uint32_t p3_dc;
+    {
+      const __amdgpu_buffer_rsrc_t q0s = bsrc(KA->old_s.m_score + om.m_off, span * 8u);
+      const __amdgpu_buffer_rsrc_t q0t = bsrc(KA->old_s.m_ts + om.m_off, span * 8u);
+      const __amdgpu_buffer_rsrc_t q0d = bsrc(KA->old_s.m_dc + om.m_off, span);
+      p3_sc = bld64(q0s, lane * 8u);
+      p3_ts = bld64(q0t, lane * 8u);
+      p3_dc = bld8(q0d, lane);
+    }
+#endif
 #if TRMV_C0PRE
     // the first chunk's ops stay in registers from here (its Ids, kinds and
     // players from this pass; Scores, Ts, DcIds loaded with them), so the
@@ -1069,9 +1086,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         for (int i = 0; i < 4; ++i) {
           const uint32_t q = g0 + 64u * i + lane;
 #if TRMV_BUFLD
-          wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
-          wts[i] = bld64(qts, q * 8u);
-          wdc[i] = bld8(qdc, q);
+#if TRMV_P3PRE
+          if (g0 == 0 && i == 0) {
+            wsc[i] = p3_sc;
+            wts[i] = p3_ts;
+            wdc[i] = p3_dc;
+          } else
+#endif
+          {
+            wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
+            wts[i] = bld64(qts, q * 8u);
+            wdc[i] = bld8(qdc, q);
+          }
 #else
           const uint64_t src = (uint64_t)om.m_off + (q < span ? q : 0u);
           wsc[i] = q < span ? KA->old_s.m_score[src] : 0;
