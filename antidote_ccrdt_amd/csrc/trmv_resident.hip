@@ -87,6 +87,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_WARM
 #define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
 #endif
+#ifndef TRMV_CNPRE
+#define TRMV_CNPRE 0  // a key's next chunk of ops loaded during the current chunk's Observed half
+#endif
 #ifndef TRMV_P3PRE
 #define TRMV_P3PRE 0  // P3's first window of old pool positions loaded at the start of P2
 #endif
@@ -1210,6 +1213,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     RPROF(2);
 
     // ---- chunks
+#if TRMV_CNPRE
+    bool nx_ok = false;
+    uint32_t nx_kd = 0, nx_dc = 0, nx_p = 0;
+    int64_t nx_id = 0, nx_sc = 0, nx_ts = 0;
+#endif
     for (uint32_t c0 = 0; c0 < nops;) {
 #if TRMV_LANELOCAL
       // this chunk's lane-indexed LDS addresses are made from a lane the
@@ -1245,13 +1253,27 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       uint32_t kind, dc, p;
       int64_t id, sc, ts;
       {
-        const uint32_t o = c0 + lane;
-        const uint32_t kb = bld8(bsrc(KA->kind + op0, nops), o);
-        const int64_t ib = bld64(bsrc(KA->id + op0, nops * 8u), o * 8u);
-        const int64_t sb = bld64(bsrc(KA->score + op0, nops * 8u), o * 8u);
-        const int64_t tb = bld64(bsrc(KA->ts + op0, nops * 8u), o * 8u);
-        const uint32_t db = bld8(bsrc(KA->dc + op0, nops), o);
-        const uint32_t pb = bld8(bsrc(KA->op_pl + op0, nops), o);
+        uint32_t kb, db, pb;
+        int64_t ib, sb, tb;
+#if TRMV_CNPRE
+        if (nx_ok) {  // loaded during the previous chunk's Observed half
+          kb = nx_kd;
+          ib = nx_id;
+          sb = nx_sc;
+          tb = nx_ts;
+          db = nx_dc;
+          pb = nx_p;
+        } else
+#endif
+        {
+          const uint32_t o = c0 + lane;
+          kb = bld8(bsrc(KA->kind + op0, nops), o);
+          ib = bld64(bsrc(KA->id + op0, nops * 8u), o * 8u);
+          sb = bld64(bsrc(KA->score + op0, nops * 8u), o * 8u);
+          tb = bld64(bsrc(KA->ts + op0, nops * 8u), o * 8u);
+          db = bld8(bsrc(KA->dc + op0, nops), o);
+          pb = bld8(bsrc(KA->op_pl + op0, nops), o);
+        }
         kind = v ? kb : 0u;
         id = v ? ib : 0;
         sc = v ? sb : 0;
@@ -1630,6 +1652,19 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       // chunk nothing reads them before P5, which waits there: the Observed
       // half runs while they drain.
       if (c0 + n < nops) __builtin_amdgcn_s_waitcnt(0x0F70);
+#if TRMV_CNPRE
+      // the next chunk's ops load while this chunk's Observed half runs
+      nx_ok = c0 + n < nops;
+      if (nx_ok) {
+        const uint32_t o = c0 + n + lane;
+        nx_kd = bld8(bsrc(KA->kind + op0, nops), o);
+        nx_id = bld64(bsrc(KA->id + op0, nops * 8u), o * 8u);
+        nx_sc = bld64(bsrc(KA->score + op0, nops * 8u), o * 8u);
+        nx_ts = bld64(bsrc(KA->ts + op0, nops * 8u), o * 8u);
+        nx_dc = bld8(bsrc(KA->dc + op0, nops), o);
+        nx_p = bld8(bsrc(KA->op_pl + op0, nops), o);
+      }
+#endif
       RPROF(5);
 
       // ---- P4. the Observed half, in stream order (recompute_observed/5
