@@ -102,6 +102,9 @@ constexpr uint32_t RNONE = 0xFFFFFFFFu;
 #ifndef TRMV_DUP4
 #define TRMV_DUP4 1  // replays: a duplicate candidate's slab scan four elements per trip
 #endif
+#ifndef TRMV_RFBLK
+#define TRMV_RFBLK 4  // replays: slab elements per block of loads in a rmv's filter
+#endif
 #ifndef TRMV_PROMOTE2
 #define TRMV_PROMOTE2 1  // rmv promotions: the largest element's fields read for each lane's best slot only
 #endif
@@ -1588,12 +1591,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             int64_t bsc = 0, bts = 0;
             // the slab in blocks of 4 elements, each block's loads issued
             // together (the compaction only writes positions already read)
-            for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
-              int64_t s4[4], t4[4];
-              uint32_t d4[4];
+            for (uint32_t j0 = 0; j0 < cnt; j0 += TRMV_RFBLK) {
+              int64_t s4[TRMV_RFBLK], t4[TRMV_RFBLK];
+              uint32_t d4[TRMV_RFBLK];
 #if TRMV_RBUF
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
+              for (int e = 0; e < TRMV_RFBLK; ++e) {
                 const uint32_t q = (ns & 0xFFFFu) + (j0 + e < cnt ? j0 + e : j0);
                 s4[e] = bld64(qS, q * 8u);
                 t4[e] = bld64(qT, q * 8u);
@@ -1601,7 +1604,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
               }
 #else
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
+              for (int e = 0; e < TRMV_RFBLK; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
                 s4[e] = Msc[base + j];
                 t4[e] = Mts[base + j];
@@ -1609,7 +1612,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
               }
 #endif
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
+              for (int e = 0; e < TRMV_RFBLK; ++e) {
                 const uint32_t j = j0 + e;
                 if (j < cnt && t4[e] > V[d4[e]]) {
                   if (w != j) {
