@@ -2125,7 +2125,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #define TRMV_R_WAVES 3
 #endif
 #ifndef TRMV_R_WG
-#define TRMV_R_WG 2
+#define TRMV_R_WG 1
 #endif
 __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApplyArgs a) {
   __shared__ RLds lds[TRMV_R_WG];
