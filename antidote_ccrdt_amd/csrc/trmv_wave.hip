@@ -73,7 +73,10 @@ constexpr int W_HCAP = 256;  // hash slots (Ids)
 constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
-constexpr int W_WAVES = 4;   // waves (keys in flight) per workgroup
+#ifndef TRMV_W_WAVES
+#define TRMV_W_WAVES 4
+#endif
+constexpr int W_WAVES = TRMV_W_WAVES;  // waves (keys in flight) per workgroup
 #ifndef TRMV_AHEAD2
 #define TRMV_AHEAD2 0  // FRESH: ops loaded two keys ahead, clocks one key ahead (measured: 1% slower since the kernel-argument re-read)
 #endif
@@ -1196,7 +1199,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 #define TRMV_FRESH_WAVES 4  // waves per SIMD the FRESH instantiation is built for
 #endif
 template <bool FRESH>
-__global__ __launch_bounds__(256, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(64 * TRMV_W_WAVES, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];
