@@ -74,7 +74,7 @@ constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
 #ifndef TRMV_W_WAVES
-#define TRMV_W_WAVES 4
+#define TRMV_W_WAVES 1
 #endif
 constexpr int W_WAVES = TRMV_W_WAVES;  // waves (keys in flight) per workgroup
 #ifndef TRMV_AHEAD2
