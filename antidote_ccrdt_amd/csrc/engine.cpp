@@ -275,9 +275,6 @@ static int check_trmv(ccrdt_engine* e) {
   return CCRDT_OK;
 }
 
-#ifndef TRMV_FRESH_R
-#define TRMV_FRESH_R 1
-#endif
 int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(check_trmv(e));
   if (!ops || !ops->key_ptr || (ops->n_ops > 0 && (!ops->kind || !ops->id || !ops->score ||
@@ -367,7 +364,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
   CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
   for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
-  if (!E.fresh || (E.k <= 128 && TRMV_FRESH_R)) CCRDT_TRY(E.op_pl.ensure(n_ops + 1));  // tier R's per-op scratch
+  if (!E.fresh || E.k <= 128) CCRDT_TRY(E.op_pl.ensure(n_ops + 1));  // tier R's per-op scratch
   a.op_pl = E.op_pl.as<uint8_t>();
   a.ex_cnt = E.ex_cnt.as<uint32_t>();
   a.ex = E.ex.as<TrmvExtraRec>();
@@ -390,7 +387,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     chain[n_chain++] = first;
     // a fresh batch: tier 0's hand-ons (P > K) go to tier R first, whose
     // per-key latency is about half of tier S's
-    if (first == 0 && E.k <= 128 && TRMV_FRESH_R) chain[n_chain++] = 3;
+    if (first == 0 && E.k <= 128) chain[n_chain++] = 3;
     chain[n_chain++] = 1;
     chain[n_chain++] = 2;
     if (first == 1) n_chain = 2, chain[1] = 2;

@@ -70,77 +70,15 @@ namespace ccrdt {
 
 namespace {
 
-#ifndef TRMV_KARGS
-#define TRMV_KARGS 1
-#endif
-#if TRMV_KARGS
 #define KA trmv_kargs()  // (trmv_kernels.hpp)
-#else
-#define KA (&a)
-#endif
 
 constexpr int RP = 256;        // players per key
 constexpr int RSL = RP / 64;   // player slots per lane
 constexpr int RCH = 64;        // ops per chunk
 constexpr int RCHR = 16;       // rmvs per chunk (rows of the clock table)
 constexpr uint32_t RNONE = 0xFFFFFFFFu;
-#ifndef TRMV_WARM
-#define TRMV_WARM 0  // the next key's lines loaded into the caches during P1-P3 (A/B r04: 0.1-0.3 ms per steady batch slower)
-#endif
-#ifndef TRMV_CNPRE
-#define TRMV_CNPRE 0  // a key's next chunk of ops loaded during the current chunk's Observed half
-#endif
-#ifndef TRMV_P3PRE
-#define TRMV_P3PRE 0  // P3's first window of old pool positions loaded at the start of P2
-#endif
-#ifndef TRMV_P2PRE
-#define TRMV_P2PRE 1  // P2's first 128 op Ids and kinds loaded at the start of P1
-#endif
-#ifndef TRMV_CLK2
-#define TRMV_CLK2 1  // chunks: both rounds of clock-row loads issued before either is stored
-#endif
-#ifndef TRMV_DUP4
-#define TRMV_DUP4 1  // replays: a duplicate candidate's slab scan four elements per trip
-#endif
-#ifndef TRMV_RFBLK
-#define TRMV_RFBLK 4  // replays: slab elements per block of loads in a rmv's filter
-#endif
-#ifndef TRMV_PROMOTE2
-#define TRMV_PROMOTE2 1  // rmv promotions: the largest element's fields read for each lane's best slot only
-#endif
-#ifndef TRMV_MBALLOT
-#define TRMV_MBALLOT 3  // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
-#endif
-#ifndef TRMV_P5BUF
-#define TRMV_P5BUF 0  // P5: a compacted slab's re-find four elements per trip (A/B r04: slower)
-#endif
-#ifndef TRMV_RBUF
-#define TRMV_RBUF 0  // replays: Removals row and slab loads through descriptors
-#endif
-#ifndef TRMV_LANELOCAL
-#define TRMV_LANELOCAL 1  // chunks: lane-derived addresses computed per chunk (VGPR pressure)
-#endif
-#ifndef TRMV_DOMPF
-#define TRMV_DOMPF 1  // chunks: a non-replayed add's Removals-row entry loaded before the sort
-#endif
-#ifndef TRMV_HOISTP
-#define TRMV_HOISTP 0  // the replays' pool column bases read once per replay, not per access (A/B r04: spills, slower)
-#endif
-#ifndef TRMV_BUFLD
-#define TRMV_BUFLD 1  // P1's record and element loads through bounds-checked buffer descriptors
-#endif
-#ifndef TRMV_C0PRE
-#define TRMV_C0PRE 0  // the first chunk's ops kept in registers from P2
-#endif
-#ifndef TRMV_RPF
-#define TRMV_RPF 0  // replays: a rmv-first player's first slab lines touched with its Removals row
-#endif
-#ifndef TRMV_DPPSCAN
-#define TRMV_DPPSCAN 1  // P4's segmented scan on DPP row shifts (0: ds_bpermute shuffles)
-#endif
-#ifndef TRMV_MSEQ
-#define TRMV_MSEQ 0  // merges of up to this many candidates run on the register array (0: off; A/B r04: 8 cost ~1 ms per steady batch)
-#endif
+constexpr int RFBLK = 4;           // replays: slab elements per block of loads in a rmv's filter
+constexpr uint32_t MBALLOT = 3;    // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
 constexpr uint32_t RH_NONE = 0xFFFFu, RH_CLAIM = 0x8000u;  // hash slots: player | CLAIM|lane | NONE
 enum : int { R_DONE = 0, R_NEXT = 1, R_REJECT = 2 };
 
@@ -580,7 +518,6 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
   const uint32_t l = (uint32_t)lane_id();
   uint32_t bp = RNONE;
   int64_t best = INT64_MIN;
-#if TRMV_PROMOTE2
   // flags and Scores of the lane's four slots, then the largest element's
   // Ts / DcId / position of its best slot only (4 + 3 LDS reads, not 20)
   uint32_t f[RSL];
@@ -602,33 +539,6 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
   const uint32_t bq = bp != RNONE ? bp : 0u;
   const int64_t bt = L.gts[bq];
   const uint32_t bd = L.gdc[bq], bg = L.gpos[bq];
-#else
-  uint32_t f[RSL], gd[RSL], gp[RSL];
-  int32_t sc[RSL];
-  int64_t gt[RSL];
-#pragma unroll
-  for (int u = 0; u < RSL; ++u) {
-    const uint32_t p = 64u * u + l;
-    f[u] = p < np ? L.pf[p] : 0u;
-    sc[u] = L.msc[p];
-    gt[u] = L.gts[p];
-    gd[u] = L.gdc[p];
-    gp[u] = L.gpos[p];
-  }
-  int64_t bt = 0;
-  uint32_t bd = 0, bg = 0;
-#pragma unroll
-  for (int u = 0; u < RSL; ++u) {
-    const int64_t k = mkkey(sc[u], pid[u]);
-    if ((f[u] & (Q_OBS | Q_HASM)) == Q_HASM && (bp == RNONE || k > best)) {
-      bp = 64u * u + l;
-      best = k;
-      bt = gt[u];
-      bd = gd[u];
-      bg = gp[u];
-    }
-  }
-#endif
   if (!ballot(bp != RNONE)) return RNONE;
   const int64_t m = wave_max_i64_dpp(bp != RNONE ? best : INT64_MIN);
   const int src = (int)__builtin_ctzll(ballot(bp != RNONE && best == m));
@@ -648,16 +558,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   unsigned long long prof_t;
   RPROF_STAMP(prof_t);
 #endif
-  // the wave's next key: its metadata and op range now (scalar loads), the
-  // lines of its state and ops after P1 (warm_next)
-  const bool warm = TRMV_WARM && nkey != RNONE && !KA->fresh;
-  KeyMeta wmeta;
-  uint64_t wo0 = 0, wo1 = 0;
-  if (warm) {
-    wmeta = KA->old_s.meta[nkey];
-    wo0 = KA->key_ptr[nkey];
-    wo1 = KA->key_ptr[nkey + 1];
-  }
   const uint64_t op0 = KA->key_ptr[key];
   const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
   // (a fresh batch: the keys tier 0 handed on, with no old state)
@@ -681,7 +581,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   if (lane == 0) L.nex = 0u;
   wave_lds_sync();
 
-#if TRMV_P2PRE
   // P2's first round of op Ids and kinds, loaded now: their latency runs
   // under P1's own load chains instead of after them
   int64_t pre_id[2];
@@ -695,7 +594,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       pre_kd[h] = bld8(bkd0, 64u * h + lane);
     }
   }
-#endif
   // ---- P1. old players: records of all four slots, then the Obs[Id] /
   // largest elements they name (two rounds of loads in flight), then LDS and
   // the Id hash (the four slots' probes interleaved).
@@ -707,17 +605,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   uint32_t odr[RSL];             // Obs[Id]'s DcId by slot
   bool wide = false;
   {
-#if TRMV_LANELOCAL > 1
-    uint32_t lane_o = lane;  // (P1's lane-derived addresses made here)
-    asm volatile("" : "+v"(lane_o));
-    const uint32_t lane = lane_o;
-#endif
     uint32_t info[RSL], slab[RSL], gb[RSL];
     {
       // (the four arrays' bases once, and pl_gb read whatever the slab's
       // count: a load conditional on another load's value waited for it, slot
       // by slot)
-#if TRMV_BUFLD
       // (bounds-checked buffer loads: the slots past np read 0, every load
       // of the four slots goes out back to back)
       const __amdgpu_buffer_rsrc_t rid = bsrc(KA->old_s.pl_id + om.p_off, om.np * 8u);
@@ -734,29 +626,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         slab[u] = bld32(rslab, p * 4u);
         gb[u] = bld16(rgb, p * 2u);
       }
-#else
-      const int64_t* const pl_id = KA->old_s.pl_id + om.p_off;
-      const uint32_t* const pl_info = KA->old_s.pl_info + om.p_off;
-      const uint32_t* const pl_slab = KA->old_s.pl_slab + om.p_off;
-      const uint16_t* const pl_gb = KA->old_s.pl_gb + om.p_off;
-#pragma unroll
-      for (int u = 0; u < RSL; ++u) {
-        const uint32_t p = 64u * u + lane;
-        const bool v = p < om.np;
-        const uint32_t pp = v ? p : 0u;
-        pid[u] = v ? pl_id[pp] : 0;
-        info[u] = v ? pl_info[pp] : RNONE;
-        slab[u] = v ? pl_slab[pp] : 0u;
-        gb[u] = v ? (uint32_t)pl_gb[pp] : 0u;
-      }
-#endif
 #pragma unroll
       for (int u = 0; u < RSL; ++u) gb[u] = (slab[u] >> 16) > 1 ? gb[u] : 0u;  // (readers take 0 below 2)
     }
     int64_t os[RSL], ot[RSL], gs[RSL], gt[RSL];
     uint32_t gd[RSL];
     {
-#if TRMV_BUFLD
       // (slabs may leave holes, so a key's pool segment is not [0, nm): the
       // range is open-ended and only the lanes with nothing to read are sent
       // past it; the others read exactly what the plain loads read)
@@ -775,23 +650,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         gt[u] = bld64(rts, hg ? qg * 8u : BOOB);
         gd[u] = bld8(rdc, hg ? qg : BOOB);
       }
-#else
-      const int64_t* const m_score = KA->old_s.m_score + om.m_off;
-      const int64_t* const m_ts = KA->old_s.m_ts + om.m_off;
-      const uint8_t* const m_dc = KA->old_s.m_dc + om.m_off;
-#pragma unroll
-      for (int u = 0; u < RSL; ++u) {
-        const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
-        const bool ho = obx != NONE16, hg = cnt != 0;
-        const uint32_t qo = off + (ho ? obx : 0u), qg = off + gb[u];
-        os[u] = ho ? m_score[qo] : 0;
-        ot[u] = ho ? m_ts[qo] : 0;
-        odr[u] = ho ? (uint32_t)m_dc[qo] : 0u;
-        gs[u] = hg ? m_score[qg] : 0;
-        gt[u] = hg ? m_ts[qg] : 0;
-        gd[u] = hg ? (uint32_t)m_dc[qg] : 0u;
-      }
-#endif
     }
     {
       // the Id hash (16-bit slots: CAS on the containing word) while the
@@ -852,31 +710,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     }
   }
   if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
-  // Next key's lines into the caches (L2 / Infinity Cache) while this key
-  // works: one load per 128-byte line of its player records, Masked pool,
-  // Removals rows and ops, so the dependent load chains of its P1-P3 and
-  // chunks find their lines there instead of in HBM.  Nothing waits for
-  // these loads until P3's own wait (their values are folded into a fake use
-  // there).
-  uint32_t tch = 0;
-  uint32_t tv[12];
-  if (warm) {
-    const uint32_t np2 = wmeta.np, nm2 = wmeta.nm, nr2 = wmeta.nr;
-    const uint64_t n2 = wo1 - wo0;
-    const void* reg[12] = {KA->old_s.pl_id + wmeta.p_off, KA->old_s.pl_info + wmeta.p_off,
-                           KA->old_s.pl_slab + wmeta.p_off, KA->old_s.pl_gb + wmeta.p_off,
-                           KA->old_s.m_score + wmeta.m_off, KA->old_s.m_ts + wmeta.m_off,
-                           KA->old_s.m_dc + wmeta.m_off, KA->old_s.r_vc + (uint64_t)wmeta.r_off * D,
-                           KA->id + wo0, KA->score + wo0, KA->ts + wo0, KA->kind + wo0};
-    const uint64_t len[12] = {8ull * np2, 4ull * np2, 4ull * np2, 2ull * np2, 8ull * nm2, 8ull * nm2, nm2,
-                              8ull * D * nr2, 8 * n2, 8 * n2, 8 * n2, n2};
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const uintptr_t b = reinterpret_cast<uintptr_t>(reg[i]);
-      const uintptr_t l0 = b >> 7, l1 = (b + len[i] + 127) >> 7;
-      tv[i] = (len[i] && l0 + lane < l1) ? *reinterpret_cast<const uint32_t*>((l0 + lane) << 7) : 0u;
-    }
-  }
   span = wave_max_u32_dpp(span);
   Obs ob;
   ob.n = om.nobs;
@@ -936,40 +769,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   RPROF(0);
   {
     // ---- P2. every op's player; ops per player; rmv players
-#if TRMV_LANELOCAL > 1
-    uint32_t lane_o = lane;  // (P2-P5's lane-derived addresses made here)
-    asm volatile("" : "+v"(lane_o));
-    const uint32_t lane = lane_o;
-#endif
     uint32_t np = om.np;
-#if TRMV_P3PRE && TRMV_BUFLD
-    // P3's first window of old pool positions, loaded now: its latency runs
-    // under P2 (the range is the key's span: past it reads 0)
-    int64_t p3_sc, p3_ts;
-    uint32_t p3_dc;
-    {
-      const __amdgpu_buffer_rsrc_t q0s = bsrc(KA->old_s.m_score + om.m_off, span * 8u);
-      const __amdgpu_buffer_rsrc_t q0t = bsrc(KA->old_s.m_ts + om.m_off, span * 8u);
-      const __amdgpu_buffer_rsrc_t q0d = bsrc(KA->old_s.m_dc + om.m_off, span);
-      p3_sc = bld64(q0s, lane * 8u);
-      p3_ts = bld64(q0t, lane * 8u);
-      p3_dc = bld8(q0d, lane);
-    }
-#endif
-#if TRMV_C0PRE
-    // the first chunk's ops stay in registers from here (its Ids, kinds and
-    // players from this pass; Scores, Ts, DcIds loaded with them), so the
-    // chunk loop's first round does not wait for its loads
-    int64_t c0id = 0, c0sc = 0, c0ts = 0;
-    uint32_t c0kd = 0, c0dc = 0, c0p = (uint32_t)RP;
-#endif
     // 128 ops per round: both halves' Ids and kinds load together, then each
     // half is resolved (one 64-lane claim table)
-#if TRMV_BUFLD
     // (the key's op columns through bounds-checked descriptors: past nops reads 0)
     const __amdgpu_buffer_rsrc_t bid = bsrc(KA->id + op0, nops * 8u);
     const __amdgpu_buffer_rsrc_t bkd = bsrc(KA->kind + op0, nops);
-#endif
     for (uint32_t c0 = 0; c0 < nops; c0 += 128) {
       int64_t idh[2];
       uint32_t kh[2];
@@ -978,30 +783,16 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       for (int h = 0; h < 2; ++h) {
         const uint32_t l = c0 + 64u * h + lane;
         vh[h] = l < nops;
-#if TRMV_BUFLD
-#if TRMV_P2PRE
         if (c0 == 0) {
           idh[h] = pre_id[h];
           kh[h] = pre_kd[h];
         } else
-#endif
         {
           idh[h] = bld64(bid, l * 8u);
           kh[h] = bld8(bkd, l);
         }
-#else
-        idh[h] = vh[h] ? KA->id[op0 + l] : 0;
-        kh[h] = vh[h] ? (uint32_t)KA->kind[op0 + l] : 0u;
-#endif
         wide |= vh[h] && !fits32(idh[h]);
       }
-#if TRMV_C0PRE
-      if (c0 == 0 && vh[0]) {
-        c0sc = KA->score[op0 + lane];
-        c0ts = KA->ts[op0 + lane];
-        c0dc = KA->dc[op0 + lane];
-      }
-#endif
       if (ballot(wide)) return R_NEXT;  // a wide Id: tier S
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -1009,13 +800,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint32_t l = c0 + 64u * h + lane;
         uint32_t p;
         if (!r_resolve(L, idh[h], vh[h], np, p)) return R_NEXT;
-#if TRMV_C0PRE
-        if (c0 == 0 && h == 0) {
-          c0id = idh[0];
-          c0kd = kh[0];
-          c0p = vh[0] ? p : (uint32_t)RP;
-        }
-#endif
         if (vh[h]) {
           KA->op_pl[op0 + l] = (uint8_t)p;
           atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
@@ -1073,7 +857,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     bool wide = false;
     if (span) {
       int32_t prev = -1;
-#if TRMV_BUFLD
       // (the old pool through bounds-checked descriptors over the key's span,
       // the new side's bases read once: the window's loads and stores issue
       // without a branch or a scalar wait each)
@@ -1083,7 +866,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       int64_t* const Nsc = KA->new_s.m_score + nm.m_off;
       int64_t* const Nts = KA->new_s.m_ts + nm.m_off;
       uint8_t* const Ndc = KA->new_s.m_dc + nm.m_off;
-#endif
       // four windows of 64 positions per round: their loads go out together
       for (uint32_t g0 = 0; g0 < span; g0 += 256) {
         int64_t wsc[4], wts[4];
@@ -1091,25 +873,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t q = g0 + 64u * i + lane;
-#if TRMV_BUFLD
-#if TRMV_P3PRE
-          if (g0 == 0 && i == 0) {
-            wsc[i] = p3_sc;
-            wts[i] = p3_ts;
-            wdc[i] = p3_dc;
-          } else
-#endif
           {
             wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
             wts[i] = bld64(qts, q * 8u);
             wdc[i] = bld8(qdc, q);
           }
-#else
-          const uint64_t src = (uint64_t)om.m_off + (q < span ? q : 0u);
-          wsc[i] = q < span ? KA->old_s.m_score[src] : 0;
-          wts[i] = q < span ? KA->old_s.m_ts[src] : 0;
-          wdc[i] = q < span ? (uint32_t)KA->old_s.m_dc[src] : 0u;
-#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1162,17 +930,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             const uint32_t off = sl & 0xFFFFu, cnt = sl >> 16;
             if (q < off + cnt) {
               wide |= !fits32(sc);
-#if TRMV_BUFLD
               const uint32_t dst = (L.nslab[o] & 0xFFFFu) + (q - off);
               Nsc[dst] = sc;
               Nts[dst] = ts;
               Ndc[dst] = (uint8_t)dc;
-#else
-              const uint64_t dst = (uint64_t)nm.m_off + (L.nslab[o] & 0xFFFFu) + (q - off);
-              KA->new_s.m_score[dst] = sc;
-              KA->new_s.m_ts[dst] = ts;
-              KA->new_s.m_dc[dst] = (uint8_t)dc;
-#endif
             }
           }
           wave_lds_sync();
@@ -1180,7 +941,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     }
     if (ballot(wide)) return R_NEXT;  // a wide Score in Masked: tier S
-#if TRMV_BUFLD
     {
       // old Removals rows, 32 per round: the round's loads, then its stores
       const __amdgpu_buffer_rsrc_t qr = bsrc(KA->old_s.r_vc + (uint64_t)om.r_off * D, om.nr * (uint32_t)D * 8u);
@@ -1200,74 +960,26 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         }
       }
     }
-#else
-    for (uint32_t r0 = 0; r0 < om.nr; r0 += 8) {
-      const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
-      if (r < om.nr && (int)d < D)
-        KA->new_s.r_vc[((uint64_t)nm.r_off + r) * D + d] = KA->old_s.r_vc[((uint64_t)om.r_off + r) * D + d];
-    }
-#endif
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
-    if (warm) {
-#pragma unroll
-      for (int i = 0; i < 12; ++i) tch ^= tv[i];
-      asm volatile("" ::"v"(tch));  // (keeps the warm-up loads)
-    }
     RPROF(2);
 
     // ---- chunks
-#if TRMV_CNPRE
-    bool nx_ok = false;
-    uint32_t nx_kd = 0, nx_dc = 0, nx_p = 0;
-    int64_t nx_id = 0, nx_sc = 0, nx_ts = 0;
-#endif
     for (uint32_t c0 = 0; c0 < nops;) {
-#if TRMV_LANELOCAL
       // this chunk's lane-indexed LDS addresses are made from a lane the
       // compiler cannot see through, so they are computed here and not held
       // in VGPRs across the whole kernel
       uint32_t lane_o = lane;
       asm volatile("" : "+v"(lane_o));
       const uint32_t lane = lane_o;
-#endif
       uint32_t n = nops - c0 < (uint32_t)RCH ? nops - c0 : (uint32_t)RCH;
       bool v = lane < n;
       [[maybe_unused]] const uint64_t gi = op0 + c0 + lane;
-#if TRMV_C0PRE
-      uint32_t kind, dc, p;
-      int64_t id, sc, ts;
-      if (c0 == 0) {
-        kind = c0kd;
-        id = c0id;
-        sc = c0sc;
-        ts = c0ts;
-        dc = c0dc;
-        p = c0p;
-      } else {
-        kind = v ? (uint32_t)KA->kind[gi] : 0u;
-        id = v ? KA->id[gi] : 0;
-        sc = v ? KA->score[gi] : 0;
-        ts = v ? KA->ts[gi] : 0;
-        dc = v ? (uint32_t)KA->dc[gi] : 0u;
-        p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
-      }
-#elif TRMV_BUFLD
       // (bounds-checked loads over the key's ops: no branch around them)
       uint32_t kind, dc, p;
       int64_t id, sc, ts;
       {
         uint32_t kb, db, pb;
         int64_t ib, sb, tb;
-#if TRMV_CNPRE
-        if (nx_ok) {  // loaded during the previous chunk's Observed half
-          kb = nx_kd;
-          ib = nx_id;
-          sb = nx_sc;
-          tb = nx_ts;
-          db = nx_dc;
-          pb = nx_p;
-        } else
-#endif
         {
           const uint32_t o = c0 + lane;
           kb = bld8(bsrc(KA->kind + op0, nops), o);
@@ -1284,28 +996,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         dc = v ? db : 0u;
         p = v ? pb : (uint32_t)RP;
       }
-#elif TRMV_HOISTP
-      // (the six columns' bases read together: one scalar wait, not one per load)
-      const uint8_t* const Ck = KA->kind;
-      const int64_t* const Ci = KA->id;
-      const int64_t* const Cs = KA->score;
-      const int64_t* const Ct = KA->ts;
-      const uint8_t* const Cd = KA->dc;
-      const uint8_t* const Cp = KA->op_pl;
-      const uint32_t kind = v ? (uint32_t)Ck[gi] : 0u;
-      const int64_t id = v ? Ci[gi] : 0;
-      const int64_t sc = v ? Cs[gi] : 0;
-      const int64_t ts = v ? Ct[gi] : 0;
-      const uint32_t dc = v ? (uint32_t)Cd[gi] : 0u;
-      const uint32_t p = v ? (uint32_t)Cp[gi] : (uint32_t)RP;
-#else
-      const uint32_t kind = v ? (uint32_t)KA->kind[gi] : 0u;
-      const int64_t id = v ? KA->id[gi] : 0;
-      const int64_t sc = v ? KA->score[gi] : 0;
-      const int64_t ts = v ? KA->ts[gi] : 0;
-      const uint32_t dc = v ? (uint32_t)KA->dc[gi] : 0u;
-      const uint32_t p = v ? (uint32_t)KA->op_pl[gi] : (uint32_t)RP;
-#endif
       bool isr = v && (kind == 2 || kind == 3);
       uint64_t rm = ballot(isr);
       if (__builtin_popcountll(rm) > RCHR) {  // cut before the chunk's 17th rmv
@@ -1317,7 +1007,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         rm = ballot(isr);
       }
       const bool add = v && kind < 2;
-#if TRMV_DOMPF
       // the Removals-row entry a non-replayed add is checked against (:234),
       // loaded here and read after the sort: a player without a rmv in the
       // batch keeps its row unchanged through the batch's replays
@@ -1330,7 +1019,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         rte = bld64(bsrc(KA->new_s.r_vc + (uint64_t)nm.r_off * D, nr * (uint32_t)D * 8u),
                     need ? (orwe * (uint32_t)D + dc) * 8u : BOOB);
       }
-#endif
       uint32_t err = 0;
       err |= (v && kind > 3) ? TRMV_ERR_KIND : 0u;
       err |= (add && (int)dc >= D) ? TRMV_ERR_DC : 0u;
@@ -1344,7 +1032,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const uint32_t rk = mbcnt(rm), nrm = (uint32_t)__builtin_popcountll(rm);
       if (isr) L.u.c.crow[rk] = (uint32_t)ts;
       wave_lds_sync();
-#if TRMV_CLK2
       {
         // (<= 16 rows: both halves' loads go out before either is stored)
         static_assert(RCHR <= 16, "two rounds of 8 clock rows");
@@ -1358,16 +1045,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         if (ra < nrm) L.u.c.vtab[ra][d] = xa;
         if (rb < nrm) L.u.c.vtab[rb][d] = xb;
       }
-#else
-      for (uint32_t r0 = 0; r0 < nrm; r0 += 8) {
-        const uint32_t r = r0 + (lane >> 3), d = lane & 7u;
-        if (r < nrm) {
-          const int64_t x = (int)d < D ? KA->rmv_vc[(uint64_t)L.u.c.crow[r] * D + d] : 0;
-          err |= x < 0 ? TRMV_ERR_VC : 0u;
-          L.u.c.vtab[r][d] = x;
-        }
-      }
-#endif
       if (ballot(err != 0)) {
         if (err) atomicOr(&KA->status[1], err);
         return R_REJECT;
@@ -1439,18 +1116,11 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const bool walk = sv && (pf0 & (Q_RMV | Q_DUP));
       bool dom = false;
       uint32_t orw = NONE16;
-#if TRMV_DOMPF
       const int64_t rts = shfl64(rte, (int)so);
       if (sv && !walk && (pf0 & Q_ROWV)) {
         orw = L.prow[sp];
         dom = rts >= sts;
       }
-#else
-      if (sv && !walk && (pf0 & Q_ROWV)) {
-        orw = L.prow[sp];
-        dom = KA->new_s.r_vc[((uint64_t)nm.r_off + orw) * D + sdc] >= sts;
-      }
-#endif
       const bool app = sv && !walk && !dom;
       const uint64_t nd = ballot(app);
       if (app) {
@@ -1480,27 +1150,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         L.u.c.cwe[k] = (uint8_t)shi;
       }
       wave_lds_sync();
-#if TRMV_RBUF
-      // (the replays' Removals rows and pool through bounds-checked
-      // descriptors made once per chunk: no scalar pointer re-read per load)
-      const __amdgpu_buffer_rsrc_t qR = bsrc(KA->new_s.r_vc + (uint64_t)nm.r_off * D, nr * (uint32_t)D * 8u);
-      const __amdgpu_buffer_rsrc_t qS = bsrc(KA->new_s.m_score + nm.m_off, BOOB);
-      const __amdgpu_buffer_rsrc_t qT = bsrc(KA->new_s.m_ts + nm.m_off, BOOB);
-      const __amdgpu_buffer_rsrc_t qD = bsrc(KA->new_s.m_dc + nm.m_off, BOOB);
-#endif
       if (lane < (uint32_t)__builtin_popcountll(wm)) {
-#if TRMV_HOISTP
-        // the pool columns' bases read once here: a kernel argument is
-        // re-read at each use (kernarg_as), and inside these loops each
-        // re-read is a scalar load the next global access waits for
-        int64_t* const Msc = KA->new_s.m_score;
-        int64_t* const Mts = KA->new_s.m_ts;
-        uint8_t* const Mdc = KA->new_s.m_dc;
-#else
 #define Msc KA->new_s.m_score
 #define Mts KA->new_s.m_ts
 #define Mdc KA->new_s.m_dc
-#endif
         const uint32_t wp = L.u.c.cwp[lane], ws = L.u.c.cws[lane], we = L.u.c.cwe[lane];
         uint32_t f = L.pf[wp];
         const uint32_t ns = L.nslab[wp];
@@ -1512,23 +1165,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint64_t rbase = ((uint64_t)nm.r_off + row) * D;
         {
           const int dn = KA->n_dc;  // (re-read here: no per-d masks held across the key)
-#if TRMV_RBUF
-#pragma unroll
-          for (int d = 0; d < TRMV_DPAD; ++d) R[d] = bld64(qR, (has_row && d < dn) ? (row * (uint32_t)D + d) * 8u : BOOB);
-#else
 #pragma unroll
           for (int d = 0; d < TRMV_DPAD; ++d) R[d] = (has_row && d < dn) ? KA->new_s.r_vc[rbase + d] : 0;
-#endif
         }
-#if TRMV_RPF
-        // a player whose first op here is a rmv: its slab's first lines are
-        // touched with the Removals row (into this CU's L1), so the filter's
-        // first block of loads does not go to L2
-        if (cnt != 0 && (L.u.c.ckd[L.u.c.csrt[ws]] & 3u) >= 2) {
-          const int64_t tch = Msc[base] ^ Mts[base] ^ (int64_t)Mdc[base];
-          asm volatile("" ::"v"(tch));
-        }
-#endif
         const int64_t wid = L.u.c.cid[ws];
         bool moved = false;
         for (uint32_t x = ws; x < we; ++x) {
@@ -1543,7 +1182,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
               continue;
             }
             uint32_t pos = RNONE;
-#if TRMV_DUP4
             if ((kd >> 5) & 1u) {  // set semantics: the element may be there
               // four elements per trip, their loads together (one round trip
               // per four elements, not one or three per element)
@@ -1562,15 +1200,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
                   if (j0 + e < cnt && t4[e] == ets && d4[e] == edc && s4[e] == esc) pos = j0 + e;
               }
             }
-#else
-            if ((kd >> 5) & 1u)  // set semantics: the element may be there
-              for (uint32_t j = 0; j < cnt; ++j)
-                if (Mts[base + j] == ets && Mdc[base + j] == edc &&
-                    Msc[base + j] == esc) {
-                  pos = j;
-                  break;
-                }
-#endif
             if (pos == RNONE) {
               pos = cnt++;
               Msc[base + pos] = esc;
@@ -1591,28 +1220,18 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             int64_t bsc = 0, bts = 0;
             // the slab in blocks of 4 elements, each block's loads issued
             // together (the compaction only writes positions already read)
-            for (uint32_t j0 = 0; j0 < cnt; j0 += TRMV_RFBLK) {
-              int64_t s4[TRMV_RFBLK], t4[TRMV_RFBLK];
-              uint32_t d4[TRMV_RFBLK];
-#if TRMV_RBUF
+            for (uint32_t j0 = 0; j0 < cnt; j0 += RFBLK) {
+              int64_t s4[RFBLK], t4[RFBLK];
+              uint32_t d4[RFBLK];
 #pragma unroll
-              for (int e = 0; e < TRMV_RFBLK; ++e) {
-                const uint32_t q = (ns & 0xFFFFu) + (j0 + e < cnt ? j0 + e : j0);
-                s4[e] = bld64(qS, q * 8u);
-                t4[e] = bld64(qT, q * 8u);
-                d4[e] = bld8(qD, q);
-              }
-#else
-#pragma unroll
-              for (int e = 0; e < TRMV_RFBLK; ++e) {
+              for (int e = 0; e < RFBLK; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
                 s4[e] = Msc[base + j];
                 t4[e] = Mts[base + j];
                 d4[e] = Mdc[base + j];
               }
-#endif
 #pragma unroll
-              for (int e = 0; e < TRMV_RFBLK; ++e) {
+              for (int e = 0; e < RFBLK; ++e) {
                 const uint32_t j = j0 + e;
                 if (j < cnt && t4[e] > V[d4[e]]) {
                   if (w != j) {
@@ -1637,11 +1256,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             L.u.c.rgd[r] = (w ? 1u : 0u) | (bdc << 8) | (bpos << 16);
           }
         }
-#if !TRMV_HOISTP
 #undef Msc
 #undef Mts
 #undef Mdc
-#endif
         L.nslab[wp] = (ns & 0xFFFFu) | (cnt << 16);
         if (has_row) {
           for (int d = 0, dn = KA->n_dc; d < dn; ++d) KA->new_s.r_vc[rbase + d] = pick8(R, (uint32_t)d);
@@ -1655,19 +1272,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       // chunk nothing reads them before P5, which waits there: the Observed
       // half runs while they drain.
       if (c0 + n < nops) __builtin_amdgcn_s_waitcnt(0x0F70);
-#if TRMV_CNPRE
-      // the next chunk's ops load while this chunk's Observed half runs
-      nx_ok = c0 + n < nops;
-      if (nx_ok) {
-        const uint32_t o = c0 + n + lane;
-        nx_kd = bld8(bsrc(KA->kind + op0, nops), o);
-        nx_id = bld64(bsrc(KA->id + op0, nops * 8u), o * 8u);
-        nx_sc = bld64(bsrc(KA->score + op0, nops * 8u), o * 8u);
-        nx_ts = bld64(bsrc(KA->ts + op0, nops * 8u), o * 8u);
-        nx_dc = bld8(bsrc(KA->dc + op0, nops), o);
-        nx_p = bld8(bsrc(KA->op_pl + op0, nops), o);
-      }
-#endif
       RPROF(5);
 
       // ---- P4. the Observed half, in stream order (recompute_observed/5
@@ -1695,7 +1299,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint32_t seg = (sp << 8) | srun;
         const uint32_t pseg = shfl32(seg, lane ? (int)lane - 1 : 0);
         const bool hf0 = lane == 0 || pseg != seg;
-#if TRMV_DPPSCAN
         int32_t vs = (int32_t)ssc, ws = (int32_t)ssc;  // (Scores of adds fit 32 bits here)
         int64_t vt = sts, wt = sts;
         uint32_t vd = sdc | ((scres >> 16) << 8) | (sadd ? (1u << 30) : 0u) | (hf0 ? (1u << 31) : 0u);
@@ -1708,39 +1311,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         seg_step<0x143, 0xc>(vs, vt, vd, ws, wt, wd);
         const bool ok = (vd >> 30) & 1u;
         vd &= 0x3FFFFFFFu;
-#else
-        bool ok = sadd, hf = hf0;
-        int64_t vs = ssc, vt = sts, ws = ssc, wt = sts;
-        uint32_t vd = sdc | ((scres >> 16) << 8), wd = vd;
-        int sl = (int)lane;
-        asm volatile("" : "+v"(sl));  // the (lane >= d) masks are made here, not held across keys
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const int src = sl >= d ? sl - d : sl;
-          const bool yok = shfl32(ok ? 1u : 0u, src) != 0;
-          const int64_t ys = shfl64(vs, src), yt = shfl64(vt, src);
-          const uint32_t yd = shfl32(vd, src);
-          const int64_t zs = shfl64(ws, src), zt = shfl64(wt, src);
-          const uint32_t zd = shfl32(wd, src);
-          const bool yhf = shfl32(hf ? 1u : 0u, src) != 0;
-          if (sl >= d && !hf) {
-            if (yok) {
-              if (!ok || gb_gt(ys, yd & 0xFFu, yt, vs, vd & 0xFFu, vt)) {
-                vs = ys;
-                vt = yt;
-                vd = yd;
-              }
-              if (!ok || !(ws > zs || (ws == zs && wt > zt))) {  // the earlier one wins ties
-                ws = zs;
-                wt = zt;
-                wd = zd;
-              }
-              ok = true;
-            }
-            hf = yhf;
-          }
-        }
-#endif
         const uint32_t nseg = shfl32(seg, lane < 63 ? (int)lane + 1 : (int)lane);
         const bool last = sv && (lane == 63 || nseg != seg);
         cu_ok = last && ok;
@@ -1801,44 +1371,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         if (!relm) return;
         RPROF(16);
         const uint32_t m = (uint32_t)__builtin_popcountll(relm);
-        if (m <= (uint32_t)TRMV_MSEQ) {
-          // Few candidates: each one applied to the register array as the
-          // add it stands for (recompute_observed/5, :301-334) -- an upgrade
-          // re-sorts its player's entry, an entry into a full Observed
-          // evicts Min (entry 0) -- one ballot rank and one DPP range shift
-          // each, no LDS round trip.  Any order of the run's candidates
-          // gives the batch merge's result (the state after a
-          // run is the top K by (largest Score, Id)); an upgraded player
-          // whose old entry an earlier candidate evicted enters as a new one.
-          const uint64_t inm = ballot(rel && inobs);
-          for (uint64_t t = relm; t; t &= t - 1) {
-            const int x = (int)__builtin_ctzll(t);
-            const int64_t kx = rl64(cm_k, x);
-            const uint32_t px = rl32(cu_p, x);
-            const uint32_t plx = px | (rl32(cm_d, x) << 16);
-            const uint32_t ix = ((inm >> x) & 1u) ? ob_find(ob, px) : RNONE;
-            bool put = true;
-            if (ix != RNONE) {
-              ob_replace(ob, ix, kx, plx);
-            } else if (ob.n < K) {
-              ob_insert(ob, kx, plx);
-              if ((int)lane == x) pf_or(L, px, Q_OBS);
-            } else if (kx > rl64(ob.key[0], 0)) {
-              const uint32_t ev = rl32(ob.pl[0], 0) & 0xFFFFu;  // evicted (:325-331)
-              if (lane == 0) pf_and(L, ev, Q_OBS);
-              ob_replace(ob, 0, kx, plx);
-              if ((int)lane == x) pf_or(L, px, Q_OBS);
-            } else {
-              put = false;
-            }
-            if (put && (int)lane == x) {  // Obs[Id] := its cmp-largest
-              L.opos[px] = (uint16_t)cm_pos;
-              L.ots[px] = cm_t;
-            }
-          }
-          wave_lds_sync();
-          return;
-        }
         // The merge's ranks.  Up to three candidates: a ballot pair per
         // candidate.  More: no loop over the candidates -- their keys are
         // listed in LDS (upgraded players flagged Q_UPG); every kept entry and
@@ -1849,7 +1381,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         // among the candidates), keys being distinct.
         bool rem0, rem1;
         uint32_t cb0 = 0, cb1 = 0, cbc = 0, abc = 0;
-        if (m <= (uint32_t)TRMV_MBALLOT) {
+        if (m <= MBALLOT) {
           // few candidates: one ballot pair per candidate
           rem0 = rem1 = false;
           for (uint64_t t = ballot(rel && inobs); t; t &= t - 1) {  // upgraded players' old entries
@@ -2018,12 +1550,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       c0 += n;
     }
 
-#if TRMV_LANELOCAL > 2
-    {
-      uint32_t lane_o = lane;  // (P5's lane-derived addresses made here)
-      asm volatile("" : "+v"(lane_o));
-      const uint32_t lane = lane_o;
-#endif
     // ---- P5. player records: Observed first (sorted), then the others in
     // player order; positions of compacted slabs; Vc; meta.  (The re-find of
     // a compacted slab reads the last chunk's stores: they must have landed.)
@@ -2037,11 +1563,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     }
     wave_lds_sync();
-#if TRMV_P5BUF
-    const __amdgpu_buffer_rsrc_t pS = bsrc(KA->new_s.m_score + nm.m_off, BOOB);
-    const __amdgpu_buffer_rsrc_t pT = bsrc(KA->new_s.m_ts + nm.m_off, BOOB);
-    const __amdgpu_buffer_rsrc_t pD = bsrc(KA->new_s.m_dc + nm.m_off, BOOB);
-#endif
     uint32_t rest = ob.n, mcount = 0;
 #pragma unroll
     for (int u = 0; u < RSL; ++u) {
@@ -2058,27 +1579,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const int64_t msv = L.msc[p], otv = ino ? L.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
-#if TRMV_P5BUF
-          // (four elements per trip, their loads together)
-          const uint32_t q0 = ns & 0xFFFFu;
-          for (uint32_t j0 = 0; j0 < cnt; j0 += 4) {
-            int64_t s4[4], t4[4];
-            uint32_t d4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const uint32_t off = j0 + e < cnt ? q0 + j0 + e : BOOB / 8u;
-              s4[e] = bld64(pS, off * 8u);
-              t4[e] = bld64(pT, off * 8u);
-              d4[e] = bld8(pD, j0 + e < cnt ? off : BOOB);
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const uint32_t j = j0 + e;
-              if (j < cnt && s4[e] == msv && t4[e] == otv && d4[e] == od) opos = j;
-              if (j < cnt && s4[e] == msv && t4[e] == gtv && d4[e] == gd) gpos = j;
-            }
-          }
-#else
           const uint64_t base = (uint64_t)nm.m_off + (ns & 0xFFFFu);
           for (uint32_t j = 0; j < cnt; ++j) {
             const int64_t s2 = KA->new_s.m_score[base + j], t2 = KA->new_s.m_ts[base + j];
@@ -2086,7 +1586,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             if (s2 == msv && t2 == otv && d2 == od) opos = j;
             if (s2 == msv && t2 == gtv && d2 == gd) gpos = j;
           }
-#endif
         }
         const uint64_t pq = (uint64_t)nm.p_off + ni;
         KA->new_s.pl_id[pq] = pid[u];
@@ -2109,9 +1608,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       KA->new_s.meta[key] = out;
       KA->ex_cnt[key] = L.nex;
     }
-#if TRMV_LANELOCAL > 2
-    }
-#endif
     RPROF(9);
   }
   return R_DONE;

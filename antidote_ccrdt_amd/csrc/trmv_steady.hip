@@ -71,14 +71,7 @@ namespace ccrdt {
 
 namespace {
 
-#ifndef TRMV_KARGS
-#define TRMV_KARGS 1
-#endif
-#if TRMV_KARGS
 #define KA trmv_kargs()  // (trmv_kernels.hpp)
-#else
-#define KA (&a)
-#endif
 
 constexpr int S_CH = 64;    // ops per chunk
 constexpr int S_CHR = 16;   // rmvs per chunk (rows of the clock table)

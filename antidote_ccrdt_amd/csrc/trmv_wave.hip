@@ -73,49 +73,12 @@ constexpr int W_HCAP = 256;  // hash slots (Ids)
 constexpr int W_ECAP = 128;  // elements: ops + old Masked elements
 constexpr int W_PCAP = 128;  // players
 constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv clocks
-#ifndef TRMV_W_WAVES
-#define TRMV_W_WAVES 1
-#endif
-constexpr int W_WAVES = TRMV_W_WAVES;  // waves (keys in flight) per workgroup
-#ifndef TRMV_AHEAD2
-#define TRMV_AHEAD2 0  // FRESH: ops loaded two keys ahead, clocks one key ahead (measured: 1% slower since the kernel-argument re-read)
-#endif
-#ifndef TRMV_NT
-#define TRMV_NT 0  // FRESH output (pool, player records) stored non-temporal
-#endif
-#if TRMV_NT
-#define ST_OUT(p, v) __builtin_nontemporal_store((v), (p))
-#else
+constexpr int W_WAVES = 1;  // waves (keys in flight) per workgroup (4 before A/B r04 run 31)
 #define ST_OUT(p, v) (*(p) = (v))
-#endif
-#ifndef TRMV_NTL
-#define TRMV_NTL 0  // ops (read once) loaded non-temporal
-#endif
-#if TRMV_NTL
-#define LD_IN(p) __builtin_nontemporal_load(p)
-#else
 #define LD_IN(p) (*(p))
-#endif
-#ifndef TRMV_DIAG_LDS
-// Diagnostic build only (wrong Ids and Min, for the LDS bank-conflict
-// counters): 1 = the records pass's gathers (Id slot, Obs element) made
-// lane-linear.  (Redirecting step 5's gathers the same way sends garbage
-// into clock-row indices and faulted: not a usable diagnostic.)
-#define TRMV_DIAG_LDS 0
-#endif
-#ifndef TRMV_EARLY
-#define TRMV_EARLY 0  // FRESH: the next key's ops loaded at the start of the current key (not after its hash)
-#endif
-constexpr bool EARLY = TRMV_EARLY && !TRMV_AHEAD2;
-#ifndef TRMV_POOLSKIP
-#define TRMV_POOLSKIP 0  // FRESH pool: only decided players' final slabs written (A/B r04: tier 0 2.24 -> 2.44 ms)
-#endif
-#ifndef TRMV_KPW
-#define TRMV_KPW 8
-#endif
-constexpr int W_KPW = TRMV_KPW;  // consecutive keys per wave chunk (1..64)
+constexpr int W_KPW = 8;  // consecutive keys per wave chunk (1..64; A/B r03: 2/3/4/16 slower)
 constexpr int W_MD = (W_KPW + 7) / 8;  // metadata registers of a chunk header
-static_assert(W_KPW >= 1 && W_KPW <= 64, "TRMV_KPW: 1..64 keys per wave chunk");
+static_assert(W_KPW >= 1 && W_KPW <= 64, "1..64 keys per wave chunk");
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
 constexpr uint32_t NONE8 = 0xFFu;
 // Sink entries: a lane with nothing to read reads the extra entry of the
@@ -169,14 +132,7 @@ struct alignas(16) WaveLds {
 #define PGB(p) L.fb((p), 2)
 #define PSLOT(p) L.fb((p), 3)
 
-#ifndef TRMV_KARGS
-#define TRMV_KARGS 1
-#endif
-#if TRMV_KARGS
 #define KA trmv_kargs()
-#else
-#define KA (&a)
-#endif
 
 __device__ __forceinline__ uint32_t whash(int64_t id) {
   const uint64_t x = (uint64_t)id * 0x9E3779B97F4A7C15ull;
@@ -323,8 +279,7 @@ enum : int { W_DONE = 0, W_NEXT_TIER = 1, W_REJECT = 2 };
 template <bool FRESH>
 __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t key, const KeyIn& in,
                                               WaveLds<FRESH>& L, bool has_next, const ChunkHdr& hdr,
-                                              uint32_t nj, KeyIn& nxt, bool has_next2, KeyIn& nxt2,
-                                              bool& issued) {
+                                              uint32_t nj, KeyIn& nxt) {
   // opaque per key: lane-derived addresses are formed where they are used
   // instead of being hoisted out of the key loop into VGPR pairs that live
   // (and spill) across every key
@@ -430,25 +385,6 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     xsc[0] = xr[0] ? (int64_t)(om.nr + r0) : xsc[0];
     xsc[1] = xr[1] ? (int64_t)(om.nr + r1) : xsc[1];
   }
-  if (EARLY && FRESH) {
-    // the rmv clocks first (their loads went out a key ago), then the next
-    // key's op loads, whose latency the hash build and steps 4-5 now hide
-#pragma unroll
-    for (int s = 0; s < W_RCAP / 8; ++s) {
-      const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
-      const int64_t v = (int)d < D ? in.rv[s] : 0;
-      err |= (r < nrmv && v < 0) ? TRMV_ERR_VC : 0u;
-      if (r < nrmv) L.rows[om.nr + r][d] = v;
-    }
-    if (ballot(err != 0)) {
-      if (err) atomicOr(&KA->status[1], err);
-      return W_REJECT;
-    }
-    if (has_next) {
-      wave_load_key(a, hdr, nj, nxt);
-      issued = true;
-    }
-  }
   wave_lds_sync();
   // ---- 3 (set-up). hash slots; an Id equal to the empty marker takes tier 1
   constexpr int NS = FRESH ? 2 : 4;
@@ -489,7 +425,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   }
   PROF_MARK(8);
   // write the rmv clocks (their loads were issued with the key's ops)
-  if (!(EARLY && FRESH)) {
+  {
 #pragma unroll
     for (int s = 0; s < W_RCAP / 8; ++s) {
       const uint32_t r = s * 8 + (lane >> 3), d = lane & 7;
@@ -551,18 +487,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   // retires them, so the next key never waits on (and its vmcnt never
   // counts) this key's stores.  (Non-FRESH keys keep more registers live
   // through step 4: their next key's loads go out at step 5.)
-#if TRMV_AHEAD2
-  // FRESH, two keys ahead: the next key's ops landed during this key's
-  // predecessor; its removal clocks and the ops of the key after it go out
-  // now, a whole key before they are consumed
-  if (FRESH) {
-    if (has_next) wave_load_rows(a, L, nxt);
-    if (has_next2) wave_load_key(a, hdr, nj + 1, nxt2);
-    issued = true;
-  }
-#else
-  if (FRESH && !EARLY && has_next) wave_load_key(a, hdr, nj, nxt);
-#endif
+  if (FRESH && has_next) wave_load_key(a, hdr, nj, nxt);
 
   PROF_MARK(2);
   // ---- 4. player of every op, Vc, op elements in player order
@@ -834,14 +759,10 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   wave_lds_sync();
   // The next key's ops are retired before this key's first store, so the
   // next key never waits on (and its vmcnt never counts) these stores.
-#if !TRMV_AHEAD2
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   // the next key's clock loads go out before this key's first store: a
   // load's data waits for every older vector-memory op, stores included
   if (FRESH && has_next) wave_load_rows(a, L, nxt);
-#else
-  if (!FRESH) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
   PROF_MARK(7);
   uint32_t best_q = NONE32;                      // Min candidate of this lane
   int64_t best_sc = INT64_MAX, best_id = INT64_MAX;
@@ -856,16 +777,17 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     // [pstart, pstart + ops) of the key's pool segment (|Masked[Id]| <= its
     // adds), so no pool order has to be built: the op positions of a decided
     // player's last segment (its slab) are written as their ops' elements
-    // (coalesced); rmv ops, the adds before a player's last rmv and replayed
-    // players' positions (written below) are skipped
+    // (coalesced).  Every op position is written, rmv ops and filtered adds
+    // included (writing only the surviving positions measured slower: the
+    // per-element lookup costs more than the bytes it saves, A/B r04);
+    // replayed players' positions are rewritten below
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t q = s * 64 + lane;
       const uint32_t qq = q < nops ? q : (uint32_t)ESINK;
       const int64_t sc = L.esc[qq], ts = L.ets[qq];
       const uint32_t kd = L.ekd[qq];
-      const uint32_t wa = L.pa[q < nops ? (kd >> 8) : (uint32_t)PSINK];  // pstart | plr | pflag | pcntf
-      if (q < nops && (!TRMV_POOLSKIP || (((wa >> 16) & 0xFFu) == 0u && q >= ((wa >> 8) & 0xFFu)))) {
+      if (q < nops) {
         ST_OUT((KA->new_s.m_score + nmeta.m_off) + (q), sc);
         ST_OUT((KA->new_s.m_ts + nmeta.m_off) + (q), ts);
         ST_OUT((KA->new_s.m_dc + nmeta.m_off) + (q), (uint8_t)((kd >> 2) & 7u));
@@ -1043,7 +965,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       const uint32_t rix = rbase + mbcnt(rm);
       rbase += (uint32_t)__builtin_popcountll(rm);
       if (prow != NONE8) L.rl[rix] = (uint8_t)prow;
-      const int64_t id = (int64_t)L.htab[TRMV_DIAG_LDS == 1 ? (uint32_t)lane : (wb >> 24)];
+      const int64_t id = (int64_t)L.htab[wb >> 24];
       // gb_sets:largest of the slab: step 5 (a decided player: its last
       // segment, strictly rising Ts, so no two elements tie) or 5b (replayed)
       const uint32_t gb = (replayed || cnt > 1) ? ((wb >> 16) & 0xFFu) - off : 0u;
@@ -1056,7 +978,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
       }
       csum += cnt;
       nobs += (uint32_t)__builtin_popcountll(ballot(o != NONE8));
-      min_cand(!replayed && o != NONE8, L.esc[TRMV_DIAG_LDS == 1 ? (uint32_t)lane : (o != NONE8 ? o : (uint32_t)ESINK)], id, p);
+      min_cand(!replayed && o != NONE8, L.esc[o != NONE8 ? o : (uint32_t)ESINK], id, p);
     }
     (void)wave_excl_scan_dpp(csum, fbase);  // |Masked| of the key
     wave_lds_sync();
@@ -1195,11 +1117,8 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
-#ifndef TRMV_FRESH_WAVES
-#define TRMV_FRESH_WAVES 4  // waves per SIMD the FRESH instantiation is built for
-#endif
 template <bool FRESH>
-__global__ __launch_bounds__(64 * TRMV_W_WAVES, FRESH ? TRMV_FRESH_WAVES : 4) void trmv_wave_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];
@@ -1212,35 +1131,23 @@ __global__ __launch_bounds__(64 * TRMV_W_WAVES, FRESH ? TRMV_FRESH_WAVES : 4) vo
     wave_load_key(a, hdr, 0, cur);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the ops are in
     wave_load_rows(a, L, cur);
-    const bool ahead2 = TRMV_AHEAD2 && FRESH;
-    if (ahead2 && cn > 1) wave_load_key(a, hdr, 1, nxt);
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
-      const bool has_next = j + 1 < cn, has_next2 = j + 2 < cn;
-      KeyIn nxt2;
-      bool issued = false;
-      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt, has_next2, nxt2, issued);
+      const bool has_next = j + 1 < cn;
+      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&KA->status[0], 1u);
           KA->ovf_list[pos] = key;
         }
-        if (ahead2) {
-          if (!issued) {
-            if (has_next) wave_load_rows(a, L, nxt);
-            if (has_next2) wave_load_key(a, hdr, j + 2, nxt2);
-          }
-        } else {
-          if (has_next && !issued) wave_load_key(a, hdr, j + 1, nxt);
-          // retire these loads here, as the common path does before its
-          // stores: otherwise every key would wait on the previous key's stores
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-          if (has_next) wave_load_rows(a, L, nxt);
-        }
+        if (has_next) wave_load_key(a, hdr, j + 1, nxt);
+        // retire these loads here, as the common path does before its
+        // stores: otherwise every key would wait on the previous key's stores
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if (has_next) wave_load_rows(a, L, nxt);
       }
       wave_lds_sync();  // LDS is reused by the wave's next key
       cur = nxt;
-      if (ahead2) nxt = nxt2;
     }
   }
 }

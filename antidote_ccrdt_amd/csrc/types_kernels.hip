@@ -761,9 +761,6 @@ __device__ __forceinline__ void lb_iput(LbPar<ET>& P, uint32_t i, int64_t sc, in
 
 // Observed as a register table, entry r in lane r % 64 of slot r / 64,
 // ascending by (Score, Id); entries >= n hold (INT64_MAX, INT64_MAX).
-#ifndef LB_MBALLOT
-#define LB_MBALLOT 0  // merges of up to this many inserts ranked by ballots on the register table
-#endif
 struct LbObs {
   int64_t sc[2], id[2];
   uint32_t e[2];  // entry index
@@ -825,21 +822,10 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
       P.ik[2 * lane + 1] = INT64_MAX;
     }
   }
-  // table entries below each insert (deleted ones subtracted below): few
-  // inserts count them on the register table by a ballot pair each, many by
-  // a binary search of the staged table per lane
-  uint32_t lo_all = 0;
-  if (LB_MBALLOT && ni <= (uint32_t)LB_MBALLOT) {
-    for (uint64_t t = im; t; t &= t - 1) {
-      const int x = (int)__builtin_ctzll(t);
-      const int64_t xs = rl64(is, x), xi = rl64(iid, x);
-      const uint32_t r = (uint32_t)__builtin_popcountll(ballot((uint32_t)lane < o.n && lb_key_lt(o.sc[0], o.id[0], xs, xi))) +
-                         (uint32_t)__builtin_popcountll(ballot((uint32_t)(64 + lane) < o.n && lb_key_lt(o.sc[1], o.id[1], xs, xi)));
-      lo_all = lane == x ? r : lo_all;
-    }
-  } else {
-    lo_all = ins ? lb_rank(P, o.n, is, iid) : 0u;
-  }
+  // table entries below each insert (deleted ones subtracted below): a
+  // binary search of the staged table per lane (ballots on the register
+  // table for up to 8 / 16 inserts measured slower, A/B r04)
+  const uint32_t lo_all = ins ? lb_rank(P, o.n, is, iid) : 0u;
   LB_MSTAMP(8);
   bool d0 = false, d1 = false;
   uint32_t ld = 0;
@@ -2153,12 +2139,7 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   b.n_chunks = n_chunks;
   // (measured: a 512-word cache at 16 waves per CU beats 1024 words at 8)
   // (16 waves sharing 2048 / 1024 cached words: +1 ms)
-#ifndef WC_VTAB
-#define WC_VTAB 512
-#endif
-#ifndef WC_VW
-#define WC_VW 4
-#endif
+  constexpr int WC_VTAB = 512, WC_VW = 4;
   hipLaunchKernelGGL((wc_verify_kernel<WC_VTAB, WC_VW>), dim3((unsigned)((n_chunks + WC_VW - 1) / WC_VW)), dim3(64 * WC_VW), 0, st, b);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;

@@ -128,10 +128,7 @@ struct LbDownArgs {
 
 // wordcount / worddocumentcount
 constexpr uint64_t WC_TILE = 4096;  // bytes of a document per wave step (64 per lane)
-#ifndef WC_TPW_N
-#define WC_TPW_N 8
-#endif
-constexpr uint64_t WC_TPW = WC_TPW_N;     // tiles per wave (a chunk)
+constexpr uint64_t WC_TPW = 8;  // tiles per wave (a chunk; measured 8 / 16 / 32: 8 best)
 
 // A word-table slot: everything one probe or one compare needs lies in one
 // 32-byte record (one cache sector), not in five arrays.  The counts live in
