@@ -124,13 +124,19 @@ def raise_host_keys(mine, extra=None, coll=None) -> None:
     and when any rank has one, EVERY rank raises KeyCapacityError with the
     same sorted global ids in .keys and its step result in .extra.  Keys
     past the engine's per-key capacity are the host path's from then on
-    (INTEGRATION.md): the drivers leave their ops out of later batches."""
+    (INTEGRATION.md): the drivers leave their ops out of later batches.
+    The keys travel on the collective's device (RCCL takes device tensors
+    only)."""
     import torch
 
     from ._lib import EKEYCAP, KeyCapacityError
     mine = np.array(sorted(int(k) for k in mine), np.int64)
     if coll is not None and coll.world > 1:
-        parts = coll.all_gather_v(torch.from_numpy(mine))
+        t = torch.from_numpy(mine)
+        dev = getattr(coll, "device", None)
+        if dev is not None:
+            t = t.to(dev)
+        parts = coll.all_gather_v(t)
         allk = np.unique(np.concatenate([p.cpu().numpy() for p in parts])) if parts else mine
     else:
         allk = mine
@@ -139,6 +145,18 @@ def raise_host_keys(mine, extra=None, coll=None) -> None:
                                f"{allk.shape[0]} key(s) over the per-key capacity went to the host path")
         err.keys, err.extra = allk, extra
         raise err
+
+
+class PeerStepError(RuntimeError):
+    """A multi-rank step failed on some rank (an invalid op in its keys, a
+    device error): every rank finished the step's collectives and then
+    raises, so no rank is left blocked inside one.  .ranks lists the ranks
+    that failed; on a failed rank the local exception is chained
+    (__cause__)."""
+
+    def __init__(self, ranks):
+        super().__init__(f"multi-rank step failed on rank(s) {list(ranks)}")
+        self.ranks = list(ranks)
 
 
 def _dist():
@@ -171,27 +189,31 @@ def pack_extras(x: TrmvExtra, op_index: np.ndarray) -> np.ndarray:
     return rows
 
 
-def all_gather_rows(rows: np.ndarray) -> np.ndarray:
+def all_gather_rows(rows: np.ndarray, tag: int = 0):
     """All-gather variable-length int64 row blocks (sizes first, then one
-    padded all_gather), concatenated in rank order."""
+    padded all_gather), concatenated in rank order.  `tag`: a per-rank count
+    that rides the sizes' gather; returns (rows, sum of the tags)."""
     import torch
     dist = _dist()
     if dist is None:
-        return rows
+        return rows, int(tag)
     world = dist.get_world_size()
     dev = _device_for(dist)
     width = rows.shape[1]
-    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    n = torch.tensor([rows.shape[0], int(tag)], dtype=torch.int64, device=dev)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n)
-    counts = [int(c.item()) for c in ns]
+    hv = torch.stack(ns).cpu().numpy()
+    counts, tags = [int(c) for c in hv[:, 0]], int(hv[:, 1].sum())
     cap = max(max(counts), 1)
+    if not sum(counts):
+        return rows[:0], tags
     buf = torch.zeros((cap, width), dtype=torch.int64, device=dev)
     if rows.shape[0]:
         buf[: rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows)).to(dev)
     outs = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(outs, buf)
-    return np.concatenate([o[:c].cpu().numpy() for o, c in zip(outs, counts)], axis=0)
+    return np.concatenate([o[:c].cpu().numpy() for o, c in zip(outs, counts)], axis=0), tags
 
 
 def all_reduce_max(v: np.ndarray) -> np.ndarray:
@@ -204,28 +226,40 @@ def all_reduce_max(v: np.ndarray) -> np.ndarray:
     return t.cpu().numpy()
 
 
+def _engine_stream(engine):
+    """The HIP stream an engine queues its work on, as a torch stream."""
+    import torch
+
+    from . import _lib
+    return torch.cuda.ExternalStream(_lib.lib.ccrdt_engine_stream(engine.h), device=torch.device("cuda", engine.device))
+
+
 class TrmvShardExchange:
     """The two per-batch exchange steps of a key-sharded topk_rmv rank
     (topk_rmv.erl:236,294 for the extras, :378-386 for the Vc
     merge) -- the ONE implementation that bench.py --gpus N times and the
     tests check.
 
-    A rank's pack is one int64 buffer on its device, [count | Vc | rows]:
-    word 0 holds the extra-effect count (low 32 bits) and the rank's number
-    of host-path keys (high 32 bits), then the rank's elementwise-max Vc,
-    then the effect rows (global op, kind, id, score, dc, ts, vc[n_dc]).  A
-    step is one fixed-size all-gather of [head | first FAST rows] -- the Vc
-    max is taken from the gathered copies, so the Vc all-reduce rides the
-    same collective -- and, only when some rank has more than FAST effects,
-    a second (variable) gather of the rest.  `coll` is a TorchCollective
-    (RCCL on device tensors over xGMI; gloo staged through the host) or an
-    in-process stand-in; None means one rank.  The pack is filled from the
-    HIP engine on the device (fill_from_engine: extras packed by a kernel,
-    local op indices mapped to global ones by a gather on the device) or
-    from host rows (fill_from_rows: engines that only have a host apply,
-    e.g. the oracle the CPU tests inject)."""
+    A rank's pack is one int64 buffer on its device, [word | Vc | rows]: the
+    word holds the extra-effect count (bits 0-31), the rank's number of new
+    host-path keys (bits 32-61) and a failure flag (bit 62: the rank's apply
+    raised), then the rank's elementwise-max Vc, then the effect rows
+    (global op, kind, id, score, dc, ts, vc[n_dc]).  A step is one
+    fixed-size all-gather of [head | first FAST rows] -- the Vc max is taken
+    from the gathered copies, so the Vc all-reduce rides the same collective
+    -- and, only when some rank has more than FAST effects, a second
+    (variable) gather of the rest; the gathered words are read on the host
+    once (one sync per step).  `coll` is a TorchCollective (RCCL on device
+    tensors over xGMI; gloo staged through the host) or an in-process
+    stand-in; None means one rank.  The pack is filled from the HIP engine
+    on the device (fill_from_engine: extras packed by a kernel on the
+    engine's stream, ordered against torch's stream by events, local op
+    indices mapped to global ones by a gather on the device) or from host
+    rows (fill_from_rows: engines that only have a host apply, e.g. the
+    oracle the CPU tests inject, or a rank whose apply failed)."""
 
     FAST = 256
+    HOST_SHIFT, HOST_MASK, FAIL_BIT = 32, (1 << 30) - 1, 62
 
     def __init__(self, n_dc: int, coll=None, device=None, rows_cap: int = 1 << 20):
         import torch
@@ -241,30 +275,41 @@ class TrmvShardExchange:
     def _rows(self):
         return self.pack[self.head:].view(self.rows_cap, self.w)
 
+    def _word(self, n_host_keys: int, failed: bool) -> int:
+        return (min(int(n_host_keys), self.HOST_MASK) << self.HOST_SHIFT) | ((1 << self.FAIL_BIT) if failed else 0)
+
     def fill_from_engine(self, engine, op_index=None, n_host_keys: int = 0) -> None:
         """The engine's last batch: its extras (ccrdt_trmv_extras_device) and
-        its shard Vc (ccrdt_trmv_replica_vc_device), packed on the device.
-        op_index: device int64 tensor, local op index -> global (None: the
-        same)."""
+        its shard Vc (ccrdt_trmv_replica_vc_device), packed on the device
+        without a host wait: the engine's stream waits for torch's (the
+        previous step's gathers read the pack), torch's waits for the
+        engine's.  op_index: device int64 tensor, local op index -> global
+        (None: the same)."""
+        torch = self.torch
+        es = _engine_stream(engine)
+        ts = torch.cuda.current_stream(self.dev)
+        es.wait_stream(ts)
         p = self.pack.data_ptr()
         engine.extras_device(p + 8 * self.head, self.rows_cap, p)
         engine.replica_vc_device(p + 8)
-        engine.sync()
-        # (the count word's high half: host-path keys; the kernel wrote the low half)
-        self.pack[0] = (self.pack[0] & 0xFFFFFFFF) | (int(n_host_keys) << 32)
+        ts.wait_stream(es)
+        # (the word's upper bits: new host-path keys; the kernel wrote the count)
+        self.pack[0] = (self.pack[0] & 0xFFFFFFFF) | self._word(n_host_keys, False)
         self.op_map = op_index
         if op_index is not None and op_index.shape[0]:
             # rows past the count are stale; mapping them is harmless
             c0 = self._rows()[:self.FAST, 0]
             c0.copy_(op_index[c0.clamp(0, op_index.shape[0] - 1)])
 
-    def fill_from_rows(self, rows: np.ndarray, vc: np.ndarray, n_host_keys: int = 0) -> None:
-        """Host extras rows (global op index first) and the shard Vc."""
+    def fill_from_rows(self, rows: np.ndarray, vc: np.ndarray, n_host_keys: int = 0, failed: bool = False) -> None:
+        """Host extras rows (global op index first) and the shard Vc;
+        `failed`: this rank's apply raised (no rows; every rank raises
+        PeerStepError after run())."""
         m = int(rows.shape[0])
         if m > self.rows_cap:
             raise RuntimeError(f"trmv exchange: {m} extra effects > {self.rows_cap} rows")
         h = np.zeros(self.head + m * self.w, np.int64)
-        h[0] = m | (int(n_host_keys) << 32)
+        h[0] = m | self._word(n_host_keys, failed)
         h[1:self.head] = vc
         h[self.head:] = np.ascontiguousarray(rows, np.int64).reshape(-1)
         self.pack[:h.shape[0]] = self.torch.from_numpy(h).to(self.dev)
@@ -273,8 +318,9 @@ class TrmvShardExchange:
     def run(self):
         """The exchange: returns (every rank's extras as an int64 tensor
         [M, 6 + n_dc] in global stream order -- identical on every rank --,
-        the replica Vc (elementwise max over the ranks), total host-path
-        keys over the ranks)."""
+        the replica Vc (elementwise max over the ranks), total new host-path
+        keys over the ranks).  When some rank's apply failed, every rank
+        finishes the collectives and then raises PeerStepError."""
         torch = self.torch
         L = self.head + self.FAST * self.w
         mine = self.pack[:L]
@@ -283,11 +329,15 @@ class TrmvShardExchange:
         else:
             parts = [mine]
         allp = torch.stack([q.to(self.dev) for q in parts])
-        cnt = allp[:, 0] & 0xFFFFFFFF
-        host = allp[:, 0] >> 32
+        w0 = allp[:, 0]
+        cnt = w0 & 0xFFFFFFFF
+        host = (w0 >> self.HOST_SHIFT) & self.HOST_MASK
+        fail = (w0 >> self.FAIL_BIT) & 1
         vc = allp[:, 1:self.head].max(0).values
-        hv = torch.cat([cnt, host.sum().view(1), mine[:1] & 0xFFFFFFFF]).cpu().tolist()
-        counts, n_host, self.count = [int(c) for c in hv[:-2]], int(hv[-2]), int(hv[-1])
+        hv = torch.cat([cnt, fail, host.sum().view(1), mine[:1] & 0xFFFFFFFF]).cpu().tolist()
+        W = len(parts)
+        counts, failed = [int(c) for c in hv[:W]], [r for r in range(W) if hv[W + r]]
+        n_host, self.count = int(hv[2 * W]), int(hv[2 * W + 1])
         if max(counts) > self.rows_cap:
             raise RuntimeError(f"trmv exchange: {max(counts)} extra effects > {self.rows_cap} rows")
         heads = [allp[r, self.head:].view(self.FAST, self.w)[:min(c, self.FAST)] for r, c in enumerate(counts)]
@@ -302,6 +352,8 @@ class TrmvShardExchange:
             parts_rows = [torch.cat([h, t]) for h, t in zip(heads, tails)]
         else:
             parts_rows = heads
+        if failed:
+            raise PeerStepError(failed)
         rows = torch.cat(parts_rows) if parts_rows else self._rows()[:0]
         if rows.shape[0]:
             rows = rows[torch.argsort(rows[:, 0], stable=True)]
@@ -331,6 +383,8 @@ class ShardedTopkRmv:
                 return TopkRmvEngine(nk, kk, d, device=device)
         self.engine = engine_factory(len(self.keys), k, n_dc)
         self.host_keys: set[int] = set()   # global ids
+        self.reported: set[int] = set()    # host keys already raised
+        self._vc = None
         if coll is None and dist is not None and self.world > 1:
             coll = TorchCollective(dist)
         self.coll = coll
@@ -352,6 +406,7 @@ class ShardedTopkRmv:
         """update/2 over this rank's keys of a global batch on the engine's
         host entry; returns the rank's extra effects as packed rows (global
         op index first).  Over-capacity keys join host_keys."""
+        self._vc = None
         sh = self.route(batch)
         x = _apply_keycap(self.engine, sh.batch, self.host_keys, self.keys)
         if isinstance(x, dict):
@@ -364,6 +419,7 @@ class ShardedTopkRmv:
         pack on the device.  op_index: device int64 tensor, local op -> global
         op.  Returns the number of keys handed to the host path."""
         from ._lib import KeyCapacityError
+        self._vc = None
         n_new = 0
         try:
             self.engine.apply_device(db)
@@ -382,26 +438,44 @@ class ShardedTopkRmv:
     def step(self, batch: TrmvBatch):
         """One batch: apply this rank's keys, then the exchange.  Returns
         (every rank's extras as int64 rows in global stream order, the
-        replica Vc), numpy, identical on every rank."""
-        sh = self.route(batch)
-        n0 = len(self.host_keys)
-        if self.on_device:
-            import torch
+        replica Vc), numpy, identical on every rank.  A rank whose apply
+        raises (an invalid op among its keys, a device error) still takes
+        part in the exchange with a failure flag, and then every rank raises
+        PeerStepError (the failed rank's own exception chained), so no rank
+        blocks in a collective the failed one never joins."""
+        self._vc = None
+        local_err = None
+        try:
+            sh = self.route(batch)
+            if self.on_device:
+                import torch
 
-            from .engine import DeviceTrmvBatch
-            db = DeviceTrmvBatch(sh.batch)
-            try:
-                self.apply_device(db, torch.from_numpy(sh.op_index).to(self.xchg.dev))
-            finally:
-                db.close()
-        else:
-            rows = pack_extras(TrmvExtra(**_as_dict(_apply_keycap(self.engine, sh.batch, self.host_keys,
-                                                                  self.keys))), sh.op_index)
-            self.xchg.fill_from_rows(rows, self._local_vc(), len(self.host_keys) - n0)
-        rows, vc, n_host = self.xchg.run()
+                from .engine import DeviceTrmvBatch
+                db = DeviceTrmvBatch(sh.batch)
+                try:
+                    self.apply_device(db, torch.from_numpy(sh.op_index).to(self.xchg.dev))
+                finally:
+                    db.close()
+            else:
+                rows = pack_extras(TrmvExtra(**_as_dict(_apply_keycap(self.engine, sh.batch, self.host_keys,
+                                                                      self.keys))), sh.op_index)
+                self.xchg.fill_from_rows(rows, self._local_vc(), len(self.host_keys - self.reported))
+        except Exception as e:  # noqa: BLE001 - re-raised on every rank after the exchange
+            local_err = e
+            self.xchg.fill_from_rows(np.zeros((0, self.xchg.w), np.int64), np.zeros(self.n_dc, np.int64),
+                                     failed=True)
+        try:
+            rows, vc, n_host = self.xchg.run()
+        except PeerStepError as pe:
+            if local_err is not None:
+                raise pe from local_err
+            raise
         out = (rows.cpu().numpy(), vc.cpu().numpy())
+        self._vc = out[1]
         if n_host:  # (the same on every rank: the sum over the gathered headers)
-            raise_host_keys(self.host_keys, out, self.coll)
+            new = self.host_keys - self.reported
+            self.reported |= new
+            raise_host_keys(new, out, self.coll)
         return out
 
     def exchange_extras(self, rows: np.ndarray) -> np.ndarray:
@@ -414,7 +488,7 @@ class ShardedTopkRmv:
 
     def replica_vc(self) -> np.ndarray:
         """Elementwise max of every key's Vc over the whole keyspace (from the
-        last exchange when there was one)."""
+        last exchange when no apply has run since; collective otherwise)."""
         v = getattr(self, "_vc", None)
         if v is not None:
             return v
@@ -566,12 +640,19 @@ class _Replica:
         on every rank once the step has quiesced (raise_host_keys)."""
         out = self.originate(batch)
         for rounds in range(max_rounds):
-            allr = all_gather_rows(out)
+            allr, n_new = all_gather_rows(out, self.new_host_keys())
             if not allr.shape[0]:
-                self.check_host_keys(rounds)
+                if n_new:  # (the same on every rank: the gathered sum)
+                    self.check_host_keys(rounds)
                 return rounds
             out = self.deliver(allr)
         raise RuntimeError("replication did not quiesce")
+
+    def new_host_keys(self) -> int:
+        """Keys this replica's codec handed to the host path and has not yet
+        reported."""
+        hk = getattr(self.codec, "host_keys", None)
+        return len(hk - self.codec.reported) if hk is not None else 0
 
     def check_host_keys(self, result=None, local: bool = False) -> None:
         """Collective (unless `local`: replicas held by one process): raise on
@@ -778,6 +859,8 @@ class TorchCollective:
             raise RuntimeError("TorchCollective needs an initialised process group")
         self.rank, self.world = self.dist.get_rank(), self.dist.get_world_size()
         self.staged = self.dist.get_backend() != "nccl"
+        # where the tensors it is handed must live (RCCL: the current GPU)
+        self.device = None if self.staged else _device_for(self.dist)
 
     def _wire(self, t):
         return t.cpu() if self.staged else t

@@ -6,13 +6,14 @@ every effect of the batch, src/antidote_ccrdt_topk_rmv.erl:140-148) over one
 batch of synthetic input: 100M effect ops (90% add / 10% rmv, 8-DC vector
 clocks) CSR-grouped over 2^20 keys (BASELINE configs[2]), applied to fresh
 keys (new(100)), with the ops already resident in HBM.  Keys are independent
-CRDT objects, so N ranks hash-shard a keyspace of N x 2^20 keys: every rank
-applies its own 2^20 keys' 100M-op batch (per-GPU work fixed: weak scaling,
-no data-path collective) and a step adds the batch's two exchange steps
-(extras all-gather, replica-Vc max, one collective: cluster.TrmvShardExchange,
-the code path the tests check).  --strong instead hash-shards ONE global
-2^20-key stream over the ranks, owner(key) = splitmix64(key) mod N (every
-rank generates it and keeps its keys' ops in stream order): total work fixed.
+CRDT objects, so N ranks hash-shard that ONE global 2^20-key, 100M-op stream,
+owner(key) = splitmix64(key) mod N (every rank generates it and keeps its
+keys' ops in stream order): total work fixed (strong scaling, the BASELINE
+config at every N), no data-path collective; a step adds the batch's two
+exchange steps (extras all-gather, replica-Vc max, one collective:
+cluster.TrmvShardExchange, the code path the tests check).  --weak instead
+gives every rank its own 2^20 keys and 100M ops (per-GPU work fixed); at N > 1
+the line's detail carries a short weak leg too.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -49,9 +50,12 @@ def parse():
     ap.add_argument("--cpu-steady-keys", type=int, default=1 << 16,
                     help="keys of every steady batch the steady-state CPU baseline replays (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "trmv_pmc.json"))
-    ap.add_argument("--strong", action="store_true",
-                    help="N > 1: the ranks shard ONE global 2^20-key stream (strong scaling) instead "
-                         "of each applying its own 2^20 keys (weak scaling, the default)")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: every rank applies its own 2^20 keys' stream (weak scaling) instead of "
+                         "the ranks sharding ONE global 2^20-key stream (strong scaling, the default)")
+    ap.add_argument("--strong", action="store_true", help="(the default; kept for old command lines)")
+    ap.add_argument("--weak-leg-steps", type=int, default=5,
+                    help="N > 1, strong: steps of the weak-scaling detail leg (0 = skip)")
     ap.add_argument("--dist-backend", default=None,
                     help="N > 1: nccl (RCCL, default on GPUs) or gloo (host-staged; tests)")
     return ap.parse_args()
@@ -123,7 +127,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    sharded = world > 1 and args.strong
+    sharded = world > 1 and not args.weak
     seed = 0xCC0DE + 2 + (0 if sharded else 1_000_003 * rank)
     t_gen = time.perf_counter()
     b = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6, rmv_pm=100,
@@ -149,24 +153,30 @@ def main():
     eng = shard.engine if shard is not None else TopkRmvEngine(n_local_keys, args.k, args.n_dc, device=device)
     xres = {}
 
+    xms = []
+
     def step():
         eng.reset()              # every key back to new(K): O(1), no traffic
         if shard is None:
             eng.apply_device(db)  # scan -> apply kernel(s) -> status
         else:                    # the apply, then the batch's two exchange steps
             shard.apply_device(db, op_index)
+            tx = time.perf_counter()
             rows, vc, _ = shard.xchg.run()
+            xms.append((time.perf_counter() - tx) * 1e3)
             xres.update(rows=rows, vc=vc)
 
     for _ in range(args.warmup):
         step()
     eng.sync()
     barrier()
+    xms.clear()
     t0 = time.perf_counter()
-    kms = []
+    kms, t0s = [], []
     for _ in range(args.steps):
         step()
         kms.append(eng.last_kernel_ms())
+        t0s.append(eng.tier_ms(0))
     eng.sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -200,7 +210,7 @@ def main():
     tier0[handed] = False
     alg_bytes = int(key_bytes.sum()) + 32 * n_extra          # whole batch
     alg_bytes_t0 = int(key_bytes[tier0].sum()) + 32 * n_extra  # extras: 46 per 100M ops, all counted here
-    t0_ms = eng.tier_ms(0)
+    t0_ms = sum(t0s) / len(t0s)  # tier 0's HIP-event interval, mean over the timed steps
     kernel_ms = t0_ms
     achieved = alg_bytes_t0 / (t0_ms * 1e-3) / 1e9
     traffic = steady_traffic = None
@@ -375,6 +385,44 @@ def main():
                 "gpu_kernel_over_cpu": {k: kern_rate / v["value"] for k, v in res.items()}}
             del cpu_samples
 
+    # Weak-scaling leg (detail only, N > 1 with the strong default): every
+    # rank its own 2^20 keys and 100M-op stream, the same apply + exchange.
+    weak = None
+    if sharded and args.weak_leg_steps > 0:
+        db.close()
+        bw = gen_trmv(args.n_ops, args.n_keys, args.n_dc, n_players=256, score_max=10**6, rmv_pm=100,
+                      lag_max=64, seed=0xCC0DE + 2 + 1_000_003 * rank)
+        wsh = ShardedTopkRmv(args.n_keys, args.k, args.n_dc, rank=0, world=1, device=device, coll=coll)
+        dbw = DeviceTrmvBatch(bw)
+        del bw
+
+        def wstep():
+            wsh.engine.reset()
+            wsh.apply_device(dbw, None)
+            wsh.xchg.run()
+        for _ in range(max(1, args.warmup)):
+            wstep()
+        wsh.engine.sync()
+        barrier()
+        tw = time.perf_counter()
+        for _ in range(args.weak_leg_steps):
+            wstep()
+        wsh.engine.sync()
+        barrier()
+        dtw = time.perf_counter() - tw
+        t = torch.tensor([dtw], dtype=torch.float64,
+                         device=torch.device("cuda", device) if backend == "nccl" else None)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dtw = float(t.item())
+        weak = {"what": "every rank its own 2^20 keys and 100M-op stream (seed 0xCC0DE+2+1000003*rank), "
+                        "the same apply + exchange; value = all ranks' ops / max-over-ranks wall time",
+                "value": world * args.n_ops * args.weak_leg_steps / dtw, "unit": "ops/s",
+                "ms_per_step": dtw * 1e3 / args.weak_leg_steps, "steps": args.weak_leg_steps,
+                "n_keys_total": world * args.n_keys, "n_ops_total": world * args.n_ops}
+        dbw.close()
+        wsh.engine.close()
+        del wsh
+
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_sample_keys > 0:  # reported at N=1 only
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -447,6 +495,9 @@ def main():
                 "algorithmic_bytes_per_launch": alg_bytes_t0,
                 "kernel_ms": kernel_ms,
                 "keys_per_launch": int(tier0.sum()),
+                "kernel_ms_steps": [round(x, 4) for x in t0s],
+                "timing": "HIP events recorded on the engine stream around the tier-0 launch, mean over "
+                          "the timed steps",
             },
             "cpu_baseline": cpu,
             "detail": {
@@ -460,8 +511,10 @@ def main():
                 "keys_handed_on_by_tier": overflow,
                 "kernel_ms_by_tier": tier_ms,
                 "gen_s": round(t_gen, 2),
+                "weak_scaling": weak,
                 "exchange": (None if shard is None else
                              {"backend": backend, "extras_all_gathered": int(xres["rows"].shape[0]),
+                              "ms_per_step": sum(xms) / max(1, len(xms)),
                               "replica_vc": [int(v) for v in xres["vc"].cpu().tolist()],
                               "in_step": "cluster.TrmvShardExchange.run: one all_gather of [count | Vc | "
                                          "first 256 effect rows] (Vc max taken from the gathered copies; a "

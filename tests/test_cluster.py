@@ -327,3 +327,99 @@ def test_replicated_keycap_raises_after_quiescence():
     assert len(ei.value.keys) > 0
     b2 = [gen_trmv(200, NK, D, n_players=12, score_max=50, seed=0xE0 + r, clock0=10 ** 6) for r in range(W)]
     replicate_local(reps, b2)
+
+
+# ------------------------------------- failure and device-placement protocol
+class _DeviceOnlyColl:
+    """An RCCL-shaped collective stub: it refuses tensors that are not on its
+    device (RCCL takes device tensors only) and returns fixed parts."""
+    world = 2
+    staged = False
+
+    def __init__(self, parts):
+        import torch
+        self.device = torch.device("meta")
+        self.parts = parts
+
+    def all_gather_v(self, t):
+        import torch
+        assert t.device == self.device, f"collective handed a {t.device} tensor"
+        return [torch.tensor(p, dtype=torch.int64) for p in self.parts]
+
+
+def test_raise_host_keys_uses_collective_device():
+    """raise_host_keys hands the collective a tensor on the collective's
+    device (a CPU tensor into RCCL failed every replicated step)."""
+    from antidote_ccrdt_amd.cluster import raise_host_keys
+    with pytest.raises(_lib.KeyCapacityError) as ei:
+        raise_host_keys({5, 1}, "x", _DeviceOnlyColl([[1, 5], [3]]))
+    assert list(ei.value.keys) == [1, 3, 5] and ei.value.extra == "x"
+    raise_host_keys(set(), None, _DeviceOnlyColl([[], []]))  # nobody has one: no raise
+
+
+def _fail_worker(rank, world, port, errf):
+    """Rank 1's apply fails: rank 0 must not block in the exchange; every rank
+    raises PeerStepError naming rank 1, rank 1 with its own error chained;
+    the next step works on every rank."""
+    import torch.distributed as dist
+
+    from antidote_ccrdt_amd.cluster import PeerStepError
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = _batch()
+        fail = {"on": True}
+
+        def factory(nk, kk, d):
+            o = orc.TrmvOracle(nk, kk, d)
+            if rank != 1:
+                return o
+
+            class _E:
+                def apply(self, bb, want_extra=True):
+                    if fail["on"]:
+                        raise _lib.CcrdtError(_lib.EINVAL, "trmv_apply", "invalid op in batch")
+                    return o.apply(bb, 1, want_extra=True)
+
+                def export(self):
+                    return o.export()
+            return _E()
+        s = ShardedTopkRmv(N_KEYS, K, D, engine_factory=factory)
+        try:
+            s.step(b)
+            raise AssertionError("no PeerStepError")
+        except PeerStepError as pe:
+            assert pe.ranks == [1], pe.ranks
+            assert (pe.__cause__ is not None) == (rank == 1)
+        fail["on"] = False
+        b2 = gen_trmv(N_OPS // 4, N_KEYS, D, n_players=12, score_max=50, rmv_pm=150, lag_max=16,
+                      seed=0xC3, clock0=10 ** 7)
+        rows, vc = s.step(b2)
+        assert np.array_equal(s.replica_vc(), vc)
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_sharded_step_failure_gloo(tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_fail_worker, args=(2, _free_port(), errf), nprocs=2, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+def test_replica_vc_not_stale_after_apply():
+    """replica_vc() after an apply reflects that apply, not the Vc an earlier
+    exchange cached."""
+    b = _batch()
+    s = ShardedTopkRmv(N_KEYS, K, D, rank=0, world=1, engine_factory=lambda nk, kk, d: orc.TrmvOracle(nk, kk, d))
+    s.exchange_extras(s.apply(b))
+    v1 = s.replica_vc().copy()
+    b2 = gen_trmv(N_OPS // 4, N_KEYS, D, n_players=12, score_max=50, rmv_pm=150, lag_max=16,
+                  seed=0xC4, clock0=10 ** 7)
+    s.apply(b2)
+    v2 = s.replica_vc()
+    assert (v2 > v1).any() and np.array_equal(v2, s.export()["vc"].max(axis=0))

@@ -92,3 +92,46 @@ def test_one_key_grows_past_5000_masked(gpu):
         assert not bad, f"batch {i}: fields differ from the oracle: {bad}"
     m = np.diff(eng.export().m_ptr.astype(np.int64))
     assert m.max() > 5000
+
+
+def _progress(msg):
+    """A progress line under gpurun_out/ (a long GPU test is otherwise silent
+    while pytest captures its output)."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root:
+        os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(root, "gpurun_out", "steady_bench_size.progress"), "a") as f:
+            f.write(msg + "\n")
+
+
+@pytest.mark.timeout(900)
+def test_steady_state_bench_size(gpu):
+    """bench.py's steady-state leg at its own size: 2^20 resident keys, the
+    bench batch (100M ops, seed 0xCC0DE+2) and then steady batches 2..4 of the
+    same stream (seeds and clocks as bench.py's detail.steady_state), each
+    through the device entry point (apply_device) and compared with the
+    threaded oracle after every batch: every key's state and every extra
+    effect, bit-exact (src/antidote_ccrdt_topk_rmv.erl:231-334).  The
+    resident buffers must grow: after the fresh batch they hold that batch's
+    100M-element bound, and the first steady batch needs old state + 100M."""
+    n_ops, nk, D, K = 100_000_000, 1 << 20, 8, 100
+    seed = 0xCC0DE + 2
+    eng = TopkRmvEngine(nk, K, D)
+    o = orc.TrmvOracle(nk, K, D)
+    for i in range(4):
+        b = gen_trmv(n_ops, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64,
+                     seed=seed + (7919 * i if i else 0), clock0=i * n_ops)
+        db = DeviceTrmvBatch(b)
+        eng.apply_device(db)
+        db.close()
+        xe = _fetch_extra(eng, n_ops, D)
+        xo = o.apply(b, THREADS, want_extra=True)
+        del b
+        se = eng.export()
+        bad = orc.trmv_mismatches(se, xe, o.export(), xo)
+        sizes = eng.sizes()
+        _progress(f"batch {i + 1}: tiers {[eng.tier_ms(t) for t in range(5)]} state {sizes} bad {bad}")
+        assert not bad, f"batch {i + 1}: fields differ from the oracle: {bad}"
+        del se, xe, xo
+    nobs = np.diff(eng.export().obs_ptr.astype(np.int64))
+    assert (nobs == K).mean() > 0.99 and sizes[1] > 2 * n_ops  # Observed full, Masked past 2x a batch
