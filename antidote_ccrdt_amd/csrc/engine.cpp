@@ -27,6 +27,9 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, uint32_t* key_rmv, hipStream_t st);
+int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, hipStream_t st);
+int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
+                          hipStream_t st);
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
@@ -59,10 +62,11 @@ static constexpr uint32_t TRMV_LATER_GRID = 4096;  // keys the grids of the late
 
 using namespace ccrdt;
 
-TrmvSide ccrdt_engine::trmv_side(int s) const {
-  const TrmvBufs& b = trmv[s];
+TrmvSide ccrdt_engine::trmv_side(int ms, int ds) const {
+  const TrmvBufs& b = trmv[ds];
   TrmvSide t;
-  t.meta = b.meta.as<KeyMeta>();
+  t.meta = trmv[ms].meta.as<KeyMeta>();
+  t.cap = trmv[ms].cap.as<KeyCap>();
   t.pl_id = b.pl_id.as<int64_t>();
   t.pl_info = b.pl_info.as<uint32_t>();
   t.m_score = b.m_score.as<int64_t>();
@@ -78,6 +82,7 @@ TrmvSide ccrdt_engine::trmv_side(int s) const {
 void ccrdt_engine::release_all() {
   for (auto& b : trmv) {
     b.meta.release();
+    b.cap.release();
     b.pl_id.release();
     b.pl_info.release();
     b.m_score.release();
@@ -91,7 +96,8 @@ void ccrdt_engine::release_all() {
   for (DevBuf& d : tier_ovf) d.release();
   for (DevBuf& d : st_n32) d.release();
   for (DevBuf& d : st_nbase) d.release();
-  for (DevBuf* d : {&partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl, &hbm_scratch, &st_kp,
+  for (DevBuf* d : {&arena, &obs_ord, &key_done, &partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl,
+                    &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
   release_types();
@@ -213,6 +219,7 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
 int ccrdt_engine_reset(ccrdt_engine* e) {
   if (!e) return CCRDT_EINVAL;
   e->fresh = true;
+  e->inplace_ready = false;
   return e->reset_type();
 }
 
@@ -275,63 +282,95 @@ static int check_trmv(ccrdt_engine* e) {
   return CCRDT_OK;
 }
 
-int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
-  CCRDT_TRY(check_trmv(e));
-  if (!ops || !ops->key_ptr || (ops->n_ops > 0 && (!ops->kind || !ops->id || !ops->score ||
-                                                   !ops->dc || !ops->ts))) {
-    set_error("trmv_apply: null op array");
-    return CCRDT_EINVAL;
-  }
-  if (ops->n_ops >= (int64_t)0xFFFFFFFFll) {
-    set_error("trmv_apply: batch too large (n_ops must fit in 32 bits)");
-    return CCRDT_EINVAL;
-  }
-  Engine& E = *e;
+namespace {
+
+// The error bits the kernels OR-ed into a status word -> the C-ABI code.
+int trmv_err_code(uint32_t err) {
+  std::string m = "trmv_apply: invalid op in batch:";
+  if (err & TRMV_ERR_KIND) m += " kind>3";
+  if (err & TRMV_ERR_DC) m += " dc>=n_dc";
+  if (err & TRMV_ERR_TS) m += " add ts<1";
+  if (err & TRMV_ERR_ROW) m += " rmv row out of range";
+  if (err & TRMV_ERR_VC) m += " negative VcRmv entry";
+  set_error(m);
+  return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW)) ? CCRDT_ERANGE
+                                                                                                  : CCRDT_EINVAL;
+}
+
+// Capacities (elements) of a data side's arrays.
+void trmv_side_caps(const Engine& E, int ds, uint64_t cap[3]) {
+  const TrmvBufs& b = E.trmv[ds];
+  cap[0] = std::min(b.pl_id.bytes / 8, std::min(b.pl_info.bytes / 4, std::min(b.pl_slab.bytes / 4, b.pl_gb.bytes / 2)));
+  cap[1] = std::min(b.m_score.bytes / 8, std::min(b.m_ts.bytes / 8, b.m_dc.bytes));
+  cap[2] = E.n_dc ? b.r_vc.bytes / (8 * (uint64_t)E.n_dc) : 0;
+}
+
+// In place (tier R alone): the batch validated, then every key updated in
+// the data arrays it lives in (meta / cap ping-pong).  Keys that cannot be
+// updated in place (outside tier R's class, or the arena is full) are left
+// as they were and listed in tier_ovf[3]; *handed = their number.
+int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status, uint32_t& handed) {
+  const uint64_t nk = (uint64_t)E.n_keys;
+  const int D = E.n_dc;
+  CCRDT_TRY(E.trmv[1 - E.mcur].meta.ensure(nk * sizeof(KeyMeta)));
+  CCRDT_TRY(E.trmv[1 - E.mcur].cap.ensure(nk * sizeof(KeyCap)));
+  a.inplace = 1;
+  a.old_s = E.trmv_side(E.mcur, E.cur);
+  a.new_s = E.trmv_side(1 - E.mcur, E.cur);
+  a.arena = E.arena.as<unsigned long long>();
+  for (int x = 0; x < 3; ++x) a.arena_cap[x] = E.arena_cap[x];
+  a.key_done = nullptr;
+  a.key_list = nullptr;
+  a.n_list = (uint32_t)nk;
+  a.n_list_dev = nullptr;
+  a.ovf_list = E.tier_ovf[3].as<uint32_t>();
+  a.status = status + 2 + 2 * 3;
+  a.verr = status + 2 + 2 * 3 + 1;  // (tier R's error word: the validation writes it)
+  CCRDT_HIP(hipEventRecord(E.evt[0], E.stream));
+  CCRDT_TRY(trmv_launch_validate(a, n_ops, status + 2 + 2 * 3 + 1, E.stream));
+  CCRDT_HIP(hipEventRecord(E.evt[1], E.stream));
+  CCRDT_TRY(trmv_launch_resident(a, nk, E.stream));
+  CCRDT_HIP(hipEventRecord(E.evt[2], E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+  CCRDT_HIP(hipStreamSynchronize(E.stream));
+  const uint32_t* hs = (const uint32_t*)E.h_status;
+  if (hs[3 + 2 * 3]) return trmv_err_code(hs[3 + 2 * 3]);
+  float mv = 0.f, mr = 0.f;
+  CCRDT_HIP(hipEventElapsedTime(&mv, E.evt[0], E.evt[1]));
+  CCRDT_HIP(hipEventElapsedTime(&mr, E.evt[1], E.evt[2]));
+  E.trmv_tier_ms[5] += mv;  // (the validation pass)
+  E.trmv_tier_ms[3] += mr;
+  handed = hs[2 + 2 * 3];
+  E.trmv_overflow_keys[5] = handed;  // (keys the in-place pass left to the full rewrite)
+  (void)D;
+  return CCRDT_OK;
+}
+
+// A full rewrite: the capacity scan lays every key out in the other data
+// arrays (with room for in-place growth when tier R can take the keys), then
+// the tier chain.  With a.key_done the keys an in-place pass completed are
+// only copied (no ops).
+int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status, int& first_tier, int& n_over) {
   const int D = E.n_dc;
   const uint64_t nk = (uint64_t)E.n_keys;
-  const int out = 1 - E.cur;
-  const uint64_t n_ops = (uint64_t)ops->n_ops;
-  TrmvApplyArgs a{};
-  a.n_keys = E.n_keys;
-  a.n_dc = D;
-  a.k = (uint32_t)std::min<int64_t>(E.k, 0xFFFFFFFFll);
-  a.key_ptr = ops->key_ptr;
-  a.kind = ops->kind;
-  a.id = ops->id;
-  a.score = ops->score;
-  a.dc = ops->dc;
-  a.ts = ops->ts;
-  a.rmv_vc = ops->rmv_vc;
-  a.n_rmv_rows = ops->rmv_vc ? ops->n_rmv_rows : 0;
+  const int out = 1 - E.cur, mout = 1 - E.mcur;
+  a.inplace = 0;
   a.fresh = E.fresh ? 1 : 0;
-  a.old_s = E.trmv_side(E.cur);
-  CCRDT_TRY(E.trmv[out].meta.ensure(nk * sizeof(KeyMeta)));
-  a.new_s = E.trmv_side(out);
+  a.slack = (!E.fresh && E.k <= 128) ? 1 : 0;
+  a.old_s = E.trmv_side(E.mcur, E.cur);
+  CCRDT_TRY(E.trmv[mout].meta.ensure(nk * sizeof(KeyMeta)));
+  CCRDT_TRY(E.trmv[mout].cap.ensure(nk * sizeof(KeyCap)));
+  a.new_s = E.trmv_side(mout, out);
   const uint64_t nb = (nk + 1023) / 1024;
   // partials: per-tile sums and totals, then each key's rmv-op count (u32)
   CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t) + nk * sizeof(uint32_t)));
-  // status words: [0..1] scan, [2+2t, 3+2t] tier t (overflow count, errors)
-  CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4));
-  uint32_t* status = E.status.as<uint32_t>();
-  CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
-  a.status = status;
   // 1) capacities -> segment offsets of the new state (a fresh batch's
   //    offsets are the keys' op offsets: trmv_new_meta, no scan)
-  if (!E.fresh)
+  uint64_t tot[3] = {n_ops, n_ops, n_ops};
+  if (!E.fresh && nk) {
     CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(),
                                reinterpret_cast<uint32_t*>(E.partials.as<uint64_t>() + nb * 3 + 3), E.stream));
-  // Sizes of the new side.  Its totals are sum(old counts + ops per key) <=
-  // (old side's totals) + n_ops, known on the host without waiting for the
-  // scan; only when that bound outgrows the buffers does the host read the
-  // exact totals (one stream sync) and grow them.
-  uint64_t tot[3];
-  for (int x = 0; x < 3; ++x) tot[x] = (E.fresh ? 0 : E.trmv_tot[E.cur][x]) + n_ops;
-  TrmvBufs& ob = E.trmv[out];
-  auto fits = [&](const TrmvBufs& b) {
-    return b.pl_id.bytes >= tot[0] * 8 && b.m_score.bytes >= tot[1] * 8 &&
-           b.r_vc.bytes >= tot[2] * 8 * D && b.vc.bytes >= nk * 8 * D;
-  };
-  if (nk && !E.fresh && !fits(ob)) {  // (fresh: tot is exact)
+    // (the exact totals size the new side)
     CCRDT_HIP(hipMemcpyAsync(E.h_status, E.partials.as<uint64_t>() + nb * 3, 3 * sizeof(uint64_t),
                              hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
@@ -341,34 +380,27 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     set_error("trmv_apply: resident state would exceed 2^32 elements");
     return CCRDT_ENOMEM;
   }
-  auto grow = [&](TrmvBufs& b) -> int {
-    CCRDT_TRY(b.meta.ensure(nk * sizeof(KeyMeta)));
-    CCRDT_TRY(b.pl_id.ensure_grow(tot[0] * 8));
-    CCRDT_TRY(b.pl_info.ensure_grow(tot[0] * 4));
-    CCRDT_TRY(b.pl_slab.ensure_grow(tot[0] * 4));
-    CCRDT_TRY(b.pl_gb.ensure_grow(tot[0] * 2));
-    CCRDT_TRY(b.m_score.ensure_grow(tot[1] * 8));
-    CCRDT_TRY(b.m_ts.ensure_grow(tot[1] * 8));
-    CCRDT_TRY(b.m_dc.ensure_grow(tot[1]));
-    CCRDT_TRY(b.r_vc.ensure_grow(tot[2] * 8 * D));
+  // Sizes of the new side: the totals, and with room to grow in place a
+  // quarter more for the keys later batches relocate (the arena)
+  auto grow = [&](TrmvBufs& b, bool room) -> int {
+    uint64_t t[3];
+    for (int x = 0; x < 3; ++x) t[x] = room ? tot[x] + tot[x] / 4 : tot[x];
+    CCRDT_TRY(b.pl_id.ensure_grow(t[0] * 8));
+    CCRDT_TRY(b.pl_info.ensure_grow(t[0] * 4));
+    CCRDT_TRY(b.pl_slab.ensure_grow(t[0] * 4));
+    CCRDT_TRY(b.pl_gb.ensure_grow(t[0] * 2));
+    CCRDT_TRY(b.m_score.ensure_grow(t[1] * 8));
+    CCRDT_TRY(b.m_ts.ensure_grow(t[1] * 8));
+    CCRDT_TRY(b.m_dc.ensure_grow(t[1]));
+    CCRDT_TRY(b.r_vc.ensure_grow(t[2] * 8 * D));
     CCRDT_TRY(b.vc.ensure(nk * 8 * D));
     return CCRDT_OK;
   };
-  CCRDT_TRY(grow(ob));
+  CCRDT_TRY(grow(E.trmv[out], a.slack != 0));
   // The current side holds nothing live after reset(): size it too, so the
   // next batch (which writes it) does not allocate.
-  if (E.fresh) CCRDT_TRY(grow(E.trmv[E.cur]));
-  a.new_s = E.trmv_side(out);
-  CCRDT_TRY(E.ex_cnt.ensure(nk * 4));
-  CCRDT_TRY(E.ex.ensure(n_ops * sizeof(TrmvExtraRec)));
-  CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
-  CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
-  for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
-  if (!E.fresh || E.k <= 128) CCRDT_TRY(E.op_pl.ensure(n_ops + 1));  // tier R's per-op scratch
-  a.op_pl = E.op_pl.as<uint8_t>();
-  a.ex_cnt = E.ex_cnt.as<uint32_t>();
-  a.ex = E.ex.as<TrmvExtraRec>();
-  a.ex_vc = E.ex_vc.as<int64_t>();
+  if (E.fresh) CCRDT_TRY(grow(E.trmv[E.cur], false));
+  a.new_s = E.trmv_side(mout, out);
   // 2) the chain: its first tier over every key, then each later tier over
   //    the keys the one before handed on.  Every later tier reads its list
   //    length from the device, so the whole chain is queued without a host
@@ -392,7 +424,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     chain[n_chain++] = 2;
     if (first == 1) n_chain = 2, chain[1] = 2;
   }
-  const int first_tier = chain[0];
+  first_tier = chain[0];
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
   DevBuf* work = nullptr;
   const uint32_t* n_dev = nullptr;
@@ -414,32 +446,17 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     work = ovf;
     n_dev = a.status;
   }
-  CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost,
-                           E.stream));
+  CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
   uint32_t err = 0;
   for (int ci = 0; ci < n_chain; ++ci) err |= hs[3 + 2 * chain[ci]];
-  if (err) {
-    std::string m = "trmv_apply: invalid op in batch:";
-    if (err & TRMV_ERR_KIND) m += " kind>3";
-    if (err & TRMV_ERR_DC) m += " dc>=n_dc";
-    if (err & TRMV_ERR_TS) m += " add ts<1";
-    if (err & TRMV_ERR_ROW) m += " rmv row out of range";
-    if (err & TRMV_ERR_VC) m += " negative VcRmv entry";
-    set_error(m);
-    return (err & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(err & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
-               ? CCRDT_ERANGE
-               : CCRDT_EINVAL;
-  }
-  E.trmv_overflow_keys.clear();
-  E.trmv_tier_ms.clear();
-  E.trmv_first_tier = first_tier;
+  if (err) return trmv_err_code(err);
   for (int ci = 0; ci < n_chain && nk; ++ci) {
     const int t = chain[ci];
     float ms = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[ci], E.evt[ci + 1]));
-    E.trmv_tier_ms[t] = ms;
+    E.trmv_tier_ms[t] += ms;
     E.trmv_overflow_keys[t] = hs[2 + 2 * t];
   }
   // Keys past the 1024-player class: tier 4 (HBM scratch), on the host-known
@@ -456,28 +473,123 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     CCRDT_TRY(trmv_launch_steady_hbm(a, waves, E.hbm_scratch.p, E.stream));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.h_status, E.status.p, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
     const uint32_t e4 = hs[3 + 2 * 4];
-    if (e4) {
-      set_error("trmv_apply: invalid op in batch (tier 4)");
-      return (e4 & (TRMV_ERR_TS | TRMV_ERR_VC)) && !(e4 & (TRMV_ERR_KIND | TRMV_ERR_DC | TRMV_ERR_ROW))
-                 ? CCRDT_ERANGE
-                 : CCRDT_EINVAL;
-    }
+    if (e4) return trmv_err_code(e4);
     float ms = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[ev - 2], E.evt[ev - 1]));
-    E.trmv_tier_ms[4] = ms;
+    E.trmv_tier_ms[4] += ms;
   }
   E.trmv_overflow_keys[4] = n_big ? hs[2 + 2 * 4] : 0u;
   // Keys over the per-key capacity (tier 4's hand-ons) keep their old state;
   // every other key commits.
-  const uint32_t n_over = E.trmv_overflow_keys[4];
+  n_over = (int)E.trmv_overflow_keys[4];
   if (n_over) {
     a.key_list = E.tier_ovf[TRMV_TIER_LAST].as<uint32_t>();
     a.n_list = 0;
     a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;  // (trmv_keep_kernel reads the count here)
-    CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>(n_over, TRMV_LATER_GRID), E.stream));
+    CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>((uint32_t)n_over, TRMV_LATER_GRID), E.stream));
+  }
+  // the arena of the new data arrays: its top = the scan's totals (a fresh
+  // batch: the ops), its capacities = the arrays'
+  {
+    static thread_local uint64_t top[3];
+    for (int x = 0; x < 3; ++x) top[x] = tot[x];
+    CCRDT_TRY(E.arena.ensure(4 * sizeof(uint64_t)));
+    CCRDT_HIP(hipMemcpyAsync(E.arena.p, top, sizeof(top), hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    trmv_side_caps(E, out, E.arena_cap);
+    // CCRDT_TRMV_ARENA_ROOM=n (tests): at most n free elements past the top,
+    // so relocations run out and the full rewrite that finishes a batch runs
+    if (const char* v = getenv("CCRDT_TRMV_ARENA_ROOM"))
+      for (int x = 0; x < 3; ++x) E.arena_cap[x] = std::min<uint64_t>(E.arena_cap[x], top[x] + strtoull(v, nullptr, 10));
+  }
+  for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
+  E.cur = out;
+  E.mcur = mout;
+  E.inplace_ready = a.slack != 0 && first_tier == 3;
+  return CCRDT_OK;
+}
+
+}  // namespace
+
+int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
+  CCRDT_TRY(check_trmv(e));
+  if (!ops || !ops->key_ptr || (ops->n_ops > 0 && (!ops->kind || !ops->id || !ops->score ||
+                                                   !ops->dc || !ops->ts))) {
+    set_error("trmv_apply: null op array");
+    return CCRDT_EINVAL;
+  }
+  if (ops->n_ops >= (int64_t)0xFFFFFFFFll) {
+    set_error("trmv_apply: batch too large (n_ops must fit in 32 bits)");
+    return CCRDT_EINVAL;
+  }
+  Engine& E = *e;
+  const int D = E.n_dc;
+  const uint64_t nk = (uint64_t)E.n_keys;
+  const uint64_t n_ops = (uint64_t)ops->n_ops;
+  TrmvApplyArgs a{};
+  a.n_keys = E.n_keys;
+  a.n_dc = D;
+  a.k = (uint32_t)std::min<int64_t>(E.k, 0xFFFFFFFFll);
+  a.key_ptr = ops->key_ptr;
+  a.kind = ops->kind;
+  a.id = ops->id;
+  a.score = ops->score;
+  a.dc = ops->dc;
+  a.ts = ops->ts;
+  a.rmv_vc = ops->rmv_vc;
+  a.n_rmv_rows = ops->rmv_vc ? ops->n_rmv_rows : 0;
+  a.fresh = E.fresh ? 1 : 0;
+  // status words: [0..1] scan, [2+2t, 3+2t] tier t (overflow count, errors)
+  CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4));
+  uint32_t* status = E.status.as<uint32_t>();
+  CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
+  a.status = status;
+  CCRDT_TRY(E.ex_cnt.ensure(nk * 4));
+  CCRDT_TRY(E.ex.ensure(n_ops * sizeof(TrmvExtraRec)));
+  CCRDT_TRY(E.ex_vc.ensure(n_ops * 8 * D));
+  CCRDT_TRY(E.ex_key_ptr.ensure((nk + 1) * 8));
+  for (DevBuf& d : E.tier_ovf) CCRDT_TRY(d.ensure(nk * 4));
+  if (E.k <= 128) {  // tier R's per-op scratch and each key's Observed order
+    CCRDT_TRY(E.op_pl.ensure(n_ops + 1));
+    CCRDT_TRY(E.obs_ord.ensure(nk * TRMV_ORD * 2));
+  }
+  a.op_pl = E.op_pl.as<uint8_t>();
+  a.obs_ord = E.obs_ord.as<uint16_t>();
+  a.ex_cnt = E.ex_cnt.as<uint32_t>();
+  a.ex = E.ex.as<TrmvExtraRec>();
+  a.ex_vc = E.ex_vc.as<int64_t>();
+  E.trmv_overflow_keys.clear();
+  E.trmv_tier_ms.clear();
+  // CCRDT_TRMV_INPLACE=0: every resident batch is a full rewrite (A/B knob)
+  static const bool inplace_env = [] {
+    const char* v = getenv("CCRDT_TRMV_INPLACE");
+    return !(v && v[0] == '0');
+  }();
+  int first_tier = 3, n_over = 0;
+  if (nk && !E.fresh && E.k <= 128 && E.inplace_ready && inplace_env) {
+    uint32_t handed = 0;
+    CCRDT_TRY(trmv_pass_inplace(E, a, n_ops, status, handed));
+    E.mcur = 1 - E.mcur;  // (meta / cap now hold the batch, except the handed-on keys)
+    if (handed) {
+      // the handed-on keys' ops in a full rewrite of every key (the others
+      // only copied): it also compacts the arena
+      CCRDT_TRY(E.key_done.ensure(nk));
+      CCRDT_TRY(trmv_launch_mark_done(E.key_done.as<uint8_t>(), nk, E.tier_ovf[3].as<uint32_t>(), handed,
+                                      status + 2 + 2 * 3, E.stream));
+      CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
+      a.key_done = E.key_done.as<uint8_t>();
+      const int rc = trmv_pass_full(E, a, n_ops, status, first_tier, n_over);
+      if (rc != CCRDT_OK) {
+        E.mcur = 1 - E.mcur;  // (the batch is not committed: back to the state before it)
+        E.inplace_ready = false;
+        return rc;
+      }
+    }
+  } else {
+    CCRDT_TRY(trmv_pass_full(E, a, n_ops, status, first_tier, n_over));
   }
   // the sum of the tiers' own intervals (tier 4 starts after a host round
   // trip, whose gap is not kernel time)
@@ -485,8 +597,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   for (const auto& tm : E.trmv_tier_ms) kernel_ms += tm.second;
   CCRDT_HIP(hipMemcpyAsync(E.ex_key_ptr.p, ops->key_ptr, (nk + 1) * 8, hipMemcpyDeviceToDevice,
                            E.stream));
-  for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
-  E.cur = out;
+  E.trmv_first_tier = first_tier;
   E.fresh = false;
   E.last_n_ops = n_ops;
   E.last_kernel_ms = kernel_ms;
@@ -503,7 +614,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
 int ccrdt_trmv_replica_vc_device(ccrdt_engine* e, int64_t* d_out) {
   CCRDT_TRY(check_trmv(e));
   if (!d_out) return CCRDT_EINVAL;
-  const TrmvBufs& b = e->trmv[e->cur];
+  const TrmvBufs& b = e->trmv[e->cur];  // (vc lives with the data arrays)
   return trmv_launch_replica_vc(e->fresh ? nullptr : b.vc.as<int64_t>(), (uint64_t)e->n_keys,
                                 e->n_dc, d_out, e->stream);
 }
@@ -691,14 +802,19 @@ int download_trmv(Engine& E, HostTrmv& h, uint64_t k0, uint64_t k1) {
   if (E.fresh || !n) return CCRDT_OK;
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const TrmvBufs& b = E.trmv[E.cur];
-  CCRDT_HIP(hipMemcpy(h.meta.data(), b.meta.as<KeyMeta>() + k0, n * sizeof(KeyMeta), hipMemcpyDeviceToHost));
+  CCRDT_HIP(hipMemcpy(h.meta.data(), E.trmv[E.mcur].meta.as<KeyMeta>() + k0, n * sizeof(KeyMeta),
+                      hipMemcpyDeviceToHost));
   CCRDT_HIP(hipMemcpy(h.vc.data(), b.vc.as<int64_t>() + k0 * D, n * D * 8, hipMemcpyDeviceToHost));
-  const uint64_t p0 = h.meta[0].p_off, r0 = h.meta[0].r_off, m0 = h.meta[0].m_off;
-  uint64_t p1 = p0, r1 = r0;
+  // (segments lie anywhere in the arena: the range's extent is min..max)
+  uint64_t p0 = UINT64_MAX, r0 = UINT64_MAX, m0 = UINT64_MAX, p1 = 0, r1 = 0;
   for (const KeyMeta& m : h.meta) {
-    p1 = std::max<uint64_t>(p1, (uint64_t)m.p_off + m.np);
-    r1 = std::max<uint64_t>(r1, (uint64_t)m.r_off + m.nr);
+    if (m.np) p0 = std::min<uint64_t>(p0, m.p_off), p1 = std::max<uint64_t>(p1, (uint64_t)m.p_off + m.np);
+    if (m.nr) r0 = std::min<uint64_t>(r0, m.r_off), r1 = std::max<uint64_t>(r1, (uint64_t)m.r_off + m.nr);
+    if (m.np) m0 = std::min<uint64_t>(m0, m.m_off);
   }
+  if (p0 == UINT64_MAX) p0 = p1 = 0;
+  if (r0 == UINT64_MAX) r0 = r1 = 0;
+  if (m0 == UINT64_MAX) m0 = 0;
   const uint64_t np = p1 - p0, nr = r1 - r0;
   h.pl_id.resize(np);
   h.pl_info.resize(np);
@@ -726,10 +842,10 @@ int download_trmv(Engine& E, HostTrmv& h, uint64_t k0, uint64_t k1) {
   }
   if (nr)
     CCRDT_HIP(hipMemcpy(h.r_vc.data(), b.r_vc.as<int64_t>() + r0 * D, nr * D * 8, hipMemcpyDeviceToHost));
-  for (KeyMeta& m : h.meta) {
-    m.p_off -= (uint32_t)p0;
-    m.m_off -= (uint32_t)m0;
-    m.r_off -= (uint32_t)r0;
+  for (KeyMeta& m : h.meta) {  // (keys without players / rows keep offsets nothing reads)
+    m.p_off = m.np ? m.p_off - (uint32_t)p0 : 0u;
+    m.m_off = m.np ? m.m_off - (uint32_t)m0 : 0u;
+    m.r_off = m.nr ? m.r_off - (uint32_t)r0 : 0u;
   }
   return CCRDT_OK;
 }
@@ -746,7 +862,7 @@ int ccrdt_trmv_key_sizes(ccrdt_engine* e, uint32_t* np, uint32_t* nm, uint32_t* 
   std::vector<KeyMeta> meta(nk);
   if (!e->fresh && nk) {
     CCRDT_HIP(hipStreamSynchronize(e->stream));
-    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.p, nk * sizeof(KeyMeta),
+    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->mcur].meta.p, nk * sizeof(KeyMeta),
                         hipMemcpyDeviceToHost));
   }
   for (uint64_t k = 0; k < nk; ++k) {
@@ -793,7 +909,7 @@ int ccrdt_trmv_range_sizes(ccrdt_engine* e, int64_t k0, int64_t k1, int64_t* n_o
   if (!e->fresh && k1 > k0) {
     std::vector<KeyMeta> meta(k1 - k0);
     CCRDT_HIP(hipStreamSynchronize(e->stream));
-    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->cur].meta.as<KeyMeta>() + k0, meta.size() * sizeof(KeyMeta),
+    CCRDT_HIP(hipMemcpy(meta.data(), e->trmv[e->mcur].meta.as<KeyMeta>() + k0, meta.size() * sizeof(KeyMeta),
                         hipMemcpyDeviceToHost));
     for (const KeyMeta& k : meta) {
       o += k.nobs;
@@ -1030,7 +1146,8 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
     h.meta[k] = m;
   }
   TrmvBufs& b = E.trmv[E.cur];
-  CCRDT_TRY(b.meta.ensure(nk * sizeof(KeyMeta)));
+  DevBuf& bmeta = E.trmv[E.mcur].meta;
+  CCRDT_TRY(bmeta.ensure(nk * sizeof(KeyMeta)));
   CCRDT_TRY(b.vc.ensure(nk * D * 8));
   CCRDT_TRY(b.pl_id.ensure(h.pl_id.size() * 8));
   CCRDT_TRY(b.pl_info.ensure(h.pl_info.size() * 4));
@@ -1042,7 +1159,7 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   CCRDT_TRY(b.r_vc.ensure(h.r_vc.size() * 8));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   if (nk) {
-    CCRDT_HIP(hipMemcpy(b.meta.p, h.meta.data(), nk * sizeof(KeyMeta), hipMemcpyHostToDevice));
+    CCRDT_HIP(hipMemcpy(bmeta.p, h.meta.data(), nk * sizeof(KeyMeta), hipMemcpyHostToDevice));
     CCRDT_HIP(hipMemcpy(b.vc.p, h.vc.data(), nk * D * 8, hipMemcpyHostToDevice));
   }
   if (!h.pl_id.empty()) {
@@ -1062,6 +1179,7 @@ int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in) {
   E.trmv_tot[E.cur][1] = h.m_score.size();
   E.trmv_tot[E.cur][2] = h.r_vc.size() / D;
   E.fresh = false;
+  E.inplace_ready = false;  // (the imported layout has no room to grow: the next batch rewrites every key)
   return CCRDT_OK;
 }
 
@@ -1205,7 +1323,7 @@ int ccrdt_trmv_downstream(ccrdt_engine* e, int64_t n, const uint64_t* key, const
   a.ts = E.st_ts.as<int64_t>();
   a.out_kind = E.st_out_kind.as<uint8_t>();
   a.out_vc = E.st_out_vc.as<int64_t>();
-  a.s = E.trmv_side(E.cur);
+  a.s = E.trmv_cur();
   a.fresh = E.fresh ? 1 : 0;
   CCRDT_TRY(trmv_launch_downstream(a, E.stream));
   CCRDT_HIP(hipMemcpyAsync(out_kind, E.st_out_kind.p, un, hipMemcpyDeviceToHost, E.stream));

@@ -8,9 +8,11 @@
 
 namespace ccrdt {
 
-// One ping-pong side of GPU-resident topk_rmv state (trmv_kernels.hpp).
+// One ping-pong side of GPU-resident topk_rmv state (trmv_kernels.hpp): the
+// meta + cap arrays of meta index s and the data arrays of data index s
+// (the two indices move apart when tier R updates keys in place).
 struct TrmvBufs {
-  DevBuf meta, pl_id, pl_info, pl_slab, pl_gb, m_score, m_ts, m_dc, r_vc, vc;
+  DevBuf meta, cap, pl_id, pl_info, pl_slab, pl_gb, m_score, m_ts, m_dc, r_vc, vc;
 };
 
 // Per-type resident state of the other CCRDTs (types_kernels.hip); [2] =
@@ -63,7 +65,14 @@ struct ccrdt_engine {
 
   // topk_rmv
   ccrdt::TrmvBufs trmv[2];
-  int cur = 0;
+  int cur = 0;   // data arrays holding the current state
+  int mcur = 0;  // meta + cap arrays holding the current state
+  // In-place updates (tier R): possible once a full rewrite laid every key
+  // out with room to grow (inplace_ready); relocations take space from the
+  // data arrays' arena (device bump counters, capacities in elements).
+  bool inplace_ready = false;
+  uint64_t arena_cap[3] = {0, 0, 0};
+  ccrdt::DevBuf arena, obs_ord, key_done;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
   ccrdt::DevBuf tier_ovf[5];    // keys each topk_rmv tier handed on (last batch)
   ccrdt::DevBuf hbm_scratch;    // tier 4's per-wave working sets
@@ -84,7 +93,8 @@ struct ccrdt_engine {
   // other types
   ccrdt::TypeBufs tb;
 
-  ccrdt::TrmvSide trmv_side(int s) const;
+  ccrdt::TrmvSide trmv_side(int ms, int ds) const;
+  ccrdt::TrmvSide trmv_cur() const { return trmv_side(mcur, cur); }
   void release_all();
   int init_type();
   int reset_type();

@@ -125,10 +125,16 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
   fresh = src.fresh;
   if (type == CCRDT_TOPK_RMV) {
     cur = src.cur;
+    mcur = src.mcur;
+    inplace_ready = src.inplace_ready;
     for (int x = 0; x < 3; ++x) trmv_tot[cur][x] = src.trmv_tot[src.cur][x];
+    for (int x = 0; x < 3; ++x) arena_cap[x] = src.arena_cap[x];
     const TrmvBufs& s = src.trmv[src.cur];
     TrmvBufs& d = trmv[cur];
-    CCRDT_TRY(copy_buf(d.meta, s.meta, stream));
+    CCRDT_TRY(copy_buf(trmv[mcur].meta, src.trmv[src.mcur].meta, stream));
+    CCRDT_TRY(copy_buf(trmv[mcur].cap, src.trmv[src.mcur].cap, stream));
+    CCRDT_TRY(copy_buf(arena, src.arena, stream));
+    CCRDT_TRY(copy_buf(obs_ord, src.obs_ord, stream));
     CCRDT_TRY(copy_buf(d.pl_id, s.pl_id, stream));
     CCRDT_TRY(copy_buf(d.pl_info, s.pl_info, stream));
     CCRDT_TRY(copy_buf(d.pl_slab, s.pl_slab, stream));

@@ -77,9 +77,16 @@ __device__ __forceinline__ uint32_t wave_rmv_counts(const uint64_t* key_ptr, con
 }
 
 __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint32_t nrmv, uint64_t c[3]) {
-  const uint64_t o0 = a.key_ptr[k], nops = a.key_ptr[k + 1] - o0;
+  const uint64_t nops = trmv_key_nops(a, k, a.key_ptr[k]);
   if (a.fresh) {
     c[0] = c[1] = c[2] = nops;
+  } else if (a.slack) {
+    // room for in-place growth (tier R writes the key: its later batches
+    // append players, slabs and rows inside these segments)
+    const KeyMeta m = a.old_s.meta[k];
+    c[0] = m.np + nops;
+    c[1] = 2 * ((uint64_t)m.nm + nops) + 32;
+    c[2] = 2 * ((uint64_t)m.nr + nrmv) + 16;
   } else {
     const KeyMeta m = a.old_s.meta[k];
     c[0] = m.np + nops;
@@ -130,7 +137,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_partials(TrmvApplyArgs a
 #pragma unroll 1
     for (int g = 0; g < 4; ++g) {
       const uint64_t k0 = tile0 + 256u * w + 64u * g;
-      const uint32_t r = k0 < (uint64_t)a.n_keys ? wave_rmv_counts(a.key_ptr, a.kind, k0, (uint64_t)a.n_keys) : 0u;
+      uint32_t r = k0 < (uint64_t)a.n_keys ? wave_rmv_counts(a.key_ptr, a.kind, k0, (uint64_t)a.n_keys) : 0u;
+      if (a.key_done && k0 + lane < (uint64_t)a.n_keys && a.key_done[k0 + lane]) r = 0u;
       cnt[256u * w + 64u * g + lane] = r;
       if (k0 + lane < (uint64_t)a.n_keys) key_rmv[k0 + lane] = r;
     }
@@ -198,6 +206,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void trmv_scan_apply(TrmvApplyArgs a, c
       m.np = m.nm = m.nr = m.nobs = 0;
       m.minq = NONE32;
       a.new_s.meta[k] = m;
+      if (a.new_s.cap) {
+        KeyCap cp;
+        cp.p_cap = (uint32_t)c[j][0];
+        cp.m_cap = c[j][1] > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c[j][1];
+        cp.r_cap = (uint32_t)c[j][2];
+        cp.m_top = 0;
+        cp.flags = 0;
+        a.new_s.cap[k] = cp;
+      }
     }
     for (int x = 0; x < 3; ++x) run[x] += c[j][x];
   }
@@ -321,7 +338,62 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
   }
 }
 
+// ------------------------------------------------------ batch validation
+// Before an in-place pass nothing may be written when any op of the batch is
+// invalid (the state must stay untouched, as the reference's update/2 crashes
+// on such an op with function_clause): the checks tier R makes per chunk --
+// kind <= 3; an add's DcId < n_dc and Ts >= 1; a rmv's clock row in range and
+// its entries >= 0 -- over every op, the error bits OR-ed into *err.
+__global__ __launch_bounds__(256) void trmv_validate_kernel(TrmvApplyArgs a, uint64_t n_ops, uint32_t* err) {
+  const int D = a.n_dc;
+  uint32_t e = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t kind = a.kind[i];
+    const int64_t ts = a.ts[i];
+    if (kind > 3) {
+      e |= TRMV_ERR_KIND;
+    } else if (kind < 2) {
+      e |= a.dc[i] >= D ? TRMV_ERR_DC : 0u;
+      e |= ts < 1 ? TRMV_ERR_TS : 0u;
+    } else if (ts < 0 || ts >= a.n_rmv_rows) {
+      e |= TRMV_ERR_ROW;
+    } else {
+      for (int d = 0; d < D; ++d) e |= a.rmv_vc[(uint64_t)ts * D + d] < 0 ? TRMV_ERR_VC : 0u;
+    }
+  }
+  // (one atomic per wave)
+  uint32_t w = e;
+  for (int s = 1; s < 64; s <<= 1) w |= (uint32_t)__shfl_xor((int)w, s);
+  if (w && lane_id() == 0) atomicOr(err, w);
+}
+
+// key_done for the pass that finishes an in-place batch: every key 1, then
+// the keys the in-place pass handed on 0.
+__global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint64_t n_keys, const uint32_t* list,
+                                                             const uint32_t* n_list) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = *n_list;
+  if (i < n) done[list[i]] = 0u;
+}
+
 // ------------------------------------------------------------- launchers
+int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, hipStream_t st) {
+  if (n_ops == 0) return CCRDT_OK;
+  const uint64_t blocks = std::min<uint64_t>((n_ops + 255) / 256, 8192);
+  hipLaunchKernelGGL(trmv_validate_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n_ops, err);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
+                          hipStream_t st) {
+  CCRDT_HIP(hipMemsetAsync(done, 1, n_keys, st));
+  if (n_list == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_mark_done_kernel, dim3((n_list + 255) / 256), dim3(256), 0, st, done, n_keys, list, n_dev);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st) {
   if (grid == 0) return CCRDT_OK;
   hipLaunchKernelGGL(trmv_keep_kernel, dim3(grid), dim3(64), 0, st, a);

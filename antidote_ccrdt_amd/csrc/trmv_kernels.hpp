@@ -23,6 +23,19 @@
 //   meta     segment offsets, counts, |Observed| and Min (a player index)
 // Observed is implicit (Observed ⊆ Masked) and Min is always
 // Obs[minq] (Min == min_observed(Observed) is an invariant of the reference).
+//
+// Segments and sides.  The data arrays (players, pool, rows, vc) form ARENAS:
+// a key's segments lie anywhere in them, and a KeyCap per key records how
+// much each segment holds.  meta and cap ping-pong every batch; the data
+// arrays ping-pong only on a full rewrite (a fresh batch, a batch that lays
+// every key out again with the capacity scan, or a compaction).  In between,
+// tier R updates resident keys IN PLACE (TrmvApplyArgs::inplace): a batch
+// reads and writes only the records, slabs and rows of the players its ops
+// name, plus every key's meta / Vc / Observed order; a player whose slab must
+// grow moves it to the pool's top (m_top), a pool that runs out is compacted
+// inside its segment, and a key whose segment is too small moves to the
+// arena's top (a device bump allocator).  Keys that cannot be updated in
+// place are handed on and the batch is finished by a full rewrite.
 #pragma once
 #include <cstdint>
 
@@ -43,9 +56,23 @@ struct alignas(32) KeyMeta {
 };
 static_assert(sizeof(KeyMeta) == 32, "KeyMeta is one 32-byte record");
 
-// One ping-pong side of the resident state.
+// The capacity of a key's segments (ping-pongs with meta).  Written by the
+// capacity scan (flags 0) and by tier R (TRMV_CAP_VALID); tier R's in-place
+// path reads it and relocates a key whose record is not VALID.
+struct alignas(16) KeyCap {
+  uint32_t p_cap, m_cap, r_cap;  // players / pool positions / Removals rows the segments hold
+  uint16_t m_top;                // pool positions in use: every slab lies in [0, m_top)
+  uint16_t flags;                // TRMV_CAP_VALID
+};
+static_assert(sizeof(KeyCap) == 16, "KeyCap is one 16-byte record");
+constexpr uint16_t TRMV_CAP_VALID = 1u;
+constexpr int TRMV_ORD = 128;  // Observed-order slots per key (tier R's class: K <= 128)
+
+// One side of the resident state: meta + cap of one ping-pong index, the
+// data arrays of one (possibly the same) data index.
 struct TrmvSide {
   KeyMeta* meta;
+  KeyCap* cap;
   int64_t* pl_id;
   uint32_t* pl_info;
   uint32_t* pl_slab;
@@ -98,7 +125,21 @@ struct TrmvApplyArgs {
   uint32_t* ovf_list;
   uint32_t* status;  // [0] overflow count, [1] error flags
   uint8_t* op_pl;    // [n_ops] tier R scratch: each op's player index in its key
+  // in-place updates (tier R) and the passes that finish them
+  int32_t inplace;                  // old_s and new_s share the data arrays; keys are updated in place
+  unsigned long long* arena;        // [3] next free player / pool / row position of the data arrays
+  unsigned long long arena_cap[3];  // their capacities (elements)
+  uint16_t* obs_ord;                // [n_keys * TRMV_ORD] each key's Observed players, ascending (tier R)
+  const uint8_t* key_done;          // non-null: 1 = the key's ops were applied already (it is rewritten, no ops)
+  const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)
+  int32_t slack;                    // capacity scan: lay segments out with room for in-place growth
 };
+
+// The ops of key k in this pass (a key whose ops an earlier pass applied has
+// none: it is only rewritten).
+__device__ __forceinline__ uint32_t trmv_key_nops(const TrmvApplyArgs& a, uint64_t k, uint64_t op0) {
+  return (a.key_done && a.key_done[k]) ? 0u : (uint32_t)(a.key_ptr[k + 1] - op0);
+}
 
 // The kernel's TrmvApplyArgs re-read at the point of use (kernarg_as,
 // common.hpp): valid in kernels whose FIRST parameter is the TrmvApplyArgs.

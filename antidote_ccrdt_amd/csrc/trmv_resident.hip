@@ -81,6 +81,7 @@ constexpr int RFBLK = 4;           // replays: slab elements per block of loads 
 constexpr uint32_t MBALLOT = 3;    // merges of up to this many candidates ranked by ballot pairs; more: LDS list + histogram
 constexpr uint32_t RH_NONE = 0xFFFFu, RH_CLAIM = 0x8000u;  // hash slots: player | CLAIM|lane | NONE
 enum : int { R_DONE = 0, R_NEXT = 1, R_REJECT = 2 };
+enum : int { LAY_TIGHT = 0, LAY_APPEND = 1, LAY_COMPACT = 2 };
 
 // pf[p] flags
 constexpr uint32_t Q_OBS = 1u;   // Id in Observed
@@ -90,6 +91,7 @@ constexpr uint32_t Q_RMV = 8u;   // a rmv of Id in this batch: its slab is repla
 constexpr uint32_t Q_WALK = 16u; // a replay compacted the slab: positions restated in P5
 constexpr uint32_t Q_DUP = 32u;  // a possibly duplicated element: replayed too
 constexpr uint32_t Q_UPG = 64u;  // (inside a merge) an Observed player whose entry the run upgrades
+constexpr uint32_t Q_DIRTY = 128u;  // the player's record changes (ops, a moved slab, a promotion): written in P5
 constexpr uint32_t R_DOM = 1u;   // cres: dominated add (:234-237)
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -234,12 +236,13 @@ struct alignas(16) RLds {
   uint16_t gpos[RP];   // the largest's position in the new slab
   uint8_t pf[RP];      // flags (atomics: pf_or / pf_and on the containing word)
   uint8_t gdc[RP];     // the largest: DcId
+  uint32_t obs0[RP / 32];  // players in Observed when the batch starts (P5 writes the records that change)
   union {
-    struct {  // P1 / P2 (P3: hs..nops hold the start map; oslab stays)
+    struct {  // P1 / P2 (P3: hs..claim hold the start map; nops (the slab need) and oslab stay)
       uint16_t hs[2 * RP];
       int32_t pid[RP];
       int32_t claim[64];
-      uint16_t nops[RP];
+      uint16_t nops[RP];   // P2: adds per player; from the plan on: the slab's need (old count + adds)
       uint32_t oslab[RP];  // old slab: offset | count << 16
     } r;
     struct {  // chunks
@@ -256,8 +259,7 @@ struct alignas(16) RLds {
       uint8_t cws[RCH], cwe[RCH], csrt[RCH];
     } c;
     struct {  // P5
-      uint16_t nidx[RP];  // a player's index in the new record order
-      uint8_t odc[RP];    // Obs[Id]'s DcId by player
+      uint8_t odc[RP];  // Obs[Id]'s DcId by player
     } f;
   } u;
   unsigned long long vc[TRMV_DPAD + 1];  // replica Vc; [TRMV_DPAD] sink
@@ -549,8 +551,10 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
   return rl32(bp, src);
 }
 
-// One key.  Returns R_NEXT for a key outside the class; the next tier redoes
-// it from the old side (whatever this one wrote of it is rewritten).
+// One key.  Returns R_NEXT for a key outside the class: the next tier redoes
+// it from the old side (whatever this one wrote of it is rewritten).  In
+// place (KA->inplace) every R_NEXT is decided before the key's first store,
+// so the key is left as it was.
 __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t nkey, RLds& L) {
   const uint32_t lane = (uint32_t)lane_id();
   const int D = KA->n_dc;
@@ -558,18 +562,27 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   unsigned long long prof_t;
   RPROF_STAMP(prof_t);
 #endif
+  const bool inpl = KA->inplace != 0;
+  // in place: an invalid op anywhere in the batch (the validation pass ran
+  // before this kernel) means nothing is written
+  if (inpl && *KA->verr) return R_REJECT;
   const uint64_t op0 = KA->key_ptr[key];
-  const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
+  // (a key whose ops an earlier pass applied is only rewritten: no ops)
+  const bool done = KA->key_done && KA->key_done[key];
+  const uint32_t nops = done ? 0u : (uint32_t)(KA->key_ptr[key + 1] - op0);
   // (a fresh batch: the keys tier 0 handed on, with no old state)
   const bool fresh = KA->fresh != 0;
-  const KeyMeta nm = trmv_new_meta(a, key);
   KeyMeta om;
+  KeyCap oc;
   if (fresh) {
     om.p_off = om.m_off = om.r_off = 0;
     om.np = om.nm = om.nr = om.nobs = 0;
     om.minq = NONE32;
+    oc.p_cap = oc.m_cap = oc.r_cap = 0;
+    oc.m_top = oc.flags = 0;
   } else {
     om = KA->old_s.meta[key];
+    if (inpl) oc = KA->old_s.cap[key];
   }
   // (per-player op counts are 16-bit here)
   if (om.np > (uint32_t)RP || om.nobs > 128u || nops > 0xFFFFu) return R_NEXT;
@@ -583,25 +596,26 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 
   // P2's first round of op Ids and kinds, loaded now: their latency runs
   // under P1's own load chains instead of after them
-  int64_t pre_id[2];
+  int64_t pre_id[2], pre_sc[2];
   uint32_t pre_kd[2];
   {
     const __amdgpu_buffer_rsrc_t bid0 = bsrc(KA->id + op0, nops * 8u);
+    const __amdgpu_buffer_rsrc_t bsc0 = bsrc(KA->score + op0, nops * 8u);
     const __amdgpu_buffer_rsrc_t bkd0 = bsrc(KA->kind + op0, nops);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       pre_id[h] = bld64(bid0, (64u * h + lane) * 8u);
+      pre_sc[h] = bld64(bsc0, (64u * h + lane) * 8u);
       pre_kd[h] = bld8(bkd0, 64u * h + lane);
     }
   }
   // ---- P1. old players: records of all four slots, then the Obs[Id] /
   // largest elements they name (two rounds of loads in flight), then LDS and
   // the Id hash (the four slots' probes interleaved).
-  // Observed's entries are players 0..nobs-1 when the key was last written
-  // by tier R (checked), else gathered and sorted here.
+  // Observed comes sorted from the order tier R recorded (obs_ord, checked),
+  // else it is gathered and sorted here.
   int64_t pid[RSL];
   uint32_t span = 0, inobs = 0;  // inobs: bit u = player of slot u in Observed
-  int64_t k01[2];                // slots 0-1: Obs[Id]'s key
   uint32_t odr[RSL];             // Obs[Id]'s DcId by slot
   bool wide = false;
   {
@@ -690,7 +704,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const uint32_t p = 64u * u + lane;
       const uint32_t off = slab[u] & 0xFFFFu, cnt = slab[u] >> 16, obx = info[u] & 0xFFFFu;
       const bool ho = obx != NONE16;
-      if (u < 2) k01[u] = mkkey(os[u], pid[u]);
       if (p < om.np) {
         wide |= !fits32(pid[u]) || !fits32(os[u]) || !fits32(gs[u]);
         L.msc[p] = (int32_t)gs[u];
@@ -711,28 +724,50 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   }
   if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
   span = wave_max_u32_dpp(span);
+#pragma unroll
+  for (int u = 0; u < RSL; ++u) {  // the players in Observed at the start
+    const uint64_t m = ballot((inobs >> u) & 1u);
+    if (lane == 0) {
+      L.obs0[2 * u] = (uint32_t)m;
+      L.obs0[2 * u + 1] = (uint32_t)(m >> 32);
+    }
+  }
+  wave_lds_sync();
   Obs ob;
   ob.n = om.nobs;
   {
-    // players 0..nobs-1 in Observed and ascending?
+    // entry r = the player obs_ord[r]: its key (Obs[Id]'s Score is the
+    // largest, I1) from LDS, its DcId from the lane that holds its slot.
+    // Accepted when every entry is an Observed player and the keys rise
+    // strictly: then the nobs entries are exactly Observed, sorted (the
+    // record can be stale: a key other tiers wrote since, or never written)
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t i = 64u * t + lane;
-      const uint32_t nlo = t == 0 ? wshl1(lo32(k01[0]), rl32(lo32(k01[1]), 0)) : wshl1(lo32(k01[1]), 0u);
-      const uint32_t nhi = t == 0 ? wshl1(hi32(k01[0]), rl32(hi32(k01[1]), 0)) : wshl1(hi32(k01[1]), 0u);
-      const bool io = (inobs >> t) & 1u;
-      if (i < ob.n) bad |= !io || (i + 1 < ob.n && !(k01[t] < mk64(nlo, nhi)));
-      else bad |= io;
-    }
-    bad |= (inobs >> 2) != 0;  // an Observed player past 127
-    if (!ballot(bad)) {
+      const bool in = i < ob.n;
+      const uint32_t q0 = in ? (uint32_t)KA->obs_ord[(uint64_t)key * TRMV_ORD + i] : 0u;
+      const bool qok = in && q0 < om.np;
+      const uint32_t q = qok ? q0 : 0u;
+      const uint32_t qf = L.pf[q];
+      uint32_t d = 0;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        ob.key[t] = k01[t];
-        ob.pl[t] = (64u * t + lane) | (odr[t] << 16);
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t v = shfl32(odr[u], (int)(q & 63u));
+        d = (q >> 6) == (uint32_t)u ? v : d;
       }
-    } else {
+      ob.key[t] = in ? mkkey(L.msc[q], L.u.r.pid[q]) : INT64_MAX;
+      ob.pl[t] = in ? (q | (d << 16)) : RNONE;
+      bad |= in && (!qok || !(qf & Q_OBS));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t i = 64u * t + lane;
+      const uint32_t nlo = t == 0 ? wshl1(lo32(ob.key[0]), rl32(lo32(ob.key[1]), 0)) : wshl1(lo32(ob.key[1]), 0u);
+      const uint32_t nhi = t == 0 ? wshl1(hi32(ob.key[0]), rl32(hi32(ob.key[1]), 0)) : wshl1(hi32(ob.key[1]), 0u);
+      if (i + 1 < ob.n) bad |= !(ob.key[t] < mk64(nlo, nhi));
+    }
+    if (ballot(bad)) {
       // the r-th Observed player in player order is pulled by entry r; then sort
       uint64_t mk[RSL];
       uint32_t base[RSL + 1];
@@ -768,15 +803,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   wave_lds_sync();
   RPROF(0);
   {
-    // ---- P2. every op's player; ops per player; rmv players
+    // ---- P2. every op's player; adds per player; rmv players
     uint32_t np = om.np;
-    // 128 ops per round: both halves' Ids and kinds load together, then each
-    // half is resolved (one 64-lane claim table)
+    // 128 ops per round: both halves' Ids, Scores and kinds load together,
+    // then each half is resolved (one 64-lane claim table).  A wide Id or add
+    // Score hands the key on here, before anything is written.
     // (the key's op columns through bounds-checked descriptors: past nops reads 0)
     const __amdgpu_buffer_rsrc_t bid = bsrc(KA->id + op0, nops * 8u);
+    const __amdgpu_buffer_rsrc_t bsc = bsrc(KA->score + op0, nops * 8u);
     const __amdgpu_buffer_rsrc_t bkd = bsrc(KA->kind + op0, nops);
     for (uint32_t c0 = 0; c0 < nops; c0 += 128) {
-      int64_t idh[2];
+      int64_t idh[2], sch[2];
       uint32_t kh[2];
       bool vh[2], wide = false;
 #pragma unroll
@@ -785,15 +822,17 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         vh[h] = l < nops;
         if (c0 == 0) {
           idh[h] = pre_id[h];
+          sch[h] = pre_sc[h];
           kh[h] = pre_kd[h];
         } else
         {
           idh[h] = bld64(bid, l * 8u);
+          sch[h] = bld64(bsc, l * 8u);
           kh[h] = bld8(bkd, l);
         }
-        wide |= vh[h] && !fits32(idh[h]);
+        wide |= vh[h] && (!fits32(idh[h]) || (kh[h] < 2 && !fits32(sch[h])));
       }
-      if (ballot(wide)) return R_NEXT;  // a wide Id: tier S
+      if (ballot(wide)) return R_NEXT;  // a wide Id or Score: tier S
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (c0 + 64u * h >= nops) break;
@@ -802,8 +841,8 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         if (!r_resolve(L, idh[h], vh[h], np, p)) return R_NEXT;
         if (vh[h]) {
           KA->op_pl[op0 + l] = (uint8_t)p;
-          atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
-          if (kh[h] == 2 || kh[h] == 3) pf_or(L, p, Q_RMV);
+          if (kh[h] < 2) atomicAdd(reinterpret_cast<uint32_t*>(&L.u.r.nops[p & ~1u]), 1u << ((p & 1u) * 16u));
+          pf_or(L, p, (kh[h] == 2 || kh[h] == 3) ? (Q_RMV | Q_DIRTY) : Q_DIRTY);
         }
       }
     }
@@ -813,8 +852,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       const uint32_t p = 64u * u + lane;
       if (p >= om.np && p < np) pid[u] = L.u.r.pid[p];
     }
-    // new Removals rows, new slab offsets (old count + ops: the new segment)
-    uint32_t nr = om.nr, mtot = 0;
+    // new Removals rows; each player's slab need (old count + adds), kept in
+    // nops; mtot = the whole pool's need, grow = the need of the players
+    // with adds (the slabs that move in place)
+    uint32_t nr = om.nr, mtot = 0, grow = 0;
 #pragma unroll
     for (int u = 0; u < RSL; ++u) {
       const uint32_t p = 64u * u + lane;
@@ -827,23 +868,118 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       if (newrow) L.prow[p] = (uint16_t)(nr + mbcnt(m));
       nr += (uint32_t)__builtin_popcountll(m);
       const uint32_t ocnt = act ? (L.u.r.oslab[q] >> 16) : 0u;
-      const uint32_t cap = act ? ocnt + L.u.r.nops[q] : 0u;
-      uint32_t tot;
-      const uint32_t ex = wave_excl_scan_dpp(cap, tot);
-      if (act) L.nslab[p] = (mtot + ex) | (ocnt << 16);
-      mtot += tot;
+      const uint32_t adds = act ? (uint32_t)L.u.r.nops[q] : 0u;
+      const uint32_t need = ocnt + adds;
+      if (act) L.u.r.nops[p] = (uint16_t)(need > 0xFFFFu ? 0xFFFFu : need);
+      uint32_t t1, t2;
+      (void)wave_excl_scan_dpp(need, t1);
+      (void)wave_excl_scan_dpp(adds ? need : 0u, t2);
+      mtot += t1;
+      grow += t2;
     }
     if (nr >= NONE16 || mtot > TRMV_SEG_MAX) return R_NEXT;  // over the per-key capacity
+    // The new state's segments.  TIGHT: every slab laid out again, in player
+    // order, in a new segment (a fresh key: its op range; a full rewrite: the
+    // capacity scan's; in place: a relocation to the arena's top).  In place,
+    // APPEND: the slabs of the players with adds move to the pool's top, the
+    // rest stay; COMPACT: the pool is first compacted inside the segment.
+    int lay = LAY_TIGHT;
+    uint32_t mbase = 0;
+    KeyMeta nm;
+    KeyCap nc;
+    if (fresh) {
+      nm = trmv_new_meta(a, key);
+      nc.p_cap = nc.m_cap = nc.r_cap = nops;
+    } else if (!inpl) {
+      nm = KA->new_s.meta[key];
+      nc = KA->new_s.cap[key];
+    } else {
+      // (pool positions stay below 2^16: slab offsets are 16-bit)
+      const uint32_t mcap = oc.m_cap < TRMV_SEG_MAX ? oc.m_cap : TRMV_SEG_MAX;
+      const bool fitpr = (oc.flags & TRMV_CAP_VALID) && np <= oc.p_cap && nr <= oc.r_cap;
+      if (fitpr && (uint32_t)oc.m_top + grow <= mcap) {
+        lay = LAY_APPEND;
+        mbase = oc.m_top;
+      } else if (fitpr && om.nm + grow <= mcap) {
+        lay = LAY_COMPACT;
+        mbase = om.nm;
+      }
+      if (lay != LAY_TIGHT) {
+        nm = om;
+        nc = oc;
+      } else {
+        // a new segment at the arena's top, with room to grow in place
+        const uint32_t pc = np + 8u + np / 4u, rc = nr + 8u + nr / 2u;
+        const uint32_t mc = 2u * mtot + 32u > TRMV_SEG_MAX ? TRMV_SEG_MAX : 2u * mtot + 32u;
+        unsigned long long b0 = 0, b1 = 0, b2 = 0;
+        if (lane == 0) {
+          b0 = atomicAdd(&KA->arena[0], (unsigned long long)pc);
+          b1 = atomicAdd(&KA->arena[1], (unsigned long long)mc);
+          b2 = atomicAdd(&KA->arena[2], (unsigned long long)rc);
+        }
+        b0 = (unsigned long long)ufl64((int64_t)b0);
+        b1 = (unsigned long long)ufl64((int64_t)b1);
+        b2 = (unsigned long long)ufl64((int64_t)b2);
+        if (b0 + pc > KA->arena_cap[0] || b1 + mc > KA->arena_cap[1] || b2 + rc > KA->arena_cap[2])
+        {
+          RCOUNT(13, 1);
+          return R_NEXT;  // the arena is full: the batch is finished by a full rewrite
+        }
+        nm = om;
+        nm.p_off = (uint32_t)b0;
+        nm.m_off = (uint32_t)b1;
+        nm.r_off = (uint32_t)b2;
+        nc.p_cap = pc;
+        nc.m_cap = mc;
+        nc.r_cap = rc;
+      }
+    }
+    nc.flags = TRMV_CAP_VALID;
+    nc.m_top = (uint16_t)(lay == LAY_TIGHT ? mtot : mbase + grow);
+    RCOUNT(10 + lay, inpl ? 1 : 0);  // (diagnostic: in-place layouts, TIGHT = relocated)
+    if (lay == LAY_TIGHT) {
+      // every slab re-laid in player order: offset = the needs before it
+      uint32_t run = 0;
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        const bool act = p < np;
+        const uint32_t need = act ? (uint32_t)L.u.r.nops[p] : 0u;
+        const uint32_t ocnt = act ? (L.u.r.oslab[p] >> 16) : 0u;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan_dpp(need, tot);
+        if (act) L.nslab[p] = (run + ex) | (ocnt << 16);
+        run += tot;
+      }
+    } else if (lay == LAY_COMPACT) {
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {  // (the compaction sets the players with elements)
+        const uint32_t p = 64u * u + lane;
+        if (p < np) L.nslab[p] = 0u;
+        if (p < np) pf_or(L, p, Q_DIRTY);  // (slabs move: every record is rewritten)
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        if (p < np) L.nslab[p] = L.u.r.oslab[p];
+      }
+    }
     wave_lds_sync();
     RPROF(1);
 
-    // ---- P3. old slabs and old Removals rows -> the new side
+    // ---- P3. TIGHT: old slabs and old Removals rows -> the new segment,
+    // position-parallel.  COMPACT: the pool compacted inside the segment
+    // (slabs in old-offset order, so every element moves down: a window's
+    // stores never reach a position not yet read).  Then, in place, the slabs
+    // of the players with adds move to the pool's top.
     // (start map: u16 per pool position of the span, player + 1 at each slab
-    // start, in the P1/P2 union, which is free from here on)
-    constexpr uint32_t SMAP = (uint32_t)(offsetof(decltype(L.u.r), oslab) / 2);  // oslab stays
+    // start, in the P1/P2 union up to nops, which with oslab stays)
+    constexpr uint32_t SMAP = (uint32_t)(offsetof(decltype(L.u.r), nops) / 2);
     uint16_t* smap16 = reinterpret_cast<uint16_t*>(&L.u.r);
     const bool smap = span <= SMAP;
-    if (span && smap) {
+    const bool copy = lay == LAY_TIGHT || lay == LAY_COMPACT;
+    if (copy && span && smap) {
       for (uint32_t i = lane; i < (span + 1) / 2; i += 64) reinterpret_cast<uint32_t*>(smap16)[i] = 0u;
       wave_lds_sync();
 #pragma unroll
@@ -855,10 +991,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       wave_lds_sync();
     }
     bool wide = false;
-    if (span) {
+    if (copy && span) {
+      const bool cmp = lay == LAY_COMPACT;
       int32_t prev = -1;
+      uint32_t carry = 0;  // COMPACT: elements of the slabs that start before the window
       // (the old pool through bounds-checked descriptors over the key's span,
-      // the new side's bases read once: the window's loads and stores issue
+      // the destination's bases read once: the window's loads and stores issue
       // without a branch or a scalar wait each)
       const __amdgpu_buffer_rsrc_t qsc = bsrc(KA->old_s.m_score + om.m_off, span * 8u);
       const __amdgpu_buffer_rsrc_t qts = bsrc(KA->old_s.m_ts + om.m_off, span * 8u);
@@ -873,11 +1011,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t q = g0 + 64u * i + lane;
-          {
-            wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
-            wts[i] = bld64(qts, q * 8u);
-            wdc[i] = bld8(qdc, q);
-          }
+          wsc[i] = bld64(qsc, q * 8u);  // (past the span: 0)
+          wts[i] = bld64(qts, q * 8u);
+          wdc[i] = bld8(qdc, q);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -887,9 +1023,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
           const int64_t sc = wsc[i], ts = wts[i];
           const uint32_t dc = wdc[i];
           // the owner of a position is the player whose slab starts last at
-          // or before it (slabs are not in player order: tier R writes
-          // players in Observed order); starts come from the start map, or
-          // for a span past its size from a sweep of every player
+          // or before it (slabs are in no particular order); starts come from
+          // the start map, or for a span past its size from a sweep of every
+          // player
           uint32_t st = 0;
           if (smap) {
             st = q < span ? (uint32_t)smap16[q] : 0u;
@@ -905,6 +1041,15 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             }
             wave_lds_sync();
             st = mark[lane];
+          }
+          if (cmp) {
+            // a slab starting here moves to the elements of the slabs before it
+            const uint32_t c = st ? (L.u.r.oslab[st - 1] >> 16) : 0u;
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan_dpp(c, tot);
+            if (st) L.nslab[st - 1] = (carry + ex) | (c << 16);
+            carry += tot;
+            wave_lds_sync();
           }
           uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
           {  // inclusive max-scan (DPP): the last start at or before the lane
@@ -931,17 +1076,19 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             if (q < off + cnt) {
               wide |= !fits32(sc);
               const uint32_t dst = (L.nslab[o] & 0xFFFFu) + (q - off);
-              Nsc[dst] = sc;
-              Nts[dst] = ts;
-              Ndc[dst] = (uint8_t)dc;
+              if (!cmp || dst != q) {
+                Nsc[dst] = sc;
+                Nts[dst] = ts;
+                Ndc[dst] = (uint8_t)dc;
+              }
             }
           }
           wave_lds_sync();
         }
       }
     }
-    if (ballot(wide)) return R_NEXT;  // a wide Score in Masked: tier S
-    {
+    if (lay == LAY_TIGHT && ballot(wide)) return R_NEXT;  // a wide Score in Masked (a new segment only): tier S
+    if (lay == LAY_TIGHT) {
       // old Removals rows, 32 per round: the round's loads, then its stores
       const __amdgpu_buffer_rsrc_t qr = bsrc(KA->old_s.r_vc + (uint64_t)om.r_off * D, om.nr * (uint32_t)D * 8u);
       int64_t* const Nr = KA->new_s.r_vc + (uint64_t)nm.r_off * D;
@@ -958,6 +1105,38 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
           const uint32_t r = r0 + 8u * i + (lane >> 3);
           if (r < om.nr && (int)d < D) Nr[r * (uint32_t)D + d] = rv[i];
         }
+      }
+    } else {
+      // in place: the slabs of the players with adds move to the pool's top
+      // (their old elements copied, one lane per player; the slab's appends
+      // follow in the chunks)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a compacted slab is read back here
+      int64_t* const Psc = KA->new_s.m_score + nm.m_off;
+      int64_t* const Pts = KA->new_s.m_ts + nm.m_off;
+      uint8_t* const Pdc = KA->new_s.m_dc + nm.m_off;
+      uint32_t run = mbase;
+#pragma unroll
+      for (int u = 0; u < RSL; ++u) {
+        const uint32_t p = 64u * u + lane;
+        const bool act = p < np;
+        const uint32_t need = act ? (uint32_t)L.u.r.nops[p] : 0u;
+        const uint32_t sl = act ? L.nslab[p] : 0u;
+        const uint32_t ocnt = sl >> 16;
+        const bool mv = need > ocnt;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan_dpp(mv ? need : 0u, tot);
+        if (mv) {
+          const uint32_t src = sl & 0xFFFFu, dst = run + ex;
+          for (uint32_t j = 0; j < ocnt; ++j) {
+            const int64_t s1 = Psc[src + j], t1 = Pts[src + j];
+            const uint8_t d1 = Pdc[src + j];
+            Psc[dst + j] = s1;
+            Pts[dst + j] = t1;
+            Pdc[dst + j] = d1;
+          }
+          L.nslab[p] = dst | (ocnt << 16);
+        }
+        run += tot;
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
@@ -1524,7 +1703,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
               // the key's count is a wave-uniform register here (nexs)
               const uint32_t pos = nexs++;
               if (lane == 0) {
-                pf_or(L, w, Q_OBS);
+                pf_or(L, w, Q_OBS | Q_DIRTY);
                 L.opos[w] = (uint16_t)gp;
                 L.ots[w] = gt;
                 TrmvExtraRec e;
@@ -1550,32 +1729,32 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       c0 += n;
     }
 
-    // ---- P5. player records: Observed first (sorted), then the others in
-    // player order; positions of compacted slabs; Vc; meta.  (The re-find of
-    // a compacted slab reads the last chunk's stores: they must have landed.)
+    // ---- P5. player records (a player's record sits at its index): TIGHT
+    // writes every record, in place only the ones that change (a player with
+    // ops, a moved slab, a change of Observed membership); positions of
+    // slabs a replay compacted; the Observed order (obs_ord, read back by
+    // the next batch's P1); Vc; meta; capacity.  (The re-find of a compacted
+    // slab reads the last chunk's stores: they must have landed.)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const uint32_t i = 64u * t + lane;
-      if (i < ob.n) {
-        L.u.f.nidx[ob.pl[t] & 0xFFFFu] = (uint16_t)i;
-        L.u.f.odc[ob.pl[t] & 0xFFFFu] = (uint8_t)(ob.pl[t] >> 16);
-      }
+      if (i < ob.n) L.u.f.odc[ob.pl[t] & 0xFFFFu] = (uint8_t)(ob.pl[t] >> 16);
     }
     wave_lds_sync();
-    uint32_t rest = ob.n, mcount = 0;
+    const bool all = lay == LAY_TIGHT;
+    uint32_t mcount = 0;
 #pragma unroll
     for (int u = 0; u < RSL; ++u) {
       const uint32_t p = 64u * u + lane;
       const bool act = p < np;
       const uint32_t f = act ? L.pf[p] : 0u;
       const bool ino = act && (f & Q_OBS);
-      const uint64_t m = ballot(act && !ino);
-      const uint32_t ni = ino ? (uint32_t)L.u.f.nidx[p] : rest + mbcnt(m);
-      rest += (uint32_t)__builtin_popcountll(m);
-      if (act) {
+      const bool was = (L.obs0[p >> 5] >> (p & 31u)) & 1u;
+      const uint32_t ns = act ? L.nslab[p] : 0u, cnt = ns >> 16;
+      mcount += cnt;
+      if (act && (all || (f & Q_DIRTY) || ino != was)) {
         uint32_t opos = L.opos[p], gpos = L.gpos[p];
-        const uint32_t ns = L.nslab[p], cnt = ns >> 16;
         if ((f & Q_WALK) && cnt) {  // a replay compacted the slab: find the elements again
           const int64_t msv = L.msc[p], otv = ino ? L.ots[p] : 0, gtv = L.gts[p];
           const uint32_t od = L.u.f.odc[p], gd = L.gdc[p];
@@ -1587,16 +1766,21 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             if (s2 == msv && t2 == gtv && d2 == gd) gpos = j;
           }
         }
-        const uint64_t pq = (uint64_t)nm.p_off + ni;
-        KA->new_s.pl_id[pq] = pid[u];
+        const uint64_t pq = (uint64_t)nm.p_off + p;
+        if (all || p >= om.np) KA->new_s.pl_id[pq] = pid[u];
         KA->new_s.pl_slab[pq] = ns;
         KA->new_s.pl_info[pq] = (ino ? (opos & 0xFFFFu) : NONE16) | ((uint32_t)L.prow[p] << 16);
         KA->new_s.pl_gb[pq] = (uint16_t)(cnt > 1 ? gpos : 0u);
-        mcount += cnt;
       }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t i = 64u * t + lane;
+      if (i < ob.n) KA->obs_ord[(uint64_t)key * TRMV_ORD + i] = (uint16_t)(ob.pl[t] & 0xFFFFu);
     }
     uint32_t mtotal;
     (void)wave_excl_scan_dpp(mcount, mtotal);
+    const uint32_t minp = rl32(ob.pl[0], 0) & 0xFFFFu;  // Min = entry 0
     if (lane < (uint32_t)D) KA->new_s.vc[(uint64_t)key * D + lane] = (int64_t)L.vc[lane];
     if (lane == 0) {
       KeyMeta out = nm;
@@ -1604,9 +1788,10 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       out.nm = mtotal;
       out.nr = nr;
       out.nobs = ob.n;
-      out.minq = ob.n ? 0u : NONE32;
+      out.minq = ob.n ? minp : NONE32;
       KA->new_s.meta[key] = out;
-      KA->ex_cnt[key] = L.nex;
+      KA->new_s.cap[key] = nc;
+      if (!done) KA->ex_cnt[key] = L.nex;
     }
     RPROF(9);
   }
@@ -1636,6 +1821,12 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
     if (r == R_NEXT && lane_id() == 0) {
       const uint32_t pos = atomicAdd(&KA->status[0], 1u);
       KA->ovf_list[pos] = key;
+      // in place the key is as it was: its record carries over, and the pass
+      // that finishes the batch applies its ops
+      if (KA->inplace) {
+        KA->new_s.meta[key] = KA->old_s.meta[key];
+        KA->new_s.cap[key] = KA->old_s.cap[key];
+      }
     }
     wave_lds_sync();
   }

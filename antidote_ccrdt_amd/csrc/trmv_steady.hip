@@ -596,7 +596,9 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
   SPROF_STAMP(prof_t);
 #endif
   const uint64_t op0 = KA->key_ptr[key];
-  const uint32_t nops = (uint32_t)(KA->key_ptr[key + 1] - op0);
+  // (a key whose ops an earlier pass applied is only rewritten: no ops)
+  const bool done = KA->key_done && KA->key_done[key];
+  const uint32_t nops = done ? 0u : (uint32_t)(KA->key_ptr[key + 1] - op0);
   const KeyMeta nm = trmv_new_meta(a, key);
   KeyMeta om;
   if (KA->fresh) {
@@ -1401,7 +1403,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     out.nobs = nobs;
     out.minq = mn.p;
     KA->new_s.meta[key] = out;
-    KA->ex_cnt[key] = L.nex;
+    if (!done) KA->ex_cnt[key] = L.nex;
   }
   SPROF(8);
   return S_DONE;

@@ -129,11 +129,16 @@ def test_downstream_batch(gpu):
     assert np.array_equal(vce[rm], vc[key[rm].astype(np.int64)])
 
 
-def test_invalid_ops_leave_state(gpu):
+@pytest.mark.parametrize("resident_batches", [1, 3])
+def test_invalid_ops_leave_state(gpu, resident_batches):
+    """An invalid op anywhere in a batch: EINVAL / ERANGE and the state as it
+    was -- after one batch (the next is a full rewrite) and after three (the
+    next runs in place: the validation pass stops it before any write)."""
     nk, D = 10, 2
     eng = TopkRmvEngine(nk, 3, D)
-    b = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=3)
-    eng.apply(b)
+    for i in range(resident_batches):
+        b = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=3, clock0=1000 * i)
+        eng.apply(b)
     before = eng.export()
     bad = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=4)
     bad.kind[7] = 9
@@ -200,6 +205,56 @@ def test_empty_batch_and_reset(gpu):
     orac = orc.TrmvOracle(nk, 100, D)
     xe, xo = eng.apply(b), orac.apply(b)
     _compare(eng, orac, b, D, xe, xo)
+
+
+@pytest.mark.parametrize("room", [None, 0, 3000])
+def test_inplace_stream_arena(gpu, room, monkeypatch):
+    """Resident batches updated in place (tier R: appends, slab moves to the
+    pool's top, pool compaction, relocation of keys to the arena's top), with
+    the arena unlimited, empty (every relocation fails: the full rewrite that
+    finishes the batch runs) or small (some fit): bit-exact after every batch,
+    then export / import / clone / downstream on the arena layout."""
+    if room is not None:
+        monkeypatch.setenv("CCRDT_TRMV_ARENA_ROOM", str(room))
+    nk, D, K = 3000, 8, 100
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    n = 95 * nk
+    inplace = finished = 0
+    for i in range(7):
+        b = gen_trmv(n, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64, dup_pm=5, swap_pm=5,
+                     seed=4100 + i, clock0=i * n)
+        xe, xo = eng.apply(b), orac.apply(b)
+        _compare(eng, orac, b, D, xe, xo)
+        inplace += eng.tier_ms(5) > 0         # (the in-place pass validated the batch)
+        finished += eng.overflow_keys(5) > 0  # (keys it left to the full rewrite)
+    assert inplace >= 4
+    if room == 0:
+        assert finished >= 1
+    st = eng.export()
+    e2 = TopkRmvEngine(nk, K, D)
+    e2.import_state(st)
+    assert not e2.export().diff(st)
+    c = eng.clone()
+    assert not c.export().diff(st)
+    b = gen_trmv(n, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64, seed=4200, clock0=8 * n)
+    xo = orac.apply(b)
+    for e in (eng, e2, c):
+        _compare(e, orac if e is eng else _Same(orac), b, D, e.apply(b), xo)
+    key = np.arange(200, dtype=np.uint64)
+    op = (np.arange(200) % 2).astype(np.uint8)
+    ke, _ = eng.downstream(key, op, np.arange(200), np.full(200, 500), np.zeros(200, np.uint8), np.full(200, 9 * n))
+    ko = orac.downstream(key, op, np.arange(200), np.full(200, 500), np.zeros(200, np.uint8), np.full(200, 9 * n))
+    assert np.array_equal(ke, ko)
+
+
+class _Same:
+    """The oracle's state for _compare without applying anything again."""
+
+    def __init__(self, o):
+        self.o = o
+
+    def export(self):
+        return self.o.export()
 
 
 def _stream_batches(eng, orac, nk, D, K, plan, seed):

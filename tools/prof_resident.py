@@ -49,3 +49,6 @@ for i in range(int(os.environ.get("BATCHES", 3))):
     per = nk / 64
     print(f"  per key: relevant adds {buf[27] / per:.1f}, runs {buf[29] / per:.1f}, "
           f"impacting rmvs {buf[31] / per:.1f}")
+    print(f"  in-place layouts (share of keys): append {buf[11] / per:.3f}, compact {buf[12] / per:.3f}, "
+          f"relocated {buf[10] / per:.3f}, arena full {buf[13] / per:.3f}; "
+          f"handed to the full rewrite {eng.overflow_keys(5)}; validation {eng.tier_ms(5):.2f} ms")
