@@ -206,6 +206,7 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   e->release_all();
   ccrdt::stage_release(*e);
   if (e->h_status) (void)hipHostFree(e->h_status);
+  if (e->h_arena) (void)hipHostFree(e->h_arena);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->evk0) (void)hipEventDestroy(e->evk0);
@@ -318,7 +319,9 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   a.old_s = E.trmv_side(E.mcur, E.cur);
   a.new_s = E.trmv_side(1 - E.mcur, E.cur);
   a.arena = E.arena.as<unsigned long long>();
-  for (int x = 0; x < 3; ++x) a.arena_cap[x] = E.arena_cap[x];
+  a.arena_lim = E.arena.as<unsigned long long>() + 3 * TRMV_NSUB;
+  a.lay_cnt = reinterpret_cast<uint32_t*>(E.arena.as<unsigned long long>() + 6 * TRMV_NSUB);
+  CCRDT_HIP(hipMemsetAsync(a.lay_cnt, 0, 4 * TRMV_NSUB * sizeof(uint32_t), E.stream));
   a.key_done = nullptr;
   a.key_list = nullptr;
   a.n_list = (uint32_t)nk;
@@ -332,9 +335,44 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   CCRDT_TRY(trmv_launch_resident(a, nk, E.stream));
   CCRDT_HIP(hipEventRecord(E.evt[2], E.stream));
   CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+  constexpr size_t ARENA_RB = sizeof(E.arena_sub[0]);  // (the counters; the layout counts follow the ends)
+  if (!E.h_arena && hipHostMalloc(&E.h_arena, 2 * ARENA_RB + 16 * TRMV_NSUB, hipHostMallocDefault) != hipSuccess) {
+    E.h_arena = nullptr;
+    set_error("trmv_apply: pinned allocation failed");
+    return CCRDT_EDEVICE;
+  }
+  CCRDT_HIP(hipMemcpyAsync(E.h_arena, E.arena.p, ARENA_RB, hipMemcpyDeviceToHost, E.stream));
+  CCRDT_HIP(hipMemcpyAsync(static_cast<char*>(E.h_arena) + 2 * ARENA_RB, a.lay_cnt, 16 * TRMV_NSUB,
+                           hipMemcpyDeviceToHost, E.stream));
   CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
   if (hs[3 + 2 * 3]) return trmv_err_code(hs[3 + 2 * 3]);
+  {
+    // the arena's use: what this pass took, what is left; the next batch
+    // runs in place only while the room left covers twice this pass's take
+    const uint64_t(*cnt)[3] = reinterpret_cast<const uint64_t(*)[3]>(E.h_arena);
+    bool roomy = true;
+    for (int x = 0; x < 3; ++x) {
+      uint64_t used = 0, room = 0;
+      for (int i = 0; i < TRMV_NSUB; ++i) {
+        const uint64_t c = std::min(cnt[i][x], E.arena_sub[1][i][x]);
+        used += c - E.arena_sub[0][i][x];
+        room += E.arena_sub[1][i][x] - c;
+      }
+      const uint64_t take = used - std::min(used, E.arena_used[x]);
+      E.arena_used[x] = used;
+      E.arena_rate[x] = std::max(E.arena_rate[x], take);
+      roomy &= room >= 2 * take;
+    }
+    E.inplace_ready = roomy;
+    // keys by layout (ccrdt_engine_overflow_keys slots 6, 7, 8: relocated, appended, compacted)
+    const uint32_t* lc = reinterpret_cast<const uint32_t*>(static_cast<const char*>(E.h_arena) + 2 * ARENA_RB);
+    for (int l = 0; l < 3; ++l) {
+      uint32_t n = 0;
+      for (int i = 0; i < TRMV_NSUB; ++i) n += lc[4 * i + l];
+      E.trmv_overflow_keys[6 + l] = n;
+    }
+  }
   float mv = 0.f, mr = 0.f;
   CCRDT_HIP(hipEventElapsedTime(&mv, E.evt[0], E.evt[1]));
   CCRDT_HIP(hipEventElapsedTime(&mr, E.evt[1], E.evt[2]));
@@ -383,8 +421,10 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
   // Sizes of the new side: the totals, and with room to grow in place a
   // quarter more for the keys later batches relocate (the arena)
   auto grow = [&](TrmvBufs& b, bool room) -> int {
+    // (room: for the keys later in-place batches relocate -- three passes'
+    // worth of the most one pass took so far, a quarter of the totals at least)
     uint64_t t[3];
-    for (int x = 0; x < 3; ++x) t[x] = room ? tot[x] + tot[x] / 4 : tot[x];
+    for (int x = 0; x < 3; ++x) t[x] = room ? tot[x] + std::max(tot[x] / 4, 3 * E.arena_rate[x]) : tot[x];
     CCRDT_TRY(b.pl_id.ensure_grow(t[0] * 8));
     CCRDT_TRY(b.pl_info.ensure_grow(t[0] * 4));
     CCRDT_TRY(b.pl_slab.ensure_grow(t[0] * 4));
@@ -492,18 +532,25 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>((uint32_t)n_over, TRMV_LATER_GRID), E.stream));
   }
   // the arena of the new data arrays: its top = the scan's totals (a fresh
-  // batch: the ops), its capacities = the arrays'
+  // batch: the ops), its free space cut into TRMV_NSUB sub-arenas
   {
-    static thread_local uint64_t top[3];
-    for (int x = 0; x < 3; ++x) top[x] = tot[x];
-    CCRDT_TRY(E.arena.ensure(4 * sizeof(uint64_t)));
-    CCRDT_HIP(hipMemcpyAsync(E.arena.p, top, sizeof(top), hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipStreamSynchronize(E.stream));
     trmv_side_caps(E, out, E.arena_cap);
     // CCRDT_TRMV_ARENA_ROOM=n (tests): at most n free elements past the top,
     // so relocations run out and the full rewrite that finishes a batch runs
     if (const char* v = getenv("CCRDT_TRMV_ARENA_ROOM"))
-      for (int x = 0; x < 3; ++x) E.arena_cap[x] = std::min<uint64_t>(E.arena_cap[x], top[x] + strtoull(v, nullptr, 10));
+      for (int x = 0; x < 3; ++x) E.arena_cap[x] = std::min<uint64_t>(E.arena_cap[x], tot[x] + strtoull(v, nullptr, 10));
+    auto& sub = E.arena_sub;
+    for (int x = 0; x < 3; ++x) {
+      const uint64_t room = E.arena_cap[x] > tot[x] ? E.arena_cap[x] - tot[x] : 0;
+      for (int i = 0; i < TRMV_NSUB; ++i) {
+        sub[0][i][x] = tot[x] + room * i / TRMV_NSUB;
+        sub[1][i][x] = tot[x] + room * (i + 1) / TRMV_NSUB;
+      }
+      E.arena_used[x] = 0;
+    }
+    CCRDT_TRY(E.arena.ensure(sizeof(sub) + 16 * TRMV_NSUB));
+    CCRDT_HIP(hipMemcpyAsync(E.arena.p, sub, sizeof(sub), hipMemcpyHostToDevice, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
   }
   for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
   E.cur = out;

@@ -72,6 +72,10 @@ struct ccrdt_engine {
   // data arrays' arena (device bump counters, capacities in elements).
   bool inplace_ready = false;
   uint64_t arena_cap[3] = {0, 0, 0};
+  uint64_t arena_sub[2][ccrdt::TRMV_NSUB][3] = {};  // each sub-arena's start and end (host copy)
+  uint64_t arena_used[3] = {0, 0, 0};               // elements the in-place passes took since the rewrite
+  uint64_t arena_rate[3] = {0, 0, 0};               // the most one in-place pass took (sizes the next rewrite's room)
+  void* h_arena = nullptr;                          // pinned: the sub-arena counters read back
   ccrdt::DevBuf arena, obs_ord, key_done;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
   ccrdt::DevBuf tier_ovf[5];    // keys each topk_rmv tier handed on (last batch)

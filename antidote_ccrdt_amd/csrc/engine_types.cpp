@@ -128,7 +128,12 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
     mcur = src.mcur;
     inplace_ready = src.inplace_ready;
     for (int x = 0; x < 3; ++x) trmv_tot[cur][x] = src.trmv_tot[src.cur][x];
-    for (int x = 0; x < 3; ++x) arena_cap[x] = src.arena_cap[x];
+    for (int x = 0; x < 3; ++x) {
+      arena_cap[x] = src.arena_cap[x];
+      arena_used[x] = src.arena_used[x];
+      arena_rate[x] = src.arena_rate[x];
+    }
+    memcpy(arena_sub, src.arena_sub, sizeof(arena_sub));
     const TrmvBufs& s = src.trmv[src.cur];
     TrmvBufs& d = trmv[cur];
     CCRDT_TRY(copy_buf(trmv[mcur].meta, src.trmv[src.mcur].meta, stream));

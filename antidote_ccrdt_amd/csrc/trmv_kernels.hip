@@ -84,9 +84,9 @@ __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint
     // room for in-place growth (tier R writes the key: its later batches
     // append players, slabs and rows inside these segments)
     const KeyMeta m = a.old_s.meta[k];
-    c[0] = m.np + nops;
+    c[0] = (3 * ((uint64_t)m.np + nops)) / 2 + 8;
     c[1] = 2 * ((uint64_t)m.nm + nops) + 32;
-    c[2] = 2 * ((uint64_t)m.nr + nrmv) + 16;
+    c[2] = (3 * ((uint64_t)m.nr + nrmv)) / 2 + 16;
   } else {
     const KeyMeta m = a.old_s.meta[k];
     c[0] = m.np + nops;
@@ -291,6 +291,7 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
         nm.np = nm.nm = nm.nr = nm.nobs = 0;
         nm.minq = NONE32;
         a.new_s.meta[key] = nm;
+        a.new_s.cap[key].flags = 0;
       }
       continue;
     }
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
       nm.nobs = om.nobs;
       nm.minq = om.minq;
       d.meta[key] = nm;
+      d.cap[key].flags = 0;
     }
   }
 }
@@ -344,23 +346,47 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
 // on such an op with function_clause): the checks tier R makes per chunk --
 // kind <= 3; an add's DcId < n_dc and Ts >= 1; a rmv's clock row in range and
 // its entries >= 0 -- over every op, the error bits OR-ed into *err.
-__global__ __launch_bounds__(256) void trmv_validate_kernel(TrmvApplyArgs a, uint64_t n_ops, uint32_t* err) {
-  const int D = a.n_dc;
+__device__ __forceinline__ uint32_t trmv_check_op(const TrmvApplyArgs& a, uint32_t kind, uint32_t dc, int64_t ts) {
   uint32_t e = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t kind = a.kind[i];
-    const int64_t ts = a.ts[i];
-    if (kind > 3) {
-      e |= TRMV_ERR_KIND;
-    } else if (kind < 2) {
-      e |= a.dc[i] >= D ? TRMV_ERR_DC : 0u;
-      e |= ts < 1 ? TRMV_ERR_TS : 0u;
-    } else if (ts < 0 || ts >= a.n_rmv_rows) {
-      e |= TRMV_ERR_ROW;
-    } else {
-      for (int d = 0; d < D; ++d) e |= a.rmv_vc[(uint64_t)ts * D + d] < 0 ? TRMV_ERR_VC : 0u;
-    }
+  if (kind > 3) {
+    e |= TRMV_ERR_KIND;
+  } else if (kind < 2) {
+    e |= dc >= (uint32_t)a.n_dc ? TRMV_ERR_DC : 0u;
+    e |= ts < 1 ? TRMV_ERR_TS : 0u;
+  } else if (ts < 0 || ts >= a.n_rmv_rows) {
+    e |= TRMV_ERR_ROW;
+  } else {
+    for (int d = 0; d < a.n_dc; ++d) e |= a.rmv_vc[(uint64_t)ts * a.n_dc + d] < 0 ? TRMV_ERR_VC : 0u;
   }
+  return e;
+}
+
+// 16 consecutive ops per thread: their kinds and DcIds in one 16-byte load
+// each, their Ts in eight (when the columns are 16-byte aligned; else and for
+// the tail, one op at a time).
+__global__ __launch_bounds__(256) void trmv_validate_kernel(TrmvApplyArgs a, uint64_t n_ops, uint32_t* err) {
+  uint32_t e = 0;
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.kind) | reinterpret_cast<uintptr_t>(a.dc) |
+                     reinterpret_cast<uintptr_t>(a.ts)) & 15u) == 0;
+  const uint64_t n16 = vec ? n_ops / 16 : 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n16; g += stride) {
+    const uint4 kv = reinterpret_cast<const uint4*>(a.kind)[g];
+    const uint4 dv = reinterpret_cast<const uint4*>(a.dc)[g];
+    int64_t ts[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const longlong2 t2 = reinterpret_cast<const longlong2*>(a.ts + 16 * g)[i];
+      ts[2 * i] = t2.x;
+      ts[2 * i + 1] = t2.y;
+    }
+    const uint32_t kw[4] = {kv.x, kv.y, kv.z, kv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      e |= trmv_check_op(a, (kw[i / 4] >> (8 * (i % 4))) & 0xFFu, (dw[i / 4] >> (8 * (i % 4))) & 0xFFu, ts[i]);
+  }
+  for (uint64_t i = 16 * n16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += stride)
+    e |= trmv_check_op(a, a.kind[i], a.dc[i], a.ts[i]);
   // (one atomic per wave)
   uint32_t w = e;
   for (int s = 1; s < 64; s <<= 1) w |= (uint32_t)__shfl_xor((int)w, s);
@@ -379,7 +405,7 @@ __global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint
 // ------------------------------------------------------------- launchers
 int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, hipStream_t st) {
   if (n_ops == 0) return CCRDT_OK;
-  const uint64_t blocks = std::min<uint64_t>((n_ops + 255) / 256, 8192);
+  const uint64_t blocks = std::min<uint64_t>((n_ops / 16 + 255) / 256 + 1, 8192);
   hipLaunchKernelGGL(trmv_validate_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n_ops, err);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;

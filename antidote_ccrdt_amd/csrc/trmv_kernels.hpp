@@ -67,6 +67,10 @@ struct alignas(16) KeyCap {
 static_assert(sizeof(KeyCap) == 16, "KeyCap is one 16-byte record");
 constexpr uint16_t TRMV_CAP_VALID = 1u;
 constexpr int TRMV_ORD = 128;  // Observed-order slots per key (tier R's class: K <= 128)
+// The arena's free space is cut into sub-arenas, one bump counter each (a
+// workgroup allocates from sub-arena blockIdx % TRMV_NSUB): one counter for
+// every relocation of a batch serialised hundreds of thousands of atomics.
+constexpr int TRMV_NSUB = 64;
 
 // One side of the resident state: meta + cap of one ping-pong index, the
 // data arrays of one (possibly the same) data index.
@@ -127,8 +131,9 @@ struct TrmvApplyArgs {
   uint8_t* op_pl;    // [n_ops] tier R scratch: each op's player index in its key
   // in-place updates (tier R) and the passes that finish them
   int32_t inplace;                  // old_s and new_s share the data arrays; keys are updated in place
-  unsigned long long* arena;        // [3] next free player / pool / row position of the data arrays
-  unsigned long long arena_cap[3];  // their capacities (elements)
+  unsigned long long* arena;            // [TRMV_NSUB][3] next free player / pool / row position of each sub-arena
+  const unsigned long long* arena_lim;  // [TRMV_NSUB][3] each sub-arena's end
+  uint32_t* lay_cnt;                    // [TRMV_NSUB][4] in-place keys by layout: TIGHT (relocated), APPEND, COMPACT
   uint16_t* obs_ord;                // [n_keys * TRMV_ORD] each key's Observed players, ascending (tier R)
   const uint8_t* key_done;          // non-null: 1 = the key's ops were applied already (it is rewritten, no ops)
   const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)

@@ -167,6 +167,25 @@ __device__ __forceinline__ void seg_step(int32_t& vs, int64_t& vt, uint32_t& vd,
   }
 }
 
+// Inclusive max-scan over the wave (DPP row shifts, then row broadcasts):
+// each lane gets the largest value at or below it.
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+  uint32_t o;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  v = o > v ? o : v;
+  return v;
+}
+
 typedef int64_t Row8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ int64_t pick8(const Row8& v, uint32_t d) {
   int64_t r = v[0];
@@ -597,8 +616,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   // P2's first round of op Ids and kinds, loaded now: their latency runs
   // under P1's own load chains instead of after them
   int64_t pre_id[2], pre_sc[2];
-  uint32_t pre_kd[2];
+  uint32_t pre_kd[2], pre_ord[2];
   {
+    // (and the Observed order tier R recorded, which P1 checks)
+    const __amdgpu_buffer_rsrc_t bor = bsrc(KA->obs_ord + (uint64_t)key * TRMV_ORD, om.nobs * 2u);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) pre_ord[h] = bld16(bor, (64u * h + lane) * 2u);
     const __amdgpu_buffer_rsrc_t bid0 = bsrc(KA->id + op0, nops * 8u);
     const __amdgpu_buffer_rsrc_t bsc0 = bsrc(KA->score + op0, nops * 8u);
     const __amdgpu_buffer_rsrc_t bkd0 = bsrc(KA->kind + op0, nops);
@@ -746,7 +769,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     for (int t = 0; t < 2; ++t) {
       const uint32_t i = 64u * t + lane;
       const bool in = i < ob.n;
-      const uint32_t q0 = in ? (uint32_t)KA->obs_ord[(uint64_t)key * TRMV_ORD + i] : 0u;
+      const uint32_t q0 = in ? pre_ord[t] : 0u;
       const bool qok = in && q0 < om.np;
       const uint32_t q = qok ? q0 : 0u;
       const uint32_t qf = L.pf[q];
@@ -908,22 +931,24 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         nm = om;
         nc = oc;
       } else {
-        // a new segment at the arena's top, with room to grow in place
-        const uint32_t pc = np + 8u + np / 4u, rc = nr + 8u + nr / 2u;
+        // a new segment at the top of the workgroup's sub-arena, with room
+        // to grow in place
+        const uint32_t pc = np + np / 2u + 8u, rc = nr + nr / 2u + 16u;
         const uint32_t mc = 2u * mtot + 32u > TRMV_SEG_MAX ? TRMV_SEG_MAX : 2u * mtot + 32u;
+        const uint32_t sub = 3u * (blockIdx.x % (uint32_t)TRMV_NSUB);
         unsigned long long b0 = 0, b1 = 0, b2 = 0;
         if (lane == 0) {
-          b0 = atomicAdd(&KA->arena[0], (unsigned long long)pc);
-          b1 = atomicAdd(&KA->arena[1], (unsigned long long)mc);
-          b2 = atomicAdd(&KA->arena[2], (unsigned long long)rc);
+          b0 = atomicAdd(&KA->arena[sub], (unsigned long long)pc);
+          b1 = atomicAdd(&KA->arena[sub + 1], (unsigned long long)mc);
+          b2 = atomicAdd(&KA->arena[sub + 2], (unsigned long long)rc);
         }
         b0 = (unsigned long long)ufl64((int64_t)b0);
         b1 = (unsigned long long)ufl64((int64_t)b1);
         b2 = (unsigned long long)ufl64((int64_t)b2);
-        if (b0 + pc > KA->arena_cap[0] || b1 + mc > KA->arena_cap[1] || b2 + rc > KA->arena_cap[2])
+        if (b0 + pc > KA->arena_lim[sub] || b1 + mc > KA->arena_lim[sub + 1] || b2 + rc > KA->arena_lim[sub + 2])
         {
           RCOUNT(13, 1);
-          return R_NEXT;  // the arena is full: the batch is finished by a full rewrite
+          return R_NEXT;  // the sub-arena is full: the batch is finished by a full rewrite
         }
         nm = om;
         nm.p_off = (uint32_t)b0;
@@ -936,7 +961,12 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     }
     nc.flags = TRMV_CAP_VALID;
     nc.m_top = (uint16_t)(lay == LAY_TIGHT ? mtot : mbase + grow);
+    // (the capacity record is final here: written now, not held to P5; a
+    // relocated key that hands on later leaves a record nothing reads -- the
+    // finishing pass rewrites every key)
+    if (lane == 0) KA->new_s.cap[key] = nc;
     RCOUNT(10 + lay, inpl ? 1 : 0);  // (diagnostic: in-place layouts, TIGHT = relocated)
+    if (inpl && lane == 0) atomicAdd(&KA->lay_cnt[4u * (blockIdx.x % (uint32_t)TRMV_NSUB) + (uint32_t)lay], 1u);
     if (lay == LAY_TIGHT) {
       // every slab re-laid in player order: offset = the needs before it
       uint32_t run = 0;
@@ -1051,22 +1081,8 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             carry += tot;
             wave_lds_sync();
           }
-          uint32_t own = st ? ((lane + 1) << 16) | st : 0u;
-          {  // inclusive max-scan (DPP): the last start at or before the lane
-            uint32_t o;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x111, 0xf, 0xf, false);
-            own = o > own ? o : own;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x112, 0xf, 0xf, false);
-            own = o > own ? o : own;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x114, 0xf, 0xf, false);
-            own = o > own ? o : own;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x118, 0xf, 0xf, false);
-            own = o > own ? o : own;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x142, 0xa, 0xf, false);
-            own = o > own ? o : own;
-            o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)own, 0x143, 0xc, 0xf, false);
-            own = o > own ? o : own;
-          }
+          // (inclusive max-scan: the last start at or before the lane)
+          uint32_t own = wave_incl_max_dpp(st ? ((lane + 1) << 16) | st : 0u);
           own &= 0xFFFFu;
           const int32_t o = own ? (int32_t)own - 1 : prev;
           prev = (int32_t)rl32((uint32_t)o, 63);
@@ -1108,13 +1124,15 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       }
     } else {
       // in place: the slabs of the players with adds move to the pool's top
-      // (their old elements copied, one lane per player; the slab's appends
-      // follow in the chunks)
+      // (the slab's appends follow in the chunks).  Their old elements are
+      // numbered in one copy stream and copied position-parallel: an LDS map
+      // marks where each mover's elements start in the stream.
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a compacted slab is read back here
-      int64_t* const Psc = KA->new_s.m_score + nm.m_off;
-      int64_t* const Pts = KA->new_s.m_ts + nm.m_off;
-      uint8_t* const Pdc = KA->new_s.m_dc + nm.m_off;
-      uint32_t run = mbase;
+      uint16_t* const emap = reinterpret_cast<uint16_t*>(&L.u.r);  // (the start map's region, free here)
+      const uint32_t eclr = om.nm < SMAP ? om.nm : SMAP;
+      for (uint32_t i = lane; i < (eclr + 1) / 2; i += 64) reinterpret_cast<uint32_t*>(emap)[i] = 0u;
+      wave_lds_sync();
+      uint32_t run = mbase, ecnt = 0;
 #pragma unroll
       for (int u = 0; u < RSL; ++u) {
         const uint32_t p = 64u * u + lane;
@@ -1123,20 +1141,59 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         const uint32_t sl = act ? L.nslab[p] : 0u;
         const uint32_t ocnt = sl >> 16;
         const bool mv = need > ocnt;
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan_dpp(mv ? need : 0u, tot);
+        uint32_t t1, t2;
+        const uint32_t ex = wave_excl_scan_dpp(mv ? need : 0u, t1);
+        const uint32_t ey = wave_excl_scan_dpp(mv ? ocnt : 0u, t2);
+        if (act) L.u.r.oslab[p] = sl;              // the source (a player that stays: the same)
         if (mv) {
-          const uint32_t src = sl & 0xFFFFu, dst = run + ex;
-          for (uint32_t j = 0; j < ocnt; ++j) {
-            const int64_t s1 = Psc[src + j], t1 = Pts[src + j];
-            const uint8_t d1 = Pdc[src + j];
-            Psc[dst + j] = s1;
-            Pts[dst + j] = t1;
-            Pdc[dst + j] = d1;
-          }
-          L.nslab[p] = dst | (ocnt << 16);
+          L.nslab[p] = (run + ex) | (ocnt << 16);  // the destination
+          L.u.r.nops[p] = (uint16_t)(ecnt + ey);   // its first element's number in the stream
+          if (ocnt && ecnt + ey < SMAP) emap[ecnt + ey] = (uint16_t)(p + 1);
         }
-        run += tot;
+        run += t1;
+        ecnt += t2;
+      }
+      wave_lds_sync();
+      int64_t* const Psc = KA->new_s.m_score + nm.m_off;
+      int64_t* const Pts = KA->new_s.m_ts + nm.m_off;
+      uint8_t* const Pdc = KA->new_s.m_dc + nm.m_off;
+      if (ecnt <= SMAP) {
+        int32_t prev = -1;
+        for (uint32_t k0 = 0; k0 < ecnt; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          const uint32_t st = k < ecnt ? (uint32_t)emap[k] : 0u;
+          const uint32_t own = wave_incl_max_dpp(st ? ((lane + 1) << 16) | st : 0u) & 0xFFFFu;
+          const int32_t o = own ? (int32_t)own - 1 : prev;
+          prev = (int32_t)rl32((uint32_t)o, 63);
+          if (k < ecnt && o >= 0) {
+            const uint32_t j = k - (uint32_t)L.u.r.nops[o];
+            const uint32_t src = (L.u.r.oslab[o] & 0xFFFFu) + j, dst = (L.nslab[o] & 0xFFFFu) + j;
+            const int64_t s1 = Psc[src], t1 = Pts[src];
+            const uint8_t d1 = Pdc[src];
+            Psc[dst] = s1;
+            Pts[dst] = t1;
+            Pdc[dst] = d1;
+          }
+        }
+      } else {
+        // (a stream past the map: one lane per mover)
+#pragma unroll
+        for (int u = 0; u < RSL; ++u) {
+          const uint32_t p = 64u * u + lane;
+          const bool act = p < np;
+          const uint32_t dl = act ? L.nslab[p] : 0u;
+          const bool mv = act && dl != L.u.r.oslab[p];
+          if (mv) {
+            const uint32_t src = L.u.r.oslab[p] & 0xFFFFu, dst = dl & 0xFFFFu;
+            for (uint32_t j = 0; j < (dl >> 16); ++j) {
+              const int64_t s1 = Psc[src + j], t1 = Pts[src + j];
+              const uint8_t d1 = Pdc[src + j];
+              Psc[dst + j] = s1;
+              Pts[dst + j] = t1;
+              Pdc[dst + j] = d1;
+            }
+          }
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the replays read these stores
@@ -1790,7 +1847,6 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
       out.nobs = ob.n;
       out.minq = ob.n ? minp : NONE32;
       KA->new_s.meta[key] = out;
-      KA->new_s.cap[key] = nc;
       if (!done) KA->ex_cnt[key] = L.nex;
     }
     RPROF(9);

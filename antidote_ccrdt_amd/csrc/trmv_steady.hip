@@ -1404,6 +1404,7 @@ __device__ int trmv_steady_key(const TrmvApplyArgs& a, uint32_t key, SLds<PCAP, 
     out.minq = mn.p;
     KA->new_s.meta[key] = out;
     if (!done) KA->ex_cnt[key] = L.nex;
+    KA->new_s.cap[key].flags = 0;  // (tier S's layout has no room recorded: tier R relocates the key)
   }
   SPROF(8);
   return S_DONE;

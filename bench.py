@@ -271,9 +271,33 @@ def main():
         def state_bytes(ks):
             # the resident layout (trmv_kernels.hpp): per player Id 8 B + info 4 +
             # slab 4 + largest 2, per Masked element 17 B, per Removals row 8*D,
-            # per key 32 B meta + 8*D Vc
+            # per key 32 B meta + 16 B capacity + 8*D Vc, 2 B per Observed entry
+            # (the recorded order)
             return int((ks["np"].astype(np.int64) * 18 + ks["nm"].astype(np.int64) * 17 +
-                        ks["nr"].astype(np.int64) * 8 * D).sum()) + n_local_keys * (32 + 8 * D)
+                        ks["nr"].astype(np.int64) * 8 * D + ks["nobs"].astype(np.int64) * 2).sum()) + \
+                n_local_keys * (48 + 8 * D)
+
+        def inplace_bytes(ks0, ks1, op_b, n_add, n_rmv, t_frac, lay):
+            # what an in-place pass reads and writes: every key's
+            # meta, capacity, Vc and Observed order read and written; P1 reads
+            # every player's record, its largest element and (Observed players)
+            # Obs[Id]; the named players' records written, their slabs moved
+            # (old elements read + written) and appended to, their rows read
+            # and written (rmv players); relocated keys copied whole, compacted
+            # keys' pools read and written; the ops
+            np0 = int(ks0["np"].astype(np.int64).sum())
+            no0 = int(ks0["nobs"].astype(np.int64).sum())
+            no1 = int(ks1["nobs"].astype(np.int64).sum())
+            nm0 = int(ks0["nm"].astype(np.int64).sum())
+            np1 = int(ks1["np"].astype(np.int64).sum())
+            keys = n_local_keys * 2 * (48 + 8 * D) + 2 * (no0 + no1)
+            p1 = np0 * 18 + (np0 + no0) * 17
+            named = int(t_frac * np1) * 18 + 17 * (2 * int(t_frac * nm0) + n_add) + n_rmv * 2 * 8 * D
+            nk = max(1, n_local_keys)
+            whole = (lay["relocated"] / nk) * (state_bytes(ks0) + state_bytes(ks1)) + \
+                (lay["compacted"] / nk) * 17 * 2 * nm0
+            return int(op_b + keys + p1 + named + whole)
+
         ks_prev = eng.key_sizes()
         # the steady CPU baseline's sample: the same first keys of every batch
         cpu_m = min(args.cpu_steady_keys, n_local_keys) if (rank == 0 and world == 1) else 0
@@ -286,6 +310,8 @@ def main():
             if cpu_m:
                 cpu_samples.append(sample_keys(bi, cpu_m))
             op_b = int(np.where(bi.kind >= 2, 9 + 8 * D, 26).astype(np.int64).sum())
+            bi_kind = np.asarray(bi.kind)
+            n_rmv_i = int((bi_kind >= 2).sum())
             # players the batch names (sample: the first keys): the share of
             # the state a batch needs to touch (steady byte model)
             tm = min(65536, n_local_keys)
@@ -303,25 +329,32 @@ def main():
             ms = (time.perf_counter() - ts0) * 1e3
             dbi.close()
             ks_new = eng.key_sizes()
-            # bytes the batch must move in this layout: its ops, the old state
-            # read, the new state written, the extra effects
-            moved = op_b + state_bytes(ks_prev) + state_bytes(ks_new) + 32 * eng.extra_count()
-            # needed: the same with only the named players' records, slabs and
-            # Removals rows read and written (an in-place layout), every key's
-            # meta + Vc read and written and its Observed order (2 B per entry)
-            # rewritten
             t_frac = touched / max(1, int(ks_new["np"][:tm].astype(np.int64).sum()))
+            # bytes the batch moves in this layout: an in-place pass (tier R on
+            # the keys where they are) or a full rewrite (old state read, new
+            # state written); a batch whose in-place pass handed keys on has both
+            inpl = eng.tier_ms(5) > 0  # (the in-place pass validated the batch)
+            lay = {"relocated": eng.overflow_keys(6), "appended": eng.overflow_keys(7),
+                   "compacted": eng.overflow_keys(8), "handed_to_rewrite": eng.overflow_keys(5)}
+            n_add = int((bi_kind < 2).sum())
+            full_b = op_b + state_bytes(ks_prev) + state_bytes(ks_new)
+            moved = (inplace_bytes(ks_prev, ks_new, op_b, n_add, n_rmv_i, t_frac, lay) if inpl else 0) + \
+                (full_b if (not inpl or lay["handed_to_rewrite"]) else 0) + 32 * eng.extra_count()
+            # needed: only the named players' records, slabs and Removals rows
+            # read and written, every key's meta + Vc read and written and its
+            # Observed order (2 B per entry) rewritten
             key_b = n_local_keys * (32 + 8 * D)
-            needed = (op_b + t_frac * (state_bytes(ks_prev) + state_bytes(ks_new) - 2 * key_b) + 2 * key_b +
-                      2 * int(ks_new["nobs"].astype(np.int64).sum()) + 32 * eng.extra_count())
+            needed = (op_b + t_frac * (state_bytes(ks_prev) + state_bytes(ks_new) - 2 * n_local_keys * (48 + 8 * D))
+                      + 2 * key_b + 2 * int(ks_new["nobs"].astype(np.int64).sum()) + 32 * eng.extra_count())
             ks_prev = ks_new
             tr_ms = eng.tier_ms(3)
             n_step = args.n_ops if (sharded or world == 1) else world * args.n_ops
-            rows.append({"batch": i + 1, "ms": round(ms, 3),
+            rows.append({"batch": i + 1, "ms": round(ms, 3), "pass": "in place" if inpl else "full rewrite",
+                         "in_place_layouts": lay if inpl else None,
                          "ops_per_s": n_step / (ms * 1e-3),
                          "apply_chain_ms": round(eng.last_kernel_ms(), 3),
                          "keys_handed_on_by_tier": {c: eng.overflow_keys(c) for c in tiers},
-                         "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers},
+                         "kernel_ms_by_tier": {c: round(eng.tier_ms(c), 3) for c in tiers + (5,)},
                          "bytes_moved": moved,
                          "bytes_needed": int(needed), "touched_player_share": round(t_frac, 4),
                          "tier_r_GBs": moved / (tr_ms * 1e-3) / 1e9 if tr_ms > 0 else None,
@@ -343,9 +376,16 @@ def main():
                                "algorithmic_bytes_per_launch": sum(mv) / len(mv),
                                "traffic": steady_traffic,
                                "kernel_ms": sum(tr) / len(tr),
-                               "bytes": "ops (add 26 B, rmv 9 + 8*D B) + old state read + new state "
-                                        "written (player 18 B, Masked element 17 B, Removals row 8*D B, "
-                                        "key 32 + 8*D B) + 32 B per extra effect",
+                               "bytes": "per batch, what its pass moves: in place (tier R updates the keys "
+                                        "where they are) = ops + every key's meta, capacity, Vc and Observed "
+                                        "order read and written + every player's record (18 B), largest "
+                                        "element and Obs[Id] (17 B each) read + the named players' records "
+                                        "written, slabs moved and appended (17 B per element), rmv players' "
+                                        "rows read and written (8*D B) + relocated keys copied whole and "
+                                        "compacted pools rewritten (their counts from the kernel); a full "
+                                        "rewrite = ops + old state read + new state written (player 18 B, "
+                                        "Masked element 17 B, Removals row 8*D B, key 48 + 8*D B, 2 B per "
+                                        "Observed entry); + 32 B per extra effect",
                                "needed": {"bytes_per_launch": sum(nd) / len(nd), "achieved": ach_n,
                                           "frac": ach_n / HBM_PEAK_GBS if ach_n else None,
                                           "bytes": "ops + the players the batch names (their records, "
