@@ -531,9 +531,10 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     a.n_list_dev = status + 2 + 2 * TRMV_TIER_LAST;  // (trmv_keep_kernel reads the count here)
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>((uint32_t)n_over, TRMV_LATER_GRID), E.stream));
   }
-  // the arena of the new data arrays: its top = the scan's totals (a fresh
-  // batch: the ops), its free space cut into TRMV_NSUB sub-arenas
-  {
+  // the arena of the new data arrays (only when in-place batches may
+  // follow: tier R wrote the keys with room): its top = the scan's totals,
+  // its free space cut into TRMV_NSUB sub-arenas
+  if (a.slack != 0 && first_tier == 3) {
     trmv_side_caps(E, out, E.arena_cap);
     // CCRDT_TRMV_ARENA_ROOM=n (tests): at most n free elements past the top,
     // so relocations run out and the full rewrite that finishes a batch runs

@@ -57,10 +57,27 @@ def main():
     ap.add_argument("--dominant", default="trmv_wave_kernel<true>")
     ap.add_argument("--steady", default="trmv_resident_kernel",
                     help="the steady-state leg's kernel (bench.py detail.steady_state.roofline)")
+    ap.add_argument("--per-dispatch", default="",
+                    help="also list FETCH/WRITE bytes of every dispatch of kernels matching this name")
     ap.add_argument("--n-ops", type=int, default=100_000_000)
     ap.add_argument("--n-keys", type=int, default=1 << 20)
     a = ap.parse_args()
     out = load(a.prof_dir)
+    if a.per_dispatch:
+        per = defaultdict(lambda: defaultdict(float))  # (pass, dispatch) -> counter -> value
+        for f in glob.glob(os.path.join(a.prof_dir, "*", "*_counter_collection.csv")):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    if a.per_dispatch in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 4096:
+                        per[(os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))][r["Counter_Name"]] += \
+                            float(r["Counter_Value"])
+        for pname in sorted({k[0] for k in per}):
+            ds = sorted(d for (pp, d) in per if pp == pname)
+            for i, d in enumerate(ds):
+                v = per[(pname, d)]
+                line = " ".join(f"{c}={x * 1024 / 1e9:.2f}GB" if c in ("FETCH_SIZE", "WRITE_SIZE") else f"{c}={x:.4g}"
+                                for c, x in sorted(v.items()))
+                print(f"[{pname}] {a.per_dispatch} dispatch #{i} (id {d}): {line}")
     for k, v in sorted(out.items()):
         if a.kernel not in k:
             continue
