@@ -574,6 +574,7 @@ __device__ __forceinline__ uint32_t r_promote(const RLds& L, const int64_t pid[R
 // it from the old side (whatever this one wrote of it is rewritten).  In
 // place (KA->inplace) every R_NEXT is decided before the key's first store,
 // so the key is left as it was.
+template <bool INPL>
 __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t nkey, RLds& L) {
   const uint32_t lane = (uint32_t)lane_id();
   const int D = KA->n_dc;
@@ -581,7 +582,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
   unsigned long long prof_t;
   RPROF_STAMP(prof_t);
 #endif
-  const bool inpl = KA->inplace != 0;
+  constexpr bool inpl = INPL;  // (KA->inplace: one instantiation per mode)
   // in place: an invalid op anywhere in the batch (the validation pass ran
   // before this kernel) means nothing is written
   if (inpl && *KA->verr) return R_REJECT;
@@ -1456,18 +1457,19 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             int64_t bsc = 0, bts = 0;
             // the slab in blocks of 4 elements, each block's loads issued
             // together (the compaction only writes positions already read)
-            for (uint32_t j0 = 0; j0 < cnt; j0 += RFBLK) {
-              int64_t s4[RFBLK], t4[RFBLK];
-              uint32_t d4[RFBLK];
+            constexpr int RFB = INPL ? 2 : RFBLK;
+            for (uint32_t j0 = 0; j0 < cnt; j0 += RFB) {
+              int64_t s4[RFB], t4[RFB];
+              uint32_t d4[RFB];
 #pragma unroll
-              for (int e = 0; e < RFBLK; ++e) {
+              for (int e = 0; e < RFB; ++e) {
                 const uint32_t j = j0 + e < cnt ? j0 + e : j0;
                 s4[e] = Msc[base + j];
                 t4[e] = Mts[base + j];
                 d4[e] = Mdc[base + j];
               }
 #pragma unroll
-              for (int e = 0; e < RFBLK; ++e) {
+              for (int e = 0; e < RFB; ++e) {
                 const uint32_t j = j0 + e;
                 if (j < cnt && t4[e] > V[d4[e]]) {
                   if (w != j) {
@@ -1864,6 +1866,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
 #ifndef TRMV_R_WG
 #define TRMV_R_WG 1
 #endif
+template <bool INPL>
 __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_kernel(TrmvApplyArgs a) {
   __shared__ RLds lds[TRMV_R_WG];
   const uint32_t wv = ufl(threadIdx.x >> 6);
@@ -1873,13 +1876,13 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
     const uint32_t key = ufl(KA->key_list ? KA->key_list[w] : w);
     const uint32_t w2 = w + gridDim.x * TRMV_R_WG;
     const uint32_t nkey = w2 < n ? ufl(KA->key_list ? KA->key_list[w2] : w2) : RNONE;
-    const int r = trmv_resident_key(a, key, nkey, L);
+    const int r = trmv_resident_key<INPL>(a, key, nkey, L);
     if (r == R_NEXT && lane_id() == 0) {
       const uint32_t pos = atomicAdd(&KA->status[0], 1u);
       KA->ovf_list[pos] = key;
       // in place the key is as it was: its record carries over, and the pass
       // that finishes the batch applies its ops
-      if (KA->inplace) {
+      if (INPL) {
         KA->new_s.meta[key] = KA->old_s.meta[key];
         KA->new_s.cap[key] = KA->old_s.cap[key];
       }
@@ -1891,7 +1894,10 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
   const uint64_t blocks = std::min<uint64_t>((grid_keys + TRMV_R_WG - 1) / TRMV_R_WG, 65536 / TRMV_R_WG);
-  hipLaunchKernelGGL(trmv_resident_kernel, dim3((unsigned)blocks), dim3(64 * TRMV_R_WG), 0, st, a);
+  if (a.inplace)
+    hipLaunchKernelGGL(trmv_resident_kernel<true>, dim3((unsigned)blocks), dim3(64 * TRMV_R_WG), 0, st, a);
+  else
+    hipLaunchKernelGGL(trmv_resident_kernel<false>, dim3((unsigned)blocks), dim3(64 * TRMV_R_WG), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
