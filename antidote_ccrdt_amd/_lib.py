@@ -127,6 +127,8 @@ SIGNATURES = {
     "ccrdt_trmv_key_sizes": (INT, [P, P, P, P, P]),
     "ccrdt_trmv_replica_vc_device": (INT, [P, P]),
     "ccrdt_trmv_extras_device": (INT, [P, P, I64, P]),
+    "ccrdt_trmv_exchange_pack": (INT, [P, P, I64, P, I64, C.c_uint32]),
+    "ccrdt_trmv_exchange_reduce": (INT, [P, P, INT, I64, P, P]),
     "ccrdt_trmv_export": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_export_range": (INT, [P, I64, I64, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import_range": (INT, [P, I64, I64, C.POINTER(TrmvState)]),

@@ -234,6 +234,39 @@ def _engine_stream(engine):
     return torch.cuda.ExternalStream(_lib.lib.ccrdt_engine_stream(engine.h), device=torch.device("cuda", engine.device))
 
 
+def _run_device_impl(self, mine, L):
+    """TrmvShardExchange.run on the device: one gather into a [world, L]
+    tensor, then one kernel (ccrdt_trmv_exchange_reduce) for the header (every
+    rank's count and flags, the host-key sum, the Vc max) and every rank's rows
+    sorted by global op; one host read of the header.  None when some rank has
+    more than FAST effects (the general path then runs, second gather and all)."""
+    torch = self.torch
+    W = self.coll.world if self.coll is not None and self.coll.world > 1 else 1
+    if W * self.FAST > 2048:
+        return None
+    g = self.coll.all_gather_into(mine) if W > 1 else mine.view(1, L)
+    hdr = torch.empty(2 * W + 1 + self.n_dc, dtype=torch.int64, device=self.dev)
+    rows = torch.empty((W * self.FAST, self.w), dtype=torch.int64, device=self.dev)
+    es = _engine_stream(self.engine)
+    ts = torch.cuda.current_stream(self.dev)
+    es.wait_stream(ts)
+    self.engine.exchange_reduce(g.data_ptr(), W, L, hdr.data_ptr(), rows.data_ptr())
+    ts.wait_stream(es)
+    hv = hdr[:2 * W + 1].cpu().tolist()
+    counts = [int(c) for c in hv[:W]]
+    failed = [r for r in range(W) if (int(hv[W + r]) >> (self.FAIL_BIT - 32)) & 1]
+    self.count = counts[self.coll.rank if W > 1 else 0]
+    if max(counts) > self.rows_cap:
+        raise RuntimeError(f"trmv exchange: {max(counts)} extra effects > {self.rows_cap} rows")
+    if max(counts) > self.FAST:
+        if failed:
+            raise PeerStepError(failed)
+        return None
+    if failed:
+        raise PeerStepError(failed)
+    return rows[:sum(counts)], hdr[2 * W + 1:], int(hv[2 * W])
+
+
 class TrmvShardExchange:
     """The two per-batch exchange steps of a key-sharded topk_rmv rank
     (topk_rmv.erl:236,294 for the extras, :378-386 for the Vc
@@ -271,6 +304,7 @@ class TrmvShardExchange:
         self.pack = torch.zeros(self.head + rows_cap * self.w, dtype=torch.int64, device=self.dev)
         self.count = 0  # this rank's effects in the pack (host-known only after run())
         self.op_map = None
+        self.engine = None  # set by fill_from_engine: run() reduces the gathered packs on the device
 
     def _rows(self):
         return self.pack[self.head:].view(self.rows_cap, self.w)
@@ -279,27 +313,23 @@ class TrmvShardExchange:
         return (min(int(n_host_keys), self.HOST_MASK) << self.HOST_SHIFT) | ((1 << self.FAIL_BIT) if failed else 0)
 
     def fill_from_engine(self, engine, op_index=None, n_host_keys: int = 0) -> None:
-        """The engine's last batch: its extras (ccrdt_trmv_extras_device) and
-        its shard Vc (ccrdt_trmv_replica_vc_device), packed on the device
+        """The engine's last batch packed on the device in one call
+        (ccrdt_trmv_exchange_pack: its extras with local op indices mapped to
+        global ones, its shard Vc, the count and the host-key bits in word 0)
         without a host wait: the engine's stream waits for torch's (the
-        previous step's gathers read the pack), torch's waits for the
-        engine's.  op_index: device int64 tensor, local op index -> global
-        (None: the same)."""
+        previous step's gathers read the pack), torch's for the engine's.
+        op_index: device int64 tensor, local op index -> global (None: the
+        same)."""
         torch = self.torch
         es = _engine_stream(engine)
         ts = torch.cuda.current_stream(self.dev)
         es.wait_stream(ts)
-        p = self.pack.data_ptr()
-        engine.extras_device(p + 8 * self.head, self.rows_cap, p)
-        engine.replica_vc_device(p + 8)
+        n_map = int(op_index.shape[0]) if op_index is not None else 0
+        engine.exchange_pack(self.pack.data_ptr(), self.rows_cap, op_index.data_ptr() if n_map else None, n_map,
+                             self._word(n_host_keys, False) >> self.HOST_SHIFT)
         ts.wait_stream(es)
-        # (the word's upper bits: new host-path keys; the kernel wrote the count)
-        self.pack[0] = (self.pack[0] & 0xFFFFFFFF) | self._word(n_host_keys, False)
-        self.op_map = op_index
-        if op_index is not None and op_index.shape[0]:
-            # rows past the count are stale; mapping them is harmless
-            c0 = self._rows()[:self.FAST, 0]
-            c0.copy_(op_index[c0.clamp(0, op_index.shape[0] - 1)])
+        self.engine = engine
+        self.op_map = None  # (every row's op is global already)
 
     def fill_from_rows(self, rows: np.ndarray, vc: np.ndarray, n_host_keys: int = 0, failed: bool = False) -> None:
         """Host extras rows (global op index first) and the shard Vc;
@@ -314,6 +344,9 @@ class TrmvShardExchange:
         h[self.head:] = np.ascontiguousarray(rows, np.int64).reshape(-1)
         self.pack[:h.shape[0]] = self.torch.from_numpy(h).to(self.dev)
         self.op_map = None
+        self.engine = None
+
+    _run_device = _run_device_impl
 
     def run(self):
         """The exchange: returns (every rank's extras as an int64 tensor
@@ -324,6 +357,10 @@ class TrmvShardExchange:
         torch = self.torch
         L = self.head + self.FAST * self.w
         mine = self.pack[:L]
+        if self.engine is not None:
+            out = self._run_device(mine, L)
+            if out is not None:
+                return out
         if self.coll is not None and self.coll.world > 1:
             parts = self.coll.all_gather(mine)
         else:
@@ -873,6 +910,16 @@ class TorchCollective:
         outs = [torch.empty_like(w) for _ in range(self.world)]
         self.dist.all_gather(outs, w)
         return [o.to(t.device) for o in outs]
+
+    def all_gather_into(self, t):
+        """Rank r's t (the same shape on every rank) -> one tensor [W, *t.shape]
+        on t's device: RCCL gathers into it directly."""
+        import torch
+        if not self.staged:
+            out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            self.dist.all_gather_into_tensor(out, t.contiguous())
+            return out
+        return torch.stack(self.all_gather(t))
 
     def all_gather_v(self, t):
         """Rank r's t (variable first dimension) -> [t of rank 0, ..., t of rank W-1]."""

@@ -27,7 +27,8 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, uint32_t* key_rmv, hipStream_t st);
-int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, hipStream_t st);
+int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,
+                         hipStream_t st);
 int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
                           hipStream_t st);
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
@@ -43,6 +44,11 @@ int trmv_launch_replica_vc(const int64_t* vc, uint64_t n_keys, int n_dc, int64_t
 int trmv_launch_pack_extras(const uint64_t* key_ptr, const uint32_t* ex_cnt, const TrmvExtraRec* ex,
                             const int64_t* ex_vc, uint64_t n_keys, int n_dc, int64_t* rows,
                             int64_t cap, uint32_t* count, hipStream_t st);
+int trmv_launch_exchange_pack(const int64_t* vc, const uint64_t* key_ptr, const uint32_t* ex_cnt,
+                              const TrmvExtraRec* ex, const int64_t* ex_vc, uint64_t n_keys, int n_dc, int64_t* pack,
+                              int64_t cap, const int64_t* op_map, int64_t n_map, uint32_t host_word, hipStream_t st);
+int trmv_launch_exchange_reduce(const int64_t* g, int world, int64_t len, int n_dc, int64_t* hdr, int64_t* out,
+                                hipStream_t st);
 
 // Tiers of the apply chain: 0 = trmv_wave (tier 0), 1 / 2 = trmv_steady with
 // up to 256 / 1024 players per key (tier S, LDS), 3 = trmv_resident (tier R),
@@ -330,7 +336,8 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   a.status = status + 2 + 2 * 3;
   a.verr = status + 2 + 2 * 3 + 1;  // (tier R's error word: the validation writes it)
   CCRDT_HIP(hipEventRecord(E.evt[0], E.stream));
-  CCRDT_TRY(trmv_launch_validate(a, n_ops, status + 2 + 2 * 3 + 1, E.stream));
+  CCRDT_TRY(trmv_launch_validate(a, n_ops, status + 2 + 2 * 3 + 1,
+                                 reinterpret_cast<unsigned long long*>(status + TRMV_STATUS_WORDS), E.stream));
   CCRDT_HIP(hipEventRecord(E.evt[1], E.stream));
   CCRDT_TRY(trmv_launch_resident(a, nk, E.stream));
   CCRDT_HIP(hipEventRecord(E.evt[2], E.stream));
@@ -591,7 +598,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   a.n_rmv_rows = ops->rmv_vc ? ops->n_rmv_rows : 0;
   a.fresh = E.fresh ? 1 : 0;
   // status words: [0..1] scan, [2+2t, 3+2t] tier t (overflow count, errors)
-  CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4));
+  CCRDT_TRY(E.status.ensure(TRMV_STATUS_WORDS * 4 + 16));  // (+ the validation's scratch flag)
   uint32_t* status = E.status.as<uint32_t>();
   CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
   a.status = status;
@@ -674,6 +681,30 @@ int ccrdt_trmv_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows,
   return trmv_launch_pack_extras(e->ex_key_ptr.as<uint64_t>(), have ? e->ex_cnt.as<uint32_t>() : nullptr,
                                  e->ex.as<TrmvExtraRec>(), e->ex_vc.as<int64_t>(),
                                  (uint64_t)e->n_keys, e->n_dc, d_rows, cap_rows, d_count, e->stream);
+}
+
+int ccrdt_trmv_exchange_pack(ccrdt_engine* e, int64_t* d_pack, int64_t cap_rows, const int64_t* d_op_map,
+                             int64_t n_map, uint32_t host_word) {
+  CCRDT_TRY(check_trmv(e));
+  if (!d_pack || cap_rows < 0 || n_map < 0) return CCRDT_EINVAL;
+  const bool have = e->last_n_ops > 0 && e->ex_cnt.p;
+  const TrmvBufs& b = e->trmv[e->cur];
+  return trmv_launch_exchange_pack(e->fresh ? nullptr : b.vc.as<int64_t>(), e->ex_key_ptr.as<uint64_t>(),
+                                   have ? e->ex_cnt.as<uint32_t>() : nullptr, e->ex.as<TrmvExtraRec>(),
+                                   e->ex_vc.as<int64_t>(), (uint64_t)e->n_keys, e->n_dc, d_pack, cap_rows, d_op_map,
+                                   n_map, host_word, e->stream);
+}
+
+int ccrdt_trmv_exchange_reduce(ccrdt_engine* e, const int64_t* d_gathered, int world, int64_t len, int64_t* d_hdr,
+                               int64_t* d_rows) {
+  CCRDT_TRY(check_trmv(e));
+  const int D = e->n_dc;
+  const int64_t per = (len - 1 - D) / (6 + D);
+  if (!d_gathered || !d_hdr || !d_rows || world < 1 || world > 64 || per < 0 || (int64_t)world * per > 2048) {
+    set_error("trmv_exchange_reduce: bad arguments (at most 2048 gathered rows)");
+    return CCRDT_EINVAL;
+  }
+  return trmv_launch_exchange_reduce(d_gathered, world, len, D, d_hdr, d_rows, e->stream);
 }
 
 int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n) {

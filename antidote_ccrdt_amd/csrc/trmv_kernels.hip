@@ -346,6 +346,7 @@ __global__ __launch_bounds__(64) void trmv_keep_kernel(TrmvApplyArgs a) {
 // on such an op with function_clause): the checks tier R makes per chunk --
 // kind <= 3; an add's DcId < n_dc and Ts >= 1; a rmv's clock row in range and
 // its entries >= 0 -- over every op, the error bits OR-ed into *err.
+// (kind, DcId and Ts of one op; a rmv's clock row only in range here)
 __device__ __forceinline__ uint32_t trmv_check_op(const TrmvApplyArgs& a, uint32_t kind, uint32_t dc, int64_t ts) {
   uint32_t e = 0;
   if (kind > 3) {
@@ -355,15 +356,20 @@ __device__ __forceinline__ uint32_t trmv_check_op(const TrmvApplyArgs& a, uint32
     e |= ts < 1 ? TRMV_ERR_TS : 0u;
   } else if (ts < 0 || ts >= a.n_rmv_rows) {
     e |= TRMV_ERR_ROW;
-  } else {
-    for (int d = 0; d < a.n_dc; ++d) e |= a.rmv_vc[(uint64_t)ts * a.n_dc + d] < 0 ? TRMV_ERR_VC : 0u;
   }
   return e;
 }
 
-// 16 consecutive ops per thread: their kinds and DcIds in one 16-byte load
-// each, their Ts in eight (when the columns are 16-byte aligned; else and for
-// the tail, one op at a time).
+__device__ __forceinline__ void trmv_err_or(uint32_t e, uint32_t* err) {  // one atomic per wave
+  uint32_t w = e;
+  for (int s = 1; s < 64; s <<= 1) w |= (uint32_t)__shfl_xor((int)w, s);
+  if (w && lane_id() == 0) atomicOr(err, w);
+}
+
+// Pass 1: every op's kind, DcId, Ts and clock-row range.  16 consecutive ops
+// per thread: their kinds and DcIds in one 16-byte load each, their Ts in
+// eight (when the columns are 16-byte aligned; else and for the tail, one op
+// at a time).
 __global__ __launch_bounds__(256) void trmv_validate_kernel(TrmvApplyArgs a, uint64_t n_ops, uint32_t* err) {
   uint32_t e = 0;
   const bool vec = ((reinterpret_cast<uintptr_t>(a.kind) | reinterpret_cast<uintptr_t>(a.dc) |
@@ -387,10 +393,32 @@ __global__ __launch_bounds__(256) void trmv_validate_kernel(TrmvApplyArgs a, uin
   }
   for (uint64_t i = 16 * n16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += stride)
     e |= trmv_check_op(a, a.kind[i], a.dc[i], a.ts[i]);
-  // (one atomic per wave)
-  uint32_t w = e;
-  for (int s = 1; s < 64; s <<= 1) w |= (uint32_t)__shfl_xor((int)w, s);
-  if (w && lane_id() == 0) atomicOr(err, w);
+  trmv_err_or(e, err);
+}
+
+// Pass 2: is any entry of the clock table negative?  (Coalesced over the
+// whole table: in a valid batch none is, and nothing more is read.)
+__global__ __launch_bounds__(256) void trmv_validate_rows_any(TrmvApplyArgs a, unsigned long long* any) {
+  const uint64_t n = (uint64_t)a.n_rmv_rows * a.n_dc;
+  bool neg = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    neg |= a.rmv_vc[i] < 0;
+  if (ballot(neg) && lane_id() == 0) atomicOr(any, 1ull);
+}
+
+// Pass 3, only when pass 2 found a negative entry: the rows the rmv ops
+// name, as tier R checks them (a row no rmv names is not an error).
+__global__ __launch_bounds__(256) void trmv_validate_rows_exact(TrmvApplyArgs a, uint64_t n_ops,
+                                                                const unsigned long long* any, uint32_t* err) {
+  if (!*any) return;
+  uint32_t e = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_ops; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t kind = a.kind[i];
+    const int64_t ts = a.ts[i];
+    if ((kind == 2 || kind == 3) && ts >= 0 && ts < a.n_rmv_rows)
+      for (int d = 0; d < a.n_dc; ++d) e |= a.rmv_vc[(uint64_t)ts * a.n_dc + d] < 0 ? TRMV_ERR_VC : 0u;
+  }
+  trmv_err_or(e, err);
 }
 
 // key_done for the pass that finishes an in-place batch: every key 1, then
@@ -403,10 +431,20 @@ __global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint
 }
 
 // ------------------------------------------------------------- launchers
-int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, hipStream_t st) {
+// (scratch: one u64 flag, zeroed here)
+int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,
+                         hipStream_t st) {
   if (n_ops == 0) return CCRDT_OK;
   const uint64_t blocks = std::min<uint64_t>((n_ops / 16 + 255) / 256 + 1, 8192);
   hipLaunchKernelGGL(trmv_validate_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n_ops, err);
+  const uint64_t nv = (uint64_t)a.n_rmv_rows * a.n_dc;
+  if (nv && a.rmv_vc) {
+    CCRDT_HIP(hipMemsetAsync(scratch, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(trmv_validate_rows_any, dim3((unsigned)std::min<uint64_t>((nv + 255) / 256, 4096)), dim3(256), 0,
+                       st, a, scratch);
+    hipLaunchKernelGGL(trmv_validate_rows_exact, dim3((unsigned)std::min<uint64_t>((n_ops + 255) / 256, 4096)),
+                       dim3(256), 0, st, a, n_ops, scratch, err);
+  }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -331,6 +331,17 @@ class TopkRmvEngine(_Engine):
         (op, kind, id, score, dc, ts, vc...) and their count (device uint32)."""
         check(lib.ccrdt_trmv_extras_device(self.h, d_rows, cap_rows, d_count), "extras_device")
 
+    def exchange_pack(self, d_pack: int, cap_rows: int, d_op_map: int | None, n_map: int, host_word: int) -> None:
+        """Enqueue this rank's whole exchange pack [word | Vc | rows] at d_pack
+        (ccrdt_trmv_exchange_pack): extras with global ops, count and host_word
+        in word 0, the shard Vc."""
+        check(lib.ccrdt_trmv_exchange_pack(self.h, d_pack, cap_rows, d_op_map, n_map, host_word & 0xFFFFFFFF),
+              "exchange_pack")
+
+    def exchange_reduce(self, d_gathered: int, world: int, length: int, d_hdr: int, d_rows: int) -> None:
+        """Enqueue the reduction of `world` gathered packs (ccrdt_trmv_exchange_reduce)."""
+        check(lib.ccrdt_trmv_exchange_reduce(self.h, d_gathered, world, length, d_hdr, d_rows), "exchange_reduce")
+
     def key_sizes(self) -> dict:
         """Per-key (players, masked, rows, observed) counts of the resident state."""
         out = {k: np.zeros(self.n_keys, np.uint32) for k in ("np", "nm", "nr", "nobs")}

@@ -556,9 +556,14 @@ def main():
                              {"backend": backend, "extras_all_gathered": int(xres["rows"].shape[0]),
                               "ms_per_step": sum(xms) / max(1, len(xms)),
                               "replica_vc": [int(v) for v in xres["vc"].cpu().tolist()],
-                              "in_step": "cluster.TrmvShardExchange.run: one all_gather of [count | Vc | "
-                                         "first 256 effect rows] (Vc max taken from the gathered copies; a "
-                                         "second gather only past 256 rows), extras sorted by global op"}),
+                              "in_step": "cluster.TrmvShardExchange: the rank's pack [word | Vc | rows] "
+                                         "written by ccrdt_trmv_exchange_pack (no host wait), one all_gather "
+                                         "of [word | Vc | first 256 effect rows] into a [world, L] tensor, "
+                                         "ccrdt_trmv_exchange_reduce (counts, flags, Vc max, rows sorted by "
+                                         "global op), one host read of the header; a second gather only past "
+                                         "256 rows",
+                              "ms_per_step_what": "wall time of TrmvShardExchange.run (includes waiting for the "
+                                                  "pack kernels queued after the apply)"}),
             },
         }
         print(json.dumps(out), flush=True)

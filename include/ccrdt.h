@@ -207,6 +207,22 @@ int ccrdt_trmv_replica_vc_device(ccrdt_engine* e, int64_t* d_out);
  * vc...}, grouped by key (order by op to get stream order); *d_count
  * (device) = how many there were (rows past cap_rows are not written). */
 int ccrdt_trmv_extras_device(ccrdt_engine* e, int64_t* d_rows, int64_t cap_rows, uint32_t* d_count);
+/* One rank's exchange pack in one call (both steps above, no host wait):
+ * d_pack = [word | Vc[n_dc] | rows[cap_rows][6 + n_dc]] (int64, device), word
+ * = extra-effect count (bits 0-31) | host_word << 32; a row's op is mapped
+ * through d_op_map[n_map] (local op -> global op; NULL: as it is). */
+int ccrdt_trmv_exchange_pack(ccrdt_engine* e, int64_t* d_pack, int64_t cap_rows, const int64_t* d_op_map,
+                             int64_t n_map, uint32_t host_word);
+/* The gathered packs of `world` ranks (d_gathered[world][len] int64, device,
+ * each the first `len` words of a rank's pack: head + its first rows) ->
+ * d_hdr (device int64[2 * world + 1 + n_dc]: per rank its count word's low
+ * 32 bits, then per rank the word's high 32 bits, then the sum of the ranks'
+ * bits 32-61, then the elementwise-max Vc) and d_rows (device, [world *
+ * rows_per][6 + n_dc]): every rank's first min(count, rows_per) rows sorted by
+ * op (ties: rank order), *then* d_hdr[...] is complete.  rows_per = (len - 1 -
+ * n_dc) / (6 + n_dc).  Enqueued on the engine stream. */
+int ccrdt_trmv_exchange_reduce(ccrdt_engine* e, const int64_t* d_gathered, int world, int64_t len, int64_t* d_hdr,
+                               int64_t* d_rows);
 
 /* Canonical state image (host arrays), used by export/import:
  *   vc[n_keys*n_dc]                                   replica Vc

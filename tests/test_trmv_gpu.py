@@ -153,6 +153,18 @@ def test_invalid_ops_leave_state(gpu, resident_batches):
         eng.apply(bad)
     assert ei.value.code == _lib.ERANGE
     assert not eng.export().diff(before)
+    # a negative entry in a clock row a rmv names: ERANGE, nothing written
+    bad = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=4, clock0=1000 * resident_batches)
+    r = int(bad.ts[np.nonzero(bad.kind >= 2)[0][0]])
+    bad.rmv_vc[r, 0] = -1
+    with pytest.raises(_lib.CcrdtError) as ei:
+        eng.apply(bad)
+    assert ei.value.code == _lib.ERANGE
+    assert not eng.export().diff(before)
+    # ... in a row no rmv names: not an error (tier R reads only named rows)
+    ok = gen_trmv(500, nk, D, 10, 10, 100, 4, 0, 0, seed=4, clock0=1000 * resident_batches)
+    ok.rmv_vc = np.ascontiguousarray(np.concatenate([ok.rmv_vc, np.full((1, D), -5, np.int64)]))
+    eng.apply(ok)
 
 
 def test_exchange_device_side(gpu):
