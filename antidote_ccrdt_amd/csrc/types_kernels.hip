@@ -906,6 +906,57 @@ __device__ __forceinline__ int32_t lb_merge(LbObs& o, LbPar<ET>& P, const V& L, 
   return ins ? posi : -1;
 }
 
+// Entry of every op of a chunk (lanes v): existing, or created by the lane
+// that claims the hash slot (0x8000 | lane) and numbered in lane order (new
+// entries: LB_NEW, Score = the type's minimum).  cid: 64 LDS Ids.
+template <typename ET, typename V>
+__device__ __forceinline__ uint32_t lb_resolve(const V& L, ET* cid, bool v, int64_t id, uint32_t& n) {
+  const int lane = lane_id();
+  cid[lane] = (ET)id;
+  wave_lds_sync();
+  uint32_t h = lb_hash(id) & L.hmask, e = 0xFFFFFFFFu, slot = 0;
+  bool pend = v, mine = false;
+  while (ballot(pend)) {
+    if (pend) {
+      // the slot's 32-bit word: one read, then (empty) one CAS on it
+      uint32_t* w = reinterpret_cast<uint32_t*>(&L.hslot[h & ~1u]);
+      const uint32_t sh = (h & 1u) * 16u, wv = *w;
+      const uint32_t s = (wv >> sh) & 0xFFFFu;
+      if (s == 0) {
+        if (atomicCAS(w, wv, wv | ((0x8000u | (uint32_t)lane) << sh)) == wv) {
+          pend = false;
+          mine = true;
+          slot = h;
+        }
+      } else if (s & 0x8000u) {
+        if ((int64_t)cid[s & 63u] == id) {
+          pend = false;
+          slot = h;
+        } else {
+          h = (h + 1) & L.hmask;
+        }
+      } else if ((int64_t)L.eid[s - 1] == id) {
+        pend = false;
+        e = s - 1;
+      } else {
+        h = (h + 1) & L.hmask;
+      }
+    }
+  }
+  const uint64_t cm = ballot(mine);
+  if (mine) {
+    e = n + mbcnt(cm);
+    L.hslot[slot] = (uint16_t)(e + 1);
+    L.eid[e] = (ET)id;
+    L.esc[e] = (ET)std::numeric_limits<ET>::min();
+    L.est[e] = LB_NEW;
+  }
+  n += (uint32_t)__builtin_popcountll(cm);
+  wave_lds_sync();
+  if (v && e == 0xFFFFFFFFu) e = (uint32_t)L.hslot[slot] - 1u;
+  return e;
+}
+
 // One board, op-parallel.  Returns false (nothing written) when the board
 // must take the sequential replay instead.
 template <typename ET, typename V>
@@ -1028,50 +1079,7 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       nid = a.id[base + 64 + lane];
       nsc = a.score[base + 64 + lane];
     }
-    // ---- entry of every op: existing, or created by the lane that claims the
-    // hash slot (0x8000 | lane) and numbered in lane order
-    P.cid[lane] = (ET)id;
-    wave_lds_sync();
-    uint32_t h = lb_hash(id) & L.hmask, e = 0xFFFFFFFFu, slot = 0;
-    bool pend = v, mine = false;
-    while (ballot(pend)) {
-      if (pend) {
-        // the slot's 32-bit word: one read, then (empty) one CAS on it
-        uint32_t* w = reinterpret_cast<uint32_t*>(&L.hslot[h & ~1u]);
-        const uint32_t sh = (h & 1u) * 16u, wv = *w;
-        const uint32_t s = (wv >> sh) & 0xFFFFu;
-        if (s == 0) {
-          if (atomicCAS(w, wv, wv | ((0x8000u | (uint32_t)lane) << sh)) == wv) {
-            pend = false;
-            mine = true;
-            slot = h;
-          }
-        } else if (s & 0x8000u) {
-          if ((int64_t)P.cid[s & 63u] == id) {
-            pend = false;
-            slot = h;
-          } else {
-            h = (h + 1) & L.hmask;
-          }
-        } else if ((int64_t)L.eid[s - 1] == id) {
-          pend = false;
-          e = s - 1;
-        } else {
-          h = (h + 1) & L.hmask;
-        }
-      }
-    }
-    const uint64_t cm = ballot(mine);
-    if (mine) {
-      e = n + mbcnt(cm);
-      L.hslot[slot] = (uint16_t)(e + 1);
-      L.eid[e] = (ET)id;
-      L.esc[e] = (ET)std::numeric_limits<ET>::min();
-      L.est[e] = LB_NEW;
-    }
-    n += (uint32_t)__builtin_popcountll(cm);
-    wave_lds_sync();
-    if (v && e == 0xFFFFFFFFu) e = (uint32_t)L.hslot[slot] - 1u;
+    const uint32_t e = lb_resolve<ET>(L, P.cid, v, id, n);
     LB_MARK(1);
     // ---- runs of adds between the chunk's bans
     const uint64_t bm = ballot(v && kd == 2);
@@ -1176,6 +1184,247 @@ __device__ bool lb_board_par(const LbArgs& a, uint32_t k, const LbMeta& om, cons
   return true;
 }
 
+// ---------------------------------------------------------------- leaderboard, by selection
+// NARROW boards (every Id and Score fits 32 bits), any Size.  By (L1)/(L2)
+// above, whatever the order of a stream of adds, every live entry (one that
+// an add reached and no ban removed) holds the max of its adds, Observed is
+// the top Size live entries by (Score, Id), Masked the rest, and Min the
+// smallest Observed entry.  So no Observed bookkeeping runs per op:
+//  * a run of adds between two bans is one LDS atomicMax per op;
+//  * ban/2 of a live entry asks where it ranks at that point: among the top
+//    Size, it leaves Observed and the live entry ranked Size + 1 -- the
+//    largest of Masked -- is promoted, the {add, {Id, Score}} extra effect
+//    (:264-286); below, nothing but the ban;
+//  * at the end one selection (the Size-th largest key) splits Observed from
+//    Masked and names Min.
+// A selection is a radix descent over the 64-bit keys lb_pack(Score, Id)
+// (sign bit flipped: unsigned order), from the highest bit in which the live
+// keys differ, one wave sum per bit.  The keys come from LDS into registers
+// (entry lane + 64 i in u[i]); an entry that is not live has key 0.
+template <int E>
+struct LbKeys {
+  static constexpr int R = E / 64;
+  uint64_t u[R];
+  uint32_t live;  // bit i: entry lane + 64 i is live
+};
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) { return rl32(wave_incl_scan_dpp(v), 63); }
+
+// Loads the keys of entries [0, n); returns false when a live entry's key is
+// 0 (Score and Id both INT32_MIN), which the non-live sentinel cannot tell apart.
+template <int E, typename V>
+__device__ __forceinline__ bool lb_load_keys(const V& L, uint32_t n, LbKeys<E>& K) {
+  static_assert(E % 64 == 0 && E / 64 <= 32, "LbKeys: E / 64 keys per lane, at most 32");
+  const int lane = lane_id();
+  K.live = 0;
+  bool zero = false;
+#pragma unroll
+  for (int i = 0; i < LbKeys<E>::R; ++i) {
+    const uint32_t j = (uint32_t)lane + 64u * i;
+    const bool in = j < n;
+    const uint32_t jj = in ? j : 0u;
+    const uint32_t st = L.est[jj];
+    const bool lv = in && (st == LB_OBS || st == LB_MASKED);
+    const uint64_t u = (uint64_t)lb_pack((int64_t)L.esc[jj], (int64_t)L.eid[jj]) ^ 0x8000000000000000ull;
+    K.u[i] = lv ? u : 0ull;
+    K.live |= lv ? (1u << i) : 0u;
+    zero |= lv && u == 0ull;
+  }
+  return ballot(zero) == 0;
+}
+
+// The need-th largest live key (1 <= need <= live entries).
+template <int E>
+__device__ __forceinline__ uint64_t lb_select(const LbKeys<E>& K, uint32_t need) {
+  uint64_t mx = 0, mn = ~0ull;
+#pragma unroll
+  for (int i = 0; i < LbKeys<E>::R; ++i) {
+    const bool lv = (K.live >> i) & 1u;
+    mx = K.u[i] > mx ? K.u[i] : mx;
+    mn = lv && K.u[i] < mn ? K.u[i] : mn;
+  }
+  constexpr uint64_t SGN = 0x8000000000000000ull;
+  mx = (uint64_t)wave_max_i64((int64_t)(mx ^ SGN)) ^ SGN;
+  mn = (uint64_t)wave_min_i64((int64_t)(mn ^ SGN)) ^ SGN;
+  const uint64_t diff = mx ^ mn;
+  if (diff == 0) return mx;
+  const int top = 63 - __builtin_clzll(diff);
+  uint64_t prefix = mx & ~((2ull << top) - 1ull);  // the bits every live key shares (none when top = 63)
+  for (int b = top; b >= 0; --b) {
+    const uint64_t bit = 1ull << b, cand = prefix | bit, hm = ~(bit - 1ull);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < LbKeys<E>::R; ++i) c += (K.u[i] & hm) == cand ? 1u : 0u;
+    const uint32_t tot = wave_sum_u32(c);
+    if (tot >= need) prefix = cand;
+    else need -= tot;
+  }
+  return prefix;
+}
+
+// Entry index of the live key x (present).
+template <int E>
+__device__ __forceinline__ uint32_t lb_key_entry(const LbKeys<E>& K, uint64_t x) {
+  uint32_t idx = 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = 0; i < LbKeys<E>::R; ++i)
+    idx = ((K.live >> i) & 1u) && K.u[i] == x ? (uint32_t)lane_id() + 64u * i : idx;
+  const uint64_t hit = ballot(idx != 0xFFFFFFFFu);
+  return hit ? rl32(idx, (int)__builtin_ctzll(hit)) : 0xFFFFFFFFu;
+}
+
+template <int E, typename V>
+__device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, const V& L, int32_t* cid) {
+  const int lane = lane_id();
+  const uint32_t K = a.k;
+  if (a.seq || K == 0) return false;
+  const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
+  for (uint32_t i = lane; i <= L.hmask; i += 64) L.hslot[i] = 0;
+  wave_lds_sync();
+  // old entries -> LDS + hash
+  for (uint32_t j = lane; j < om.n; j += 64) {
+    const int64_t id = a.id_in[om.off + j];
+    L.eid[j] = (int32_t)id;
+    L.esc[j] = (int32_t)a.score_in[om.off + j];
+    L.est[j] = a.st_in[om.off + j];
+    uint32_t h = lb_hash(id) & L.hmask;
+    while (!lb_claim(&L.hslot[h], j + 1)) h = (h + 1) & L.hmask;
+  }
+  wave_lds_sync();
+  // the imported state must satisfy (L1), (L2) and Min = min/1 of Observed
+  {
+    uint32_t cobs = 0;
+    bool anym = false;
+    int64_t mino = INT64_MAX, maxm = INT64_MIN;
+    uint32_t mine = 0xFFFFFFFFu;
+    for (uint32_t j = lane; j < om.n; j += 64) {
+      const uint32_t st = L.est[j];
+      const int64_t key = lb_pack((int64_t)L.esc[j], (int64_t)L.eid[j]);
+      if (st == LB_OBS) {
+        ++cobs;
+        if (key < mino) {
+          mino = key;
+          mine = j;
+        }
+      } else if (st == LB_MASKED) {
+        anym = true;
+        maxm = key > maxm ? key : maxm;
+      }
+    }
+    const uint32_t nobs = wave_sum_u32(cobs);
+    const bool any_m = ballot(anym) != 0;
+    if (nobs != om.nobs || nobs > K || (any_m && nobs < K)) return false;
+    if (nobs) {
+      const int64_t gmin = wave_min_i64(mino);
+      const uint32_t minq = rl32(mine, (int)__builtin_ctzll(ballot(mine != 0xFFFFFFFFu && mino == gmin)));
+      if (om.minq != minq) return false;
+      if (any_m && !(wave_max_i64(maxm) < gmin)) return false;
+    } else if (om.minq != 0xFFFFFFFFu) {
+      return false;
+    }
+  }
+  uint32_t n = om.n, nex = 0;
+  uint32_t nkd = 0;
+  int64_t nid = 0, nsc = 0;
+  if (op0 + lane < op1) {
+    nkd = a.kind[op0 + lane];
+    nid = a.id[op0 + lane];
+    nsc = a.score[op0 + lane];
+  }
+  for (uint64_t base = op0; base < op1; base += 64) {
+    const uint32_t cn = (uint32_t)((op1 - base) < 64 ? (op1 - base) : 64);
+    const bool v = (uint32_t)lane < cn;
+    const uint32_t kd = nkd;
+    const int64_t id = nid, sc = nsc;
+    if (ballot(v && kd > 2)) {
+      if (lane == 0) atomicOr(&a.status[1], LB_ERR_KIND);
+      return true;
+    }
+    // the next chunk's ops load while this one runs
+    nkd = 0;
+    nid = nsc = 0;
+    if (base + 64 + lane < op1) {
+      nkd = a.kind[base + 64 + lane];
+      nid = a.id[base + 64 + lane];
+      nsc = a.score[base + 64 + lane];
+    }
+    const uint32_t e = lb_resolve<int32_t>(L, cid, v, id, n);
+    const uint64_t bm = ballot(v && kd == 2);
+    for (uint32_t j = 0; j < cn;) {
+      const uint64_t nb = bm & (~0ull << j);
+      const uint32_t hi = nb ? (uint32_t)__builtin_ctzll(nb) : cn;
+      if (hi > j) {  // a run of adds: banned Ids ignore them (:217-218)
+        const bool inr = v && (uint32_t)lane >= j && (uint32_t)lane < hi;
+        const uint32_t st = inr ? (uint32_t)L.est[e] : (uint32_t)LB_BANNED;
+        const bool act = inr && st != LB_BANNED;
+        if (act) atomicMax(&L.esc[e], (int32_t)sc);
+        if (act && st == LB_NEW) L.est[e] = LB_MASKED;  // live
+        wave_lds_sync();
+      }
+      if (hi >= cn) break;
+      // ---- ban/2 at hi (:264-286)
+      const uint32_t xe = rl32(e, (int)hi);
+      const uint32_t st = L.est[xe];
+      if (st == LB_OBS || st == LB_MASKED) {
+        LbKeys<E> ks;
+        if (!lb_load_keys(L, n, ks)) return false;
+        const uint64_t ux = (uint64_t)lb_pack((int64_t)L.esc[xe], (int64_t)L.eid[xe]) ^ 0x8000000000000000ull;
+        uint32_t ca = 0;
+#pragma unroll
+        for (int i = 0; i < LbKeys<E>::R; ++i) ca += ks.u[i] > ux ? 1u : 0u;
+        const uint32_t above = wave_sum_u32(ca), nlive = wave_sum_u32(__builtin_popcount(ks.live));
+        if (above < K && nlive > K) {  // in Observed, and Masked is not empty
+          const uint32_t w = lb_key_entry(ks, lb_select(ks, K + 1));
+          if (lane == 0) {
+            LbExtraRec rec;
+            rec.op = (uint32_t)(base + hi);
+            rec.pad = 0;
+            rec.id = (int64_t)L.eid[w];
+            rec.score = (int64_t)L.esc[w];
+            a.ex[op0 + nex] = rec;
+          }
+          ++nex;
+        }
+      }
+      if (lane == 0) L.est[xe] = LB_BANNED;
+      wave_lds_sync();
+      j = hi + 1;
+    }
+  }
+  // Observed = the top Size live entries, Min the smallest of them (:297-303)
+  LbKeys<E> ks;
+  if (!lb_load_keys(L, n, ks)) return false;
+  const uint32_t nlive = wave_sum_u32(__builtin_popcount(ks.live));
+  uint32_t nobs = 0, minq = 0xFFFFFFFFu;
+  uint64_t t = ~0ull;
+  if (nlive > K) {
+    t = lb_select(ks, K);
+    nobs = K;
+  } else if (nlive) {
+    uint64_t mn = ~0ull;
+#pragma unroll
+    for (int i = 0; i < LbKeys<E>::R; ++i) mn = ((ks.live >> i) & 1u) && ks.u[i] < mn ? ks.u[i] : mn;
+    t = (uint64_t)wave_min_i64((int64_t)(mn ^ 0x8000000000000000ull)) ^ 0x8000000000000000ull;
+    nobs = nlive;
+  }
+  if (nobs) minq = lb_key_entry(ks, t);
+#pragma unroll
+  for (int i = 0; i < LbKeys<E>::R; ++i)
+    if ((ks.live >> i) & 1u) L.est[(uint32_t)lane + 64u * i] = ks.u[i] >= t ? LB_OBS : LB_MASKED;
+  wave_lds_sync();
+  const uint32_t noff = (uint32_t)a.off_out[k];
+  for (uint32_t j = lane; j < n; j += 64) {
+    a.id_out[noff + j] = (int64_t)L.eid[j];
+    a.score_out[noff + j] = (int64_t)L.esc[j];
+    a.st_out[noff + j] = L.est[j];
+  }
+  if (lane == 0) {
+    LbMeta m{noff, n, nobs, minq};
+    a.meta_out[k] = m;
+    a.ex_cnt[k] = nex;
+  }
+  return true;
+}
 
 template <int E, int H, bool NARROW>
 __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
@@ -1225,10 +1474,16 @@ __global__ __launch_bounds__(64) void lb_apply_kernel(LbArgs a) {
   // per-entry lead bytes share their LDS
   constexpr int UB = (2 * LB_OL > E) ? 2 * LB_OL : E;
   __shared__ alignas(16) uint8_t U[UB];
-  __shared__ LbPar<ET> PL;
   uint16_t* OL = reinterpret_cast<uint16_t*>(U);
   const LbView<uint16_t, ET> view{S.eid, S.esc, S.est, S.hslot, H - 1, OL, a.k <= LB_OL && om.nobs <= LB_OL};
-  if (lb_board_par<ET>(a, k, om, view, PL, U)) return;
+  if constexpr (NARROW) {
+    // (the chunk's Ids share U with the replay's Observed list, which the
+    // replay rebuilds from the state if it runs)
+    if (lb_board_sel<E>(a, k, om, view, reinterpret_cast<int32_t*>(U))) return;
+  } else {
+    __shared__ LbPar<ET> PL;
+    if (lb_board_par<ET>(a, k, om, view, PL, U)) return;
+  }
   lb_board(a, k, om, view);
 }
 
