@@ -389,7 +389,8 @@ struct LbLds {
   ET eid[E];
   ET esc[E];
   uint8_t est[E];
-  uint16_t hslot[H];  // entry + 1, 0 = empty (E <= 2048 fits 16 bits); H >= 1.6 E
+  alignas(8) uint16_t hslot[H];  // entry + 1, 0 = empty (E <= 2048 fits 16 bits); H >= 1.6 E
+  // (lb_board_sel: fingerprinted slots instead, lb_fslot)
 };
 
 // The board's storage: LDS (classes 0/1) or an HBM scratch region (class 2,
@@ -916,6 +917,9 @@ __device__ __forceinline__ uint32_t lb_resolve(const V& L, ET* cid, bool v, int6
   wave_lds_sync();
   uint32_t h = lb_hash(id) & L.hmask, e = 0xFFFFFFFFu, slot = 0;
   bool pend = v, mine = false;
+  // (Measured r05: issuing a probe's claim and both Id compares together,
+  // branch-free at clamped indices, took this loop from 64k to 101k cycles
+  // per bench board.)
   while (ballot(pend)) {
     if (pend) {
       // the slot's 32-bit word: one read, then (empty) one CAS on it
@@ -1233,33 +1237,73 @@ __device__ __forceinline__ bool lb_load_keys(const V& L, uint32_t n, LbKeys<E>& 
   return ballot(zero) == 0;
 }
 
-// The need-th largest live key (1 <= need <= live entries).
-template <int E>
-__device__ __forceinline__ uint64_t lb_select(const LbKeys<E>& K, uint32_t need) {
-  uint64_t mx = 0, mn = ~0ull;
-#pragma unroll
-  for (int i = 0; i < LbKeys<E>::R; ++i) {
-    const bool lv = (K.live >> i) & 1u;
-    mx = K.u[i] > mx ? K.u[i] : mx;
-    mn = lv && K.u[i] < mn ? K.u[i] : mn;
-  }
-  constexpr uint64_t SGN = 0x8000000000000000ull;
-  mx = (uint64_t)wave_max_i64((int64_t)(mx ^ SGN)) ^ SGN;
-  mn = (uint64_t)wave_min_i64((int64_t)(mn ^ SGN)) ^ SGN;
-  const uint64_t diff = mx ^ mn;
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) {
+  uint32_t o;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xa, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xc, 0xf, false);
+  v = o < v ? o : v;
+  return rl32(v, 63);
+}
+
+// The need-th largest of the multiset of values x[i] (every lane's R of
+// them; 0 = not a member, and a member 0 only ever ranks last, which the
+// descent returns as 0 too), 1 <= need <= members; mx / mn = the members'
+// max / min.  Radix descent from the highest bit in which they differ.
+template <int R>
+__device__ __forceinline__ uint32_t lb_descend32(const uint32_t (&x)[R], uint32_t need, uint32_t mx, uint32_t mn) {
+  const uint32_t diff = mx ^ mn;
   if (diff == 0) return mx;
-  const int top = 63 - __builtin_clzll(diff);
-  uint64_t prefix = mx & ~((2ull << top) - 1ull);  // the bits every live key shares (none when top = 63)
+  const int top = 31 - __builtin_clz(diff);
+  uint32_t prefix = mx & ~((2u << top) - 1u);  // the bits every member shares (none when top = 31)
   for (int b = top; b >= 0; --b) {
-    const uint64_t bit = 1ull << b, cand = prefix | bit, hm = ~(bit - 1ull);
+    const uint32_t bit = 1u << b, cand = prefix | bit, hm = ~(bit - 1u);
     uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < LbKeys<E>::R; ++i) c += (K.u[i] & hm) == cand ? 1u : 0u;
+    for (int i = 0; i < R; ++i) c += (x[i] & hm) == cand ? 1u : 0u;
     const uint32_t tot = wave_sum_u32(c);
     if (tot >= need) prefix = cand;
     else need -= tot;
   }
   return prefix;
+}
+
+// The need-th largest live key (1 <= need <= live entries): the Score word
+// first (the keys' high halves, a multiset), then, only when that Score is
+// shared, the Id word among the entries holding it.
+template <int E>
+__device__ __forceinline__ uint64_t lb_select(const LbKeys<E>& K, uint32_t need) {
+  constexpr int R = LbKeys<E>::R;
+  uint32_t hi[R], mx = 0, mn = ~0u;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    hi[i] = (uint32_t)(K.u[i] >> 32);
+    mx = hi[i] > mx ? hi[i] : mx;
+    mn = ((K.live >> i) & 1u) && hi[i] < mn ? hi[i] : mn;
+  }
+  const uint32_t s = lb_descend32<R>(hi, need, wave_max_u32_dpp(mx), wave_min_u32_dpp(mn));
+  uint32_t ca = 0, ct = 0, lo[R], lmx = 0, lmn = ~0u;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const bool at = ((K.live >> i) & 1u) && hi[i] == s;
+    ca += hi[i] > s ? 1u : 0u;
+    ct += at ? 1u : 0u;
+    lo[i] = at ? (uint32_t)K.u[i] : 0u;
+    lmx = lo[i] > lmx ? lo[i] : lmx;
+    lmn = at && lo[i] < lmn ? lo[i] : lmn;
+  }
+  const uint32_t above = wave_sum_u32(ca), tied = wave_sum_u32(ct);
+  lmx = wave_max_u32_dpp(lmx);
+  const uint32_t l = tied == 1 ? lmx : lb_descend32<R>(lo, need - above, lmx, wave_min_u32_dpp(lmn));
+  return ((uint64_t)s << 32) | l;
 }
 
 // Entry index of the live key x (present).
@@ -1273,11 +1317,84 @@ __device__ __forceinline__ uint32_t lb_key_entry(const LbKeys<E>& K, uint64_t x)
   return hit ? rl32(idx, (int)__builtin_ctzll(hit)) : 0xFFFFFFFFu;
 }
 
+// The selection path's hash slots carry a 5-bit fingerprint of the Id, so a
+// probe passes an occupied slot of another Id without reading that Id, and
+// one 8-byte read covers four slots: an entry slot is fp << 10 | entry (E <=
+// 1024), a slot claimed by lane l of the chunk being resolved 0x8000 | fp << 6
+// | l, 0 = empty.
+__device__ __forceinline__ uint32_t lb_fp(int64_t id) {
+  const uint32_t f = (uint32_t)(((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 20) & 31u;
+  return f ? f : 1u;
+}
+__device__ __forceinline__ uint32_t lb_slot_fp(uint32_t s) { return (s & 0x8000u) ? (s >> 6) & 31u : (s >> 10) & 31u; }
+
+template <typename V>
+__device__ __forceinline__ uint32_t lb_resolve_fp(const V& L, int32_t* cid, bool v, int64_t id, uint32_t& n) {
+  const int lane = lane_id();
+  cid[lane] = (int32_t)id;
+  wave_lds_sync();
+  const uint32_t fp = lb_fp(id);
+  uint32_t h = lb_hash(id) & L.hmask, e = 0xFFFFFFFFu, slot = 0;
+  bool pend = v, mine = false;
+  while (ballot(pend)) {
+    if (pend) {
+      const uint32_t w0 = h & ~3u;
+      const uint64_t wv = *reinterpret_cast<const uint64_t*>(&L.hslot[w0]);
+      // the first slot from h on in this window that is empty or carries fp
+      uint32_t q = 4, s = 0;
+#pragma unroll
+      for (int t = 3; t >= 0; --t) {
+        const uint32_t st = (uint32_t)(wv >> (16 * t)) & 0xFFFFu;
+        if ((uint32_t)t >= (h & 3u) && (st == 0 || lb_slot_fp(st) == fp)) {
+          q = (uint32_t)t;
+          s = st;
+        }
+      }
+      if (q == 4) {
+        h = (w0 + 4) & L.hmask;  // the next window
+      } else if (s == 0) {       // claim it: a CAS on its 32-bit half of the window
+        const uint32_t hq = w0 + q, dw = (uint32_t)(wv >> (32 * (q >> 1)));
+        uint32_t* wp = reinterpret_cast<uint32_t*>(&L.hslot[hq & ~1u]);
+        if (atomicCAS(wp, dw, dw | ((0x8000u | (fp << 6) | (uint32_t)lane) << (16 * (q & 1u)))) == dw) {
+          pend = false;
+          mine = true;
+          slot = hq;
+        } else {
+          h = hq;  // (read the window again)
+        }
+      } else if ((s & 0x8000u) ? (int64_t)cid[s & 63u] == id : (int64_t)L.eid[s & 1023u] == id) {
+        pend = false;
+        if (s & 0x8000u) slot = w0 + q;
+        else e = s & 1023u;
+      } else {
+        h = (w0 + q + 1) & L.hmask;  // a fingerprint collision: probe on
+      }
+    }
+  }
+  const uint64_t cm = ballot(mine);
+  if (mine) {
+    e = n + mbcnt(cm);
+    L.hslot[slot] = (uint16_t)((fp << 10) | e);
+    L.eid[e] = (int32_t)id;
+    L.esc[e] = std::numeric_limits<int32_t>::min();
+    L.est[e] = LB_NEW;
+  }
+  n += (uint32_t)__builtin_popcountll(cm);
+  wave_lds_sync();
+  if (v && e == 0xFFFFFFFFu) e = (uint32_t)L.hslot[slot] & 1023u;
+  return e;
+}
+
 template <int E, typename V>
 __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, const V& L, int32_t* cid) {
+  static_assert(E <= 1024, "lb_board_sel: entry indices fit the 10 bits of a fingerprinted slot");
   const int lane = lane_id();
   const uint32_t K = a.k;
   if (a.seq || K == 0) return false;
+#ifdef TRMV_PROF
+  unsigned long long lb_t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lb_t)::"memory");
+#endif
   const uint64_t op0 = a.key_ptr[k], op1 = a.key_ptr[k + 1];
   for (uint32_t i = lane; i <= L.hmask; i += 64) L.hslot[i] = 0;
   wave_lds_sync();
@@ -1288,7 +1405,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     L.esc[j] = (int32_t)a.score_in[om.off + j];
     L.est[j] = a.st_in[om.off + j];
     uint32_t h = lb_hash(id) & L.hmask;
-    while (!lb_claim(&L.hslot[h], j + 1)) h = (h + 1) & L.hmask;
+    while (!lb_claim(&L.hslot[h], (lb_fp(id) << 10) | j)) h = (h + 1) & L.hmask;
   }
   wave_lds_sync();
   // the imported state must satisfy (L1), (L2) and Min = min/1 of Observed
@@ -1323,6 +1440,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       return false;
     }
   }
+  LB_MARK(0);
   uint32_t n = om.n, nex = 0;
   uint32_t nkd = 0;
   int64_t nid = 0, nsc = 0;
@@ -1348,7 +1466,8 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       nid = a.id[base + 64 + lane];
       nsc = a.score[base + 64 + lane];
     }
-    const uint32_t e = lb_resolve<int32_t>(L, cid, v, id, n);
+    const uint32_t e = lb_resolve_fp(L, cid, v, id, n);
+    LB_MARK(1);
     const uint64_t bm = ballot(v && kd == 2);
     for (uint32_t j = 0; j < cn;) {
       const uint64_t nb = bm & (~0ull << j);
@@ -1360,6 +1479,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
         if (act) atomicMax(&L.esc[e], (int32_t)sc);
         if (act && st == LB_NEW) L.est[e] = LB_MASKED;  // live
         wave_lds_sync();
+        LB_MARK(2);
       }
       if (hi >= cn) break;
       // ---- ban/2 at hi (:264-286)
@@ -1388,6 +1508,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
       }
       if (lane == 0) L.est[xe] = LB_BANNED;
       wave_lds_sync();
+      LB_MARK(3);
       j = hi + 1;
     }
   }
@@ -1412,6 +1533,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
   for (int i = 0; i < LbKeys<E>::R; ++i)
     if ((ks.live >> i) & 1u) L.est[(uint32_t)lane + 64u * i] = ks.u[i] >= t ? LB_OBS : LB_MASKED;
   wave_lds_sync();
+  LB_MARK(4);
   const uint32_t noff = (uint32_t)a.off_out[k];
   for (uint32_t j = lane; j < n; j += 64) {
     a.id_out[noff + j] = (int64_t)L.eid[j];
@@ -1423,6 +1545,7 @@ __device__ bool lb_board_sel(const LbArgs& a, uint32_t k, const LbMeta& om, cons
     a.meta_out[k] = m;
     a.ex_cnt[k] = nex;
   }
+  LB_MARK(5);
   return true;
 }
 

@@ -13,8 +13,11 @@ sys.path.insert(0, ROOT)
 from antidote_ccrdt_amd import _lib  # noqa: E402
 from antidote_ccrdt_amd.types import DeviceBatch, LeaderboardEngine  # noqa: E402
 
-NAMES = ["board init (+ old state, table)", "chunk ops + entry resolve", "run: prefilter, max, lead, rank",
-         "run: merge + statuses", "ban/2", "write-out"]
+# NARROW boards (lb_board_sel): init, resolve, runs (atomicMax), bans, final
+# selection, write-out.  (Wide boards, lb_board_par: the same slots 0/1/4/5,
+# 2 = run prefilter/max/lead/rank, 3 = run merge + statuses, 6-11 merges.)
+NAMES = ["board init (+ old state, table)", "chunk ops + entry resolve", "runs of adds",
+         "ban/2", "final selection + statuses", "write-out"]
 rng = np.random.default_rng(0xCC0DE)
 n, nk = int(os.environ.get("N_OPS", 50_000_000)), 100_000
 keys = np.sort(rng.integers(0, nk, n))
