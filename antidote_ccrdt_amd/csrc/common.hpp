@@ -193,6 +193,23 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
   v = o > v ? o : v;
   return rl32(v, 63);
 }
+// Wave minimum of a uint32 (DPP, identity 0xFFFFFFFF), wave-uniform result.
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) {
+  uint32_t o;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xf, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xa, 0xf, false);
+  v = o < v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xc, 0xf, false);
+  v = o < v ? o : v;
+  return rl32(v, 63);
+}
 // Exclusive DPP scan; `total` = wave sum (wave-uniform).
 __device__ __forceinline__ uint32_t wave_excl_scan_dpp(uint32_t v, uint32_t& total) {
   const uint32_t inc = wave_incl_scan_dpp(v);

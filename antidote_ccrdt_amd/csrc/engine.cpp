@@ -472,40 +472,56 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     if (first == 1) n_chain = 2, chain[1] = 2;
   }
   first_tier = chain[0];
+  for (int ci = 0; ci < n_chain; ++ci) E.trmv_overflow_keys[chain[ci]] = 0;
+  // The chain's head -- tier 0 and / or tier R, which take every key of the
+  // bench streams -- is queued in one go; its tier S tail only when the
+  // status read after the head says the head handed keys on (a chain that
+  // starts at tier S, K > 128, is all head).  Each segment's kernels read
+  // their list lengths from the device.
+  int n_head = 0;
+  while (n_head < n_chain && (chain[n_head] == 0 || chain[n_head] == 3)) ++n_head;
+  if (n_head == 0) n_head = n_chain;
   const uint32_t later_grid = (uint32_t)std::min<uint64_t>(nk, TRMV_LATER_GRID);
   DevBuf* work = nullptr;
   const uint32_t* n_dev = nullptr;
   int ev = 0;
-  CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-  for (int ci = 0; ci < n_chain && nk; ++ci) {
-    const int t = chain[ci];
-    DevBuf* ovf = &E.tier_ovf[t];
-    a.key_list = work ? work->as<uint32_t>() : nullptr;
-    a.n_list = work ? 0u : (uint32_t)nk;
-    a.n_list_dev = n_dev;
-    a.ovf_list = ovf->as<uint32_t>();
-    a.status = status + 2 + 2 * t;
-    const uint64_t grid = work ? later_grid : nk;
-    if (t == 0) CCRDT_TRY(trmv_launch_wave(a, grid, E.stream));
-    else if (t == 3) CCRDT_TRY(trmv_launch_resident(a, grid, E.stream));
-    else CCRDT_TRY(trmv_launch_steady(a, t - 1, grid, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    work = ovf;
-    n_dev = a.status;
-  }
-  CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
-  CCRDT_HIP(hipStreamSynchronize(E.stream));
   const uint32_t* hs = (const uint32_t*)E.h_status;
-  uint32_t err = 0;
-  for (int ci = 0; ci < n_chain; ++ci) err |= hs[3 + 2 * chain[ci]];
-  if (err) return trmv_err_code(err);
-  for (int ci = 0; ci < n_chain && nk; ++ci) {
-    const int t = chain[ci];
-    float ms = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[ci], E.evt[ci + 1]));
-    E.trmv_tier_ms[t] += ms;
-    E.trmv_overflow_keys[t] = hs[2 + 2 * t];
-  }
+  // chain[c0, c1): launches, one status read, the tiers' errors, times and hand-on counts
+  auto segment = [&](int c0, int c1) -> int {
+    const int e0 = ev;
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    for (int ci = c0; ci < c1 && nk; ++ci) {
+      const int t = chain[ci];
+      DevBuf* ovf = &E.tier_ovf[t];
+      a.key_list = work ? work->as<uint32_t>() : nullptr;
+      a.n_list = work ? 0u : (uint32_t)nk;
+      a.n_list_dev = n_dev;
+      a.ovf_list = ovf->as<uint32_t>();
+      a.status = status + 2 + 2 * t;
+      const uint64_t grid = work ? later_grid : nk;
+      if (t == 0) CCRDT_TRY(trmv_launch_wave(a, grid, E.stream));
+      else if (t == 3) CCRDT_TRY(trmv_launch_resident(a, grid, E.stream));
+      else CCRDT_TRY(trmv_launch_steady(a, t - 1, grid, E.stream));
+      CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+      work = ovf;
+      n_dev = a.status;
+    }
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    uint32_t err = 0;
+    for (int ci = c0; ci < c1; ++ci) err |= hs[3 + 2 * chain[ci]];
+    if (err) return trmv_err_code(err);
+    for (int ci = c0; ci < c1 && nk; ++ci) {
+      const int t = chain[ci];
+      float ms = 0.f;
+      CCRDT_HIP(hipEventElapsedTime(&ms, E.evt[e0 + ci - c0], E.evt[e0 + ci - c0 + 1]));
+      E.trmv_tier_ms[t] += ms;
+      E.trmv_overflow_keys[t] = hs[2 + 2 * t];
+    }
+    return CCRDT_OK;
+  };
+  CCRDT_TRY(segment(0, n_head));
+  if (n_head < n_chain && nk && hs[2 + 2 * chain[n_head - 1]] != 0) CCRDT_TRY(segment(n_head, n_chain));
   // Keys past the 1024-player class: tier 4 (HBM scratch), on the host-known
   // list tier 2 handed on.
   const uint32_t n_big = nk ? hs[2 + 2 * 2] : 0u;

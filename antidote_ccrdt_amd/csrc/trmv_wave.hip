@@ -1089,12 +1089,15 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     if (!ballot(has)) {
       best_q = NONE32;
     } else if (!ballot(has && !narrow)) {
-      // 32-bit Scores and Ids: (Score, Id) as one signed 64-bit key (the
-      // Id's sign bit flipped so it orders unsigned): one reduction
-      const int64_t k = (int64_t)(((uint64_t)(uint32_t)(int32_t)best_sc << 32) |
-                                  ((uint32_t)(int32_t)best_id ^ 0x80000000u));
-      const int64_t mk = wave_min_i64_dpp(has ? k : INT64_MAX);
-      best_q = rl32(best_q, (int)__builtin_ctzll(ballot(has && k == mk)));
+      // 32-bit Scores and Ids (sign bits flipped: unsigned order): the least
+      // Score, then the least Id among the lanes holding it -- two 32-bit DPP
+      // reductions (fused min per step) instead of one over 64-bit keys
+      const uint32_t us = has ? (uint32_t)(int32_t)best_sc ^ 0x80000000u : 0xFFFFFFFFu;
+      const uint32_t ms = wave_min_u32_dpp(us);
+      const bool at = has && us == ms;
+      const uint32_t ui = at ? (uint32_t)(int32_t)best_id ^ 0x80000000u : 0xFFFFFFFFu;
+      const uint32_t mi = wave_min_u32_dpp(ui);
+      best_q = rl32(best_q, (int)__builtin_ctzll(ballot(at && ui == mi)));
     } else {
       const int64_t ms = wave_min_i64_dpp(has ? best_sc : INT64_MAX);
       const int64_t mi = wave_min_i64_dpp(has && best_sc == ms ? best_id : INT64_MAX);

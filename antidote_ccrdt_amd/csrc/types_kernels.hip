@@ -1237,23 +1237,6 @@ __device__ __forceinline__ bool lb_load_keys(const V& L, uint32_t n, LbKeys<E>& 
   return ballot(zero) == 0;
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) {
-  uint32_t o;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xf, 0xf, false);
-  v = o < v ? o : v;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xf, 0xf, false);
-  v = o < v ? o : v;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xf, 0xf, false);
-  v = o < v ? o : v;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xf, 0xf, false);
-  v = o < v ? o : v;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xa, 0xf, false);
-  v = o < v ? o : v;
-  o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xc, 0xf, false);
-  v = o < v ? o : v;
-  return rl32(v, 63);
-}
-
 // The need-th largest of the multiset of values x[i] (every lane's R of
 // them; 0 = not a member, and a member 0 only ever ranks last, which the
 // descent returns as 0 too), 1 <= need <= members; mx / mn = the members'
