@@ -492,15 +492,24 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
   PROF_MARK(2);
   // ---- 4. player of every op, Vc, op elements in player order
   uint32_t xrank[2], xp[2];
+  {
+    // every lane reads its slots' player bytes and adds to a counter word
+    // (a lane without an op adds 0 to the word of its own lane index), so
+    // both slots' LDS round trips go out together instead of one after the
+    // other behind exec-masked branches
+    uint32_t hpv[2], cr[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const uint32_t p = xv[s] ? (uint32_t)L.hp[hs[s]] : PSINK;
-    xp[s] = p;
-    if (xa[s]) atomicMax(&L.vc[xdc[s]], (unsigned long long)xts[s]);  // vc_update (:233)
-    if (!FRESH && xr[s]) PFLAG(p) = 1;                              // a rmv: replayed
-    const uint32_t sh = 16 * (p & 1);
-    xrank[s] = 0;
-    if (xv[s]) xrank[s] = (atomicAdd(&L.pcnt2[p >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    for (int s = 0; s < 2; ++s) hpv[s] = L.hp[hs[s]];  // hs[s] < W_HCAP for every lane
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = xv[s] ? hpv[s] : PSINK;
+      xp[s] = p;
+      if (xa[s]) atomicMax(&L.vc[xdc[s]], (unsigned long long)xts[s]);  // vc_update (:233)
+      if (!FRESH && xr[s]) PFLAG(p) = 1;                              // a rmv: replayed
+      cr[s] = atomicAdd(&L.pcnt2[(xv[s] ? p : (uint32_t)lane) >> 1], xv[s] ? 1u << (16 * (p & 1)) : 0u);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) xrank[s] = xv[s] ? (cr[s] >> (16 * (xp[s] & 1))) & 0xFFFFu : 0u;
   }
   wave_lds_sync();
   // per player (lane, lane + 64): first position of its ops
