@@ -125,6 +125,7 @@ SIGNATURES = {
     "ccrdt_trmv_state_sizes": (INT, [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_trmv_range_sizes": (INT, [P, I64, I64, C.POINTER(I64), C.POINTER(I64), C.POINTER(I64)]),
     "ccrdt_trmv_key_sizes": (INT, [P, P, P, P, P]),
+    "ccrdt_trmv_set_fresh_room": (INT, [P, INT]),
     "ccrdt_trmv_replica_vc_device": (INT, [P, P]),
     "ccrdt_trmv_extras_device": (INT, [P, P, I64, P]),
     "ccrdt_trmv_exchange_pack": (INT, [P, P, I64, P, I64, C.c_uint32]),

@@ -227,6 +227,7 @@ int ccrdt_engine_reset(ccrdt_engine* e) {
   if (!e) return CCRDT_EINVAL;
   e->fresh = true;
   e->inplace_ready = false;
+  e->arena_pending = false;
   return e->reset_type();
 }
 
@@ -304,6 +305,18 @@ int trmv_err_code(uint32_t err) {
                                                                                                   : CCRDT_EINVAL;
 }
 
+// The pool's capacity factor of segments laid out for in-place growth
+// (a.slack): capacity = factor x (elements + the batch's ops) + 32, so later
+// batches append slabs in place (CCRDT_TRMV_POOL_SLACK = 2..8, tuning knob).
+int trmv_pool_slack() {
+  static const int v = [] {
+    const char* e = getenv("CCRDT_TRMV_POOL_SLACK");
+    const int x = e ? atoi(e) : 2;
+    return x < 2 ? 2 : (x > 8 ? 8 : x);
+  }();
+  return v;
+}
+
 // Capacities (elements) of a data side's arrays.
 void trmv_side_caps(const Engine& E, int ds, uint64_t cap[3]) {
   const TrmvBufs& b = E.trmv[ds];
@@ -322,8 +335,13 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   CCRDT_TRY(E.trmv[1 - E.mcur].meta.ensure(nk * sizeof(KeyMeta)));
   CCRDT_TRY(E.trmv[1 - E.mcur].cap.ensure(nk * sizeof(KeyCap)));
   a.inplace = 1;
+  a.slack = trmv_pool_slack();  // (relocations' pool capacity)
   a.old_s = E.trmv_side(E.mcur, E.cur);
   a.new_s = E.trmv_side(1 - E.mcur, E.cur);
+  if (E.arena_pending) {  // the sub-arena table the last full pass laid out
+    CCRDT_HIP(hipMemcpyAsync(E.arena.p, E.arena_sub, sizeof(E.arena_sub), hipMemcpyHostToDevice, E.stream));
+    E.arena_pending = false;
+  }
   a.arena = E.arena.as<unsigned long long>();
   a.arena_lim = E.arena.as<unsigned long long>() + 3 * TRMV_NSUB;
   a.lay_cnt = reinterpret_cast<uint32_t*>(E.arena.as<unsigned long long>() + 6 * TRMV_NSUB);
@@ -401,7 +419,14 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
   const int out = 1 - E.cur, mout = 1 - E.mcur;
   a.inplace = 0;
   a.fresh = E.fresh ? 1 : 0;
-  a.slack = (!E.fresh && E.k <= 128) ? 1 : 0;
+  // room for in-place growth when tier R can take the keys (K <= 128): the
+  // capacity scan's slack, or a fresh batch's roomy layout while its offsets
+  // fit 32 bits
+  a.slack = E.k <= 128 ? trmv_pool_slack() : 0;
+  if (E.fresh && !E.fresh_room) a.slack = 0;  // (ccrdt_trmv_set_fresh_room)
+  if (E.fresh && a.slack)
+    for (int x = 0; x < 3; ++x)
+      if (trmv_fresh_off(true, x, nk, n_ops) >= 0xFFFFFFFFull) a.slack = 0;
   a.old_s = E.trmv_side(E.mcur, E.cur);
   CCRDT_TRY(E.trmv[mout].meta.ensure(nk * sizeof(KeyMeta)));
   CCRDT_TRY(E.trmv[mout].cap.ensure(nk * sizeof(KeyCap)));
@@ -411,7 +436,8 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
   CCRDT_TRY(E.partials.ensure((nb * 3 + 3) * sizeof(uint64_t) + nk * sizeof(uint32_t)));
   // 1) capacities -> segment offsets of the new state (a fresh batch's
   //    offsets are the keys' op offsets: trmv_new_meta, no scan)
-  uint64_t tot[3] = {n_ops, n_ops, n_ops};
+  uint64_t tot[3];
+  for (int x = 0; x < 3; ++x) tot[x] = trmv_fresh_off(a.slack != 0, x, nk, n_ops);  // (fresh: no scan)
   if (!E.fresh && nk) {
     CCRDT_TRY(trmv_launch_scan(a, E.partials.as<uint64_t>(),
                                reinterpret_cast<uint32_t*>(E.partials.as<uint64_t>() + nb * 3 + 3), E.stream));
@@ -555,9 +581,12 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     CCRDT_TRY(trmv_launch_keep(a, std::min<uint32_t>((uint32_t)n_over, TRMV_LATER_GRID), E.stream));
   }
   // the arena of the new data arrays (only when in-place batches may
-  // follow: tier R wrote the keys with room): its top = the scan's totals,
-  // its free space cut into TRMV_NSUB sub-arenas
-  if (a.slack != 0 && first_tier == 3) {
+  // follow: tier 0 / tier R wrote the keys with room): its top = the
+  // layout's totals, its free space cut into TRMV_NSUB sub-arenas.  The
+  // device copy of the table is made by the next in-place pass (arena_pending),
+  // so a fresh batch that no resident batch follows pays no round trip for it.
+  const bool roomy = a.slack != 0 && (first_tier == 3 || first_tier == 0);
+  if (roomy) {
     trmv_side_caps(E, out, E.arena_cap);
     // CCRDT_TRMV_ARENA_ROOM=n (tests): at most n free elements past the top,
     // so relocations run out and the full rewrite that finishes a batch runs
@@ -573,13 +602,12 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
       E.arena_used[x] = 0;
     }
     CCRDT_TRY(E.arena.ensure(sizeof(sub) + 16 * TRMV_NSUB));
-    CCRDT_HIP(hipMemcpyAsync(E.arena.p, sub, sizeof(sub), hipMemcpyHostToDevice, E.stream));
-    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    E.arena_pending = true;
   }
   for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
   E.cur = out;
   E.mcur = mout;
-  E.inplace_ready = a.slack != 0 && first_tier == 3;
+  E.inplace_ready = roomy;
   return CCRDT_OK;
 }
 
@@ -679,6 +707,12 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
               "state, the other keys committed; ccrdt_engine_handed_on(e, 4) lists them");
     return CCRDT_EKEYCAP;
   }
+  return CCRDT_OK;
+}
+
+int ccrdt_trmv_set_fresh_room(ccrdt_engine* e, int on) {
+  CCRDT_TRY(check_trmv(e));
+  e->fresh_room = on != 0;
   return CCRDT_OK;
 }
 

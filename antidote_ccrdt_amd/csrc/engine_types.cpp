@@ -127,6 +127,8 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
     cur = src.cur;
     mcur = src.mcur;
     inplace_ready = src.inplace_ready;
+    arena_pending = src.arena_pending;
+    fresh_room = src.fresh_room;
     for (int x = 0; x < 3; ++x) trmv_tot[cur][x] = src.trmv_tot[src.cur][x];
     for (int x = 0; x < 3; ++x) {
       arena_cap[x] = src.arena_cap[x];

@@ -85,7 +85,7 @@ __device__ __forceinline__ void caps_of(const TrmvApplyArgs& a, uint64_t k, uint
     // append players, slabs and rows inside these segments)
     const KeyMeta m = a.old_s.meta[k];
     c[0] = (3 * ((uint64_t)m.np + nops)) / 2 + 8;
-    c[1] = 2 * ((uint64_t)m.nm + nops) + 32;
+    c[1] = (uint64_t)a.slack * ((uint64_t)m.nm + nops) + 32;  // (a.slack: the pool's factor)
     c[2] = (3 * ((uint64_t)m.nr + nrmv)) / 2 + 16;
   } else {
     const KeyMeta m = a.old_s.meta[k];

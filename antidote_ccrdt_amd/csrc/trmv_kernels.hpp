@@ -137,7 +137,8 @@ struct TrmvApplyArgs {
   uint16_t* obs_ord;                // [n_keys * TRMV_ORD] each key's Observed players, ascending (tier R)
   const uint8_t* key_done;          // non-null: 1 = the key's ops were applied already (it is rewritten, no ops)
   const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)
-  int32_t slack;                    // capacity scan: lay segments out with room for in-place growth
+  int32_t slack;                    // > 0: segments laid out with room for in-place growth, the pool's
+                                    // capacity slack x (its elements + the batch's ops) + 32
 };
 
 // The ops of key k in this pass (a key whose ops an earlier pass applied has
@@ -152,14 +153,28 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TrmvApplyArgs
   return kernarg_as<TrmvApplyArgs>();
 }
 
-// New-side metadata of key k before its tier writes it.  A fresh batch's
-// segments hold exactly the key's ops (capacity = ops for players, pool and
-// rows), so their offsets are the key's op offset and the capacity scan is
-// skipped; otherwise the scan laid them out in new_s.meta.
+// The fresh layout (no capacity scan): array x's segment of key k (x = 0
+// players, 1 pool, 2 rows) starts at F_x * o + C_x * k, o = key_ptr[k] (the
+// key's op offset), and holds F_x * ops + C_x.  With a.slack (later batches
+// may grow the keys in place) F = 3 / 6 / 1, C = 16 / 32 / 8: room for the
+// players, slabs and rows of the next batches without a relocation, and the
+// first resident batch runs in place; without, exactly the ops (F = 1, C = 0).
+__host__ __device__ __forceinline__ uint64_t trmv_fresh_off(bool room, int x, uint64_t k, uint64_t o) {
+  return room ? (x == 0 ? 3 * o + 16 * k : (x == 1 ? 6 * o + 32 * k : o + 8 * k)) : o;
+}
+__host__ __device__ __forceinline__ uint32_t trmv_fresh_cap(bool room, int x, uint32_t nops) {
+  return room ? (x == 0 ? 3 * nops + 16 : (x == 1 ? 6 * nops + 32 : nops + 8)) : nops;
+}
+
+// New-side metadata of key k before its tier writes it: a fresh batch's from
+// the fresh layout, otherwise what the capacity scan laid out in new_s.meta.
 __device__ __forceinline__ KeyMeta trmv_new_meta(const TrmvApplyArgs& a, uint64_t k) {
   if (a.fresh) {
     KeyMeta m;
-    m.p_off = m.m_off = m.r_off = (uint32_t)a.key_ptr[k];
+    const uint64_t o = a.key_ptr[k];
+    m.p_off = (uint32_t)trmv_fresh_off(a.slack != 0, 0, k, o);
+    m.m_off = (uint32_t)trmv_fresh_off(a.slack != 0, 1, k, o);
+    m.r_off = (uint32_t)trmv_fresh_off(a.slack != 0, 2, k, o);
     m.np = m.nm = m.nr = m.nobs = 0;
     m.minq = NONE32;
     return m;

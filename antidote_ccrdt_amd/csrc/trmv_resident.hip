@@ -913,7 +913,9 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
     KeyCap nc;
     if (fresh) {
       nm = trmv_new_meta(a, key);
-      nc.p_cap = nc.m_cap = nc.r_cap = nops;
+      nc.p_cap = trmv_fresh_cap(a.slack != 0, 0, nops);
+      nc.m_cap = trmv_fresh_cap(a.slack != 0, 1, nops);
+      nc.r_cap = trmv_fresh_cap(a.slack != 0, 2, nops);
     } else if (!inpl) {
       nm = KA->new_s.meta[key];
       nc = KA->new_s.cap[key];
@@ -935,7 +937,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
         // a new segment at the top of the workgroup's sub-arena, with room
         // to grow in place
         const uint32_t pc = np + np / 2u + 8u, rc = nr + nr / 2u + 16u;
-        const uint32_t mc = 2u * mtot + 32u > TRMV_SEG_MAX ? TRMV_SEG_MAX : 2u * mtot + 32u;
+        const uint32_t mc0 = (uint32_t)KA->slack * mtot + 32u, mc = mc0 > TRMV_SEG_MAX ? TRMV_SEG_MAX : mc0;
         const uint32_t sub = 3u * (blockIdx.x % (uint32_t)TRMV_NSUB);
         unsigned long long b0 = 0, b1 = 0, b2 = 0;
         if (lane == 0) {

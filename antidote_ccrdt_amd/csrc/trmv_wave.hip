@@ -196,9 +196,10 @@ __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t
     const uint32_t m = 8 * i + (lane >> 3);
     const uint32_t jm = m < n ? m : 0u;
     const uint32_t km = KA->key_list ? KA->key_list[c0 + jm] : c0 + jm;
-    if (KA->fresh) {  // trmv_new_meta: offsets = the key's op offset, counts 0, Min nil
+    if (KA->fresh) {  // trmv_new_meta: the fresh layout's offsets, counts 0, Min nil
       const uint32_t d = lane & 7;
-      h.meta[i] = d < 3 ? (uint32_t)KA->key_ptr[km] : (d == 7 ? NONE32 : 0u);
+      h.meta[i] = d < 3 ? (uint32_t)trmv_fresh_off(KA->slack != 0, (int)d, km, KA->key_ptr[km])
+                        : (d == 7 ? NONE32 : 0u);
     } else {
       h.meta[i] = reinterpret_cast<const uint32_t*>(a.new_s.meta + km)[lane & 7];
     }
@@ -1123,6 +1124,15 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
     out.minq = best_q;
     KA->new_s.meta[key] = out;
     KA->ex_cnt[key] = L.nex;
+    if (FRESH && KA->slack) {  // the fresh layout's room: later batches grow the key in place
+      KeyCap c;
+      c.p_cap = trmv_fresh_cap(true, 0, nops);
+      c.m_cap = trmv_fresh_cap(true, 1, nops);
+      c.r_cap = trmv_fresh_cap(true, 2, nops);
+      c.m_top = (uint16_t)nops;  // (every slab lies in the key's op positions)
+      c.flags = TRMV_CAP_VALID;
+      KA->new_s.cap[key] = c;
+    }
   }
   PROF_MARK(5);
   return W_DONE;

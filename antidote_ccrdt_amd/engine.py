@@ -322,6 +322,11 @@ class TopkRmvEngine(_Engine):
         check(lib.ccrdt_trmv_state_sizes(self.h, C.byref(a), C.byref(b), C.byref(c)), "sizes")
         return int(a.value), int(b.value), int(c.value)
 
+    def set_fresh_room(self, on: bool) -> None:
+        """Lay the next fresh batches out with room to grow in place
+        (ccrdt_trmv_set_fresh_room): for a stream of resident batches to follow."""
+        check(lib.ccrdt_trmv_set_fresh_room(self.h, 1 if on else 0), "set_fresh_room")
+
     def replica_vc_device(self, d_out: int) -> None:
         """Enqueue the shard's elementwise-max Vc into device int64[n_dc] at d_out."""
         check(lib.ccrdt_trmv_replica_vc_device(self.h, d_out), "replica_vc_device")

@@ -195,6 +195,15 @@ int ccrdt_trmv_extra_count(ccrdt_engine* e, int64_t* n);
 /* Copy the last apply's extra effects into op-indexed host arrays. */
 int ccrdt_trmv_fetch_extra(ccrdt_engine* e, ccrdt_trmv_extra* extra);
 
+/* Layout of the next fresh batches (after ccrdt_engine_create / _reset):
+ * on != 0 lays each key out with room to grow (players 3x its ops + 16,
+ * Masked pool 6x + 32, Removals rows 1x + 8), so the resident batches that
+ * follow update it in place from the first one on, instead of rewriting
+ * every key once to give it room; 0 (the default) lays the fresh batch out
+ * tight, which writes it about 3% faster.  Only with Size <= 128 (tier R's
+ * class) and while the layout's offsets fit 32 bits; else ignored. */
+int ccrdt_trmv_set_fresh_room(ccrdt_engine* e, int on);
+
 /* Device side of the cluster's two exchange steps (the
  * collectives are the caller's, e.g. RCCL).  Both are enqueued on the engine
  * stream (ccrdt_engine_stream) and do not wait.

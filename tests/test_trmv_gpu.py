@@ -219,27 +219,31 @@ def test_empty_batch_and_reset(gpu):
     _compare(eng, orac, b, D, xe, xo)
 
 
-@pytest.mark.parametrize("room", [None, 0, 3000])
-def test_inplace_stream_arena(gpu, room, monkeypatch):
+@pytest.mark.parametrize("room,fresh_room", [(None, False), (0, False), (3000, False), (None, True), (0, True)])
+def test_inplace_stream_arena(gpu, room, fresh_room, monkeypatch):
     """Resident batches updated in place (tier R: appends, slab moves to the
     pool's top, pool compaction, relocation of keys to the arena's top), with
     the arena unlimited, empty (every relocation fails: the full rewrite that
-    finishes the batch runs) or small (some fit): bit-exact after every batch,
-    then export / import / clone / downstream on the arena layout."""
+    finishes the batch runs) or small (some fit), the first batch laid out
+    tight or with room (ccrdt_trmv_set_fresh_room: tier 0's closed-form roomy
+    segments, then in place from the second batch on): bit-exact after every
+    batch, then export / import / clone / downstream on the arena layout."""
     if room is not None:
         monkeypatch.setenv("CCRDT_TRMV_ARENA_ROOM", str(room))
     nk, D, K = 3000, 8, 100
     eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    eng.set_fresh_room(fresh_room)
     n = 95 * nk
-    inplace = finished = 0
+    inplace, finished = [], 0
     for i in range(7):
         b = gen_trmv(n, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64, dup_pm=5, swap_pm=5,
                      seed=4100 + i, clock0=i * n)
         xe, xo = eng.apply(b), orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
-        inplace += eng.tier_ms(5) > 0         # (the in-place pass validated the batch)
+        inplace.append(eng.tier_ms(5) > 0)    # (the in-place pass validated the batch)
         finished += eng.overflow_keys(5) > 0  # (keys it left to the full rewrite)
-    assert inplace >= 4
+    assert sum(inplace) >= 4
+    assert inplace[1] == fresh_room  # the first resident batch: in place only on a roomy fresh layout
     if room == 0:
         assert finished >= 1
     st = eng.export()

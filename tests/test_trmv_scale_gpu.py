@@ -105,20 +105,25 @@ def _progress(msg):
 
 
 @pytest.mark.timeout(900)
-def test_steady_state_bench_size(gpu):
+@pytest.mark.parametrize("fresh_room", [False, True])
+def test_steady_state_bench_size(gpu, fresh_room):
     """bench.py's steady-state leg at its own size: 2^20 resident keys, the
     bench batch (100M ops, seed 0xCC0DE+2) and then steady batches 2..4 of the
     same stream (seeds and clocks as bench.py's detail.steady_state), each
     through the device entry point (apply_device) and compared with the
     threaded oracle after every batch: every key's state and every extra
-    effect, bit-exact (src/antidote_ccrdt_topk_rmv.erl:231-334).  The
-    resident buffers must grow: after the fresh batch they hold that batch's
-    100M-element bound, and the first steady batch needs old state + 100M."""
+    effect, bit-exact (src/antidote_ccrdt_topk_rmv.erl:231-334).  Tight
+    fresh layout: the resident buffers must grow (after the fresh batch they
+    hold that batch's 100M-element bound, and the first steady batch needs old
+    state + 100M), and the steady batches run as full rewrite, then in place.
+    Roomy fresh layout (bench.py's steady leg, ccrdt_trmv_set_fresh_room):
+    the fresh batch and two steady batches, both in place."""
     n_ops, nk, D, K = 100_000_000, 1 << 20, 8, 100
     seed = 0xCC0DE + 2
     eng = TopkRmvEngine(nk, K, D)
+    eng.set_fresh_room(fresh_room)
     o = orc.TrmvOracle(nk, K, D)
-    for i in range(4):
+    for i in range(3 if fresh_room else 4):
         b = gen_trmv(n_ops, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64,
                      seed=seed + (7919 * i if i else 0), clock0=i * n_ops)
         db = DeviceTrmvBatch(b)
@@ -132,6 +137,8 @@ def test_steady_state_bench_size(gpu):
         sizes = eng.sizes()
         _progress(f"batch {i + 1}: tiers {[eng.tier_ms(t) for t in range(5)]} state {sizes} bad {bad}")
         assert not bad, f"batch {i + 1}: fields differ from the oracle: {bad}"
+        if i == 1:  # the first resident batch: in place only on the roomy fresh layout
+            assert (eng.tier_ms(5) > 0) == fresh_room
         del se, xe, xo
     nobs = np.diff(eng.export().obs_ptr.astype(np.int64))
     assert (nobs == K).mean() > 0.99 and sizes[1] > 2 * n_ops  # Observed full, Masked past 2x a batch
