@@ -71,8 +71,8 @@ struct ccrdt_engine {
   // out with room to grow (inplace_ready); relocations take space from the
   // data arrays' arena (device bump counters, capacities in elements).
   bool inplace_ready = false;
-  bool arena_pending = false;
-  bool fresh_room = false;     // fresh batches laid out with room to grow in place (ccrdt_trmv_set_fresh_room)  // arena_sub not yet copied to the device (the next in-place pass does it)
+  bool arena_pending = false;  // arena_sub not yet copied to the device (the next in-place pass does it)
+  bool fresh_room = false;     // fresh batches laid out with room to grow in place (ccrdt_trmv_set_fresh_room)
   uint64_t arena_cap[3] = {0, 0, 0};
   uint64_t arena_sub[2][ccrdt::TRMV_NSUB][3] = {};  // each sub-arena's start and end (host copy)
   uint64_t arena_used[3] = {0, 0, 0};               // elements the in-place passes took since the rewrite
