@@ -94,10 +94,13 @@ def main():
         dom = [k for k in out if a.dominant in k and "[grid" not in k]
         if len(dom) != 1 or "hbm_bytes" not in out[dom[0]]:
             raise SystemExit(f"dominant kernel {a.dominant!r} not found with FETCH/WRITE counters")
-        st = [k for k in out if a.steady and a.steady in k and "[grid" not in k and "hbm_bytes" in out[k]]
+        # (tier R has two instantiations, in place and full rewrite; the steady
+        # leg's batches are the launches that move the most bytes)
+        st = sorted((k for k in out if a.steady and a.steady in k and "[grid" not in k and "hbm_bytes" in out[k]),
+                    key=lambda k: out[k]["hbm_bytes"], reverse=True)
         steady = ({"kernel": st[0], "hbm_bytes_per_launch": out[st[0]]["hbm_bytes"],
                    "fetch_kib": out[st[0]]["FETCH_SIZE"], "write_kib": out[st[0]]["WRITE_SIZE"]}
-                  if len(st) == 1 else None)
+                  if st else None)
         with open(a.bench_json, "w") as f:
             json.dump({"n_ops": a.n_ops, "n_keys": a.n_keys, "kernel": dom[0], "steady": steady,
                        "hbm_bytes_per_launch": out[dom[0]]["hbm_bytes"],
