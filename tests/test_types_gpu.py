@@ -338,3 +338,36 @@ def test_leaderboard_hbm_class(gpu):
         m = xo["kind"] == 0
         assert np.array_equal(xe["id"][m], xo["id"][m]) and np.array_equal(xe["score"][m], xo["score"][m])
         assert not e.export().diff(o.export())
+
+
+def _lb_check(e, o, b):
+    xe, xo = e.apply(*b), o.apply(*b)
+    assert np.array_equal(xe["kind"], xo["kind"])
+    m = xo["kind"] == 0
+    assert np.array_equal(xe["id"][m], xo["id"][m]) and np.array_equal(xe["score"][m], xo["score"][m])
+    assert not e.export().diff(o.export())
+
+
+@pytest.mark.parametrize("K", [1, 3, 100, 200, 1000])
+def test_leaderboard_selection_edges(gpu, K):
+    """The 32-bit boards by selection (types_kernels.hip lb_board_sel) at their
+    edges, over three batches (state carried): Size 1 to past every board's
+    entries (Size > 128 included), ban-heavy boards (bans of absent, banned and
+    Observed Ids, adds after bans), ties on Score (the Id word decides), and
+    the 32-bit extremes -- INT32_MIN / INT32_MAX Scores and Ids, and the one
+    key (Score, Id) = (INT32_MIN, INT32_MIN) the selection hands to the replay."""
+    rng = np.random.default_rng(1000 + K)
+    lo, hi = -(2**31), 2**31 - 1
+    nk = 40
+    e, o = LeaderboardEngine(nk, K), orc.LbOracle(nk, K)
+    for it in range(3):
+        n = 12000
+        kp, kind, pid, sc = _lb_stream(rng, n, nk, 300, 50, 0.15 if it == 1 else 0.02)
+        pid = pid.astype(np.int64) + lo // 2
+        sc = sc.astype(np.int64) - 25
+        ext = rng.choice(n, 40, replace=False)
+        sc[ext[:10]], sc[ext[10:20]] = lo, hi
+        pid[ext[20:25]], pid[ext[25:30]] = lo, hi
+        if it == 2:  # the (INT32_MIN, INT32_MIN) key on one board
+            pid[ext[30]], sc[ext[30]], kind[ext[30]] = lo, lo, 0
+        _lb_check(e, o, (kp, kind, pid, sc))
