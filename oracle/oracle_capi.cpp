@@ -110,20 +110,49 @@ int orc_trmv_apply(void* h, const uint64_t* key_ptr, const uint8_t* kind, const 
   return 0;
 }
 
+// (the export's passes run on every host CPU, at most 16: a 2^20-key state of
+// 370M Masked elements took ~40 s on one thread)
+int export_threads() {
+  const unsigned hw = std::thread::hardware_concurrency();
+  return (int)std::min<unsigned>(16u, hw ? hw : 1u);
+}
+
+// Per key: |Observed|, |Masked| (all Ids), |Removals|.
+void trmv_key_counts(const TrmvSet* s, std::vector<uint64_t>& co, std::vector<uint64_t>& cm,
+                     std::vector<uint64_t>& cr) {
+  const int64_t nk = (int64_t)s->keys.size();
+  co.assign(nk, 0);
+  cm.assign(nk, 0);
+  cr.assign(nk, 0);
+  parallel_keys(nk, export_threads(), [&](int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const TopkRmv& st = s->keys[k];
+      uint64_t m = 0;
+      for (auto& [i, set] : st.masked) m += set.size();
+      co[k] = st.obs.size();
+      cm[k] = m;
+      cr[k] = st.removals.size();
+    }
+  });
+}
+
 void orc_trmv_sizes(void* h, int64_t* n_obs, int64_t* n_masked, int64_t* n_rows) {
   auto* s = (TrmvSet*)h;
+  std::vector<uint64_t> co, cm, cr;
+  trmv_key_counts(s, co, cm, cr);
   int64_t o = 0, m = 0, r = 0;
-  for (auto& st : s->keys) {
-    o += st.obs.size();
-    for (auto& [i, set] : st.masked) m += set.size();
-    r += st.removals.size();
+  for (size_t k = 0; k < co.size(); ++k) {
+    o += co[k];
+    m += cm[k];
+    r += cr[k];
   }
   *n_obs = o;
   *n_masked = m;
   *n_rows = r;
 }
 
-// Canonical image, same layout as ccrdt_trmv_state.
+// Canonical image, same layout as ccrdt_trmv_state: the per-key offsets from
+// one counting pass, then every key written in parallel.
 void orc_trmv_export(void* h, int64_t* vc, uint64_t* obs_ptr, int64_t* obs_id, int64_t* obs_score,
                      uint8_t* obs_dc, int64_t* obs_ts, uint64_t* m_ptr, int64_t* m_id,
                      int64_t* m_score, uint8_t* m_dc, int64_t* m_ts, uint64_t* r_ptr, int64_t* r_id,
@@ -131,41 +160,48 @@ void orc_trmv_export(void* h, int64_t* vc, uint64_t* obs_ptr, int64_t* obs_id, i
                      uint8_t* min_dc, int64_t* min_ts) {
   auto* s = (TrmvSet*)h;
   const int D = s->D;
-  uint64_t po = 0, pm = 0, pr = 0;
+  const int64_t nk = (int64_t)s->keys.size();
+  std::vector<uint64_t> co, cm, cr;
+  trmv_key_counts(s, co, cm, cr);
   obs_ptr[0] = m_ptr[0] = r_ptr[0] = 0;
-  for (size_t k = 0; k < s->keys.size(); ++k) {
-    const TopkRmv& st = s->keys[k];
-    for (int d = 0; d < D; ++d) vc[k * D + d] = vc_get(st.vc, d);
-    for (auto& [i, e] : st.obs) {  // std::map: sorted by id
-      obs_id[po] = e.id;
-      obs_score[po] = e.score;
-      obs_dc[po] = (uint8_t)e.dc;
-      obs_ts[po] = e.ts;
-      ++po;
-    }
-    for (auto& [i, set] : st.masked) {  // by id, then term order inside
-      for (auto& e : set) {
-        m_id[pm] = e.id;
-        m_score[pm] = e.score;
-        m_dc[pm] = (uint8_t)e.dc;
-        m_ts[pm] = e.ts;
-        ++pm;
-      }
-    }
-    for (auto& [i, v] : st.removals) {
-      r_id[pr] = i;
-      for (int d = 0; d < D; ++d) r_vc[pr * D + d] = vc_get(v, d);
-      ++pr;
-    }
-    obs_ptr[k + 1] = po;
-    m_ptr[k + 1] = pm;
-    r_ptr[k + 1] = pr;
-    min_valid[k] = st.min ? 1 : 0;
-    min_id[k] = st.min ? st.min->id : 0;
-    min_score[k] = st.min ? st.min->score : 0;
-    min_dc[k] = st.min ? (uint8_t)st.min->dc : 0;
-    min_ts[k] = st.min ? st.min->ts : 0;
+  for (int64_t k = 0; k < nk; ++k) {
+    obs_ptr[k + 1] = obs_ptr[k] + co[k];
+    m_ptr[k + 1] = m_ptr[k] + cm[k];
+    r_ptr[k + 1] = r_ptr[k] + cr[k];
   }
+  parallel_keys(nk, export_threads(), [&](int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const TopkRmv& st = s->keys[k];
+      uint64_t po = obs_ptr[k], pm = m_ptr[k], pr = r_ptr[k];
+      for (int d = 0; d < D; ++d) vc[k * D + d] = vc_get(st.vc, d);
+      for (auto& [i, el] : st.obs) {  // std::map: sorted by id
+        obs_id[po] = el.id;
+        obs_score[po] = el.score;
+        obs_dc[po] = (uint8_t)el.dc;
+        obs_ts[po] = el.ts;
+        ++po;
+      }
+      for (auto& [i, set] : st.masked) {  // by id, then term order inside
+        for (auto& el : set) {
+          m_id[pm] = el.id;
+          m_score[pm] = el.score;
+          m_dc[pm] = (uint8_t)el.dc;
+          m_ts[pm] = el.ts;
+          ++pm;
+        }
+      }
+      for (auto& [i, v] : st.removals) {
+        r_id[pr] = i;
+        for (int d = 0; d < D; ++d) r_vc[pr * D + d] = vc_get(v, d);
+        ++pr;
+      }
+      min_valid[k] = st.min ? 1 : 0;
+      min_id[k] = st.min ? st.min->id : 0;
+      min_score[k] = st.min ? st.min->score : 0;
+      min_dc[k] = st.min ? (uint8_t)st.min->dc : 0;
+      min_ts[k] = st.min ? st.min->ts : 0;
+    }
+  });
 }
 
 // downstream/2: op 0 add (dc, ts supplied), 1 rmv.  out_kind: 0 add 1 add_r
