@@ -393,39 +393,6 @@ __device__ __forceinline__ void ob_remove(Obs& o, uint32_t r) {
   ob_clear_tail(o);
 }
 
-// Bitonic sort of the 128 positions ascending by key (sentinels last).  Used
-// once for a key whose players were not written in sorted-Observed order.
-__device__ __forceinline__ void ob_sort(Obs& o) {
-  const uint32_t l = (uint32_t)lane_id();
-#pragma unroll 1
-  for (uint32_t k = 2; k <= 128; k <<= 1) {
-#pragma unroll 1
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      if (j == 64) {  // partner = the other slot, same lane (k == 128: ascending)
-        if (o.key[1] < o.key[0]) {
-          const int64_t t = o.key[0]; o.key[0] = o.key[1]; o.key[1] = t;
-          const uint32_t u = o.pl[0]; o.pl[0] = o.pl[1]; o.pl[1] = u;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t i = 64u * s + l;
-        const int src = (int)(l ^ j);
-        const int64_t pk = shfl64(o.key[s], src);
-        const uint32_t pp = shfl32(o.pl[s], src);
-        const bool lower = (i & j) == 0;  // this position is the lower of its pair
-        const bool asc = (i & k) == 0;    // this block sorts ascending
-        const bool take = (lower == asc) ? pk < o.key[s] : o.key[s] < pk;
-        if (take) {
-          o.key[s] = pk;
-          o.pl[s] = pp;
-        }
-      }
-    }
-  }
-}
-
 __device__ __forceinline__ void r_emit(const TrmvApplyArgs& a, RLds& L, uint64_t op0, uint64_t op, uint8_t kind,
                                        int64_t id, int64_t sc, uint32_t dc, int64_t ts, const Row8* vc) {
   const uint32_t pos = atomicAdd(&L.nex, 1u);
@@ -820,7 +787,30 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
           }
         }
       }
-      ob_sort(ob);
+      // sorted by rank: each entry counts the keys below it (distinct Ids,
+      // so distinct keys), every key broadcast from its lane, one round per
+      // entry; then each entry goes to its rank through LDS (nslab is first
+      // written in P2) and its key is made again from its player.  (A bitonic
+      // sort on LDS-crossbar shuffles took ~18k cycles per key here.)
+      uint32_t rk[2] = {0u, 0u};
+      for (uint32_t i = 0; i < ob.n; ++i) {
+        const int64_t ki = i < 64u ? rl64(ob.key[0], (int)i) : rl64(ob.key[1], (int)(i - 64u));
+        rk[0] += ki < ob.key[0] ? 1u : 0u;
+        rk[1] += ki < ob.key[1] ? 1u : 0u;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (64u * t + lane < ob.n) L.nslab[rk[t]] = ob.pl[t];
+      wave_lds_sync();
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (64u * t + lane < ob.n) {
+          const uint32_t pl = L.nslab[64u * t + lane], p = pl & 0xFFFFu;
+          ob.pl[t] = pl;
+          ob.key[t] = mkkey(L.msc[p], L.u.r.pid[p]);
+        }
+      }
+      wave_lds_sync();
     }
   }
   ob_clear_tail(ob);
