@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of rocprofv3 PMC passes (tools/profile.sh output).
+"""Per-kernel averages of rocprofv3 PMC passes (tools/pmc.sh output).
 
     python tools/pmc_summary.py gpurun_out/prof [--json out.json] [--kernel NAME]
 
@@ -107,7 +107,7 @@ def main():
                        "fetch_kib": out[dom[0]]["FETCH_SIZE"], "write_kib": out[dom[0]]["WRITE_SIZE"],
                        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 counts half "
                                "of a wide coalesced read); averaged over the dispatches of the "
-                               "tools/profile.sh passes"}, f, indent=1)
+                               "tools/pmc.sh passes"}, f, indent=1)
 
 
 if __name__ == "__main__":
