@@ -1038,8 +1038,9 @@ class _TorchBatch:
 
 def _lb_apply_csr_device(engine, kp, kind, id_, score):
     """Apply a batch already in canonical order (CSR by key) on the device;
-    returns the extras as rows [m, 6] (key, -, op index in the batch, kind,
-    id, score; origin and seq are the caller's)."""
+    returns its extras as one run (key, kind, id, score) in (key, op index)
+    order, i.e. the stream order of leaderboard.erl:282-284's re-broadcast
+    (kind 0 = {add, {Id, Score}})."""
     import torch
 
     from . import _lib
@@ -1053,103 +1054,121 @@ def _lb_apply_csr_device(engine, kp, kind, id_, score):
                "lb_extras_device")
     engine.sync()
     m = int(cnt.item())
-    out = torch.empty((m, 6), dtype=torch.int64, device=dev)
-    if m:
-        e = ex[:m]
-        out[:, 0] = e[:, 0]
-        out[:, 2] = e[:, 1]  # op index in the applied batch: stream order of the extras
-        out[:, 3] = 0        # {add, {Id, Score}} (leaderboard.erl:282-284)
-        out[:, 4] = e[:, 2]
-        out[:, 5] = e[:, 3]
-    return out
-
-
-def _lb_canonical(rows):
-    """rows sorted by (key, origin, seq): one sort of a packed 64-bit key
-    when key < 2^23, origin < 16 and seq < 2^36, else three stable sorts."""
-    import torch
-    if not rows.shape[0]:
-        return rows
-    if (int(rows[:, 0].max()) < (1 << 23) and int(rows[:, 1].max()) < 16 and int(rows[:, 2].max()) < (1 << 36)
-            and int(rows[:, :3].min()) >= 0):
-        return rows[torch.argsort((rows[:, 0] << 40) | (rows[:, 1] << 36) | rows[:, 2])]
-    order = torch.argsort(rows[:, 2], stable=True)
-    for c in (1, 0):
-        order = order[torch.argsort(rows[order, c], stable=True)]
-    return rows[order]
-
-
-def _lb_apply_rows_device(engine, rows, by_key_only: bool = False):
-    """Apply effect rows in canonical order (key, origin, seq) on the device;
-    returns the extras as rows (origin/seq left to the caller).
-    by_key_only: the rows are already in (origin, seq) order within every key
-    (origins concatenated in order, each in (key, seq) order), so a stable
-    sort by the key alone puts them in canonical order."""
-    import torch
-    nk = engine.n_keys
-    if by_key_only:
-        ks, order = torch.sort(rows[:, 0], stable=True)
-        r = rows.index_select(0, order)
+    if not m:
+        return None
+    e = ex[:m]  # (key, op index, id, score), in the order the kernel appended them
+    if n < (1 << 40) and engine.n_keys < (1 << 23):
+        order = torch.argsort((e[:, 0] << 40) | e[:, 1])
     else:
-        r = _lb_canonical(rows)
-        ks = r[:, 0].contiguous()
-    kp = torch.searchsorted(ks, torch.arange(nk + 1, dtype=ks.dtype, device=ks.device))
-    return _lb_apply_csr_device(engine, kp, r[:, 3].to(torch.uint8).contiguous(), r[:, 4].contiguous(),
-                                r[:, 5].contiguous())
+        order = torch.argsort(e[:, 1], stable=True)
+        order = order[torch.argsort(e[order, 0], stable=True)]
+    e = e.index_select(0, order)
+    return (e[:, 0].contiguous(), torch.zeros(m, dtype=torch.int64, device=dev), e[:, 2].contiguous(),
+            e[:, 3].contiguous())
+
+
+# A replica's message for one delivery round is one flat int64 tensor of RUNS,
+# each run sorted by key and holding rows of one origin in seq order: a
+# replica's first message is its batch (seq 0..n-1) and then the batch's
+# extras (seq n..), later messages one run of extras.  Layout:
+# [n_runs, len_0, len_1 | run 0: key[len_0] kind[len_0] id[len_0] score[len_0] | run 1 ...]
+# (an empty message is a zero-length tensor).  The canonical order of
+# ReplicatedLeaderboard (key, origin, seq) is then a merge of the runs, each
+# row's position counted by binary search in the other runs: no sort and no
+# gather of rows (the [n, 6] rows of the host protocol cost 3x the step).
+_LB_HDR = 3
+
+
+def _lb_message(runs):
+    import torch
+    runs = [r for r in runs if r is not None and int(r[0].shape[0])]
+    if not runs:
+        return torch.empty(0, dtype=torch.int64, device="cuda")
+    dev = runs[0][0].device
+    lens = [int(r[0].shape[0]) for r in runs]
+    hdr = torch.tensor([len(runs)] + lens + [0] * (_LB_HDR - 1 - len(runs)), dtype=torch.int64, device=dev)
+    return torch.cat([hdr] + [c.to(torch.int64) for r in runs for c in r])
+
+
+def _lb_runs(msgs):
+    """The runs of several messages, in message order (one header read)."""
+    import torch
+    msgs = [m for m in msgs if int(m.shape[0])]
+    if not msgs:
+        return []
+    hdrs = torch.stack([m[:_LB_HDR] for m in msgs]).cpu().tolist()
+    runs = []
+    for m, h in zip(msgs, hdrs):
+        off = _LB_HDR
+        for L in h[1:1 + h[0]]:
+            runs.append(tuple(m[off + j * L:off + (j + 1) * L] for j in range(4)))
+            off += 4 * L
+    return runs
+
+
+def _lb_merge_runs(runs, n_keys: int):
+    """(key_ptr, kind u8, id, score) of the runs merged into canonical order:
+    a row of run a with key k at index i lands at i + (rows of earlier runs
+    with key <= k) + (rows of later runs with key < k)."""
+    import torch
+    q = torch.arange(n_keys + 1, dtype=torch.int64, device=runs[0][0].device)
+    if len(runs) == 1:
+        k, kind, id_, sc = runs[0]
+        return torch.searchsorted(k, q), kind.to(torch.uint8), id_, sc
+    N = sum(int(r[0].shape[0]) for r in runs)
+    dev = runs[0][0].device
+    kind_o = torch.empty(N, dtype=torch.uint8, device=dev)
+    id_o = torch.empty(N, dtype=torch.int64, device=dev)
+    sc_o = torch.empty(N, dtype=torch.int64, device=dev)
+    kp = torch.zeros(n_keys + 1, dtype=torch.int64, device=dev)
+    for a, (ka, kind, id_, sc) in enumerate(runs):
+        pos = torch.arange(int(ka.shape[0]), dtype=torch.int64, device=dev)
+        for b, r in enumerate(runs):
+            if b != a:
+                pos += torch.searchsorted(r[0], ka, right=b < a)
+        kind_o[pos] = kind.to(torch.uint8)
+        id_o[pos] = id_
+        sc_o[pos] = sc
+        kp += torch.searchsorted(ka, q)
+    return kp, kind_o, id_o, sc_o
 
 
 class LbDeviceReplica:
     """One DC replica of n_keys leaderboards with its effect rows on the
     device (BASELINE configs[3]; the protocol of ReplicatedLeaderboard,
-    leaderboard.erl:128-134,282-284).  Rows are int64 [n, 6] = key, origin,
-    seq, kind, id, score.  A step is originate() and then deliver() per
-    round; the exchange between them is injected: lb_replicate_step with a
+    leaderboard.erl:128-134,282-284, whose canonical (key, origin, seq) order
+    the run merge reproduces).  A step is originate() and then deliver() per
+    round, each returning the message (runs, above) this replica sends; the
+    exchange between them is injected: lb_replicate_step with a
     TorchCollective (one process per GPU) or lb_replicate_device_local
     (replicas held by one process, exchange = the list of every replica's
-    rows).  Both run exactly these two methods."""
+    messages).  Both run exactly these two methods."""
 
     def __init__(self, engine, rank: int, world: int):
         self.engine, self.rank, self.world = engine, rank, world
-        self.seq = 0
-        self.first = True
 
     def originate(self, batch):
         """Apply this replica's own batch (device (key_ptr, kind, id, score),
         CSR by key, stream order) -- already canonical for one origin -- and
-        return the rows it sends: the batch, then its extras, each in (key,
-        seq) order."""
+        return its message: the batch, then its extras."""
         import torch
         kp, kind, id_, score = batch
         kp = kp.long()
         n, nk = int(kind.shape[0]), int(kp.shape[0]) - 1
         dev = kind.device
         ex = _lb_apply_csr_device(self.engine, kp, kind.contiguous(), id_.contiguous(), score.contiguous())
-        own = torch.empty((n, 6), dtype=torch.int64, device=dev)
-        own[:, 0] = torch.repeat_interleave(torch.arange(nk, device=dev), kp[1:] - kp[:-1], output_size=n)
-        own[:, 1] = self.rank
-        own[:, 2] = torch.arange(n, device=dev)
-        own[:, 3] = kind.long()
-        own[:, 4] = id_
-        own[:, 5] = score
-        ex[:, 1] = self.rank
-        ex[:, 2] += n  # extras: seq = n + op index
-        self.seq, self.first = 2 * n, True
-        return torch.cat([own, _lb_canonical(ex)])
+        keys = torch.repeat_interleave(torch.arange(nk, device=dev), kp[1:] - kp[:-1], output_size=n)
+        return _lb_message([(keys, kind, id_, score), ex])
 
     def deliver(self, parts):
-        """Apply the rows of every other origin (parts[o] = origin o's rows)
-        in canonical order; returns the extras that produced, stamped as
-        this replica's rows."""
-        import torch
-        rows = torch.cat([p for o, p in enumerate(parts) if o != self.rank])
-        first, self.first = self.first, False
-        if not rows.shape[0]:
-            return rows
-        ex = _lb_apply_rows_device(self.engine, rows, by_key_only=first)
-        ex[:, 1] = self.rank
-        ex[:, 2] += self.seq
-        self.seq += int(rows.shape[0])
-        return ex
+        """Apply the messages of every other origin (parts[o] = origin o's)
+        merged into canonical order; returns the message of the extras that
+        produced."""
+        runs = _lb_runs([p for o, p in enumerate(parts) if o != self.rank])
+        if not runs:
+            return _lb_message([])
+        kp, kind, id_, sc = _lb_merge_runs(runs, self.engine.n_keys)
+        return _lb_message([_lb_apply_csr_device(self.engine, kp, kind, id_, sc)])
 
 
 def lb_replicate_step(replica: LbDeviceReplica, batch, coll, max_rounds: int = 64) -> int:
@@ -1167,7 +1186,7 @@ def lb_replicate_step(replica: LbDeviceReplica, batch, coll, max_rounds: int = 6
 
 def lb_replicate_device_local(engines, batches, max_rounds: int = 64) -> int:
     """lb_replicate_step for several replicas held by one process (the
-    all-gather is the list of every replica's rows).  `batches` are
+    all-gather is the list of every replica's messages).  `batches` are
     (key_ptr, kind, id, score) device tensors, CSR by key.  Returns the
     number of delivery rounds."""
     reps = [LbDeviceReplica(e, r, len(engines)) for r, e in enumerate(engines)]
