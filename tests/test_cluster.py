@@ -423,3 +423,71 @@ def test_replica_vc_not_stale_after_apply():
     s.apply(b2)
     v2 = s.replica_vc()
     assert (v2 > v1).any() and np.array_equal(v2, s.export()["vc"].max(axis=0))
+
+
+def _rccl_worker(rank, world, port, errf):
+    """TorchCollective on the nccl backend (RCCL; device tensors, nothing
+    staged through the host): every primitive the exchanges use, then a
+    leaderboard replication step over it (lb_replicate_step) checked against
+    a replica applied on its own."""
+    import torch
+    import torch.distributed as dist
+
+    from antidote_ccrdt_amd.cluster import LbDeviceReplica, TorchCollective, lb_replicate_step
+    from antidote_ccrdt_amd.types import LeaderboardEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        c = TorchCollective(dist)
+        assert not c.staged and c.device.type == "cuda"
+        t = torch.arange(10, dtype=torch.int64, device="cuda") + 100 * rank
+        assert [int(x[3]) for x in c.all_gather(t)] == [100 * r + 3 for r in range(world)]
+        g = c.all_gather_into(t)
+        assert g.shape == (world, 10) and g.is_cuda and int(g[-1, 9]) == 100 * (world - 1) + 9
+        v = torch.arange(3 + rank, dtype=torch.int64, device="cuda")
+        assert [int(x.shape[0]) for x in c.all_gather_v(v)] == [3 + r for r in range(world)]
+        out, sizes = c.all_to_all_v(torch.arange(2 * world, dtype=torch.int64, device="cuda"), [2] * world)
+        assert sizes == [2] * world and out.is_cuda
+        # a leaderboard replication step over RCCL vs the replica's batch alone
+        nk, n = 64, 4000
+        rng = np.random.default_rng(7 + rank)
+        key = np.sort(rng.integers(0, nk, n))
+        kp = np.searchsorted(key, np.arange(nk + 1)).astype(np.int64)
+        kind = np.where(rng.random(n) < 0.05, 2, 0).astype(np.uint8)
+        pid = rng.integers(0, 300, n, dtype=np.int64)
+        sc = rng.integers(0, 10 ** 6, n, dtype=np.int64)
+        dev = tuple(torch.as_tensor(x).cuda() for x in (kp, kind, pid, sc))
+        e = LeaderboardEngine(nk, 10)
+        rounds = lb_replicate_step(LbDeviceReplica(e, rank, world), dev, c)
+        assert rounds >= 1
+        if world == 1:
+            e1 = LeaderboardEngine(nk, 10)
+            e1.apply_device(_TB(n, key_ptr=dev[0], kind=dev[1], id=dev[2], score=dev[3]))
+            e1.sync()
+            a, b = e.export(), e1.export()
+            assert all(np.array_equal(getattr(a, f), getattr(b, f)) for f in a.__dataclass_fields__)
+    except Exception as ex:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(ex).__name__}: {ex}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+class _TB:
+    def __init__(self, n, **cols):
+        self.n, self.cols = n, cols
+
+    def __getitem__(self, k):
+        return self.cols[k].data_ptr()
+
+
+@pytest.mark.gpu
+def test_torch_collective_rccl_one_rank_gpu(gpu, tmp_path):
+    """The RCCL branch of TorchCollective (what bench.py --gpus N and the
+    replication drivers use on a multi-GPU node): one rank here, since RCCL
+    does not take two ranks on one device."""
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_rccl_worker, args=(1, _free_port(), errf), nprocs=1, join=True)
+    assert not os.path.exists(errf), open(errf).read()
