@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <initializer_list>
 #include <string>
 
 #include "../../include/ccrdt.h"
@@ -272,5 +273,16 @@ __device__ __forceinline__ int64_t wave_max_i64_dpp(int64_t v) {
 // six DPP steps, no LDS-crossbar round trips on the reduction's latency chain.
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) { return wave_min_i64_dpp(v); }
 __device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return wave_max_i64_dpp(v); }
+
+// A kernel's first launch in a process sets up its function object (about
+// 0.1 ms each, measured: tools/first_use.py); hipFuncGetAttributes does the
+// same set-up, so an engine does it for its kernels at creation instead of
+// inside its first batch.
+template <typename... Kern>
+inline void preload_kernels(Kern... k) {
+  hipFuncAttributes at;
+  (void)std::initializer_list<int>{((void)hipFuncGetAttributes(&at, reinterpret_cast<const void*>(k)), 0)...};
+  (void)hipGetLastError();  // (a failure here only means the first launch does the set-up)
+}
 
 }  // namespace ccrdt

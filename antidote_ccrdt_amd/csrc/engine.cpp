@@ -28,6 +28,10 @@ static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 int trmv_launch_scan(const TrmvApplyArgs& a, uint64_t* partials, uint32_t* key_rmv, hipStream_t st);
+void trmv_kernels_preload();
+void trmv_wave_preload();
+void trmv_resident_preload();
+void trmv_steady_preload();
 int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,
                          hipStream_t st);
 int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
@@ -209,6 +213,12 @@ int ccrdt_engine_create(int type, int64_t k, int64_t n_keys, int n_dc, int devic
     set_error("engine_create: stream/event/pinned allocation failed");
     delete e;
     return CCRDT_EDEVICE;
+  }
+  if (type == CCRDT_TOPK_RMV) {  // the apply chain's kernels set up now, not in the first batches
+    trmv_kernels_preload();
+    trmv_wave_preload();
+    trmv_resident_preload();
+    trmv_steady_preload();
   }
   int rc = e->init_type();
   if (rc != CCRDT_OK) {

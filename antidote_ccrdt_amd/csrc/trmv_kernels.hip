@@ -432,6 +432,11 @@ __global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint
 
 // ------------------------------------------------------------- launchers
 // (scratch: one u64 flag, zeroed here)
+void trmv_kernels_preload() {
+  preload_kernels(trmv_scan_partials, trmv_scan_tops, trmv_scan_apply, trmv_validate_kernel, trmv_validate_rows_any,
+                  trmv_validate_rows_exact, trmv_keep_kernel, trmv_mark_done_kernel);
+}
+
 int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,
                          hipStream_t st) {
   if (n_ops == 0) return CCRDT_OK;

@@ -1431,6 +1431,11 @@ __global__ __launch_bounds__(64 * WAVES) void trmv_steady_kernel(TrmvApplyArgs a
 
 // cls 0: up to 256 players per key, two keys per workgroup; cls 1: up to 1024
 // players.  grid_keys bounds the work list (its length may live on the device).
+void trmv_steady_preload() {
+  preload_kernels(trmv_steady_kernel<256, 2, true>, trmv_steady_kernel<256, 2, false>, trmv_steady_kernel<1024, 1, true>,
+                  trmv_steady_kernel<1024, 1, false>);
+}
+
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
   // Observed in registers when K <= 128 (ObsTab), else in LDS

@@ -1175,6 +1175,8 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)
+void trmv_wave_preload() { preload_kernels(trmv_wave_kernel<true>, trmv_wave_kernel<false>); }
+
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
   const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
