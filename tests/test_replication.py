@@ -529,3 +529,40 @@ def test_device_steps_gloo_two_processes_gpu(gpu, tmp_path):
     errf = str(tmp_path / "err.txt")
     mp.spawn(_gpu_gloo_worker, args=(2, _free_port(), errf), nprocs=2, join=True)
     assert not os.path.exists(errf), open(errf).read()
+
+
+@pytest.mark.parametrize("n_runs", [1, 2, 3, 5])
+def test_lb_run_merge_is_canonical(n_runs):
+    """The device replication's delivery order (cluster._lb_merge_runs, on CPU
+    tensors here): runs of rows, each sorted by key and in sequence order,
+    merged by binary-search rank equal a stable sort by (key, run, index) --
+    the canonical (key, origin, seq) order of ReplicatedLeaderboard -- with
+    many equal keys across and inside runs, empty keys and empty runs; and the
+    messages round-trip through _lb_message / _lb_runs."""
+    import torch
+
+    from antidote_ccrdt_amd.cluster import _lb_merge_runs, _lb_message, _lb_runs
+    rng = np.random.default_rng(n_runs)
+    nk = 40
+    runs = []
+    for r in range(n_runs):
+        n = 0 if r == 1 else int(rng.integers(1, 300))
+        key = np.sort(rng.integers(0, nk, n)).astype(np.int64)
+        cols = (key, rng.integers(0, 3, n).astype(np.int64), rng.integers(0, 10**6, n).astype(np.int64),
+                np.arange(n, dtype=np.int64) + 1000 * r)  # score: (run, index) tag
+        runs.append(tuple(torch.from_numpy(c) for c in cols))
+    msgs = [_lb_message(runs[i:i + 2]) for i in range(0, n_runs, 2)]
+    back = _lb_runs(msgs)
+    nonempty = [r for r in runs if r[0].shape[0]]
+    assert len(back) == len(nonempty)
+    for a, b in zip(back, nonempty):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+    kp, kind, id_, sc = _lb_merge_runs(back, nk)
+    key = np.concatenate([r[0].numpy() for r in nonempty])
+    run = np.concatenate([np.full(r[0].shape[0], i) for i, r in enumerate(nonempty)])
+    idx = np.concatenate([np.arange(r[0].shape[0]) for r in nonempty])
+    order = np.lexsort((idx, run, key))
+    assert np.array_equal(sc.numpy(), np.concatenate([r[3].numpy() for r in nonempty])[order])
+    assert np.array_equal(id_.numpy(), np.concatenate([r[2].numpy() for r in nonempty])[order])
+    assert np.array_equal(kind.numpy(), np.concatenate([r[1].numpy() for r in nonempty])[order].astype(np.uint8))
+    assert np.array_equal(kp.numpy(), np.searchsorted(np.sort(key), np.arange(nk + 1)))
