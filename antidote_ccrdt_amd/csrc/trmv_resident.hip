@@ -50,16 +50,20 @@ __device__ unsigned long long g_resident_prof[32];
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
     __builtin_amdgcn_sched_barrier(0);                                        \
   } while (0)
+// (stamped keys: key & RPROF_MASK == 3 & RPROF_MASK; -DRPROF_MASK=0u stamps every key)
+#ifndef RPROF_MASK
+#define RPROF_MASK 63u
+#endif
 #define RPROF(i)                                                                         \
   do {                                                                                   \
     unsigned long long _t;                                                               \
     RPROF_STAMP(_t);                                                                     \
-    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_resident_prof[i], _t - prof_t); \
+    if (lane_id() == 0 && (key & RPROF_MASK) == (3u & RPROF_MASK)) atomicAdd(&g_resident_prof[i], _t - prof_t); \
     prof_t = _t;                                                                         \
   } while (0)
 #define RCOUNT(i, v)                                                                              \
   do {                                                                                            \
-    if (lane_id() == 0 && (key & 63u) == 3) atomicAdd(&g_resident_prof[i], (unsigned long long)(v)); \
+    if (lane_id() == 0 && (key & RPROF_MASK) == (3u & RPROF_MASK)) atomicAdd(&g_resident_prof[i], (unsigned long long)(v)); \
   } while (0)
 #else
 #define RPROF(i) (void)0

@@ -3,7 +3,10 @@
 (diagnostic build, -DTRMV_PROF):
     make -C antidote_ccrdt_amd/csrc OUT=../lib/libccrdt_prof.so OBJDIR=../../build/objprof EXTRA=-DTRMV_PROF
     CCRDT_LIB=antidote_ccrdt_amd/lib/libccrdt_prof.so python tools/prof_resident.py
-Batch 1 of the bench stream on fresh keys, then batches 2.. onto them."""
+Batch 1 of the bench stream on fresh keys, then batches 2.. onto them.
+FRESH=1: the phases of batch 1's tier R keys alone (the keys tier 0 hands on, P > K), per
+stamped key (the build stamps keys with key & RPROF_MASK == 3: one in 64 by default; every
+key with -DRPROF_MASK=0u, whose shared counters' atomics then slow the kernel ~10x)."""
 import ctypes as C
 import os
 import sys
@@ -40,13 +43,15 @@ for i in range(int(os.environ.get("BATCHES", 3))):
     db.close()
     print(f"batch {i + 1}: chain {eng.last_kernel_ms():.2f} ms, tier R {eng.tier_ms(3):.2f} ms, "
           f"tier S {eng.tier_ms(1):.2f} ms", flush=True)
-    if not f or i == 0:
+    fresh = os.environ.get("FRESH") == "1"
+    if not f or (i == 0) != fresh:
         continue
     f(buf, 1)
+    mask = int(os.environ.get("RPROF_MASK", 63))
+    per = max(1, int(((eng.handed_on(0).astype(int) & mask) == (3 & mask)).sum())) if fresh else nk / 64
     tot = sum(buf[j] for j in NAMES) or 1
     for j, n in NAMES.items():
-        print(f"  {n:30s} {buf[j] / tot * 100:6.1f} %   {buf[j] / (nk / 64):9.0f} cyc/key")
-    per = nk / 64
+        print(f"  {n:30s} {buf[j] / tot * 100:6.1f} %   {buf[j] / per:9.0f} cyc/key")
     print(f"  per key: relevant adds {buf[27] / per:.1f}, runs {buf[29] / per:.1f}, "
           f"impacting rmvs {buf[31] / per:.1f}")
     print(f"  in-place layouts (share of keys): append {buf[11] / per:.3f}, compact {buf[12] / per:.3f}, "
