@@ -1079,11 +1079,11 @@ def _lb_apply_csr_device(engine, kp, kind, id_, score):
 _LB_HDR = 3
 
 
-def _lb_message(runs):
+def _lb_message(runs, device=None):
     import torch
     runs = [r for r in runs if r is not None and int(r[0].shape[0])]
     if not runs:
-        return torch.empty(0, dtype=torch.int64, device="cuda")
+        return torch.empty(0, dtype=torch.int64, device=device if device is not None else "cuda")
     dev = runs[0][0].device
     lens = [int(r[0].shape[0]) for r in runs]
     hdr = torch.tensor([len(runs)] + lens + [0] * (_LB_HDR - 1 - len(runs)), dtype=torch.int64, device=dev)
@@ -1166,7 +1166,7 @@ class LbDeviceReplica:
         produced."""
         runs = _lb_runs([p for o, p in enumerate(parts) if o != self.rank])
         if not runs:
-            return _lb_message([])
+            return _lb_message([], parts[self.rank].device if len(parts) > self.rank else None)
         kp, kind, id_, sc = _lb_merge_runs(runs, self.engine.n_keys)
         return _lb_message([_lb_apply_csr_device(self.engine, kp, kind, id_, sc)])
 
