@@ -1453,7 +1453,7 @@ __device__ int trmv_resident_key(const TrmvApplyArgs& a, uint32_t key, uint32_t 
             int64_t bsc = 0, bts = 0;
             // the slab in blocks of 4 elements, each block's loads issued
             // together (the compaction only writes positions already read)
-            constexpr int RFB = INPL ? 2 : RFBLK;
+            constexpr int RFB = INPL ? 1 : RFBLK;  // (in place one: blocks of 2 spilled two VGPRs and ran slower)
             for (uint32_t j0 = 0; j0 < cnt; j0 += RFB) {
               int64_t s4[RFB], t4[RFB];
               uint32_t d4[RFB];
