@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # -DTRMV_PROF build of tools/prof_phases.py); the default is the in-tree one.
 LIB_PATH = os.environ.get("CCRDT_LIB") or os.path.join(_HERE, "lib", "libccrdt.so")
 
-OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS, EKEYCAP = range(7)
+OK, EINVAL, ERANGE, ENOMEM, EDEVICE, ENOSYS, EKEYCAP, EPARTIAL = range(8)
 AVERAGE, TOPK, TOPK_RMV, LEADERBOARD, WORDCOUNT, WORDDOCUMENTCOUNT = range(6)
 TRMV_ADD, TRMV_ADD_R, TRMV_RMV, TRMV_RMV_R = range(4)
 NOOP = 255
@@ -43,8 +43,17 @@ class KeyCapacityError(CcrdtError):
     extra = None
 
 
+class PartialCommitError(CcrdtError):
+    """CCRDT_EPARTIAL: the topk_rmv batch committed for every key except
+    `keys` (the in-place pass handed them on and the full rewrite that
+    applies their ops failed); they keep their previous state and produce no
+    extras.  `extra` holds the batch's extra effects when they were asked for."""
+    keys = None
+    extra = None
+
+
 _ERRNAMES = {EINVAL: "EINVAL", ERANGE: "ERANGE", ENOMEM: "ENOMEM", EDEVICE: "EDEVICE",
-             ENOSYS: "ENOSYS", EKEYCAP: "EKEYCAP"}
+             ENOSYS: "ENOSYS", EKEYCAP: "EKEYCAP", EPARTIAL: "EPARTIAL"}
 
 
 class TrmvOps(C.Structure):
@@ -202,7 +211,8 @@ lib = _load()
 def check(rc: int, where: str) -> None:
     if rc != OK:
         msg = lib.ccrdt_last_error().decode(errors="replace")
-        raise (KeyCapacityError if rc == EKEYCAP else CcrdtError)(rc, where, msg)
+        cls = {EKEYCAP: KeyCapacityError, EPARTIAL: PartialCommitError}.get(rc, CcrdtError)
+        raise cls(rc, where, msg)
 
 
 def ptr(a) -> int | None:

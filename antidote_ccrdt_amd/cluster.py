@@ -234,17 +234,12 @@ def _engine_stream(engine):
     return torch.cuda.ExternalStream(_lib.lib.ccrdt_engine_stream(engine.h), device=torch.device("cuda", engine.device))
 
 
-def _run_device_impl(self, mine, L):
-    """TrmvShardExchange.run on the device: one gather into a [world, L]
-    tensor, then one kernel (ccrdt_trmv_exchange_reduce) for the header (every
-    rank's count and flags, the host-key sum, the Vc max) and every rank's rows
-    sorted by global op; one host read of the header.  None when some rank has
-    more than FAST effects (the general path then runs, second gather and all)."""
+def _reduce_device_impl(self, g, W, L):
+    """The gathered packs [W, L] -> (header, rows) by one kernel on the
+    engine's stream (ccrdt_trmv_exchange_reduce): header = every rank's count,
+    every rank's high word (host keys, failure flag), the host-key sum, the Vc
+    max; rows = every rank's first FAST rows sorted by global op."""
     torch = self.torch
-    W = self.coll.world if self.coll is not None and self.coll.world > 1 else 1
-    if W * self.FAST > 2048:
-        return None
-    g = self.coll.all_gather_into(mine) if W > 1 else mine.view(1, L)
     hdr = torch.empty(2 * W + 1 + self.n_dc, dtype=torch.int64, device=self.dev)
     rows = torch.empty((W * self.FAST, self.w), dtype=torch.int64, device=self.dev)
     es = _engine_stream(self.engine)
@@ -252,19 +247,7 @@ def _run_device_impl(self, mine, L):
     es.wait_stream(ts)
     self.engine.exchange_reduce(g.data_ptr(), W, L, hdr.data_ptr(), rows.data_ptr())
     ts.wait_stream(es)
-    hv = hdr[:2 * W + 1].cpu().tolist()
-    counts = [int(c) for c in hv[:W]]
-    failed = [r for r in range(W) if (int(hv[W + r]) >> (self.FAIL_BIT - 32)) & 1]
-    self.count = counts[self.coll.rank if W > 1 else 0]
-    if max(counts) > self.rows_cap:
-        raise RuntimeError(f"trmv exchange: {max(counts)} extra effects > {self.rows_cap} rows")
-    if max(counts) > self.FAST:
-        if failed:
-            raise PeerStepError(failed)
-        return None
-    if failed:
-        raise PeerStepError(failed)
-    return rows[:sum(counts)], hdr[2 * W + 1:], int(hv[2 * W])
+    return hdr, rows
 
 
 class TrmvShardExchange:
@@ -346,51 +329,57 @@ class TrmvShardExchange:
         self.op_map = None
         self.engine = None
 
-    _run_device = _run_device_impl
+    _reduce_device = _reduce_device_impl
+    XR_MAX = 2048  # rows the reduce kernel sorts in one workgroup (trmv_exchange.hip)
 
     def run(self):
         """The exchange: returns (every rank's extras as an int64 tensor
         [M, 6 + n_dc] in global stream order -- identical on every rank --,
         the replica Vc (elementwise max over the ranks), total new host-path
-        keys over the ranks).  When some rank's apply failed, every rank
-        finishes the collectives and then raises PeerStepError."""
+        keys over the ranks).  Every rank issues the same collectives whatever
+        its engine or failure state: one fixed-size gather, and then a second
+        one only when the gathered counts (the same on every rank) say some
+        rank has more than FAST effects.  When some rank's apply failed, every
+        rank raises PeerStepError right after the first gather."""
         torch = self.torch
         L = self.head + self.FAST * self.w
         mine = self.pack[:L]
-        if self.engine is not None:
-            out = self._run_device(mine, L)
-            if out is not None:
-                return out
-        if self.coll is not None and self.coll.world > 1:
-            parts = self.coll.all_gather(mine)
+        multi = self.coll is not None and self.coll.world > 1
+        W, me = (self.coll.world, self.coll.rank) if multi else (1, 0)
+        g = (self.coll.all_gather_into(mine) if multi else mine.view(1, L)).to(self.dev)
+        dev_rows = None
+        if self.engine is not None and W * self.FAST <= self.XR_MAX:
+            # the header and the sorted rows on the device, one host read
+            hdr, dev_rows = self._reduce_device(g, W, L)
+            hv = [int(v) for v in hdr[:2 * W + 1].cpu().tolist()]
+            counts = hv[:W]
+            failed = [r for r in range(W) if (hv[W + r] >> (self.FAIL_BIT - 32)) & 1]
+            n_host = hv[2 * W]
+            vc = hdr[2 * W + 1:]
         else:
-            parts = [mine]
-        allp = torch.stack([q.to(self.dev) for q in parts])
-        w0 = allp[:, 0]
-        cnt = w0 & 0xFFFFFFFF
-        host = (w0 >> self.HOST_SHIFT) & self.HOST_MASK
-        fail = (w0 >> self.FAIL_BIT) & 1
-        vc = allp[:, 1:self.head].max(0).values
-        hv = torch.cat([cnt, fail, host.sum().view(1), mine[:1] & 0xFFFFFFFF]).cpu().tolist()
-        W = len(parts)
-        counts, failed = [int(c) for c in hv[:W]], [r for r in range(W) if hv[W + r]]
-        n_host, self.count = int(hv[2 * W]), int(hv[2 * W + 1])
+            w0 = g[:, 0]
+            cnt = w0 & 0xFFFFFFFF
+            host = (w0 >> self.HOST_SHIFT) & self.HOST_MASK
+            fail = (w0 >> self.FAIL_BIT) & 1
+            vc = g[:, 1:self.head].max(0).values
+            hv = [int(v) for v in torch.cat([cnt, fail, host.sum().view(1)]).cpu().tolist()]
+            counts, failed, n_host = hv[:W], [r for r in range(W) if hv[W + r]], hv[2 * W]
+        self.count = counts[me]
+        if failed:
+            raise PeerStepError(failed)
         if max(counts) > self.rows_cap:
             raise RuntimeError(f"trmv exchange: {max(counts)} extra effects > {self.rows_cap} rows")
-        heads = [allp[r, self.head:].view(self.FAST, self.w)[:min(c, self.FAST)] for r, c in enumerate(counts)]
-        if max(counts) > self.FAST:  # rare: the rest of the rows in a second gather
+        if max(counts) <= self.FAST and dev_rows is not None:
+            return dev_rows[:sum(counts)], vc, n_host
+        heads = [g[r, self.head:].view(self.FAST, self.w)[:min(c, self.FAST)] for r, c in enumerate(counts)]
+        if max(counts) > self.FAST:  # rare: the rest of the rows in a second gather, on every rank
             rest = self._rows()[self.FAST:max(self.count, self.FAST)]
             if self.op_map is not None and rest.shape[0]:
                 rest[:, 0] = self.op_map[rest[:, 0].clamp(0, self.op_map.shape[0] - 1)]
-            if self.coll is not None and self.coll.world > 1:
-                tails = [t.to(self.dev) for t in self.coll.all_gather_v(rest.contiguous())]
-            else:
-                tails = [rest]
+            tails = [t.to(self.dev) for t in self.coll.all_gather_v(rest.contiguous())] if multi else [rest]
             parts_rows = [torch.cat([h, t]) for h, t in zip(heads, tails)]
         else:
             parts_rows = heads
-        if failed:
-            raise PeerStepError(failed)
         rows = torch.cat(parts_rows) if parts_rows else self._rows()[:0]
         if rows.shape[0]:
             rows = rows[torch.argsort(rows[:, 0], stable=True)]

@@ -35,7 +35,7 @@ void trmv_steady_preload();
 int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,
                          hipStream_t st);
 int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
-                          hipStream_t st);
+                          uint32_t* ex_cnt, hipStream_t st);
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
@@ -137,6 +137,7 @@ const char* ccrdt_strerror(int code) {
     case CCRDT_ERANGE: return "integer outside engine range";
     case CCRDT_ENOMEM: return "out of device memory or per-key capacity";
     case CCRDT_EKEYCAP: return "keys over the per-key capacity were left out of the batch";
+    case CCRDT_EPARTIAL: return "the batch committed except for the keys whose finishing pass failed";
     case CCRDT_EDEVICE: return "HIP device error";
     case CCRDT_ENOSYS: return "operation not supported for this CCRDT type";
     default: return "unknown error";
@@ -358,6 +359,14 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   const int D = E.n_dc;
   CCRDT_TRY(E.trmv[1 - E.mcur].meta.ensure(nk * sizeof(KeyMeta)));
   CCRDT_TRY(E.trmv[1 - E.mcur].cap.ensure(nk * sizeof(KeyCap)));
+  constexpr size_t ARENA_RB = sizeof(E.arena_sub[0]);  // (the counters; the layout counts follow the ends)
+  // the readback's pinned buffer before anything is queued: a failure here
+  // leaves the state untouched
+  if (!E.h_arena && hipHostMalloc(&E.h_arena, 2 * ARENA_RB + 16 * TRMV_NSUB, hipHostMallocDefault) != hipSuccess) {
+    E.h_arena = nullptr;
+    set_error("trmv_apply: pinned allocation failed");
+    return CCRDT_EDEVICE;
+  }
   a.inplace = 1;
   a.slack = trmv_pool_slack();  // (relocations' pool capacity)
   a.old_s = E.trmv_side(E.mcur, E.cur);
@@ -384,12 +393,6 @@ int trmv_pass_inplace(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* stat
   CCRDT_TRY(trmv_launch_resident(a, nk, E.stream));
   CCRDT_HIP(hipEventRecord(E.evt[2], E.stream));
   CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
-  constexpr size_t ARENA_RB = sizeof(E.arena_sub[0]);  // (the counters; the layout counts follow the ends)
-  if (!E.h_arena && hipHostMalloc(&E.h_arena, 2 * ARENA_RB + 16 * TRMV_NSUB, hipHostMallocDefault) != hipSuccess) {
-    E.h_arena = nullptr;
-    set_error("trmv_apply: pinned allocation failed");
-    return CCRDT_EDEVICE;
-  }
   CCRDT_HIP(hipMemcpyAsync(E.h_arena, E.arena.p, ARENA_RB, hipMemcpyDeviceToHost, E.stream));
   CCRDT_HIP(hipMemcpyAsync(static_cast<char*>(E.h_arena) + 2 * ARENA_RB, a.lay_cnt, 16 * TRMV_NSUB,
                            hipMemcpyDeviceToHost, E.stream));
@@ -443,6 +446,15 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
   const int out = 1 - E.cur, mout = 1 - E.mcur;
   a.inplace = 0;
   a.fresh = E.fresh ? 1 : 0;
+  // CCRDT_TRMV_FAIL_FINISH=1 (tests): the full rewrite that finishes an
+  // in-place batch fails as an allocation would (CCRDT_EPARTIAL's path)
+  if (a.key_done) {
+    const char* ff = getenv("CCRDT_TRMV_FAIL_FINISH");
+    if (ff && ff[0] == '1') {
+      set_error("trmv_apply: injected failure of the finishing pass (CCRDT_TRMV_FAIL_FINISH)");
+      return CCRDT_ENOMEM;
+    }
+  }
   // room for in-place growth when tier R can take the keys (K <= 128): the
   // capacity scan's slack, or a fresh batch's roomy layout while its offsets
   // fit 32 bits
@@ -692,23 +704,49 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
     return !(v && v[0] == '0');
   }();
   int first_tier = 3, n_over = 0;
+  int partial = CCRDT_OK;
   if (nk && !E.fresh && E.k <= 128 && E.inplace_ready && inplace_env) {
     uint32_t handed = 0;
     CCRDT_TRY(trmv_pass_inplace(E, a, n_ops, status, handed));
     E.mcur = 1 - E.mcur;  // (meta / cap now hold the batch, except the handed-on keys)
     if (handed) {
       // the handed-on keys' ops in a full rewrite of every key (the others
-      // only copied): it also compacts the arena
-      CCRDT_TRY(E.key_done.ensure(nk));
-      CCRDT_TRY(trmv_launch_mark_done(E.key_done.as<uint8_t>(), nk, E.tier_ovf[3].as<uint32_t>(), handed,
-                                      status + 2 + 2 * 3, E.stream));
-      CCRDT_HIP(hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream));
-      a.key_done = E.key_done.as<uint8_t>();
-      const int rc = trmv_pass_full(E, a, n_ops, status, first_tier, n_over);
+      // only copied): it also compacts the arena.  Until it commits, the live
+      // state (meta[mcur] over data side cur) is the batch applied to every
+      // key but the handed-on ones, which kept theirs; the rewrite writes only
+      // the other sides, so when it fails that state stands: a partial commit
+      // (CCRDT_EPARTIAL), not a rollback -- the in-place pass already changed
+      // the data arrays of the keys it completed.
+      // (the list, host-side: the rewrite's own tier R overwrites tier_ovf[3])
+      std::vector<uint32_t> hkeys(handed);
+      CCRDT_HIP(hipMemcpy(hkeys.data(), E.tier_ovf[3].p, (size_t)handed * 4, hipMemcpyDeviceToHost));
+      int rc = E.key_done.ensure(nk);
+      if (rc == CCRDT_OK)
+        rc = trmv_launch_mark_done(E.key_done.as<uint8_t>(), nk, E.tier_ovf[3].as<uint32_t>(), handed, nullptr,
+                                   nullptr, E.stream);
+      if (rc == CCRDT_OK && hipMemsetAsync(E.status.p, 0, TRMV_STATUS_WORDS * 4, E.stream) != hipSuccess)
+        rc = CCRDT_EDEVICE;
+      if (rc == CCRDT_OK) {
+        a.key_done = E.key_done.as<uint8_t>();
+        rc = trmv_pass_full(E, a, n_ops, status, first_tier, n_over);
+      }
       if (rc != CCRDT_OK) {
-        E.mcur = 1 - E.mcur;  // (the batch is not committed: back to the state before it)
-        E.inplace_ready = false;
-        return rc;
+        const std::string why = g_last_error;
+        E.inplace_ready = false;  // (the next batch lays every key out again)
+        // the handed-on keys listed again and their extra counts zeroed (a
+        // failed rewrite may have written some): they produce no extras
+        CCRDT_HIP(hipStreamSynchronize(E.stream));  // (whatever the failed rewrite queued)
+        CCRDT_HIP(hipMemcpy(E.tier_ovf[3].p, hkeys.data(), (size_t)handed * 4, hipMemcpyHostToDevice));
+        CCRDT_TRY(trmv_launch_mark_done(E.key_done.as<uint8_t>(), nk, E.tier_ovf[3].as<uint32_t>(), handed, nullptr,
+                                        a.ex_cnt, E.stream));
+        CCRDT_HIP(hipStreamSynchronize(E.stream));
+        E.trmv_overflow_keys[3] = handed;
+        set_error("trmv_apply: the batch committed except for " + std::to_string(handed) +
+                  " key(s) the in-place pass handed on (ccrdt_engine_handed_on(e, 3)); they keep their previous "
+                  "state: the full rewrite that applies their ops failed: " + why);
+        partial = CCRDT_EPARTIAL;
+        first_tier = 3;
+        n_over = 0;
       }
     }
   } else {
@@ -724,6 +762,7 @@ int ccrdt_trmv_apply_device(ccrdt_engine* e, const ccrdt_trmv_ops* ops) {
   E.fresh = false;
   E.last_n_ops = n_ops;
   E.last_kernel_ms = kernel_ms;
+  if (partial != CCRDT_OK) return partial;
   if (n_over) {
     set_error("trmv_apply: " + std::to_string(n_over) +
               " key(s) would exceed the per-key capacity (" + std::to_string(trmv_steady_hbm_players()) +
@@ -912,8 +951,8 @@ int ccrdt_trmv_apply(ccrdt_engine* e, const ccrdt_trmv_ops* ops, ccrdt_trmv_extr
   mark();
   const int rc = ccrdt_trmv_apply_device(e, &d);
   mark();
-  if (rc != CCRDT_OK && rc != CCRDT_EKEYCAP) return rc;
-  if (extra) {  // EKEYCAP: the batch committed; its extras are fetched too
+  if (rc != CCRDT_OK && rc != CCRDT_EKEYCAP && rc != CCRDT_EPARTIAL) return rc;
+  if (extra) {  // EKEYCAP / EPARTIAL: the batch committed (but for some keys); its extras are fetched too
     const std::string msg = g_last_error;
     CCRDT_TRY(ccrdt_trmv_fetch_extra(e, extra));
     if (rc != CCRDT_OK) set_error(msg);

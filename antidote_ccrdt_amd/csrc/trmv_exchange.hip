@@ -179,8 +179,9 @@ int trmv_launch_exchange_pack(const int64_t* vc, const uint64_t* key_ptr, const 
 }
 
 // The gathered packs -> header + every rank's first rows, sorted by op (a
-// stable order: (op, rank, position) as one key, bitonic in one workgroup's
-// LDS; at most 8 ranks x 256 rows per rank on this path).
+// stable order: the full 64-bit global op, then the row's (rank, position)
+// index, bitonic in one workgroup's LDS; at most 8 ranks x 256 rows per rank
+// on this path).
 constexpr int XR_MAX = 2048;
 __global__ __launch_bounds__(1024) void trmv_exchange_reduce_kernel(const int64_t* g, int world, int64_t len, int n_dc,
                                                                     int64_t* hdr, int64_t* out) {
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(1024) void trmv_exchange_reduce_kernel(const int64_
       while (base[r + 1] <= i) ++r;
       const uint32_t j = i - base[r];
       const int64_t op = g[r * len + 1 + n_dc + (int64_t)j * w];
-      key[i] = ((unsigned long long)(uint32_t)op << 24) | ((unsigned long long)r << 16) | j;  // (op < 2^32)
+      key[i] = (unsigned long long)op;  // i = (rank, position) in rank order: the tie-break
       src[i] = i;
     } else {
       key[i] = ~0ull;
@@ -233,7 +234,8 @@ __global__ __launch_bounds__(1024) void trmv_exchange_reduce_kernel(const int64_
         const uint32_t l = i ^ j;
         if (l > i) {
           const bool up = (i & k) == 0;
-          if ((key[i] > key[l]) == up) {
+          const bool gt = key[i] > key[l] || (key[i] == key[l] && src[i] > src[l]);
+          if (gt == up) {
             const unsigned long long t = key[i];
             key[i] = key[l];
             key[l] = t;

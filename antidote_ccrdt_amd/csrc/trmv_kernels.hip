@@ -423,11 +423,16 @@ __global__ __launch_bounds__(256) void trmv_validate_rows_exact(TrmvApplyArgs a,
 
 // key_done for the pass that finishes an in-place batch: every key 1, then
 // the keys the in-place pass handed on 0.
+// done[k] = 0 for the listed keys (n_list: the device count, else n_host);
+// with ex_cnt their extra counts are zeroed too
 __global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint64_t n_keys, const uint32_t* list,
-                                                             const uint32_t* n_list) {
+                                                             const uint32_t* n_list, uint32_t n_host, uint32_t* ex_cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t n = *n_list;
-  if (i < n) done[list[i]] = 0u;
+  const uint32_t n = n_list ? *n_list : n_host;
+  if (i < n && list[i] < n_keys) {
+    done[list[i]] = 0u;
+    if (ex_cnt) ex_cnt[list[i]] = 0u;
+  }
 }
 
 // ------------------------------------------------------------- launchers
@@ -455,10 +460,11 @@ int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, 
 }
 
 int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, uint32_t n_list, const uint32_t* n_dev,
-                          hipStream_t st) {
+                          uint32_t* ex_cnt, hipStream_t st) {
   CCRDT_HIP(hipMemsetAsync(done, 1, n_keys, st));
   if (n_list == 0) return CCRDT_OK;
-  hipLaunchKernelGGL(trmv_mark_done_kernel, dim3((n_list + 255) / 256), dim3(256), 0, st, done, n_keys, list, n_dev);
+  hipLaunchKernelGGL(trmv_mark_done_kernel, dim3((n_list + 255) / 256), dim3(256), 0, st, done, n_keys, list, n_dev,
+                     n_list, ex_cnt);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

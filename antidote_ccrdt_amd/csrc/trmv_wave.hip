@@ -1,20 +1,21 @@
-// trmv_wave.hip — tier 0 of the topk_rmv apply: one wavefront per key, four
-// independent keys per 256-thread workgroup, ~8.5 KB of LDS per key.
+// trmv_wave.hip — tier 0 of the topk_rmv apply: one wavefront per key, one
+// wave per 64-thread workgroup (W_WAVES), each wave taking W_KPW consecutive
+// keys; one key's working set (WaveLds<true>) is ~8 KB of LDS.
 //
-// Exactness argument: the per-player decomposition of trmv_fast.hip (P <= K
-// players => recompute_observed/5 never evicts, promotion candidates of rmv/3
+// Exactness argument: the per-player decomposition (P <= K players =>
+// recompute_observed/5 never evicts, and the promotion candidates of rmv/3
 // are the removed player's own survivors; src/antidote_ccrdt_topk_rmv.erl
-// :231-334).  Keys outside this tier's caps go to the next tier.
+// :231-334).  Keys outside this tier's caps go to the next tier (tier R).
 //
-// What differs from the LDS tier of trmv_fast.hip is the mapping onto gfx950:
+// The mapping onto gfx950:
 //  * occupancy: elements are addressed by index, Masked slabs are u8 index
-//    lists, removal clocks are one shared table of 24 rows, so four keys fit
-//    per SIMD;
+//    lists, removal clocks are one shared table of 24 rows, so a key's LDS
+//    stays small and four waves fit per SIMD (__launch_bounds__);
 //  * latency: every global load a key needs is issued before its first use:
 //    a key's ops, and then its removal clocks (8 lanes per clock row,
 //    coalesced), are loaded while the wave still works on the previous key;
-//  * no workgroup barriers: the four keys of a workgroup are independent and
-//    each wave orders its own LDS accesses (wave_lds_sync);
+//  * no workgroup barriers: each wave orders its own LDS accesses
+//    (wave_lds_sync);
 //  * grouping: 64-bit LDS compare-and-swap on the Id itself (one probe loop,
 //    no claim protocol); players are numbered in hash-slot order (new ones
 //    after the old ones), so the device layout is deterministic;

@@ -305,11 +305,16 @@ class TopkRmvEngine(_Engine):
         self._checked(lib.ccrdt_trmv_apply_device(self.h, C.byref(db.c)), "trmv_apply_device")
 
     def _checked(self, rc: int, where: str, extra=None) -> None:
-        """check(), with the over-capacity keys attached to KeyCapacityError."""
+        """check(), with the keys left out attached to KeyCapacityError
+        (over the per-key capacity) / PartialCommitError (a failed finishing
+        pass: the keys the in-place pass handed on, tier 3)."""
         try:
             check(rc, where)
         except _lib.KeyCapacityError as err:
             err.keys, err.extra = self.handed_on(TRMV_TIER_LAST), extra
+            raise
+        except _lib.PartialCommitError as err:
+            err.keys, err.extra = self.handed_on(3), extra
             raise
 
     def extra_count(self) -> int:

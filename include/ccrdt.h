@@ -49,6 +49,15 @@ extern "C" {
                            previous state, produce no extras, and are listed
                            by ccrdt_engine_handed_on(e, 4).  Their ops go to
                            the host (Erlang) path. */
+#define CCRDT_EPARTIAL 7 /* topk_rmv: the batch COMMITTED except for the keys
+                           listed by ccrdt_engine_handed_on(e, 3): the in-place
+                           pass updated every other key, and the full rewrite
+                           that applies these keys' ops failed (device memory,
+                           2^32 elements, a HIP error: ccrdt_last_error says
+                           which).  They keep their previous state and produce
+                           no extras; the engine stays usable (the next batch
+                           is a full rewrite).  Their ops may be re-applied in
+                           a later batch. */
 
 /* Registry: antidote_ccrdt:?CCRDTS (src/antidote_ccrdt.erl:28-35). */
 #define CCRDT_AVERAGE 0

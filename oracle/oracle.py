@@ -150,6 +150,7 @@ def _setup_types(l):
     l.orc_lb_create.argtypes = [I64, I64]
     l.orc_lb_destroy.argtypes = [P]
     l.orc_lb_apply.argtypes = [P, P, P, P, P, P, P, P]
+    l.orc_lb_apply_mt.argtypes = [P, P, P, P, P, P, P, P, INT]
     l.orc_lb_sizes.argtypes = [P, P, P, P]
     l.orc_lb_export.argtypes = [P] + [P] * 11
     l.orc_lb_downstream.argtypes = [P, I64, P, P, P, P, P]
@@ -215,8 +216,9 @@ class TopkOracle:
 
 
 class LbOracle:
-    def __init__(self, n_keys, k=100):
-        self.n_keys = n_keys
+    def __init__(self, n_keys, k=100, n_threads: int = 1):
+        """n_threads > 1: apply() splits the boards over threads (configs[3]-sized tests)."""
+        self.n_keys, self.n_threads = n_keys, n_threads
         self.h = tlib().orc_lb_create(n_keys, k)
 
     def __del__(self):
@@ -228,8 +230,12 @@ class LbOracle:
         x = {"kind": np.zeros(n, np.uint8), "id": np.zeros(n, np.int64), "score": np.zeros(n, np.int64)}
         kp, kd = _a(key_ptr, np.uint64), _a(kind, np.uint8)
         i, s = _a(id, np.int64), _a(score, np.int64)
-        tlib().orc_lb_apply(self.h, _p(kp), _p(kd), _p(i), _p(s), _p(x["kind"]), _p(x["id"]),
-                            _p(x["score"]))
+        if self.n_threads > 1:
+            tlib().orc_lb_apply_mt(self.h, _p(kp), _p(kd), _p(i), _p(s), _p(x["kind"]), _p(x["id"]),
+                                   _p(x["score"]), int(self.n_threads))
+        else:
+            tlib().orc_lb_apply(self.h, _p(kp), _p(kd), _p(i), _p(s), _p(x["kind"]), _p(x["id"]),
+                                _p(x["score"]))
         return x
 
     def export(self) -> dict:

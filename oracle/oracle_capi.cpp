@@ -292,6 +292,28 @@ void orc_lb_apply(void* h, const uint64_t* key_ptr, const uint8_t* kind, const i
       }
     }
 }
+// The same fold with the boards split over n_threads threads (boards are
+// independent objects: leaderboard.erl:215-286 touches one board per op).
+void orc_lb_apply_mt(void* h, const uint64_t* key_ptr, const uint8_t* kind, const int64_t* id,
+                     const int64_t* score, uint8_t* ex_kind, int64_t* ex_id, int64_t* ex_score, int n_threads) {
+  auto* s = (LbSet*)h;
+  if (n_threads < 1) n_threads = 1;
+  const size_t nk = s->keys.size();
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t)
+    th.emplace_back([&, t] {
+      for (size_t k = nk * t / n_threads; k < nk * (t + 1) / n_threads; ++k)
+        for (uint64_t i = key_ptr[k]; i < key_ptr[k + 1]; ++i) {
+          LExtra x = kind[i] == 2 ? s->keys[k].ban(id[i]) : s->keys[k].add(id[i], score[i]);
+          if (ex_kind) ex_kind[i] = x.kind == L_ADD ? 0 : 255;
+          if (x.kind == L_ADD) {
+            if (ex_id) ex_id[i] = x.elem.id;
+            if (ex_score) ex_score[i] = x.elem.score;
+          }
+        }
+    });
+  for (auto& x : th) x.join();
+}
 void orc_lb_sizes(void* h, int64_t* n_obs, int64_t* n_masked, int64_t* n_bans) {
   int64_t o = 0, m = 0, b = 0;
   for (auto& l : ((LbSet*)h)->keys) {

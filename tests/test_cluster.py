@@ -172,7 +172,7 @@ def _step_worker(rank, world, port, errf):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_step_gloo(world, tmp_path):
     errf = str(tmp_path / "err.txt")
     mp.spawn(_step_worker, args=(world, _free_port(), errf), nprocs=world, join=True)
@@ -491,3 +491,113 @@ def test_torch_collective_rccl_one_rank_gpu(gpu, tmp_path):
     errf = str(tmp_path / "err.txt")
     mp.spawn(_rccl_worker, args=(1, _free_port(), errf), nprocs=1, join=True)
     assert not os.path.exists(errf), open(errf).read()
+
+
+# ------------------- the exchange's collective sequence is the same on every rank
+def _reduce_ref(x, g, W, L):
+    """What ccrdt_trmv_exchange_reduce computes, in torch on the host: the
+    header (counts, high words, host-key sum, Vc max) and every rank's first
+    FAST rows sorted by global op (ties: rank, then position)."""
+    import torch
+    w0 = g[:, 0]
+    hdr = torch.cat([w0 & 0xFFFFFFFF, w0 >> 32, ((w0 >> 32) & x.HOST_MASK).sum().view(1),
+                     g[:, 1:x.head].max(0).values])
+    parts = [g[r, x.head:].view(x.FAST, x.w)[:min(int(w0[r] & 0xFFFFFFFF), x.FAST)] for r in range(W)]
+    rows = torch.cat(parts)
+    rows = rows[torch.argsort(rows[:, 0], stable=True)]
+    out = torch.zeros((W * x.FAST, x.w), dtype=torch.int64)
+    out[:rows.shape[0]] = rows
+    return hdr, out
+
+
+def _rows_for(rank, n, n_dc=D):
+    rows = np.zeros((n, 6 + n_dc), np.int64)
+    rows[:, 0] = np.arange(n, dtype=np.int64) * 2 + rank + (1 << 33)  # global ops past 2^32
+    rows[:, 1] = 1
+    rows[:, 2] = 1000 * rank + np.arange(n)
+    return rows
+
+
+def _xchg_worker(rank, world, port, errf, mode):
+    """Rank 0 reduces on the "device" (its engine set; the kernel emulated by
+    _reduce_ref), the other ranks on the general path.  mode "fail": the last
+    rank's apply failed and rank 0 has more than FAST effects -- every rank
+    raises PeerStepError after the first gather (rank 0 used to
+    raise there while the failed rank blocked in the second gather); mode
+    "big": only the last rank has more than FAST effects -- every rank takes
+    the second gather and gets the same rows."""
+    import torch.distributed as dist
+
+    from antidote_ccrdt_amd.cluster import PeerStepError, TorchCollective, TrmvShardExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = TrmvShardExchange(D, TorchCollective(dist), rows_cap=1024)
+        x.FAST = 8
+        last = rank == world - 1
+        n = {"fail": 20 if rank == 0 else 3, "big": 13 if last else 5}[mode]
+        vc = np.full(D, 10 + rank, np.int64)
+        if mode == "fail" and last:
+            x.fill_from_rows(np.zeros((0, x.w), np.int64), np.zeros(D, np.int64), failed=True)
+        else:
+            x.fill_from_rows(_rows_for(rank, n), vc)
+        if rank == 0:
+            x.engine = object()
+            x._reduce_device = lambda g, W, L: _reduce_ref(x, g, W, L)
+        if mode == "fail":
+            with pytest.raises(PeerStepError) as ei:
+                x.run()
+            assert ei.value.ranks == [world - 1]
+        else:
+            rows, v, n_host = x.run()
+            want = np.concatenate([_rows_for(r, 13 if r == world - 1 else 5) for r in range(world)])
+            want = want[np.argsort(want[:, 0], kind="stable")]
+            assert np.array_equal(rows.numpy(), want)
+            assert np.array_equal(v.numpy(), np.full(D, 10 + world - 1)) and n_host == 0
+        dist.barrier()  # every rank got here: nobody is left inside a collective
+    except Exception as e:  # noqa: BLE001
+        with open(errf, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode", ["fail", "big"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_exchange_mixed_paths_gloo(world, mode, tmp_path):
+    errf = str(tmp_path / "err.txt")
+    mp.spawn(_xchg_worker, args=(world, _free_port(), errf, mode), nprocs=world, join=True)
+    assert not os.path.exists(errf), open(errf).read()
+
+
+@pytest.mark.gpu
+def test_exchange_reduce_kernel_wide_ops(gpu):
+    """ccrdt_trmv_exchange_reduce vs its definition (_reduce_ref) with global
+    ops past 2^32 interleaved across ranks (the sort key kept only
+    the op's low 32 bits)."""
+    import torch
+
+    from antidote_ccrdt_amd.cluster import TrmvShardExchange
+    from antidote_ccrdt_amd.engine import TopkRmvEngine
+    eng = TopkRmvEngine(16, K, D, device=0)
+    x = TrmvShardExchange(D, None, device=0, rows_cap=1024)
+    W, L = 4, x.head + x.FAST * x.w
+    rng = np.random.default_rng(5)
+    g = torch.zeros((W, L), dtype=torch.int64)
+    ops = rng.permutation(np.arange(W * 200, dtype=np.int64)) * (1 << 31) + 7  # low 32 bits collide
+    for r in range(W):
+        c = 150 + 30 * r
+        rows = _rows_for(r, x.FAST)
+        rows[:c, 0] = ops[r * 200:r * 200 + c]
+        g[r, 0] = c | ((r + 1) << 32)
+        g[r, 1:x.head] = torch.from_numpy(rng.integers(0, 1 << 40, D))
+        g[r, x.head:] = torch.from_numpy(rows.reshape(-1))
+    x.engine = eng
+    hdr, rows = x._reduce_device(g.cuda(), W, L)
+    torch.cuda.synchronize()
+    h0, r0 = _reduce_ref(x, g, W, L)
+    n = int(h0[:W].sum())
+    assert torch.equal(hdr.cpu(), h0)
+    assert torch.equal(rows.cpu()[:n], r0[:n])

@@ -128,3 +128,21 @@ def test_wordcount_threaded_oracle_matches(wdc):
     b.apply(kp, off, b"".join(flat), n_threads=7)
     for x, y in zip(a.export(), b.export()):
         assert np.array_equal(x, y)
+
+
+def test_lb_oracle_threads_match_sequential():
+    """The threaded leaderboard fold (boards split over threads, used by the
+    configs[3]-sized GPU tests) equals the sequential one: state and extras."""
+    rng = np.random.default_rng(33)
+    nk, n = 500, 60000
+    key = np.sort(rng.integers(0, nk, n))
+    kp = np.searchsorted(key, np.arange(nk + 1)).astype(np.uint64)
+    kind = np.where(rng.random(n) < 0.05, 2, rng.integers(0, 2, n)).astype(np.uint8)
+    pid = rng.integers(0, 300, n, dtype=np.int64)
+    sc = rng.integers(0, 1000, n, dtype=np.int64)
+    a, b = orc.LbOracle(nk, 10), orc.LbOracle(nk, 10, n_threads=7)
+    xa, xb = a.apply(kp, kind, pid, sc), b.apply(kp, kind, pid, sc)
+    for f in xa:
+        assert np.array_equal(xa[f], xb[f])
+    sa, sb = a.export(), b.export()
+    assert all(np.array_equal(sa[f], sb[f]) for f in sa)

@@ -120,7 +120,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_replication_gloo(mode, world, tmp_path):
     errf = str(tmp_path / "err.txt")
     mp.spawn(_rep_worker, args=(world, _free_port(), mode, errf), nprocs=world, join=True)
@@ -216,7 +216,7 @@ def _wc_worker(rank, world, port, wdc, errf):
 
 
 @pytest.mark.parametrize("wdc", [False, True])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_wordcount_gloo(world, wdc, tmp_path):
     errf = str(tmp_path / "err.txt")
     mp.spawn(_wc_worker, args=(world, _free_port(), wdc, errf), nprocs=world, join=True)

@@ -359,3 +359,52 @@ def test_host_entry_narrow_columns(gpu, shift):
             xe = TrmvExtra(*(getattr(xout, f)[:b.n_ops] for f in ("kind", "id", "score", "dc", "ts", "vc")))
         xo = orac.apply(b)
         _compare(eng, orac, b, D, xe, xo)
+
+
+def test_inplace_finish_failure_partial_commit(gpu, monkeypatch):
+    """when the full rewrite that finishes an in-place batch fails
+    (injected: CCRDT_TRMV_FAIL_FINISH=1, as an allocation failure would), the
+    engine does not claim a rollback -- the in-place pass already changed the
+    keys it completed.  It reports CCRDT_EPARTIAL: every key but the ones the
+    in-place pass handed on holds the batch, those keep their previous state
+    and produce no extras (bit-exact vs the oracle applying the batch without
+    their ops), and later batches, those keys' ops re-applied, go on exactly."""
+    from antidote_ccrdt_amd.cluster import _drop_keys
+    monkeypatch.setenv("CCRDT_TRMV_ARENA_ROOM", "0")  # relocations run out: keys get handed on
+    nk, D, K = 3000, 8, 100
+    eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
+    eng.set_fresh_room(True)
+    n = 95 * nk
+    hit = None
+    for i in range(8):
+        b = gen_trmv(n, nk, D, n_players=256, score_max=10**6, rmv_pm=100, lag_max=64, dup_pm=5, swap_pm=5,
+                     seed=4300 + i, clock0=i * n)
+        if hit is None and i >= 1:
+            monkeypatch.setenv("CCRDT_TRMV_FAIL_FINISH", "1")
+            try:
+                xe = eng.apply(b)
+            except _lib.PartialCommitError as err:
+                hit = i
+                keys = np.sort(np.asarray(err.keys, np.int64))
+                assert keys.shape[0] > 0 and err.extra is not None
+                kp = np.asarray(b.key_ptr, np.int64)
+                keep = np.ones(b.n_ops, bool)
+                for k in keys:
+                    keep[kp[k]:kp[k + 1]] = False
+                xs = orac.apply(_drop_keys(b, keys))
+                xo = {f: np.zeros((b.n_ops,) + np.asarray(v).shape[1:], np.asarray(v).dtype) for f, v in xs.items()}
+                xo["kind"][:] = 255
+                for f in xo:
+                    xo[f][keep] = xs[f]
+                _compare(eng, orac, b, D, err.extra, xo)
+                # the left-out keys' ops, re-applied alone, bring them up to date
+                monkeypatch.delenv("CCRDT_TRMV_FAIL_FINISH")
+                rest = np.setdiff1d(np.arange(nk), keys)
+                br = _drop_keys(b, rest)
+                _compare(eng, orac, br, D, eng.apply(br), orac.apply(br))
+                continue
+            monkeypatch.delenv("CCRDT_TRMV_FAIL_FINISH")
+            _compare(eng, orac, b, D, xe, orac.apply(b))  # nothing handed on: no finishing pass ran
+            continue
+        _compare(eng, orac, b, D, eng.apply(b), orac.apply(b))
+    assert hit is not None, "no in-place batch handed keys on"
