@@ -586,11 +586,11 @@ def test_exchange_reduce_kernel_wide_ops(gpu):
     W, L = 4, x.head + x.FAST * x.w
     rng = np.random.default_rng(5)
     g = torch.zeros((W, L), dtype=torch.int64)
-    ops = rng.permutation(np.arange(W * 200, dtype=np.int64)) * (1 << 31) + 7  # low 32 bits collide
+    ops = rng.permutation(np.arange(W * 256, dtype=np.int64)) * (1 << 31) + 7  # low 32 bits collide
     for r in range(W):
         c = 150 + 30 * r
         rows = _rows_for(r, x.FAST)
-        rows[:c, 0] = ops[r * 200:r * 200 + c]
+        rows[:c, 0] = ops[r * 256:r * 256 + c]
         g[r, 0] = c | ((r + 1) << 32)
         g[r, 1:x.head] = torch.from_numpy(rng.integers(0, 1 << 40, D))
         g[r, x.head:] = torch.from_numpy(rows.reshape(-1))

@@ -98,7 +98,7 @@ def test_wordcount_config4_full_share(gpu, wdc):
     from antidote_ccrdt_amd.cluster import ShardedWordcount, exchange_local_device
     b, off = _corpus()
     want = _wc_oracle(wdc)
-    assert int(want[0][-1]) > 900_000  # (nearly the whole 10^6-word vocabulary)
+    assert int(want[0][-1]) > 700_000  # (the 10^6-word vocabulary regime: ~760k distinct words)
     E = WordDocumentCountEngine if wdc else WordcountEngine
     e = E(1)
     d = DeviceBatch(WC_DOCS, key_ptr=np.array([0, WC_DOCS], np.uint64), doc_off=off, bytes=b)

@@ -16,6 +16,9 @@ step() {  # name, timeout, command...
 [ -z "$SKIP_TESTS" ] && step pytest_gpu 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 900 --timeout-method thread
 [ -z "$SKIP_TESTS" ] && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [ -z "$SKIP_BENCH" ] && step bench 600 python bench.py
+# EIGHTH=1: what one rank of the N=8 strong line does, on one GPU (1/8 of the keys and ops)
+[ -n "$EIGHTH" ] && step bench_eighth 300 python bench.py --n-keys 131072 --n-ops 12500000 --steps 50 --warmup 10 \
+  --cpu-sample-keys 0 --cpu-steady-keys 0 --steady-batches 0
 if [ -z "$SKIP_PROF" ]; then
   echo "== kernel trace of the driver's bench command"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
