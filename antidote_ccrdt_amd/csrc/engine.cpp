@@ -651,14 +651,15 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     // CCRDT_TRMV_OVERLAP_STALL=1 (tests): the consumers give up at once when
     // no hand-on is there yet, so the stall fallback runs
     const char* stall_env = getenv("CCRDT_TRMV_OVERLAP_STALL");
-    a3.spin_limit = stall_env && stall_env[0] == '1' ? 0u : (1u << 19);
+    const bool force_stall = stall_env && stall_env[0] == '1';
+    a3.spin_limit = force_stall ? 0u : (1u << 19);
     CCRDT_TRY(trmv_launch_resident_consume(a3, overlap_waves, E.stream2));
     CCRDT_HIP(hipEventRecord(E.ev_ovl, E.stream2));
     CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_ovl, 0));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
-    if (hs[3 + 2 * 3] & TRMV_ERR_STALL) {
+    if ((hs[3 + 2 * 3] & TRMV_ERR_STALL) || force_stall) {
       // tier 0 did not run beside the consumers: tier R over the whole list
       // after it (a fresh key's tier R rewrites the same result)
       CCRDT_HIP(hipMemsetAsync(status + 2 + 2 * 3, 0, 8, E.stream));
