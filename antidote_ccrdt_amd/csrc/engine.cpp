@@ -39,7 +39,6 @@ int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, 
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
-uint32_t trmv_wave_waves(uint64_t grid_keys);
 int trmv_launch_first_list(const uint64_t* key_ptr, uint64_t n_keys, uint32_t thresh, uint32_t* list,
                            uint32_t* count, hipStream_t st);
 int trmv_launch_resident_consume(const TrmvApplyArgs& a, uint32_t waves, hipStream_t st);
@@ -611,7 +610,9 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     if (!E.stream2) {
       int lo = 0, hi = 0;
       CCRDT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      CCRDT_HIP(hipStreamCreateWithPriority(&E.stream2, hipStreamNonBlocking, hi));
+      // CCRDT_TRMV_OVERLAP_PRIO=0: the consumers' stream at normal priority (A/B knob)
+      const char* pe = getenv("CCRDT_TRMV_OVERLAP_PRIO");
+      CCRDT_HIP(hipStreamCreateWithPriority(&E.stream2, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
       CCRDT_HIP(hipEventCreateWithFlags(&E.ev_ovl, hipEventDisableTiming));
     }
     CCRDT_TRY(E.first_list.ensure(nk * 4));
@@ -637,6 +638,7 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     a0.prod_done = ov;
     CCRDT_TRY(trmv_launch_wave(a0, nk, E.stream));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    CCRDT_HIP(hipMemsetAsync(ov, 0xFF, 4, E.stream));  // tier 0 is finished (the consumers' exit flag)
     CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.evt[e0], 0));
     TrmvApplyArgs a3 = a;
     a3.key_list = E.tier_ovf[0].as<uint32_t>();
@@ -645,14 +647,13 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     a3.ovf_list = E.tier_ovf[3].as<uint32_t>();
     a3.status = status + 2 + 2 * 3;
     a3.prod_done = ov;
-    a3.prod_blocks = trmv_wave_waves(nk);
     a3.claim = ov + 1;
     a3.n_sent = n_sent;
     // CCRDT_TRMV_OVERLAP_STALL=1 (tests): the consumers give up at once when
     // no hand-on is there yet, so the stall fallback runs
     const char* stall_env = getenv("CCRDT_TRMV_OVERLAP_STALL");
     const bool force_stall = stall_env && stall_env[0] == '1';
-    a3.spin_limit = force_stall ? 0u : (1u << 19);
+    a3.spin_limit = force_stall ? 0u : (1u << 19);  // (~2 s)
     CCRDT_TRY(trmv_launch_resident_consume(a3, overlap_waves, E.stream2));
     CCRDT_HIP(hipEventRecord(E.ev_ovl, E.stream2));
     CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_ovl, 0));

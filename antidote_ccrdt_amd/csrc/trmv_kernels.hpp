@@ -142,16 +142,19 @@ struct TrmvApplyArgs {
   // The overlapped hand-on of a fresh batch: tier 0 takes the
   // keys of first_list (count *n_first: the keys with more than first_thresh
   // ops, the likely hand-ons) before every other key in key order (those with
-  // more than first_thresh ops skipped), and each of its workgroups adds one
-  // to *prod_done when it is finished; tier R, on a second stream, takes the
-  // keys tier 0 hands on as they appear in its list (claim: the consumers'
-  // next list index; entries below n_sent start as NONE32).
+  // more than first_thresh ops skipped) and publishes its hand-ons with
+  // device-scope atomics (prod_done non-null); tier R, on a second stream,
+  // takes the keys tier 0 hands on as they appear in its list (claim: the
+  // consumers' next list index; entries below n_sent start as NONE32) until
+  // *prod_done, a flag set by a 4-byte copy queued after tier 0, says tier 0
+  // is finished.  (Tier 0 counting its finished waves on one word instead:
+  // 131k device atomics on one address, polled by the consumers, made tier 0
+  // 1.8x slower.)
   const uint32_t* first_list;
   const uint32_t* n_first;
   uint32_t first_thresh;
-  uint32_t prod_blocks;             // tier 0's waves
   uint32_t n_sent;
-  uint32_t spin_limit;              // tier R's polls (~3 us each) before it gives up waiting for tier 0
+  uint32_t spin_limit;              // tier R's polls (~4 us each) before it gives up waiting for tier 0
   uint32_t* prod_done;
   uint32_t* claim;
 };

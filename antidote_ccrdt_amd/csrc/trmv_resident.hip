@@ -1890,12 +1890,12 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
 // Tier R over a fresh batch's hand-ons WHILE tier 0 runs (the overlapped
 // hand-on): each wave claims the next index of tier 0's hand-on
 // list (a.key_list, entries below a.n_sent start as NONE32), waits until tier
-// 0 has published that entry, and applies the key; it leaves when tier 0 has
-// finished (every wave of it added to *prod_done) and the index is past tier
-// 0's final count (*n_list_dev).  Every access the two kernels share is a
-// device-scope atomic (the XCDs' L2s are not coherent with each other).  A
-// wave that has waited ~1 s sets TRMV_ERR_STALL and leaves; the host then
-// re-runs tier R over the whole list (a fresh key's tier R is idempotent).
+// 0 has published that entry, and applies the key; it leaves when tier 0 is
+// finished (*prod_done set after it) and the index is past tier 0's final
+// count (*n_list_dev).  Every access the two kernels share is a device-scope
+// atomic (the XCDs' L2s are not coherent with each other).  A wave that has
+// waited ~2 s sets TRMV_ERR_STALL and leaves; the host then re-runs tier R
+// over the whole list (a fresh key's tier R is idempotent).
 // Launched after tier 0 on another stream: if the two do not run side by
 // side, this one runs after tier 0 and takes the list as the chain would.
 __device__ __forceinline__ uint32_t r_atomic_read(uint32_t* p) { return atomicOr(p, 0u); }
@@ -1922,7 +1922,7 @@ __global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_consume_kernel
         key = v;
         break;
       }
-      if (d >= a.prod_blocks) {  // tier 0 is finished: its count is final, its entries written
+      if (d != 0) {  // tier 0 is finished: its count is final, its entries written
         uint32_t c = 0;
         if (lane_id() == 0) c = r_atomic_read(cnt);
         c = ufl(c);
@@ -1934,12 +1934,12 @@ __global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_consume_kernel
         key = ufl(v);
         break;
       }
-      if (spin >= a.spin_limit) {  // (~1 s: tier 0 is not running beside this kernel as it should)
+      if (spin >= a.spin_limit) {  // (~2 s: tier 0 is not running beside this kernel as it should)
         if (lane_id() == 0) atomicOr(&a.status[1], TRMV_ERR_STALL);
         fin = true;
         break;
       }
-      __builtin_amdgcn_s_sleep(40);
+      __builtin_amdgcn_s_sleep(127);  // (~4 us between polls: the poll is cheap for tier 0 that way)
     }
     if (fin) break;
     const int r = trmv_resident_key<false>(a, key, RNONE, L);

@@ -1173,10 +1173,15 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&KA->status[0], 1u);
-          // (published with a device-scope atomic: tier R may be taking the
-          // list while this kernel runs)
-          if (KA->prod_done) atomicExch(&KA->ovf_list[pos], key);
-          else KA->ovf_list[pos] = key;
+          // (published with a device-scope atomic, performed before the wave
+          // goes on: tier R may be taking the list while this kernel runs)
+          if (KA->prod_done) {
+            const uint32_t old = atomicExch(&KA->ovf_list[pos], key);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the exchange is done
+            asm volatile("" ::"v"(old));
+          } else {
+            KA->ovf_list[pos] = key;
+          }
         }
         if (has_next) wave_load_key(a, hdr, j + 1, nxt);
         // retire these loads here, as the common path does before its
@@ -1188,19 +1193,10 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
       cur = nxt;
     }
   }
-  // the wave's hand-ons are all published (release: the list stores before the count)
-  if (a.prod_done && lane_id() == 0)
-    __hip_atomic_fetch_add(KA->prod_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)
 void trmv_wave_preload() { preload_kernels(trmv_wave_kernel<true>, trmv_wave_kernel<false>); }
-
-// waves of the launch trmv_launch_wave makes for grid_keys keys
-uint32_t trmv_wave_waves(uint64_t grid_keys) {
-  const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
-  return (uint32_t)((grid_keys + per_block - 1) / per_block) * W_WAVES;
-}
 
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
