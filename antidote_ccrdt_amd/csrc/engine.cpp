@@ -41,7 +41,6 @@ int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_first_list(const uint64_t* key_ptr, uint64_t n_keys, uint32_t thresh, uint32_t* list,
                            uint32_t* count, hipStream_t st);
-int trmv_launch_resident_consume(const TrmvApplyArgs& a, uint32_t waves, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady_hbm(const TrmvApplyArgs& a, uint32_t waves, void* scratch, hipStream_t st);
@@ -124,7 +123,7 @@ void ccrdt_engine::release_all() {
   for (DevBuf& d : st_n32) d.release();
   for (DevBuf& d : st_nbase) d.release();
   for (DevBuf* d : {&arena, &obs_ord, &key_done, &partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl,
-                    &first_list, &ovl,
+                    &first_list, &ovf_b, &ovl,
                     &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -591,95 +590,94 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     }
     return CCRDT_OK;
   };
-  // The overlapped hand-on: a fresh batch's head [tier 0,
-  // tier R] with tier R on a second stream beside tier 0, taking the keys
-  // tier 0 hands on while it runs; tier 0 takes the likely hand-ons (more
-  // than min(128, 1.2 pmax) ops) first, so tier R's per-key latency is spent
-  // while tier 0 still works instead of after it.
-  // CCRDT_TRMV_OVERLAP=0: tier R after tier 0 (A/B knob); CCRDT_TRMV_OVERLAP_WAVES: tier R's waves.
+  // The split head: a fresh batch's head [tier 0, tier R] as
+  // tier 0 over the likely hand-ons (keys with more than min(128, 1.2 pmax)
+  // ops: first_list) followed by tier R on their hand-ons, on a second stream,
+  // beside tier 0 over every other key on this one -- so tier R's per-key
+  // latency is spent while tier 0 still works, not after it.  Nothing polls:
+  // the two launches write disjoint keys and hand-on lists.  The rare hand-on
+  // of the big launch (a key with few ops but more players than K) takes tier
+  // R after it, once the status read says there is one.
+  // CCRDT_TRMV_OVERLAP=0: the chain's head as one tier-0 launch, then tier R (A/B knob).
   static const bool overlap_env = [] {
     const char* v = getenv("CCRDT_TRMV_OVERLAP");
     return !(v && v[0] == '0');
   }();
-  static const uint32_t overlap_waves = [] {
-    const char* v = getenv("CCRDT_TRMV_OVERLAP_WAVES");
-    const int x = v ? atoi(v) : 64;
-    return (uint32_t)(x < 1 ? 1 : (x > 4096 ? 4096 : x));
-  }();
   auto head_overlapped = [&]() -> int {
     if (!E.stream2) {
-      int lo = 0, hi = 0;
-      CCRDT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      // CCRDT_TRMV_OVERLAP_PRIO=0: the consumers' stream at normal priority (A/B knob)
-      const char* pe = getenv("CCRDT_TRMV_OVERLAP_PRIO");
-      CCRDT_HIP(hipStreamCreateWithPriority(&E.stream2, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
+      CCRDT_HIP(hipStreamCreateWithFlags(&E.stream2, hipStreamNonBlocking));
       CCRDT_HIP(hipEventCreateWithFlags(&E.ev_ovl, hipEventDisableTiming));
     }
     CCRDT_TRY(E.first_list.ensure(nk * 4));
+    CCRDT_TRY(E.ovf_b.ensure(nk * 4));
     CCRDT_TRY(E.ovl.ensure(64));
     uint32_t* ov = E.ovl.as<uint32_t>();
     CCRDT_HIP(hipMemsetAsync(ov, 0, 16, E.stream));
-    const uint32_t n_sent = (uint32_t)std::min<uint64_t>(nk, 1u << 16);
-    CCRDT_HIP(hipMemsetAsync(E.tier_ovf[0].p, 0xFF, (size_t)n_sent * 4, E.stream));
     const uint32_t pmax = (uint32_t)std::min<int64_t>(E.k, 128);
     const uint32_t thresh = std::min<uint32_t>(128u, pmax + pmax / 5);
-    CCRDT_TRY(trmv_launch_first_list(a.key_ptr, nk, thresh, E.first_list.as<uint32_t>(), ov + 2, E.stream));
+    CCRDT_TRY(trmv_launch_first_list(a.key_ptr, nk, thresh, E.first_list.as<uint32_t>(), ov, E.stream));
     const int e0 = ev;
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    TrmvApplyArgs a0 = a;
-    a0.key_list = nullptr;
-    a0.n_list = (uint32_t)nk;
-    a0.n_list_dev = nullptr;
-    a0.ovf_list = E.tier_ovf[0].as<uint32_t>();
-    a0.status = status + 2;
-    a0.first_list = E.first_list.as<uint32_t>();
-    a0.n_first = ov + 2;
-    a0.first_thresh = thresh;
-    a0.prod_done = ov;
-    CCRDT_TRY(trmv_launch_wave(a0, nk, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    CCRDT_HIP(hipMemsetAsync(ov, 0xFF, 4, E.stream));  // tier 0 is finished (the consumers' exit flag)
     CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.evt[e0], 0));
+    // stream 2: the likely hand-ons, one key per wave, then tier R on theirs
+    TrmvApplyArgs aa = a;
+    aa.key_list = E.first_list.as<uint32_t>();
+    aa.n_list = 0;
+    aa.n_list_dev = ov;
+    aa.ovf_list = E.tier_ovf[0].as<uint32_t>();
+    aa.status = status + 2;
+    aa.kpw = 1;
+    CCRDT_TRY(trmv_launch_wave(aa, std::min<uint64_t>(nk, 4096), E.stream2));
     TrmvApplyArgs a3 = a;
     a3.key_list = E.tier_ovf[0].as<uint32_t>();
     a3.n_list = 0;
     a3.n_list_dev = status + 2;
     a3.ovf_list = E.tier_ovf[3].as<uint32_t>();
     a3.status = status + 2 + 2 * 3;
-    a3.prod_done = ov;
-    a3.claim = ov + 1;
-    a3.n_sent = n_sent;
-    // CCRDT_TRMV_OVERLAP_STALL=1 (tests): the consumers give up at once when
-    // no hand-on is there yet, so the stall fallback runs
-    const char* stall_env = getenv("CCRDT_TRMV_OVERLAP_STALL");
-    const bool force_stall = stall_env && stall_env[0] == '1';
-    a3.spin_limit = force_stall ? 0u : (1u << 19);  // (~2 s)
-    CCRDT_TRY(trmv_launch_resident_consume(a3, overlap_waves, E.stream2));
+    CCRDT_TRY(trmv_launch_resident(a3, later_grid, E.stream2));
     CCRDT_HIP(hipEventRecord(E.ev_ovl, E.stream2));
+    // this stream: every other key
+    TrmvApplyArgs ab = a;
+    ab.key_list = nullptr;
+    ab.n_list = (uint32_t)nk;
+    ab.n_list_dev = nullptr;
+    ab.ovf_list = E.ovf_b.as<uint32_t>();
+    ab.status = ov + 1;
+    ab.skip_thresh = thresh;
+    CCRDT_TRY(trmv_launch_wave(ab, nk, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_ovl, 0));
     CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
     CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+    uint32_t* hov = reinterpret_cast<uint32_t*>(static_cast<char*>(E.h_status) + 128);
+    CCRDT_HIP(hipMemcpyAsync(hov, ov, 16, hipMemcpyDeviceToHost, E.stream));
     CCRDT_HIP(hipStreamSynchronize(E.stream));
-    if ((hs[3 + 2 * 3] & TRMV_ERR_STALL) || force_stall) {
-      // tier 0 did not run beside the consumers: tier R over the whole list
-      // after it (a fresh key's tier R rewrites the same result)
-      CCRDT_HIP(hipMemsetAsync(status + 2 + 2 * 3, 0, 8, E.stream));
-      a3.prod_done = nullptr;
-      CCRDT_TRY(trmv_launch_resident(a3, later_grid, E.stream));
-      CCRDT_HIP(hipEventRecord(E.evt[ev - 1], E.stream));
-      CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
-      CCRDT_HIP(hipStreamSynchronize(E.stream));
-      E.trmv_overflow_keys[9] = 1;  // (diagnostic: the stall fallback ran)
-    }
-    const uint32_t err = hs[3] | hs[3 + 2 * 3];
+    uint32_t err = hs[3] | hs[3 + 2 * 3] | hov[2];
     if (err) return trmv_err_code(err);
+    const uint32_t n_a = hs[2], n_b = hov[1];
     float m0 = 0.f, m3 = 0.f;
     CCRDT_HIP(hipEventElapsedTime(&m0, E.evt[e0], E.evt[e0 + 1]));
     CCRDT_HIP(hipEventElapsedTime(&m3, E.evt[e0 + 1], E.evt[e0 + 2]));
-    E.trmv_tier_ms[0] += m0;
-    E.trmv_tier_ms[3] += m3;  // (tier R's tail past tier 0: the rest ran beside it)
-    E.trmv_overflow_keys[0] = hs[2];
+    if (n_b) {  // (rare) the big launch's hand-ons: tier R after it, then one hand-on list
+      a3.key_list = E.ovf_b.as<uint32_t>();
+      a3.n_list_dev = ov + 1;
+      CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+      CCRDT_TRY(trmv_launch_resident(a3, std::min<uint64_t>(n_b, TRMV_LATER_GRID), E.stream));
+      CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+      CCRDT_HIP(hipMemcpyAsync(E.tier_ovf[0].as<uint32_t>() + n_a, E.ovf_b.p, (size_t)n_b * 4,
+                               hipMemcpyDeviceToDevice, E.stream));
+      CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+      CCRDT_HIP(hipStreamSynchronize(E.stream));
+      if (hs[3 + 2 * 3]) return trmv_err_code(hs[3 + 2 * 3]);
+      float mb = 0.f;
+      CCRDT_HIP(hipEventElapsedTime(&mb, E.evt[ev - 2], E.evt[ev - 1]));
+      m3 += mb;
+    }
+    E.trmv_tier_ms[0] += m0;  // (the big launch's interval; the small one ran beside it)
+    E.trmv_tier_ms[3] += m3;  // (tier R past the big launch: the rest ran beside it)
+    E.trmv_overflow_keys[0] = n_a + n_b;
     E.trmv_overflow_keys[3] = hs[2 + 2 * 3];
+    E.trmv_overflow_keys[9] = n_b;  // (diagnostic: the big launch's hand-ons)
     work = &E.tier_ovf[3];
     n_dev = status + 2 + 2 * 3;
     return CCRDT_OK;

@@ -139,28 +139,13 @@ struct TrmvApplyArgs {
   const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)
   int32_t slack;                    // > 0: segments laid out with room for in-place growth, the pool's
                                     // capacity slack x (its elements + the batch's ops) + 32
-  // The overlapped hand-on of a fresh batch: tier 0 takes the
-  // keys of first_list (count *n_first: the keys with more than first_thresh
-  // ops, the likely hand-ons) before every other key in key order (those with
-  // more than first_thresh ops skipped) and publishes its hand-ons with
-  // device-scope atomics (prod_done non-null); tier R, on a second stream,
-  // takes the keys tier 0 hands on as they appear in its list (claim: the
-  // consumers' next list index; entries below n_sent start as NONE32) until
-  // *prod_done, a flag set by a 4-byte copy queued after tier 0, says tier 0
-  // is finished.  (Tier 0 counting its finished waves on one word instead:
-  // 131k device atomics on one address, polled by the consumers, made tier 0
-  // 1.8x slower.)
-  const uint32_t* first_list;
-  const uint32_t* n_first;
-  uint32_t first_thresh;
-  uint32_t n_sent;
-  uint32_t spin_limit;              // tier R's polls (~4 us each) before it gives up waiting for tier 0
-  uint32_t* prod_done;
-  uint32_t* claim;
+  // The split fresh head: tier 0 over every key but the likely
+  // hand-ons (skip_thresh > 0: keys with more ops are skipped; they are a
+  // key_list launch of their own on a second stream, followed there by tier R
+  // on their hand-ons while this launch runs).
+  uint32_t skip_thresh;
+  uint32_t kpw;  // tier 0: keys per wave chunk (0 = W_KPW; the split head's small launch takes 1)
 };
-// (tier R's consumer gave up waiting for tier 0: the host re-runs tier R
-// over the whole hand-on list)
-constexpr uint32_t TRMV_ERR_STALL = 1u << 30;
 
 // The ops of key k in this pass (a key whose ops an earlier pass applied has
 // none: it is only rewritten).
