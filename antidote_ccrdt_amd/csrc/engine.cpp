@@ -39,8 +39,6 @@ int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, 
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
-int trmv_launch_first_list(const uint64_t* key_ptr, uint64_t n_keys, uint32_t thresh, uint32_t* list,
-                           uint32_t* count, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady_hbm(const TrmvApplyArgs& a, uint32_t waves, void* scratch, hipStream_t st);
@@ -123,7 +121,6 @@ void ccrdt_engine::release_all() {
   for (DevBuf& d : st_n32) d.release();
   for (DevBuf& d : st_nbase) d.release();
   for (DevBuf* d : {&arena, &obs_ord, &key_done, &partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl,
-                    &first_list, &ovf_b, &ovl,
                     &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -246,11 +243,6 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   if (e->evk0) (void)hipEventDestroy(e->evk0);
   if (e->evk1) (void)hipEventDestroy(e->evk1);
   e->destroy_tier_events();
-  if (e->ev_ovl) (void)hipEventDestroy(e->ev_ovl);
-  if (e->stream2) {
-    (void)hipStreamSynchronize(e->stream2);
-    (void)hipStreamDestroy(e->stream2);
-  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return CCRDT_OK;
@@ -590,101 +582,7 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     }
     return CCRDT_OK;
   };
-  // The split head: a fresh batch's head [tier 0, tier R] as
-  // tier 0 over the likely hand-ons (keys with more than min(128, 1.2 pmax)
-  // ops: first_list) followed by tier R on their hand-ons, on a second stream,
-  // beside tier 0 over every other key on this one -- so tier R's per-key
-  // latency is spent while tier 0 still works, not after it.  Nothing polls:
-  // the two launches write disjoint keys and hand-on lists.  The rare hand-on
-  // of the big launch (a key with few ops but more players than K) takes tier
-  // R after it, once the status read says there is one.
-  // CCRDT_TRMV_OVERLAP=0: the chain's head as one tier-0 launch, then tier R (A/B knob).
-  static const bool overlap_env = [] {
-    const char* v = getenv("CCRDT_TRMV_OVERLAP");
-    return !(v && v[0] == '0');
-  }();
-  auto head_overlapped = [&]() -> int {
-    if (!E.stream2) {
-      CCRDT_HIP(hipStreamCreateWithFlags(&E.stream2, hipStreamNonBlocking));
-      CCRDT_HIP(hipEventCreateWithFlags(&E.ev_ovl, hipEventDisableTiming));
-    }
-    CCRDT_TRY(E.first_list.ensure(nk * 4));
-    CCRDT_TRY(E.ovf_b.ensure(nk * 4));
-    CCRDT_TRY(E.ovl.ensure(64));
-    uint32_t* ov = E.ovl.as<uint32_t>();
-    CCRDT_HIP(hipMemsetAsync(ov, 0, 16, E.stream));
-    const uint32_t pmax = (uint32_t)std::min<int64_t>(E.k, 128);
-    const uint32_t thresh = std::min<uint32_t>(128u, pmax + pmax / 5);
-    CCRDT_TRY(trmv_launch_first_list(a.key_ptr, nk, thresh, E.first_list.as<uint32_t>(), ov, E.stream));
-    const int e0 = ev;
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.evt[e0], 0));
-    // stream 2: the likely hand-ons, one key per wave, then tier R on theirs
-    TrmvApplyArgs aa = a;
-    aa.key_list = E.first_list.as<uint32_t>();
-    aa.n_list = 0;
-    aa.n_list_dev = ov;
-    aa.ovf_list = E.tier_ovf[0].as<uint32_t>();
-    aa.status = status + 2;
-    aa.kpw = 1;
-    CCRDT_TRY(trmv_launch_wave(aa, std::min<uint64_t>(nk, 4096), E.stream2));
-    TrmvApplyArgs a3 = a;
-    a3.key_list = E.tier_ovf[0].as<uint32_t>();
-    a3.n_list = 0;
-    a3.n_list_dev = status + 2;
-    a3.ovf_list = E.tier_ovf[3].as<uint32_t>();
-    a3.status = status + 2 + 2 * 3;
-    CCRDT_TRY(trmv_launch_resident(a3, later_grid, E.stream2));
-    CCRDT_HIP(hipEventRecord(E.ev_ovl, E.stream2));
-    // this stream: every other key
-    TrmvApplyArgs ab = a;
-    ab.key_list = nullptr;
-    ab.n_list = (uint32_t)nk;
-    ab.n_list_dev = nullptr;
-    ab.ovf_list = E.ovf_b.as<uint32_t>();
-    ab.status = ov + 1;
-    ab.skip_thresh = thresh;
-    CCRDT_TRY(trmv_launch_wave(ab, nk, E.stream));
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_ovl, 0));
-    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-    CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
-    uint32_t* hov = reinterpret_cast<uint32_t*>(static_cast<char*>(E.h_status) + 128);
-    CCRDT_HIP(hipMemcpyAsync(hov, ov, 16, hipMemcpyDeviceToHost, E.stream));
-    CCRDT_HIP(hipStreamSynchronize(E.stream));
-    uint32_t err = hs[3] | hs[3 + 2 * 3] | hov[2];
-    if (err) return trmv_err_code(err);
-    const uint32_t n_a = hs[2], n_b = hov[1];
-    float m0 = 0.f, m3 = 0.f;
-    CCRDT_HIP(hipEventElapsedTime(&m0, E.evt[e0], E.evt[e0 + 1]));
-    CCRDT_HIP(hipEventElapsedTime(&m3, E.evt[e0 + 1], E.evt[e0 + 2]));
-    if (n_b) {  // (rare) the big launch's hand-ons: tier R after it, then one hand-on list
-      a3.key_list = E.ovf_b.as<uint32_t>();
-      a3.n_list_dev = ov + 1;
-      CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-      CCRDT_TRY(trmv_launch_resident(a3, std::min<uint64_t>(n_b, TRMV_LATER_GRID), E.stream));
-      CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
-      CCRDT_HIP(hipMemcpyAsync(E.tier_ovf[0].as<uint32_t>() + n_a, E.ovf_b.p, (size_t)n_b * 4,
-                               hipMemcpyDeviceToDevice, E.stream));
-      CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
-      CCRDT_HIP(hipStreamSynchronize(E.stream));
-      if (hs[3 + 2 * 3]) return trmv_err_code(hs[3 + 2 * 3]);
-      float mb = 0.f;
-      CCRDT_HIP(hipEventElapsedTime(&mb, E.evt[ev - 2], E.evt[ev - 1]));
-      m3 += mb;
-    }
-    E.trmv_tier_ms[0] += m0;  // (the big launch's interval; the small one ran beside it)
-    E.trmv_tier_ms[3] += m3;  // (tier R past the big launch: the rest ran beside it)
-    E.trmv_overflow_keys[0] = n_a + n_b;
-    E.trmv_overflow_keys[3] = hs[2 + 2 * 3];
-    E.trmv_overflow_keys[9] = n_b;  // (diagnostic: the big launch's hand-ons)
-    work = &E.tier_ovf[3];
-    n_dev = status + 2 + 2 * 3;
-    return CCRDT_OK;
-  };
-  const bool overlap = overlap_env && E.fresh && nk && n_head == 2 && chain[0] == 0 && chain[1] == 3;
-  if (overlap) CCRDT_TRY(head_overlapped());
-  else CCRDT_TRY(segment(0, n_head));
+  CCRDT_TRY(segment(0, n_head));
   if (n_head < n_chain && nk && hs[2 + 2 * chain[n_head - 1]] != 0) CCRDT_TRY(segment(n_head, n_chain));
   // Keys past the 1024-player class: tier 4 (HBM scratch), on the host-known
   // list tier 2 handed on.

@@ -49,7 +49,7 @@ struct ccrdt_engine {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the main apply kernel
-  hipEvent_t evt[12] = {};                     // topk_rmv tier boundaries
+  hipEvent_t evt[8] = {};                      // topk_rmv tier boundaries
   bool create_tier_events() {
     for (hipEvent_t& v : evt)
       if (hipEventCreate(&v) != hipSuccess) return false;
@@ -81,13 +81,6 @@ struct ccrdt_engine {
   ccrdt::DevBuf arena, obs_ord, key_done;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
   ccrdt::DevBuf tier_ovf[5];    // keys each topk_rmv tier handed on (last batch)
-  // the split head of fresh batches: the likely hand-ons
-  // (first_list) through tier 0 and tier R on a second stream (created on
-  // first use) beside tier 0 over the other keys (its hand-ons: ovf_b);
-  // ovl = [first_list count, ovf_b count, that launch's error word]
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_ovl = nullptr;
-  ccrdt::DevBuf first_list, ovf_b, ovl;
   ccrdt::DevBuf hbm_scratch;    // tier 4's per-wave working sets
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;

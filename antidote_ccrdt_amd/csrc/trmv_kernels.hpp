@@ -139,12 +139,6 @@ struct TrmvApplyArgs {
   const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)
   int32_t slack;                    // > 0: segments laid out with room for in-place growth, the pool's
                                     // capacity slack x (its elements + the batch's ops) + 32
-  // The split fresh head: tier 0 over every key but the likely
-  // hand-ons (skip_thresh > 0: keys with more ops are skipped; they are a
-  // key_list launch of their own on a second stream, followed there by tier R
-  // on their hand-ons while this launch runs).
-  uint32_t skip_thresh;
-  uint32_t kpw;  // tier 0: keys per wave chunk (0 = W_KPW; the split head's small launch takes 1)
 };
 
 // The ops of key k in this pass (a key whose ops an earlier pass applied has

@@ -1889,7 +1889,6 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
 
 void trmv_resident_preload() { preload_kernels(trmv_resident_kernel<true>, trmv_resident_kernel<false>); }
 
-
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
   const uint64_t blocks = std::min<uint64_t>((grid_keys + TRMV_R_WG - 1) / TRMV_R_WG, 65536 / TRMV_R_WG);

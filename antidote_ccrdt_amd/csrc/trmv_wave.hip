@@ -183,7 +183,6 @@ struct ChunkHdr {
   uint32_t key;         // lane j < n: key j
   uint64_t lo, hi;      // lane j < n: key_ptr[key j], key_ptr[key j + 1]
   uint32_t meta[W_MD];  // meta[i], lane 8m + d: dword d of new_s.meta[key 8i + m]
-  uint64_t skip;        // bit j: key j is left to the split head's other launch (skip_thresh)
 };
 
 __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t c0, uint32_t n,
@@ -193,12 +192,11 @@ __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t
   h.key = KA->key_list ? KA->key_list[c0 + j] : c0 + j;
   h.lo = KA->key_ptr[h.key];
   h.hi = KA->key_ptr[h.key + 1];
-  h.skip = KA->skip_thresh ? ballot((uint32_t)lane < n && h.hi - h.lo > KA->skip_thresh) : 0ull;
 #pragma unroll
   for (int i = 0; i < W_MD; ++i) {
     const uint32_t m = 8 * i + (lane >> 3);
     const uint32_t jm = m < n ? m : 0u;
-    const uint32_t km = shfl32(h.key, (int)jm);
+    const uint32_t km = KA->key_list ? KA->key_list[c0 + jm] : c0 + jm;
     if (KA->fresh) {  // trmv_new_meta: the fresh layout's offsets, counts 0, Min nil
       const uint32_t d = lane & 7;
       h.meta[i] = d < 3 ? (uint32_t)trmv_fresh_off(KA->slack != 0, (int)d, km, KA->key_ptr[km])
@@ -1148,9 +1146,8 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];
   const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
-  const uint32_t kpw = a.kpw ? a.kpw : (uint32_t)W_KPW;  // keys per wave chunk (a.kpw <= W_KPW)
-  for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * kpw; c0 < n; c0 += gridDim.x * W_WAVES * kpw) {
-    const uint32_t cn = c0 + kpw < n ? kpw : n - c0;
+  for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * W_KPW; c0 < n; c0 += gridDim.x * W_WAVES * W_KPW) {
+    const uint32_t cn = c0 + W_KPW < n ? W_KPW : n - c0;
     ChunkHdr hdr;
     wave_load_chunk(a, c0, cn, hdr);
     KeyIn cur, nxt;
@@ -1160,9 +1157,7 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
       const bool has_next = j + 1 < cn;
-      // a key the split head's other launch takes: only the next key's loads
-      const int r = (hdr.skip >> j) & 1u ? W_REJECT + 1
-                                         : trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
+      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&KA->status[0], 1u);
@@ -1185,8 +1180,7 @@ void trmv_wave_preload() { preload_kernels(trmv_wave_kernel<true>, trmv_wave_ker
 
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;
-  if (a.kpw > (uint32_t)W_KPW) return CCRDT_EINVAL;
-  const uint64_t per_block = (uint64_t)W_WAVES * (a.kpw ? a.kpw : W_KPW);
+  const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
   const uint64_t blocks = (grid_keys + per_block - 1) / per_block;
   if (a.fresh)
     hipLaunchKernelGGL(trmv_wave_kernel<true>, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
