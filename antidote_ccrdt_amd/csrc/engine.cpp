@@ -639,6 +639,15 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     }
     CCRDT_TRY(E.arena.ensure(sizeof(sub) + 16 * TRMV_NSUB));
     E.arena_pending = true;
+    // what the next (in-place) pass writes and reads back, allocated now: its
+    // first use made the first in-place batch after a fresh one 2.4 ms slower
+    // in wall time than its kernels (meta / cap of the other side, 48 B per
+    // key, and the pinned read-back)
+    CCRDT_TRY(E.trmv[1 - mout].meta.ensure(nk * sizeof(KeyMeta)));
+    CCRDT_TRY(E.trmv[1 - mout].cap.ensure(nk * sizeof(KeyCap)));
+    if (!E.h_arena && hipHostMalloc(&E.h_arena, 2 * sizeof(E.arena_sub[0]) + 16 * TRMV_NSUB,
+                                    hipHostMallocDefault) != hipSuccess)
+      E.h_arena = nullptr;  // (the in-place pass allocates it, or fails cleanly)
   }
   for (int x = 0; x < 3; ++x) E.trmv_tot[out][x] = tot[x];
   E.cur = out;
