@@ -144,6 +144,8 @@ SIGNATURES = {
     "ccrdt_trmv_import_range": (INT, [P, I64, I64, C.POINTER(TrmvState)]),
     "ccrdt_trmv_import": (INT, [P, C.POINTER(TrmvState)]),
     "ccrdt_trmv_downstream": (INT, [P, I64, P, P, P, P, P, P, P, P]),
+    "ccrdt_trmv_key_to_binary": (INT, [C.POINTER(TrmvState), INT, I64, I64, P, P, P, U64, C.POINTER(U64)]),
+    "ccrdt_trmv_key_from_binary": (INT, [P, U64, INT, P, P, C.POINTER(TrmvState), P, P, C.POINTER(I64)]),
     # average
     "ccrdt_avg_apply": (INT, [P, C.POINTER(AvgOps)]),
     "ccrdt_avg_apply_device": (INT, [P, C.POINTER(AvgOps)]),

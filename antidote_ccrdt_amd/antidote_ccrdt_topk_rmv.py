@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import etf, terms
+from . import _lib, etf, terms
 from ._lib import NOOP
 from .engine import TopkRmvEngine, TrmvState
 
@@ -162,59 +162,41 @@ def _atom(dc):
     return etf.Atom(dc) if isinstance(dc, str) and not isinstance(dc, etf.Atom) else dc
 
 
-def _dc_rank(d) -> int:
-    """Registry rank of a decoded DcId term (an atom, or any term such as a
-    {Node, {Mega, Sec, Micro}} tuple); an unregistered one is an EtfError."""
-    try:
-        return terms.DC_REGISTRY.rank(d)
-    except KeyError as e:
-        raise etf.EtfError(str(e)) from None
+def _dc_terms():
+    """Every DC rank's DcId as canonical ETF bytes (no version byte) for the
+    native codec: the registered DcIds in rank (= term) order, then a
+    placeholder atom per unused rank (never written: no clock entry or
+    element of a state names an unused rank, and no decoded term matches it)."""
+    reg = terms.DC_REGISTRY
+    parts = [etf.term_to_binary(_atom(reg.dc(d)) if d < len(reg) else etf.Atom(f"$ccrdt_unused_dc{d}"))[1:]
+             for d in range(reg.capacity)]
+    off = np.zeros(len(parts) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in parts])
+    return np.frombuffer(b"".join(parts), np.uint8).copy(), off
 
 
 def to_binary(state: TopkRmv) -> bytes:
     """to_binary/1 (topk_rmv.erl:156-158): term_to_binary of the 6-tuple
     {Observed, Masked, Removals, Vc, Min, Size}; Masked[Id] is a gb_sets set
-    and DcIds are atoms (etf.py)."""
-    obs, masked, rem, vc, mn, size = state.to_term()
-    el = lambda e: (e[0], e[1], (_atom(e[2][0]), e[2][1]))
-    term = ({i: el(e) for i, e in obs.items()},
-            {i: etf.GbSet(el(e) for e in v) for i, v in masked.items()},
-            {i: {_atom(d): t for d, t in v.items()} for i, v in rem.items()},
-            {_atom(d): t for d, t in vc.items()},
-            el(mn) if mn != NIL else (etf.Atom("nil"),) * 3, size)
-    return etf.term_to_binary(term)
+    and DcIds are atoms.  Written by the native codec
+    (ccrdt_trmv_key_to_binary) from the key's state image: the same bytes as
+    etf.term_to_binary(...) of to_term() with atom DcIds."""
+    dt, do = _dc_terms()
+    return state.engine.export().key_to_binary(0, state.size, dt, do)
 
 
 def from_binary(b: bytes):
     """from_binary/1 (topk_rmv.erl:161-163): decodes any ERTS shape of the
-    6-tuple (gb_sets trees, maps) into an engine-resident state."""
-    t = etf.binary_to_term(b)
-    if not (isinstance(t, tuple) and len(t) == 6 and all(isinstance(x, dict) for x in t[:4])):
-        raise etf.EtfError("not a topkrmv() term")
-    obs, masked, rem, vc, mn, size = t
-    if not (_is_int(size) and size > 0):
-        raise etf.EtfError("topkrmv() Size must be a positive integer")
-    rank = _dc_rank
-    nd = terms.DC_REGISTRY.capacity
-    el = lambda e: (int(e[1]), int(e[0]), rank(e[2][0]), int(e[2][1]))  # (id, score, dc, ts)
-    o = sorted(el(e) for e in obs.values())
-    m = sorted(el(e) for v in masked.values() for e in etf.gb_set_items(v))
-    r = sorted(rem.items())
-    st = TrmvState.empty(1, nd, len(o), len(m), len(r))
-    for d, ts in vc.items():
-        st.vc[0, rank(d)] = ts
-    st.obs_ptr[1], st.m_ptr[1], st.r_ptr[1] = len(o), len(m), len(r)
-    for j, (i, sc, d, ts) in enumerate(o):
-        st.obs_id[j], st.obs_score[j], st.obs_dc[j], st.obs_ts[j] = i, sc, d, ts
-    for j, (i, sc, d, ts) in enumerate(m):
-        st.m_id[j], st.m_score[j], st.m_dc[j], st.m_ts[j] = i, sc, d, ts
-    for j, (i, v) in enumerate(r):
-        st.r_id[j] = i
-        for d, ts in v.items():
-            st.r_vc[j, rank(d)] = ts
-    if mn != (etf.Atom("nil"),) * 3:
-        i, sc, d, ts = el(mn)
-        st.min_valid[0], st.min_id[0], st.min_score[0], st.min_dc[0], st.min_ts[0] = 1, i, sc, d, ts
+    6-tuple (gb_sets trees, maps, any integer / atom tag) into an
+    engine-resident state, in native code (ccrdt_trmv_key_from_binary).  A
+    malformed term or a DcId the registry lacks is an EtfError (badarg)."""
+    dt, do = _dc_terms()
+    try:
+        st, size = TrmvState.key_from_binary(b, terms.DC_REGISTRY.capacity, dt, do)
+    except _lib.CcrdtError as e:
+        if e.code == _lib.EINVAL:
+            raise etf.EtfError(str(e)) from None
+        raise
     eng = _engine(size)
     eng.import_state(st)
     return ("ok", TopkRmv(size, eng))

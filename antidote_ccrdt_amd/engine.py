@@ -102,6 +102,34 @@ class TrmvState:
             min_id=z(n_keys, np.int64), min_score=z(n_keys, np.int64), min_dc=z(n_keys, np.uint8),
             min_ts=z(n_keys, np.int64))
 
+    def key_to_binary(self, k: int, size: int, dc_term: np.ndarray, dc_off: np.ndarray) -> bytes:
+        """to_binary/1 of key k in native code (ccrdt_trmv_key_to_binary): the
+        ETF bytes of its {Observed, Masked, Removals, Vc, Min, Size}; DC rank d
+        is written as dc_term[dc_off[d]:dc_off[d + 1]]."""
+        n_dc = int(self.vc.shape[1])
+        c, n = self.as_c(), C.c_uint64(0)
+        args = (C.byref(c), n_dc, int(k), int(size), ptr(dc_term), ptr(dc_off))
+        rc = lib.ccrdt_trmv_key_to_binary(*args, None, 0, C.byref(n))
+        if rc not in (_lib.OK, _lib.ENOMEM):
+            check(rc, "trmv_key_to_binary")
+        buf = np.empty(max(int(n.value), 1), np.uint8)
+        check(lib.ccrdt_trmv_key_to_binary(*args, ptr(buf), int(n.value), C.byref(n)), "trmv_key_to_binary")
+        return buf[:int(n.value)].tobytes()
+
+    @staticmethod
+    def key_from_binary(b: bytes, n_dc: int, dc_term: np.ndarray, dc_off: np.ndarray) -> tuple["TrmvState", int]:
+        """from_binary/1 in native code (ccrdt_trmv_key_from_binary): the ETF
+        bytes of one state -> (its one-key image, Size)."""
+        raw = np.frombuffer(bytes(b), np.uint8) if len(b) else np.zeros(1, np.uint8)
+        counts, size = np.zeros(3, np.int64), C.c_int64(0)
+        args = (ptr(raw), len(b), int(n_dc), ptr(dc_term), ptr(dc_off))
+        check(lib.ccrdt_trmv_key_from_binary(*args, None, None, ptr(counts), C.byref(size)), "trmv_key_from_binary")
+        st = TrmvState.empty(1, n_dc, *(int(x) for x in counts))
+        c, caps = st.as_c(), counts.copy()
+        check(lib.ccrdt_trmv_key_from_binary(*args, C.byref(c), ptr(caps), ptr(counts), C.byref(size)),
+              "trmv_key_from_binary")
+        return st, int(size.value)
+
     def as_c(self) -> _lib.TrmvState:
         s = _lib.TrmvState()
         for f in fields(self):

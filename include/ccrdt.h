@@ -286,6 +286,34 @@ int ccrdt_trmv_import_range(ccrdt_engine* e, int64_t k0, int64_t k1, const ccrdt
  * (sorting not required); invariants of the reference are checked. */
 int ccrdt_trmv_import(ccrdt_engine* e, const ccrdt_trmv_state* in);
 
+/* to_binary/1 of one key of a state image (topk_rmv.erl:156-158: term_to_binary
+ * of {Observed, Masked, Removals, Vc, Min, Size}) in native code: key k of `st`
+ * (the ccrdt_trmv_state layout, n_dc clock columns) as Erlang external term
+ * format -- elements {Score, Id, {DcId, Ts}}, Masked[Id] as the balanced
+ * gb_sets {Size, Tree} of gb_sets:from_ordset/1, clocks as maps without their
+ * 0 entries, Min {nil, nil, nil} when absent, map keys in term order.  DC rank
+ * d is written as the ETF term dc_term[dc_off[d] .. dc_off[d+1]) (no version
+ * byte; atoms as SMALL_ATOM_UTF8; ranks in term order, as the engine's are).
+ * Writes at most `cap` bytes into buf; *len = the term's size in bytes
+ * (CCRDT_ENOMEM when cap < *len: call with cap = 0 to size the buffer).  The
+ * same bytes as the Python codec (antidote_ccrdt_amd/etf.py). */
+int ccrdt_trmv_key_to_binary(const ccrdt_trmv_state* st, int n_dc, int64_t k, int64_t size,
+                             const uint8_t* dc_term, const uint64_t* dc_off, uint8_t* buf, uint64_t cap,
+                             uint64_t* len);
+/* from_binary/1 (topk_rmv.erl:161-163): an ETF state 6-tuple as ERTS writes it
+ * (maps in any order, any integer / atom / tuple tag, gb_sets trees of any
+ * shape) -> the canonical image of ONE key in `out` (ptr arrays [2], vc /
+ * min arrays [1]; sorted as ccrdt_trmv_export sorts).  DcIds are matched by
+ * their canonical encoding against dc_term (as for to_binary).  counts[3] =
+ * the key's |Observed|, Masked elements, Removals rows; *size = Size.  With
+ * out or caps NULL only counts and size are set (the sizing call); a count
+ * above caps[i] is CCRDT_ENOMEM.  A malformed term or unknown DcId is
+ * CCRDT_EINVAL (binary_to_term badarg / a DC the engine does not hold), an
+ * integer outside int64 CCRDT_ERANGE. */
+int ccrdt_trmv_key_from_binary(const uint8_t* buf, uint64_t len, int n_dc, const uint8_t* dc_term,
+                               const uint64_t* dc_off, ccrdt_trmv_state* out, const int64_t* caps,
+                               int64_t* counts, int64_t* size);
+
 /* downstream/2 (topk_rmv.erl:102-124) for n requests against the current
  * state (read-only).  op[i] 0 = {add, {Id, Score}}, 1 = {rmv, Id}.  For add,
  * dc[i]/ts[i] are the origin's DC rank and clock (?DC_META_DATA, ?TIME).
