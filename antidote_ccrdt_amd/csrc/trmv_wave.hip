@@ -706,15 +706,7 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
         // (:234), or kept by the first later one (:255-266) -> replay
         const uint64_t Mneed = Mya & Misr & (Mbefore | ~Mseen);
         const bool need = (Mneed >> lane) & 1u;
-#if TRMV_RT_COND
-        // (a clock is needed only by an add with a rmv of its player before
-        // or after it: most positions of most waves need none, and skip the
-        // LDS round trip)
-        int64_t rt = 0;
-        if (Mneed) rt = L.rows[need ? (uint32_t)sx : 0u][adc];
-#else
         const int64_t rt = L.rows[need ? (uint32_t)sx : 0u][adc];
-#endif
         const uint32_t pn = x + 1 < c ? st + x + 1 : (uint32_t)ESINK;
         sxn = L.esc[pn];
         txn = L.ets[pn];
