@@ -39,6 +39,10 @@ int trmv_launch_mark_done(uint8_t* done, uint64_t n_keys, const uint32_t* list, 
 int trmv_launch_keep(const TrmvApplyArgs& a, uint32_t grid, hipStream_t st);
 int trmv_launch_downstream(const TrmvDownArgs& a, hipStream_t st);
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
+int trmv_launch_first_list(const uint64_t* key_ptr, uint64_t n_keys, uint32_t thresh, uint32_t* list,
+                           uint32_t* count, hipStream_t st);
+uint32_t trmv_wave_waves(uint64_t grid_keys);
+int trmv_launch_resident_consume(const TrmvApplyArgs& a, uint32_t waves, hipStream_t st);
 int trmv_launch_steady(const TrmvApplyArgs& a, int cls, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st);
 int trmv_launch_steady_hbm(const TrmvApplyArgs& a, uint32_t waves, void* scratch, hipStream_t st);
@@ -121,6 +125,7 @@ void ccrdt_engine::release_all() {
   for (DevBuf& d : st_n32) d.release();
   for (DevBuf& d : st_nbase) d.release();
   for (DevBuf* d : {&arena, &obs_ord, &key_done, &partials, &ex_cnt, &ex, &ex_vc, &ex_key_ptr, &status, &op_pl,
+                    &first_list, &ovl,
                     &hbm_scratch, &st_kp,
                     &st_kind, &st_id, &st_score, &st_dc, &st_ts, &st_rvc, &st_out_kind, &st_out_vc})
     d->release();
@@ -243,6 +248,11 @@ int ccrdt_engine_destroy(ccrdt_engine* e) {
   if (e->evk0) (void)hipEventDestroy(e->evk0);
   if (e->evk1) (void)hipEventDestroy(e->evk1);
   e->destroy_tier_events();
+  if (e->ev_ovl) (void)hipEventDestroy(e->ev_ovl);
+  if (e->stream2) {
+    (void)hipStreamSynchronize(e->stream2);
+    (void)hipStreamDestroy(e->stream2);
+  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return CCRDT_OK;
@@ -582,7 +592,117 @@ int trmv_pass_full(Engine& E, TrmvApplyArgs a, uint64_t n_ops, uint32_t* status,
     }
     return CCRDT_OK;
   };
-  CCRDT_TRY(segment(0, n_head));
+  // The overlapped hand-on: a fresh batch's head [tier 0,
+  // tier R] with tier R on a second, high-priority stream beside tier 0,
+  // taking the keys tier 0 hands on while it runs; tier 0 takes the likely
+  // hand-ons (more than min(128, 1.2 pmax) ops) first, so tier R's per-key
+  // latency is spent while tier 0 still works instead of after it.  On for
+  // engines of at most CCRDT_TRMV_OVERLAP_KEYS keys (default 2^18: a rank of
+  // the strong line at N >= 4): the tail it hides is one key's latency, a
+  // larger share of a smaller shard's step, and tier 0 runs ~5 % slower beside
+  // it (profiles/r06/ab_overlap_waves.txt: 2^17 keys, step 0.404 -> 0.374 ms;
+  // 2^20 keys, 2.29 -> 2.34 ms, so off there).
+  // CCRDT_TRMV_OVERLAP=0: never; CCRDT_TRMV_OVERLAP_WAVES: tier R's waves
+  // (32: 16 could not keep up with the hand-ons, 48 and 64 slowed tier 0).
+  static const bool overlap_env = [] {
+    const char* v = getenv("CCRDT_TRMV_OVERLAP");
+    return !(v && v[0] == '0');
+  }();
+  static const uint64_t overlap_keys = [] {
+    const char* v = getenv("CCRDT_TRMV_OVERLAP_KEYS");
+    return v ? strtoull(v, nullptr, 10) : (1ull << 18);
+  }();
+  static const uint32_t overlap_waves = [] {
+    const char* v = getenv("CCRDT_TRMV_OVERLAP_WAVES");
+    const int x = v ? atoi(v) : 32;
+    return (uint32_t)(x < 1 ? 1 : (x > 4096 ? 4096 : x));
+  }();
+  auto head_overlapped = [&]() -> int {
+    if (!E.stream2) {
+      // (created through the priority API at the highest priority: a plain
+      // second stream shared a hardware queue with the engine's and ran after it)
+      int lo = 0, hi = 0;
+      CCRDT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      CCRDT_HIP(hipStreamCreateWithPriority(&E.stream2, hipStreamNonBlocking, hi));
+      CCRDT_HIP(hipEventCreateWithFlags(&E.ev_ovl, hipEventDisableTiming));
+    }
+    // ovl: [done words | claim | first_list count | pad | published hand-ons (key + 1), one per key]
+    constexpr uint32_t O_CLAIM = TRMV_NDONE, O_NFIRST = TRMV_NDONE + 1, O_PUB = TRMV_NDONE + 4;
+    CCRDT_TRY(E.first_list.ensure(nk * 4));
+    CCRDT_TRY(E.ovl.ensure((O_PUB + nk) * 4));
+    uint32_t* ov = E.ovl.as<uint32_t>();
+    CCRDT_HIP(hipMemsetAsync(ov, 0, (O_PUB + nk) * 4, E.stream));
+    const uint32_t pmax = (uint32_t)std::min<int64_t>(E.k, 128);
+    const uint32_t thresh = std::min<uint32_t>(128u, pmax + pmax / 5);
+    CCRDT_TRY(trmv_launch_first_list(a.key_ptr, nk, thresh, E.first_list.as<uint32_t>(), ov + O_NFIRST, E.stream));
+    const int e0 = ev;
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    TrmvApplyArgs a0 = a;
+    a0.key_list = nullptr;
+    a0.n_list = (uint32_t)nk;
+    a0.n_list_dev = nullptr;
+    a0.ovf_list = E.tier_ovf[0].as<uint32_t>();
+    a0.status = status + 2;
+    a0.first_list = E.first_list.as<uint32_t>();
+    a0.n_first = ov + O_NFIRST;
+    a0.first_thresh = thresh;
+    a0.pub = ov + O_PUB;
+    a0.n_pub = (uint32_t)nk;
+    a0.done = ov;
+    CCRDT_TRY(trmv_launch_wave(a0, nk, E.stream));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    CCRDT_HIP(hipStreamWaitEvent(E.stream2, E.evt[e0], 0));
+    TrmvApplyArgs a3 = a;
+    a3.key_list = E.tier_ovf[0].as<uint32_t>();
+    a3.n_list = 0;
+    a3.n_list_dev = status + 2;
+    a3.ovf_list = E.tier_ovf[3].as<uint32_t>();
+    a3.status = status + 2 + 2 * 3;
+    a3.pub = ov + O_PUB;
+    a3.n_pub = (uint32_t)nk;
+    a3.done = ov;
+    a3.prod_waves = trmv_wave_waves(nk);
+    a3.claim = ov + O_CLAIM;
+    // CCRDT_TRMV_OVERLAP_STALL=1 (tests): the consumers give up at once when
+    // no hand-on is there yet, and the host's fallback runs
+    const char* stall_env = getenv("CCRDT_TRMV_OVERLAP_STALL");
+    const bool force_stall = stall_env && stall_env[0] == '1';
+    a3.spin_limit = force_stall ? 0u : (1u << 19);  // (~2 s)
+    CCRDT_TRY(trmv_launch_resident_consume(a3, overlap_waves, E.stream2));
+    CCRDT_HIP(hipEventRecord(E.ev_ovl, E.stream2));
+    CCRDT_HIP(hipStreamWaitEvent(E.stream, E.ev_ovl, 0));
+    CCRDT_HIP(hipEventRecord(E.evt[ev++], E.stream));
+    CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+    CCRDT_HIP(hipStreamSynchronize(E.stream));
+    if ((hs[3 + 2 * 3] & TRMV_ERR_STALL) || force_stall) {
+      // tier 0 did not run beside the consumers: tier R over the whole list
+      // after it (a fresh key's tier R rewrites the same result)
+      CCRDT_HIP(hipMemsetAsync(status + 2 + 2 * 3, 0, 8, E.stream));
+      a3.pub = nullptr;
+      a3.done = nullptr;
+      CCRDT_TRY(trmv_launch_resident(a3, later_grid, E.stream));
+      CCRDT_HIP(hipEventRecord(E.evt[ev - 1], E.stream));
+      CCRDT_HIP(hipMemcpyAsync(E.h_status, status, TRMV_STATUS_WORDS * 4, hipMemcpyDeviceToHost, E.stream));
+      CCRDT_HIP(hipStreamSynchronize(E.stream));
+      E.trmv_overflow_keys[9] = 1;  // (diagnostic: the stall fallback ran)
+    }
+    const uint32_t err = hs[3] | hs[3 + 2 * 3];
+    if (err) return trmv_err_code(err);
+    float m0 = 0.f, m3 = 0.f;
+    CCRDT_HIP(hipEventElapsedTime(&m0, E.evt[e0], E.evt[e0 + 1]));
+    CCRDT_HIP(hipEventElapsedTime(&m3, E.evt[e0 + 1], E.evt[e0 + 2]));
+    E.trmv_tier_ms[0] += m0;
+    E.trmv_tier_ms[3] += m3;  // (tier R's tail past tier 0: the rest ran beside it)
+    E.trmv_overflow_keys[0] = hs[2];
+    E.trmv_overflow_keys[3] = hs[2 + 2 * 3];
+    work = &E.tier_ovf[3];
+    n_dev = status + 2 + 2 * 3;
+    return CCRDT_OK;
+  };
+  const bool overlap = overlap_env && E.fresh && nk && nk <= overlap_keys && n_head == 2 && chain[0] == 0 &&
+                       chain[1] == 3;
+  if (overlap) CCRDT_TRY(head_overlapped());
+  else CCRDT_TRY(segment(0, n_head));
   if (n_head < n_chain && nk && hs[2 + 2 * chain[n_head - 1]] != 0) CCRDT_TRY(segment(n_head, n_chain));
   // Keys past the 1024-player class: tier 4 (HBM scratch), on the host-known
   // list tier 2 handed on.

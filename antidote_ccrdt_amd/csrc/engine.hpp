@@ -81,6 +81,12 @@ struct ccrdt_engine {
   ccrdt::DevBuf arena, obs_ord, key_done;
   ccrdt::DevBuf partials, ex_cnt, ex, ex_vc, ex_key_ptr, status, op_pl;
   ccrdt::DevBuf tier_ovf[5];    // keys each topk_rmv tier handed on (last batch)
+  // the overlapped hand-on of fresh batches: tier R on a second stream beside
+  // tier 0 (created on first use); first_list = the likely hand-ons, taken
+  // first; ovl = [tier 0 waves finished, consumer claim counter, first_list count]
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_ovl = nullptr;
+  ccrdt::DevBuf first_list, ovl;
   ccrdt::DevBuf hbm_scratch;    // tier 4's per-wave working sets
   int trmv_first_tier = 0;
   uint64_t last_n_ops = 0;

@@ -435,11 +435,34 @@ __global__ __launch_bounds__(256) void trmv_mark_done_kernel(uint8_t* done, uint
   }
 }
 
+// The likely hand-ons of a fresh batch (keys with more than `thresh` ops) ->
+// list (any order; *count = how many): tier 0 takes them first.
+__global__ __launch_bounds__(256) void trmv_first_list_kernel(const uint64_t* key_ptr, uint64_t n_keys,
+                                                              uint32_t thresh, uint32_t* list, uint32_t* count) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool f = k < n_keys && key_ptr[k + 1] - key_ptr[k] > thresh;
+  const uint64_t m = ballot(f);
+  if (!m) return;
+  uint32_t base = 0;
+  if (lane_id() == (int)__builtin_ctzll(m)) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
+  base = shfl32(base, (int)__builtin_ctzll(m));
+  if (f) list[base + mbcnt(m)] = (uint32_t)k;
+}
+
+int trmv_launch_first_list(const uint64_t* key_ptr, uint64_t n_keys, uint32_t thresh, uint32_t* list,
+                           uint32_t* count, hipStream_t st) {
+  if (n_keys == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_first_list_kernel, dim3((unsigned)((n_keys + 255) / 256)), dim3(256), 0, st, key_ptr,
+                     n_keys, thresh, list, count);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
 // ------------------------------------------------------------- launchers
 // (scratch: one u64 flag, zeroed here)
 void trmv_kernels_preload() {
   preload_kernels(trmv_scan_partials, trmv_scan_tops, trmv_scan_apply, trmv_validate_kernel, trmv_validate_rows_any,
-                  trmv_validate_rows_exact, trmv_keep_kernel, trmv_mark_done_kernel);
+                  trmv_validate_rows_exact, trmv_keep_kernel, trmv_mark_done_kernel, trmv_first_list_kernel);
 }
 
 int trmv_launch_validate(const TrmvApplyArgs& a, uint64_t n_ops, uint32_t* err, unsigned long long* scratch,

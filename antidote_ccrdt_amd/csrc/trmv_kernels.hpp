@@ -139,7 +139,30 @@ struct TrmvApplyArgs {
   const uint32_t* verr;             // in place: the batch validation's error flags (non-zero: nothing is written)
   int32_t slack;                    // > 0: segments laid out with room for in-place growth, the pool's
                                     // capacity slack x (its elements + the batch's ops) + 32
+  // The overlapped hand-on of a fresh batch: tier 0 takes the
+  // keys of first_list (count *n_first: the keys with more than first_thresh
+  // ops, the likely hand-ons) before every other key in key order (those with
+  // more than first_thresh ops skipped), publishes each hand-on also as key + 1
+  // in pub[pos] (pos < n_pub; 0 = not yet) with a device-scope atomic, and
+  // each of its waves adds one to done[wave % TRMV_NDONE] when it is finished
+  // (TRMV_NDONE words: 131k adds on one word, polled by the consumers, had
+  // made tier 0 1.8x slower).  Tier R, on a second stream, takes the keys as
+  // they are published (claim: the consumers' next list index) until the done
+  // words sum to prod_waves and its index is past tier 0's final count.
+  const uint32_t* first_list;
+  const uint32_t* n_first;
+  uint32_t first_thresh;
+  uint32_t n_pub;
+  uint32_t prod_waves;              // tier 0's waves (what the done words sum to when it is finished)
+  uint32_t spin_limit;              // tier R's polls (~4 us each) before it gives up waiting for tier 0
+  uint32_t* pub;
+  uint32_t* done;
+  uint32_t* claim;
 };
+constexpr int TRMV_NDONE = 64;
+// (tier R's consumer gave up waiting for tier 0: the host re-runs tier R
+// over the whole hand-on list)
+constexpr uint32_t TRMV_ERR_STALL = 1u << 30;
 
 // The ops of key k in this pass (a key whose ops an earlier pass applied has
 // none: it is only rewritten).

@@ -1887,7 +1887,79 @@ __global__ __launch_bounds__(64 * TRMV_R_WG, TRMV_R_WAVES) void trmv_resident_ke
   }
 }
 
-void trmv_resident_preload() { preload_kernels(trmv_resident_kernel<true>, trmv_resident_kernel<false>); }
+// Tier R over a fresh batch's hand-ons WHILE tier 0 runs (the overlapped
+// hand-on): each wave claims the next index of tier 0's hand-on
+// list, waits until tier 0 has published that entry (a.pub[idx] = key + 1),
+// and applies the key; it leaves when tier 0 is finished (its done words sum
+// to a.prod_waves) and the index is past tier 0's final count
+// (*a.n_list_dev).  Every access the two kernels share is a device-scope
+// atomic (the XCDs' L2s are not coherent with each other).  A wave that has
+// waited ~2 s sets TRMV_ERR_STALL and leaves; the host then re-runs tier R
+// over the whole list (a fresh key's tier R is idempotent).  Launched after
+// tier 0 on a high-priority stream: if the two do not run side by side, this
+// one runs after tier 0 and takes the list as the chain would.
+__device__ __forceinline__ uint32_t r_atomic_read(uint32_t* p) { return atomicOr(p, 0u); }
+
+__global__ __launch_bounds__(64, TRMV_R_WAVES) void trmv_resident_consume_kernel(TrmvApplyArgs a) {
+  __shared__ RLds L;
+  uint32_t* const cnt = const_cast<uint32_t*>(a.n_list_dev);
+  const uint32_t lane = (uint32_t)lane_id();
+  for (;;) {
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(a.claim, 1u);
+    idx = ufl(idx);
+    uint32_t key = RNONE;
+    bool fin = idx >= a.n_pub;  // (n_pub covers every key: no hand-on lies past it)
+    for (uint32_t spin = 0; !fin; ++spin) {
+      uint32_t v = 0;
+      if (lane == 0) v = r_atomic_read(&a.pub[idx]);
+      v = ufl(v);
+      if (v != 0u) {
+        key = v - 1u;
+        break;
+      }
+      // tier 0 finished?  (its waves' done words, one per lane; looking at
+      // them only every fourth poll measured no faster for tier 0 and a
+      // longer tail, profiles/r06/ab_overlap_waves.txt)
+      const uint32_t dn = lane < (uint32_t)TRMV_NDONE ? r_atomic_read(&a.done[lane]) : 0u;
+      uint32_t tot;
+      (void)wave_excl_scan_dpp(dn, tot);
+      if (ufl(tot) >= a.prod_waves) {  // its count is final, every entry below it published
+        uint32_t c = 0;
+        if (lane == 0) c = r_atomic_read(cnt);
+        if (idx >= ufl(c)) {
+          fin = true;
+          break;
+        }
+        continue;  // (published before its wave's done add: the next read finds it)
+      }
+      if (spin >= a.spin_limit) {  // (~2 s: tier 0 is not running beside this kernel as it should)
+        if (lane == 0) atomicOr(&a.status[1], TRMV_ERR_STALL);
+        fin = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(127);  // (~4 us between polls)
+    }
+    if (fin) break;
+    const int r = trmv_resident_key<false>(a, key, RNONE, L);
+    if (r == R_NEXT && lane == 0) {
+      const uint32_t pos = atomicAdd(&KA->status[0], 1u);
+      KA->ovf_list[pos] = key;
+    }
+    wave_lds_sync();
+  }
+}
+
+void trmv_resident_preload() {
+  preload_kernels(trmv_resident_kernel<true>, trmv_resident_kernel<false>, trmv_resident_consume_kernel);
+}
+
+int trmv_launch_resident_consume(const TrmvApplyArgs& a, uint32_t waves, hipStream_t st) {
+  if (waves == 0) return CCRDT_OK;
+  hipLaunchKernelGGL(trmv_resident_consume_kernel, dim3(waves), dim3(64), 0, st, a);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
 
 int trmv_launch_resident(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;

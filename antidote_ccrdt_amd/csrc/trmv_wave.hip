@@ -183,20 +183,29 @@ struct ChunkHdr {
   uint32_t key;         // lane j < n: key j
   uint64_t lo, hi;      // lane j < n: key_ptr[key j], key_ptr[key j + 1]
   uint32_t meta[W_MD];  // meta[i], lane 8m + d: dword d of new_s.meta[key 8i + m]
+  uint64_t skip;        // bit j: key j was taken from first_list already (overlapped hand-on)
 };
 
+// Key at work-list position i: the list's entry, or (overlapped hand-on)
+// first_list's entries first and then every key in order.
+__device__ __forceinline__ uint32_t wave_list_key(uint32_t i, uint32_t n_first) {
+  if (KA->first_list) return i < n_first ? KA->first_list[i] : i - n_first;
+  return KA->key_list ? KA->key_list[i] : i;
+}
+
 __device__ __forceinline__ void wave_load_chunk(const TrmvApplyArgs& a, uint32_t c0, uint32_t n,
-                                                ChunkHdr& h) {
+                                                uint32_t n_first, ChunkHdr& h) {
   const int lane = lane_id();
   const uint32_t j = (uint32_t)lane < n ? (uint32_t)lane : 0u;
-  h.key = KA->key_list ? KA->key_list[c0 + j] : c0 + j;
+  h.key = wave_list_key(c0 + j, n_first);
   h.lo = KA->key_ptr[h.key];
   h.hi = KA->key_ptr[h.key + 1];
+  h.skip = KA->first_list ? ballot((uint32_t)lane < n && c0 + j >= n_first && h.hi - h.lo > KA->first_thresh) : 0ull;
 #pragma unroll
   for (int i = 0; i < W_MD; ++i) {
     const uint32_t m = 8 * i + (lane >> 3);
     const uint32_t jm = m < n ? m : 0u;
-    const uint32_t km = KA->key_list ? KA->key_list[c0 + jm] : c0 + jm;
+    const uint32_t km = shfl32(h.key, (int)jm);
     if (KA->fresh) {  // trmv_new_meta: the fresh layout's offsets, counts 0, Min nil
       const uint32_t d = lane & 7;
       h.meta[i] = d < 3 ? (uint32_t)trmv_fresh_off(KA->slack != 0, (int)d, km, KA->key_ptr[km])
@@ -1145,11 +1154,12 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];
-  const uint32_t n = a.n_list_dev ? *a.n_list_dev : a.n_list;
+  const uint32_t n_first = a.first_list ? *a.n_first : 0u;
+  const uint32_t n = (a.n_list_dev ? *a.n_list_dev : a.n_list) + n_first;
   for (uint32_t c0 = (blockIdx.x * W_WAVES + wv) * W_KPW; c0 < n; c0 += gridDim.x * W_WAVES * W_KPW) {
     const uint32_t cn = c0 + W_KPW < n ? W_KPW : n - c0;
     ChunkHdr hdr;
-    wave_load_chunk(a, c0, cn, hdr);
+    wave_load_chunk(a, c0, cn, n_first, hdr);
     KeyIn cur, nxt;
     wave_load_key(a, hdr, 0, cur);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the ops are in
@@ -1157,11 +1167,20 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
     for (uint32_t j = 0; j < cn; ++j) {
       const uint32_t key = rl32(hdr.key, (int)j);
       const bool has_next = j + 1 < cn;
-      const int r = trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
+      // a key first_list held is done already: only the next key's loads
+      const int r = (hdr.skip >> j) & 1u ? W_REJECT + 1
+                                         : trmv_wave_key<FRESH>(a, key, cur, L, has_next, hdr, j + 1, nxt);
       if (r != W_DONE) {
         if (r == W_NEXT_TIER && lane_id() == 0) {
           const uint32_t pos = atomicAdd(&KA->status[0], 1u);
           KA->ovf_list[pos] = key;
+          // published for tier R beside this kernel: a device-scope atomic,
+          // performed before the wave goes on (and before its done add)
+          if (KA->pub && pos < KA->n_pub) {
+            const uint32_t old = atomicExch(&KA->pub[pos], key + 1u);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the exchange is done
+            asm volatile("" ::"v"(old));
+          }
         }
         if (has_next) wave_load_key(a, hdr, j + 1, nxt);
         // retire these loads here, as the common path does before its
@@ -1173,10 +1192,19 @@ __global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArg
       cur = nxt;
     }
   }
+  // this wave is finished (its hand-ons published above); relaxed: an
+  // agent-scope release here would write the XCD's L2 back once per wave
+  if (a.done && lane_id() == 0) atomicAdd(&KA->done[(blockIdx.x * W_WAVES + wv) % TRMV_NDONE], 1u);
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)
 void trmv_wave_preload() { preload_kernels(trmv_wave_kernel<true>, trmv_wave_kernel<false>); }
+
+// waves of the launch trmv_launch_wave makes for grid_keys keys
+uint32_t trmv_wave_waves(uint64_t grid_keys) {
+  const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
+  return (uint32_t)((grid_keys + per_block - 1) / per_block) * W_WAVES;
+}
 
 int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st) {
   if (grid_keys == 0) return CCRDT_OK;

@@ -410,11 +410,16 @@ def test_inplace_finish_failure_partial_commit(gpu, monkeypatch):
     assert hit is not None, "no in-place batch handed keys on"
 
 
+@pytest.mark.parametrize("stall", [False, True])
 @pytest.mark.parametrize("K,ops_per_key,players", [(100, 118, 400), (8, 9, 64)])
-def test_fresh_many_handons(gpu, K, ops_per_key, players):
+def test_fresh_many_handons(gpu, K, ops_per_key, players, stall, monkeypatch):
     """Fresh batches whose tier 0 hands many keys on to tier R: more players
     than K and more than 128 ops (K = 100), or few ops but more players than
-    K (K = 8).  Bit-exact vs the oracle, then a resident batch on top."""
+    K (K = 8).  The overlapped hand-on takes them while tier 0 runs, or --
+    stall -- its consumers give up at once and the host re-runs tier R over
+    the whole list.  Bit-exact vs the oracle, then a resident batch on top."""
+    if stall:
+        monkeypatch.setenv("CCRDT_TRMV_OVERLAP_STALL", "1")
     nk, D = 4000, 8
     eng, orac = TopkRmvEngine(nk, K, D), orc.TrmvOracle(nk, K, D)
     for i in range(2):
@@ -424,3 +429,4 @@ def test_fresh_many_handons(gpu, K, ops_per_key, players):
         _compare(eng, orac, b, D, eng.apply(b), orac.apply(b))
         if i == 0:
             assert eng.overflow_keys(0) > 50  # (tier 0 handed keys on)
+            assert eng.overflow_keys(9) == (1 if stall else 0)  # (the fallback ran)
