@@ -41,7 +41,8 @@ int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_
                          hipStream_t st);
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
                     int verify, hipStream_t st);
-int wc_launch_rehash(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
+int wc_launch_check(const WcArgs& a, uint32_t n, hipStream_t st);
+int wc_launch_rehash(const WcSlot* old, const WcMeta* oldm, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
                      hipStream_t st);
 }  // namespace ccrdt
 
@@ -109,12 +110,12 @@ void ccrdt_engine::release_types() {
   for (int s = 0; s < 2; ++s) {
     for (DevBuf* d : {&tb.avg_sum[s], &tb.avg_num[s], &tb.tk_off[s], &tb.tk_cnt[s], &tb.tk_id[s],
                       &tb.tk_score[s], &tb.lb_meta[s], &tb.lb_id[s], &tb.lb_score[s], &tb.lb_st[s],
-                      &tb.t_tab[s], &tb.t_cnt[s]})
+                      &tb.t_tab[s], &tb.t_meta[s], &tb.t_cnt[s]})
       d->release();
   }
   for (DevBuf* d : {&tb.hb_off, &tb.hb_cap, &tb.hb_a, &tb.hb_b, &tb.hb_c, &tb.hb_d})
     d->release();
-  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
+  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.chk, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
                     &tb.status, &tb.ex_cnt, &tb.ex, &tb.kp})
     d->release();
   for (auto& d : tb.stage) d.release();
@@ -160,7 +161,8 @@ int ccrdt_engine::clone_from(const ccrdt_engine& src) {
                           {&tb.tk_cnt[c], &s.tk_cnt[c]}, {&tb.tk_id[c], &s.tk_id[c]},
                           {&tb.tk_score[c], &s.tk_score[c]}, {&tb.lb_meta[c], &s.lb_meta[c]},
                           {&tb.lb_id[c], &s.lb_id[c]}, {&tb.lb_score[c], &s.lb_score[c]},
-                          {&tb.lb_st[c], &s.lb_st[c]}, {&tb.t_tab[c], &s.t_tab[c]}, {&tb.t_cnt[c], &s.t_cnt[c]},
+                          {&tb.lb_st[c], &s.lb_st[c]}, {&tb.t_tab[c], &s.t_tab[c]}, {&tb.t_meta[c], &s.t_meta[c]},
+                          {&tb.t_cnt[c], &s.t_cnt[c]},
                           {&tb.arena, &s.arena},
                           {&tb.arena_top, &s.arena_top}})
       CCRDT_TRY(copy_buf(*dd, *ss, stream));
@@ -205,6 +207,12 @@ static int read_status(ccrdt_engine* e, uint32_t* out2) {
   CCRDT_HIP(hipMemcpyAsync(e->h_status, e->tb.status.p, 8, hipMemcpyDeviceToHost, e->stream));
   CCRDT_HIP(hipStreamSynchronize(e->stream));
   memcpy(out2, e->h_status, 8);
+  return CCRDT_OK;
+}
+static int read_status3(ccrdt_engine* e, uint32_t* out3) {
+  CCRDT_HIP(hipMemcpyAsync(e->h_status, e->tb.status.p, 12, hipMemcpyDeviceToHost, e->stream));
+  CCRDT_HIP(hipStreamSynchronize(e->stream));
+  memcpy(out3, e->h_status, 12);
   return CCRDT_OK;
 }
 
@@ -1061,6 +1069,7 @@ static WcArgs wc_table_args(ccrdt_engine* e, int side) {
   a.n_keys = e->n_keys;
   a.wdc = e->type == CCRDT_WORDDOCUMENTCOUNT;
   a.t = T.t_tab[side].as<WcSlot>();
+  a.tm = T.t_meta[side].as<WcMeta>();
   a.t_cnt = T.t_cnt[side].as<unsigned long long>();
   a.t_mask = T.t_slots[side] ? T.t_slots[side] - 1 : 0;
   a.seed = T.wc_seed;
@@ -1072,7 +1081,12 @@ static WcArgs wc_table_args(ccrdt_engine* e, int side) {
 
 static int wc_alloc_table(ccrdt_engine* e, int side, uint64_t slots) {
   TypeBufs& T = e->tb;
+  if (slots > (1ull << 32)) {  // (check records hold 32-bit slot indices)
+    set_error("wc: word table above 2^32 slots");
+    return CCRDT_ENOMEM;
+  }
   CCRDT_TRY(T.t_tab[side].ensure(slots * sizeof(WcSlot)));
+  CCRDT_TRY(T.t_meta[side].ensure(slots * sizeof(WcMeta)));
   CCRDT_TRY(T.t_cnt[side].ensure(slots * 8));
   CCRDT_HIP(hipMemsetAsync(T.t_tab[side].p, 0, slots * sizeof(WcSlot), e->stream));
   CCRDT_HIP(hipMemsetAsync(T.t_cnt[side].p, 0, slots * 8, e->stream));
@@ -1166,13 +1180,23 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   bool reseeded = false;
   uint64_t dmul = 1;  // worddocumentcount dedupe table: multiple of its first size
   if (getenv("CCRDT_WC_SLOTS")) slots = strtoull(getenv("CCRDT_WC_SLOTS"), nullptr, 0);
+  // the check list: tokens whose identity the insert kernel leaves open
+  // (words of more than WC_SHORT bytes; slots whose identity was not yet
+  // visible); a batch that fills it is verified token by token instead
+  // (CCRDT_WC_CHK_CAP: test hook for the list's capacity)
+  uint64_t chk_cap = std::min<uint64_t>(docs->n_bytes / 128 + 65536, 1ull << 27);
+  if (getenv("CCRDT_WC_CHK_CAP")) chk_cap = strtoull(getenv("CCRDT_WC_CHK_CAP"), nullptr, 0);
+  CCRDT_TRY(T.chk.ensure(std::max<uint64_t>(chk_cap, 1) * sizeof(WcChk)));
   for (int attempt = 0;; ++attempt) {
     // new table (rehash of the current words), then the batch
     CCRDT_TRY(wc_alloc_table(e, out, slots));
     WcArgs a = wc_table_args(e, out);
     if (!e->fresh && T.t_slots[in])
-      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
-    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
+      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_meta[in].as<WcMeta>(), T.t_cnt[in].as<unsigned long long>(),
+                                 T.t_slots[in], a, e->stream));
+    CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 16, e->stream));
+    a.chk = T.chk.as<WcChk>();
+    a.chk_cap = (uint32_t)std::min<uint64_t>(chk_cap, 0xFFFFFFFFull);
     a.doc_off = docs->doc_off;
     a.bytes = docs->bytes;
     a.n_bytes = docs->n_bytes;
@@ -1216,8 +1240,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       d0 = d1;
     }
     CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
-    uint32_t st[2];
-    CCRDT_TRY(read_status(e, st));
+    uint32_t st[3];
+    CCRDT_TRY(read_status3(e, st));
     CCRDT_HIP(hipEventElapsedTime(&e->last_kernel_ms, e->evk0, e->evk1));
     if (st[0] && attempt < 4) {  // table (or dedupe table) too small
       if (st[0] & 1u) slots *= 4;
@@ -1228,8 +1252,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       set_error("wc_apply: word table overflow");
       return CCRDT_ENOMEM;
     }
-    // the batch's new words into the arena first (the verify pass then
-    // compares every token against a compact, cache-resident copy)
+    // the batch's new words into the arena first (the check list's long
+    // words are compared against a compact, cache-resident copy)
     a.doc_key = T.stage[0].as<uint64_t>();
     a.doc_off = docs->doc_off;
     a.n_docs = (int64_t)nd;
@@ -1241,13 +1265,15 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     a.arena = T.arena.as<uint8_t>();
     CCRDT_HIP(hipMemsetAsync((uint64_t*)T.arena_top.p + 1, 0, 8, e->stream));
     CCRDT_TRY(wc_launch_persist(a, T.arena.as<uint8_t>(), T.arena_top.as<unsigned long long>(), e->stream));
-    // exactness: every token equals its word's representative
-    {
-      const char* dg = getenv("CCRDT_WC_DBG");
-      a.dbg = dg ? atoi(dg) : 0;
-    }
-    CCRDT_TRY(wc_launch_verify(a, tptr[nd], e->stream));
+    // exactness: every token equals its word's identity -- the insert kernel
+    // compared all but the check list's tokens (a full list: every token
+    // again; CCRDT_WC_VERIFY=1 forces that pass)
+    const bool full = (st[1] & 16u) || (getenv("CCRDT_WC_VERIFY") && atoi(getenv("CCRDT_WC_VERIFY")));
+    T.wc_checks = full ? -1 : (int64_t)st[2];
+    if (full) CCRDT_TRY(wc_launch_verify(a, tptr[nd], e->stream));
+    else CCRDT_TRY(wc_launch_check(a, st[2], e->stream));
     CCRDT_TRY(read_status(e, st));
+    st[1] &= ~16u;
     if (st[1]) {
       // the state is unchanged: the new table side is dropped, the arena
       // top goes back to the words it held
@@ -1370,7 +1396,8 @@ static int wc_merge_core(ccrdt_engine* e, uint64_t nw, const uint64_t* wk, const
     CCRDT_TRY(wc_alloc_table(e, out, slots));
     a = wc_table_args(e, out);
     if (!start_empty && T.t_slots[in])
-      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_cnt[in].as<unsigned long long>(), T.t_slots[in], a, e->stream));
+      CCRDT_TRY(wc_launch_rehash(T.t_tab[in].as<WcSlot>(), T.t_meta[in].as<WcMeta>(), T.t_cnt[in].as<unsigned long long>(),
+                                 T.t_slots[in], a, e->stream));
     CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 8, e->stream));
     a.bytes = bytes;
     a.n_bytes = nb;
@@ -1517,6 +1544,13 @@ int ccrdt_wc_merge_device(ccrdt_engine* e, int64_t n_words, const int64_t* d_met
                        d_bytes, (uint64_t)n_bytes, false);
 }
 
+int ccrdt_wc_last_checks(ccrdt_engine* e, int64_t* n_checked) {
+  CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
+  if (!n_checked) return CCRDT_EINVAL;
+  *n_checked = e->tb.wc_checks;
+  return CCRDT_OK;
+}
+
 int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes) {
   CCRDT_TRY(check_type(e, CCRDT_WORDCOUNT));
   if (e->fresh) {
@@ -1544,17 +1578,19 @@ int ccrdt_wc_export(ccrdt_engine* e, uint64_t* key_ptr, uint64_t* word_off, uint
   const int c = T.tcur;
   const uint64_t n = T.t_slots[c];
   std::vector<WcSlot> tab;
+  std::vector<WcMeta> meta;
   std::vector<unsigned long long> cnt;
   std::vector<uint64_t> top;
   std::vector<uint8_t> arena;
   CCRDT_TRY(d2h(tab, T.t_tab[c], n, e->stream));
+  CCRDT_TRY(d2h(meta, T.t_meta[c], n, e->stream));
   CCRDT_TRY(d2h(cnt, T.t_cnt[c], n, e->stream));
   CCRDT_TRY(d2h(top, T.arena_top, 2, e->stream));
   CCRDT_TRY(d2h(arena, T.arena, top[0], e->stream));
   std::vector<std::tuple<uint32_t, std::string, uint64_t>> words;
   for (uint64_t i = 0; i < n; ++i)
     if (tab[i].h)
-      words.emplace_back(tab[i].key, std::string((const char*)arena.data() + tab[i].ref, tab[i].len), cnt[i]);
+      words.emplace_back(meta[i].key, std::string((const char*)arena.data() + meta[i].ref, meta[i].len), cnt[i]);
   std::sort(words.begin(), words.end());
   uint64_t w = 0, b = 0, p = 0;
   for (uint64_t k = 0; k < nk; ++k) {

@@ -1717,20 +1717,22 @@ int lb_launch_downstream(const LbDownArgs& a, hipStream_t st) {
 // binary:split(File, [<<"\n">>, <<" ">>], [global]) — tokens start at the
 // document start and after every 0x0A / 0x20 byte, empty tokens included
 // (Q13); wordcount adds 1 per token, worddocumentcount 1 per distinct token
-// of the document.  One wave per document; each lane owns a 64-byte segment
-// of a 4 KiB tile and handles the tokens that start in it (reading past its
-// segment when a token does).  Words are keyed by h = mix(FNV-1a(bytes),
-// key, len); a per-document LDS table aggregates counts (wordcount: the Zipf
-// head costs one global atomic per document) or de-duplicates
-// (worddocumentcount); misses go to the global table (CAS on h).  Exactness
-// does not rest on the hash: wc_verify_kernel byte-compares every token with
-// its word's representative and flags any collision.
+// of the document.  One tokenizer pass: one wave per 32 KiB chunk of a
+// document, each lane owning a 64-byte segment of a 4 KiB tile and handling
+// the tokens that start in it (reading past its segment when a token does).
+// A token is identified exactly by its identity (wc_ident: its length and
+// bytes, for tokens of up to WC_SHORT bytes) and located by h = mix(word
+// hash, key, len).  A workgroup's LDS table holds identities, so the Zipf
+// head is counted (wordcount) or de-duplicated per document
+// (worddocumentcount) by exact compares; misses go to the global table (CAS
+// on h), whose slots carry the identity too: a token that finds its word
+// there compares identities on the spot.  Only the tokens the kernel cannot
+// settle -- words of more than WC_SHORT bytes, and slots whose identity words
+// were not yet visible -- go to a check list that wc_check_kernel compares
+// after the kernel; a full list falls back to the verify pass.
 // linear probes of the global tables before an insert reports the table full
 // (the batch is then re-run on a table four times larger)
 constexpr uint64_t WC_MAXPROBE = 4096;
-// (measured on the 8 GiB corpus: 1 bucket 28.9 ms, 2 buckets 29.3, 3 buckets
-// 33.7 -- a word whose bucket is full goes to the global table)
-constexpr int WC_BPROBE = 1;  // LDS buckets (of 4 slots) probed per token
 
 __device__ __forceinline__ bool wc_sep(uint8_t c) { return c == 0x0A || c == 0x20; }
 
@@ -1757,8 +1759,8 @@ __device__ __forceinline__ uint64_t wc_hkey(const WcArgs& a, uint64_t wh, uint64
 // bytes as little-endian 8-byte words (the last one zero-padded), folded as
 // x = (x ^ w) * M from x = 0 -- one multiply per 8 bytes, instead of a
 // dependent multiply per byte (a token of up to 8 bytes costs one).  Every
-// site that hashes a word (tokenizer fast and slow paths, wc_merge_kernel)
-// uses this one definition.
+// site that hashes a word (tokenizer fast and slow paths, wc_hash_regs,
+// wc_merge_kernel, wc_rehash_kernel) computes this one function.
 constexpr uint64_t WC_SEED = 0ull;
 __device__ __forceinline__ uint64_t wc_fold(uint64_t x, uint64_t w) { return (x ^ w) * 0xFF51AFD7ED558CCDull; }
 // bytes p[0..n) from global memory
@@ -1772,6 +1774,67 @@ __device__ __forceinline__ uint64_t wc_hash_bytes(const uint8_t* p, uint64_t n) 
     }
   }
   return (n & 7) ? wc_fold(x, acc) : x;
+}
+// the same for a token held as lo / hi (its first 16 bytes, zero past its
+// length tl <= 16)
+__device__ __forceinline__ uint64_t wc_hash_regs(uint64_t lo, uint64_t hi, uint32_t tl) {
+  uint64_t x = tl ? wc_fold(WC_SEED, lo) : WC_SEED;
+  if (tl > 8) x = wc_fold(x, hi);
+  return x;
+}
+
+// A word's identity from lo / hi (its first 16 bytes, zero past its length):
+// w0 = WC_MARK | length << 56 | bytes 0..6, w1 = WC_MARK | bytes 7..13, so two
+// short words are equal iff their (w0, w1) are; a longer word gets the long
+// code (length 0x7F) and is compared byte by byte after the kernel.
+constexpr uint64_t WC_B7 = 0x00FFFFFFFFFFFFFFull;
+__device__ __forceinline__ void wc_ident(uint64_t lo, uint64_t hi, uint32_t tl, uint64_t& w0, uint64_t& w1) {
+  if (tl <= WC_SHORT) {
+    w0 = WC_MARK | ((uint64_t)tl << 56) | (lo & WC_B7);
+    w1 = WC_MARK | (((lo >> 56) | (hi << 8)) & WC_B7);
+  } else {
+    w0 = WC_MARK | (0x7Full << 56);
+    w1 = WC_MARK;
+  }
+}
+__device__ __forceinline__ uint32_t wc_ident_len(uint64_t w0) { return (uint32_t)(w0 >> 56) & 0x7Fu; }
+__device__ __forceinline__ void wc_ident_bytes(uint64_t w0, uint64_t w1, uint64_t& lo, uint64_t& hi) {
+  lo = (w0 & WC_B7) | (w1 << 56);
+  hi = (w1 & WC_B7) >> 8;
+}
+// identity of bytes p[0..n) in global memory
+__device__ __forceinline__ void wc_ident_mem(const uint8_t* p, uint32_t n, uint64_t& w0, uint64_t& w1) {
+  uint64_t lo = 0, hi = 0;
+  for (uint32_t j = 0; j < n && j < 16; ++j) {
+    if (j < 8) lo |= (uint64_t)p[j] << (8 * j);
+    else hi |= (uint64_t)p[j] << (8 * (j - 8));
+  }
+  wc_ident(lo, hi, n, w0, w1);
+}
+
+// A table word read coherently (an agent-scope load: another XCD may have
+// written it in this launch).  A word goes 0 -> final once per table, so a
+// stale read can only be a zero.
+__device__ __forceinline__ uint64_t wc_ld(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A slot's hash and identity in two 16-byte loads (one cache line per lane,
+// as a single 8-byte read would be; four 8-byte agent-scope reads cost four
+// address passes per wave).  Plain loads: a stale line reads as zeros, which
+// a probe settles by its CAS and an identity compare by the check list.
+struct WcPeek {
+  uint64_t h, w0, w1, w2;
+};
+typedef unsigned int __attribute__((ext_vector_type(4))) wc_u32x4_t;
+__device__ __forceinline__ WcPeek wc_peek(const WcArgs& a, uint64_t sl) {
+  const __attribute__((address_space(1))) wc_u32x4_t* p = (const __attribute__((address_space(1))) wc_u32x4_t*)(a.t + sl);
+  const wc_u32x4_t x = p[0], y = p[1];
+  WcPeek r;
+  r.h = (uint64_t)x.y << 32 | x.x;
+  r.w0 = (uint64_t)x.w << 32 | x.z;
+  r.w1 = (uint64_t)y.y << 32 | y.x;
+  r.w2 = (uint64_t)y.w << 32 | y.z;
+  return r;
 }
 
 // A tile staged in LDS: bytes [tile - 16 + sh .. ) of the document, read as
@@ -1866,19 +1929,13 @@ __device__ __forceinline__ uint64_t wc_sep_mask(uint64_t x) {
   return ((a - L1) & ~a & H1) | ((b - L1) & ~b & H1);
 }
 
-// Token starting at document position s: returns its end.  Fast path: the
-// 16 staged bytes from s, read as three aligned 8-byte LDS words, hold the
-// token's end (a separator, or the document end); the token's bytes are then
-// in tb[0..1] (little-endian) and the hash runs on registers.  Otherwise
-// (a token of 16+ bytes, or one running out of the staged window) the byte
-// loop; *fast says which.
 // Token at tile offset t (tile position s = tile + t): returns its length.
 // Fast path (32-bit offsets): the 16 staged bytes from the token's stage index
 // i = toff + t, read as three aligned 8-byte LDS words, hold the token's end
 // (a separator, or the document end: rem = bytes from s to the document end,
 // clamped to 32 bits); the token's bytes are then in lo / hi (little-endian)
 // and the hash runs on registers.  Otherwise (16+ bytes, or past the staged
-// window) the byte loop; fast says which.
+// window) the byte loop, which also collects lo / hi; fast says which.
 __device__ __forceinline__ uint32_t wc_token_t(const WcTileView& v, const uint8_t* sbuf, uint32_t toff, uint32_t vn,
                                                uint32_t rem, uint32_t t, uint64_t tile, uint64_t len, uint64_t& wh,
                                                uint64_t& lo, uint64_t& hi, bool& fast) {
@@ -1910,11 +1967,16 @@ __device__ __forceinline__ uint32_t wc_token_t(const WcTileView& v, const uint8_
   const uint64_t s = tile + t;
   uint64_t x = WC_SEED, acc = 0;
   uint64_t e = s;
+  lo = hi = 0;  // the token's first 16 bytes (its identity)
   while (e < len) {
     const uint8_t c = v.at(e);
     if (wc_sep(c)) break;
-    acc |= (uint64_t)c << (8 * ((e - s) & 7));
-    if (((e - s) & 7) == 7) {
+    const uint64_t j = e - s;
+    const uint64_t cb = (uint64_t)c << (8 * (j & 7));
+    acc |= cb;
+    lo |= j < 8 ? cb : 0ull;  // (selects: a branch made lo / hi a stack array)
+    hi |= j - 8 < 8 ? cb : 0ull;
+    if ((j & 7) == 7) {
       x = wc_fold(x, acc);
       acc = 0;
     }
@@ -1993,34 +2055,73 @@ __device__ __forceinline__ uint32_t wc_emit(uint64_t m, uint32_t o, uint32_t tot
 
 // Insert (or find) h in the word table, probing from slot sl whose hash was
 // already read as `seen` (the caller issues that first read early, so its
-// latency overlaps other work).
-__device__ __forceinline__ uint64_t wc_global_insert_at(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
-                                                        uint64_t pos, uint64_t sl, uint64_t seen) {
+// latency overlaps other work).  claimed: this call took the slot (the caller
+// then publishes the word's identity).
+__device__ __forceinline__ uint64_t wc_global_insert_at(const WcArgs& a, uint64_t h, uint64_t sl, uint64_t seen,
+                                                        bool& claimed) {
+  claimed = false;
   for (uint64_t probe = 0; probe <= a.t_mask && probe < WC_MAXPROBE; ++probe) {
     // a slot goes 0 -> h once, so a (possibly stale) nonzero value is final
     // and only an empty-looking slot needs the CAS
     if (seen == h) return sl;
     if (seen == 0ull) {
       const unsigned long long prev = atomicCAS(&a.t[sl].h, 0ull, (unsigned long long)h);
-      if (prev == 0ull) {  // new word: this token is its representative
-        a.t[sl].key = key;
-        a.t[sl].len = len;
-        a.t[sl].ref = WC_REF_BATCH | pos;
+      if (prev == 0ull) {
+        claimed = true;
         return sl;
       }
       if (prev == h) return sl;
     }
     sl = (sl + 1) & a.t_mask;
-    seen = __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    seen = wc_ld(&a.t[sl].h);
   }
   atomicOr(&a.status[0], 1u);  // table full
   return ~0ull;
 }
-__device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, uint32_t key, uint32_t len,
-                                                     uint64_t pos) {
+__device__ __forceinline__ uint64_t wc_global_insert(const WcArgs& a, uint64_t h, bool& claimed) {
   const uint64_t sl = h & a.t_mask;
-  return wc_global_insert_at(a, h, key, len, pos, sl,
-                             __hip_atomic_load(&a.t[sl].h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return wc_global_insert_at(a, h, sl, wc_ld(&a.t[sl].h), claimed);
+}
+
+// The claimer of a slot writes the word's identity (device-scope exchanges:
+// readers on other XCDs see each word either zero or final) and its plain
+// key / length / representative (read only after the kernel).
+__device__ __forceinline__ void wc_publish(const WcArgs& a, uint64_t sl, uint64_t w0, uint64_t w1, uint32_t key,
+                                           uint32_t len, uint64_t ref) {
+  atomicExch(&a.t[sl].w0, (unsigned long long)w0);
+  atomicExch(&a.t[sl].w1, (unsigned long long)w1);
+  atomicExch(&a.t[sl].w2, (unsigned long long)(WC_MARK | key));
+  WcMeta m;
+  m.ref = ref;
+  m.key = key;
+  m.len = len;
+  a.tm[sl] = m;
+}
+
+// A token (identity tw0 / tw1, key) that found its word's slot holding the
+// identity words sw0..sw2 as read: equal -> settled; different -> two
+// distinct words on one 64-bit hash (the batch is re-run under a new seed);
+// a long word, or identity words not yet visible -> true: the token goes to
+// the check list.
+__device__ __forceinline__ bool wc_settle(const WcArgs& a, uint64_t tw0, uint64_t tw1, uint32_t key, uint64_t sw0,
+                                          uint64_t sw1, uint64_t sw2) {
+  if (wc_ident_len(tw0) > WC_SHORT) return true;
+  if (!(sw0 & sw1 & sw2 & WC_MARK)) return true;
+  if (sw0 != tw0 || sw1 != tw1 || sw2 != (WC_MARK | key)) atomicOr(&a.status[1], 1u);
+  return false;
+}
+__device__ __forceinline__ void wc_chk_push(const WcArgs& a, uint64_t sl, uint32_t key, uint32_t tl, uint64_t tw0,
+                                            uint64_t tw1, uint64_t pos) {
+  const uint32_t i = atomicAdd(&a.status[2], 1u);
+  if (i >= a.chk_cap) {  // list full: the verify pass checks every token instead
+    atomicOr(&a.status[1], 16u);
+    return;
+  }
+  WcChk* r = a.chk + i;
+  r->slot = (uint32_t)sl;
+  r->key = key;
+  r->a = tl <= WC_SHORT ? tw0 : pos;  // (a short identity has WC_MARK set, a position never)
+  r->b = tl <= WC_SHORT ? tw1 : (uint64_t)tl;
 }
 
 __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64_t doc) {
@@ -2050,44 +2151,60 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
   s0 = (t - a.tile_ptr[d]) * (uint64_t)(WC_TILE * WC_TPW);
 }
 
+// A token that missed the LDS table, resolved one round after its first-slot
+// read (pk: that slot's hash and identity words as read then): find or claim
+// its word, settle its identity, count it.
+__device__ __forceinline__ void wc_resolve(const WcArgs& a, const WcPeek& pk, uint64_t h, uint32_t key, uint32_t tl,
+                                           uint64_t pos, uint64_t tw0, uint64_t tw1, uint64_t doc) {
+  bool claimed = false;
+  uint64_t gs, sw0 = pk.w0, sw1 = pk.w1, sw2 = pk.w2;
+  if (pk.h == h) {
+    gs = h & a.t_mask;  // (the common case stays out of the probe loop)
+  } else {
+    gs = wc_global_insert_at(a, h, h & a.t_mask, pk.h, claimed);
+    if (gs == ~0ull) return;
+    if (!claimed) {
+      const WcPeek q = wc_peek(a, gs);
+      sw0 = q.w0;
+      sw1 = q.w1;
+      sw2 = q.w2;
+    }
+  }
+  if (claimed) wc_publish(a, gs, tw0, tw1, key, tl, WC_REF_BATCH | pos);
+  else if (wc_settle(a, tw0, tw1, key, sw0, sw1, sw2)) wc_chk_push(a, gs, key, tl, tw0, tw1, pos);
+  if (a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, doc))) atomicAdd(&a.t_cnt[gs], 1ull);
+}
+
 // The tokens that START in a chunk (WC_TPW tiles of WC_TILE bytes of one
 // document; the position len counts: a document ending in a separator, or an
 // empty one, has a trailing empty token), one wave per chunk, each lane owning
 // 64 bytes of a tile.  The WAVES waves of a workgroup take consecutive chunks
-// and share one LDS table of TAB words (hash, count, representative), so the
-// Zipf head is counted in LDS and costs one global insert per word per
-// workgroup; LDS misses and tokens of 2 KiB or more go to the global table.
-// The waves never wait for each other inside the chunk loop (each has its own
-// staging buffer and token list); only the table's set-up and its final flush
-// are workgroup-wide.
-// TAB x WAVES: 4096 x 16 (wordcount: one workgroup per CU), 1024 x 4
-// (worddocumentcount).  wordcount: chunks of different documents may share the
-// workgroup (the table keys on the hash, which includes the key, and each
-// entry remembers its wave for the document); worddocumentcount: its LDS
-// entries are per (document, word), so a workgroup's chunks are chunks of one
-// document (group_doc / group_ptr; the last group of a document may leave
-// waves idle).
-// (Measured on the 8 GiB corpus with diagnostic builds of the step, now
-// removed -- their early exits made the loop-carried miss below cost a full
-// vmcnt(0) wait per round: tokenizer 9.9 ms, + LDS table 18.8, + global
-// lookups 25.7, full 29.2; the device-scope count adds of the LDS misses
-// (~40% of the Zipf tokens) took the same time at workgroup scope.  a.dbg 5,
-// CCRDT_WC_IDBG: the global lookups without the count adds.)
-// An entry's representative is one u32: position - group base (RELB bits) |
-// length << RELB (LENB bits; longer tokens go global) | wave << (RELB + LENB).
+// and share one LDS table of TAB identities (buckets of 4), so the Zipf head
+// is counted in LDS by exact compares and costs one global insert per word
+// per workgroup; LDS misses, words of more than WC_SHORT bytes and tokens of
+// another key than the group's first go to the global table.  The waves never
+// wait for each other inside the chunk loop (each has its own staging buffer
+// and token list); only the table's set-up and its final flush are
+// workgroup-wide.
+// TAB x WAVES: 4096 x 12 (wordcount: one workgroup per CU), 1024 x 4
+// (worddocumentcount).  worddocumentcount: its LDS entries are per (document,
+// word), so a workgroup's chunks are chunks of one document (group_doc /
+// group_ptr; the last group of a document may leave waves idle).
+// An entry is claimed by a CAS on its w0 and completed by its w1 store; a
+// reader that finds w0 but not yet w1 takes another entry: two entries of one
+// word only cost two flushes (wordcount adds both counts; worddocumentcount's
+// dedupe table admits one of them).
 template <int TAB, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
-  constexpr uint32_t WB = WAVES == 1 ? 0 : WAVES == 2 ? 1 : WAVES == 4 ? 2 : WAVES == 8 ? 3 : 4;
-  constexpr uint32_t CB = WC_TPW == 8 ? 15 : WC_TPW == 16 ? 16 : 17;  // log2(chunk bytes)
-  constexpr uint32_t WC_RELB = CB + 1 + WB, WC_LENB = 32 - WC_RELB - WB, WS = WB ? WC_RELB + WC_LENB : 0;
-  static_assert(WAVES == (1 << WB) && WAVES * WC_TPW * WC_TILE < (1ull << WC_RELB), "group span");
-  __shared__ unsigned long long lh[TAB];
+  static_assert(TAB % 4 == 0, "buckets of 4 entries");
+  constexpr uint64_t NB = TAB / 4;
+  __shared__ unsigned long long lw0[TAB];  // identity w0 (0: empty entry)
+  __shared__ unsigned long long lw1[TAB];  // identity w1
   __shared__ uint32_t lc[TAB];
-  __shared__ uint32_t lp[TAB];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf_w[WAVES][WC_STAGE];
   __shared__ uint16_t tlist_w[WAVES][WC_LIST];
-  __shared__ uint64_t gdoc[WAVES];
-  __shared__ uint64_t gbase;
+  __shared__ uint64_t gdoc;
+  __shared__ uint32_t gkey;
   const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
   uint8_t* sbuf = sbuf_w[wv];
   uint16_t* tlist = tlist_w[wv];
@@ -2110,20 +2227,24 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   }
   const uint32_t key = act ? (uint32_t)a.doc_key[d] : 0u;
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
-    lh[i] = 0ull;
+    lw0[i] = 0ull;
+    lw1[i] = 0ull;
     lc[i] = 0u;
   }
-  if (lane == 0) {
-    gdoc[wv] = d;
-    if (wv == 0) gbase = b0 + tile;
+  if (wv == 0 && lane == 0) {  // (wave 0 is active whenever any wave of the group is)
+    gdoc = d;
+    gkey = key;
   }
   WcStageRegs g;
   if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
   __syncthreads();
-  const uint64_t base_pos = gbase;
-  uint64_t ph = 0, ppos = 0, pseen = 0, pseen2 = 0;  // this lane's miss of the previous round
+  const uint32_t group_key = gkey;
+  const bool lds_key = key == group_key;  // wave-uniform
+  // this lane's LDS miss of the previous round
+  uint64_t ph = 0, ppos = 0, ptw0 = 0, ptw1 = 0;
   uint32_t ptl = 0;
   bool pend = false;
+  WcPeek pk0 = {0, 0, 0, 0}, pk1 = {0, 0, 0, 0};
 
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();  // the previous tile's staged bytes are no longer read
@@ -2136,13 +2257,13 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
       const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
       // One round per 64 tokens, two rounds per iteration: a round issues its
-      // misses' first-slot reads into one register and resolves the previous
-      // round's misses from the other, so the loop carries no copy of an
-      // in-flight load (a copy at the latch waited for it every round).
-      auto round = [&](uint32_t k, uint64_t& seen_prev, uint64_t& seen_new) {
+      // misses' first-slot reads (hash and identity) into one register set
+      // and resolves the previous round's misses from the other, so the loop
+      // carries no copy of an in-flight load.
+      auto round = [&](uint32_t k, const WcPeek& pk_prev, WcPeek& pk_new) {
         const bool valid = k < ntk;
         bool counted = true;
-        uint64_t h = 0, s = 0;
+        uint64_t h = 0, s = 0, tw0 = 0, tw1 = 0;
         uint32_t tl = 0;
         if (valid) {
           const uint32_t t = tlist[k];
@@ -2151,105 +2272,129 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
           bool fast;
           tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
           h = wc_hkey(a, wh, key, tl);
-          // buckets of 4 slots (32 B): one pair of 16-byte reads finds a word
-          // already in the table (the common case) without an atomic; the CAS
-          // only claims an empty slot
-          uint32_t bk = (uint32_t)(h >> 17) & (TAB / 4 - 1);
+          wc_ident(lo, hi, tl, tw0, tw1);
           counted = false;
-          const int nprobe = tl < (1u << WC_LENB) - 1 ? WC_BPROBE : 0;
-          for (int p = 0; p < nprobe && !counted; ++p, bk = (bk + 1) & (TAB / 4 - 1)) {
-            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&lh[bk * 4]);
+          if (lds_key && tl <= WC_SHORT) {
+            // one bucket of 4 entries: their w0 words (32 B) in one pair of
+            // 16-byte reads, then the w1 of the entry whose w0 matched; a word
+            // already in the table (the common case) is found without an
+            // atomic, the CAS only claims an empty entry
+            const uint32_t bk = (uint32_t)(((h >> 32) * NB) >> 32);
+            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&lw0[bk * 4]);
             const ulonglong2 x0 = q[0], x1 = q[1];
-            uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
-            int hit = -1;
+            const uint64_t ex[4] = {x0.x, x0.y, x1.x, x1.y};
+            int m = -1;
 #pragma unroll
             for (int i = 3; i >= 0; --i)
-              if (e4[i] == h) hit = i;
-            if (hit >= 0) {
-              if (!a.wdc) atomicAdd(&lc[bk * 4 + hit], 1u);
+              if (ex[i] == tw0) m = i;
+            if (m >= 0 && lw1[bk * 4 + m] == tw1) {
+              if (!a.wdc) atomicAdd(&lc[bk * 4 + m], 1u);
               counted = true;
-              break;
-            }
+            } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              if (counted || e4[i] != 0ull) continue;
-              const uint32_t sl = bk * 4 + (uint32_t)i;
-              const unsigned long long prev = atomicCAS(&lh[sl], 0ull, (unsigned long long)h);
-              if (prev == 0ull) {  // new word of the group: this token represents it
-                lp[sl] = (uint32_t)(b0 + s - base_pos) | tl << WC_RELB | ((uint32_t)wv << WS);
-                if (!a.wdc) atomicAdd(&lc[sl], 1u);
-                else lc[sl] = 1u;
-                counted = true;
-              } else if (prev == h) {
-                if (!a.wdc) atomicAdd(&lc[sl], 1u);
-                counted = true;
+              for (int i = 0; i < 4; ++i) {
+                if (counted || ex[i] != 0ull) continue;
+                const uint32_t sl = bk * 4 + (uint32_t)i;
+                const unsigned long long prev = atomicCAS(&lw0[sl], 0ull, (unsigned long long)tw0);
+                if (prev == 0ull) {  // new word of the group
+                  lw1[sl] = tw1;
+                  if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                  else lc[sl] = 1u;
+                  counted = true;
+                } else if (prev == tw0 && lw1[sl] == tw1) {
+                  if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                  counted = true;
+                }
               }
             }
           }
         }
-        // global path (LDS table full, or a long token), one round behind:
-        // every lane issues this round's first-slot read (a lane without a
-        // miss reads slot 0), then the previous round's misses are resolved
-        seen_new = __hip_atomic_load(&a.t[counted ? 0ull : (h & a.t_mask)].h, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (pend) {
-          // (the common case -- the word at its first slot -- stays out of the
-          // probe loop, whose header would wait for every outstanding load)
-          const uint64_t gs = seen_prev == ph ? (ph & a.t_mask)
-                                              : wc_global_insert_at(a, ph, key, ptl, ppos, ph & a.t_mask, seen_prev);
-          if (gs != ~0ull && a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
-        }
+        // global path (LDS table full, a long word, another key), one round
+        // behind: every lane issues this round's first-slot reads (a lane
+        // without a miss reads slot 0), then the previous round's misses are
+        // resolved
+        pk_new = wc_peek(a, counted ? 0ull : (h & a.t_mask));
+        if (pend) wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d);
         pend = !counted;
         ph = h;
         ptl = tl;
         ppos = b0 + s;
+        ptw0 = tw0;
+        ptw1 = tw1;
       };
       for (uint32_t k0 = 0; k0 < ntk; k0 += 128) {
-        round(k0 + (uint32_t)lane, pseen, pseen2);
-        round(k0 + 64u + (uint32_t)lane, pseen2, pseen);
+        round(k0 + (uint32_t)lane, pk0, pk1);
+        round(k0 + 64u + (uint32_t)lane, pk1, pk0);
       }
     }
   }
-  if (pend) {
-    const uint64_t gs = wc_global_insert_at(a, ph, key, ptl, ppos, ph & a.t_mask, pseen);
-    if (gs != ~0ull && a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, d))) atomicAdd(&a.t_cnt[gs], 1ull);
-  }
+  if (pend) wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d);
   __syncthreads();
+  // flush: every entry into the global table (its identity settled there or
+  // left to the check list), with its count (worddocumentcount: once per
+  // document, through the dedupe table: other workgroups of the document may
+  // hold the word too)
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
-    const uint64_t h = lh[i];
-    if (h == 0ull) continue;
-    const uint32_t u = lp[i];
-    const uint64_t dd = gdoc[WB ? u >> WS : 0u];
-    const uint32_t tl = (u >> WC_RELB) & ((1u << WC_LENB) - 1);
-    const uint64_t gs = wc_global_insert(a, h, (uint32_t)a.doc_key[dd], tl, base_pos + (u & ((1u << WC_RELB) - 1)));
-    // worddocumentcount: other workgroups of the document may hold the word
-    // too; the (document, word) dedupe table admits one of them
-    if (gs != ~0ull && (!a.wdc || wc_doc_first(a, gs, dd))) atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
+    const ulonglong2 e = make_ulonglong2(lw0[i], lw1[i]);
+    if (e.x == 0ull) continue;
+    const uint32_t tl = wc_ident_len(e.x);
+    uint64_t lo, hi;
+    wc_ident_bytes(e.x, e.y, lo, hi);
+    const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
+    bool claimed;
+    const uint64_t gs = wc_global_insert(a, h, claimed);
+    if (gs == ~0ull) continue;
+    if (claimed) {
+      wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
+    } else {
+      const WcPeek q = wc_peek(a, gs);
+      if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
+    }
+    if (!a.wdc || wc_doc_first(a, gs, gdoc)) atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
   }
 }
 
-// Exactness: every token must equal its word's representative byte-for-byte.
-// The WAVES waves of a workgroup take consecutive chunks and share an LDS
-// cache of VTAB words already checked against the table (hash, key | length,
-// the 16 bytes): a repeated word of up to 16 bytes is compared with the cache
-// instead of probing the global table and reading its representative again.
-// An entry is usable once its key | length word is set (its writer stores the
-// bytes first; LDS runs a wave's stores in order), so a reader that finds it
-// unset just takes the global path.
-template <int VTAB, int WAVES>
+// The check list: tokens whose identity the insert kernel left open, compared
+// now that every slot's identity and representative are final (after the
+// persist pass: representatives are arena bytes).
+__global__ __launch_bounds__(256) void wc_check_kernel(WcArgs a, uint32_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const WcChk r = a.chk[i];
+  const WcSlot s = a.t[r.slot];
+  if (r.a & WC_MARK) {  // a short word: its identity
+    if (s.w0 != r.a || s.w1 != r.b || s.w2 != (WC_MARK | r.key)) atomicOr(&a.status[1], 1u);
+    return;
+  }
+  const WcMeta m = a.tm[r.slot];
+  const uint32_t tl = (uint32_t)r.b;
+  bool eq = m.key == r.key && m.len == tl;
+  const uint8_t* rep = (m.ref & WC_REF_BATCH) ? a.bytes + (m.ref & ~WC_REF_BATCH) : a.arena + m.ref;
+  const uint8_t* tok = a.bytes + r.a;
+  // 8 independent byte loads per step (one latency per 8 bytes)
+  for (uint32_t j0 = 0; eq && j0 < tl; j0 += 8) {
+    uint8_t x[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = j0 + j < tl ? rep[j0 + j] : 0;
+      y[j] = j0 + j < tl ? tok[j0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) eq = eq && x[j] == y[j];
+  }
+  if (!eq) atomicOr(&a.status[1], 1u);
+}
+
+// Fallback when the check list filled up: every token of the batch is
+// re-tokenized and checked against its word's slot (identity compare, or the
+// bytes of a long word against its representative).
+template <int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
-  __shared__ unsigned long long vh[VTAB];
-  __shared__ unsigned long long vkl[VTAB];  // key << 32 | (length + 1); 0 = not ready
-  __shared__ ulonglong2 vb[VTAB];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf_w[WAVES][WC_STAGE];
   __shared__ uint16_t tlist_w[WAVES][WC_LIST];
   const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
   uint8_t* sbuf = sbuf_w[wv];
   uint16_t* tlist = tlist_w[wv];
-  for (int i = (int)threadIdx.x; i < VTAB; i += 64 * WAVES) {
-    vh[i] = 0ull;
-    vkl[i] = 0ull;
-  }
   const uint64_t chunk = (uint64_t)blockIdx.x * WAVES + (uint64_t)wv;
   const bool act = chunk < a.n_chunks;
   uint64_t d = 0, tile = 1, b0 = 0, len = 0;
@@ -2261,125 +2406,47 @@ __global__ __launch_bounds__(64 * WAVES) void wc_verify_kernel(WcArgs a) {
   const uint32_t key = act ? (uint32_t)a.doc_key[d] : 0u;
   WcStageRegs g;
   if (act && tile <= len) wc_stage_load(a, b0, len, tile, g);
-  __syncthreads();
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();
     const WcTileView v = wc_stage_store(a, sbuf, b0, g);
     if (ti + 1 < (int)WC_TPW && tile + WC_TILE <= len) wc_stage_load(a, b0, len, tile + WC_TILE, g);
     uint32_t mo, tot;
     const uint64_t mm = wc_start_mask(v, sbuf, len, tile, mo, tot);
-    const uint32_t toff = (uint32_t)(tile - v.lo), vn = (uint32_t)v.n;  // stage index of the tile start, staged bytes
+    const uint32_t toff = (uint32_t)(tile - v.lo), vn = (uint32_t)v.n;
     const uint32_t lrc = len - tile < 0xFFFFFFFFull ? (uint32_t)(len - tile) : 0xFFFFFFFFu;
     for (uint32_t base = 0; base < tot; base += WC_LIST) {
       const uint32_t ntk = wc_emit(mm, mo, tot, base, tlist);
       for (uint32_t k = (uint32_t)lane; k < ntk; k += 64) {
         const uint32_t t = tlist[k];
         const uint64_t s = tile + t;
-        uint64_t wh, tb[2];
+        uint64_t wh, lo, hi, tw0, tw1;
         bool fast;
-        const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, tb[0], tb[1], fast);
+        const uint32_t tl = wc_token_t(v, sbuf, toff, vn, lrc - t, t, tile, len, wh, lo, hi, fast);
         const uint64_t h = wc_hkey(a, wh, key, tl);
-        if (a.dbg == 2) {
-          if (h == 0x1234567ull) atomicOr(&a.status[1], 4u);  // keeps the hash live
-          continue;
-        }
-        const uint64_t mlo = tl >= 8 ? ~0ull : ((1ull << (8 * tl)) - 1);
-        const uint64_t mhi = tl >= 16 ? ~0ull : (tl > 8 ? ((1ull << (8 * (tl - 8))) - 1) : 0ull);
-        const uint64_t kl = (uint64_t)key << 32 | (tl + 1);
-        // the LDS cache (one bucket of 4)
-        const uint32_t bk = (uint32_t)(h >> 17) & (VTAB / 4 - 1);
-        if (fast) {
-          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&vh[bk * 4]);
-          const ulonglong2 x0 = q[0], x1 = q[1];
-          const uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
-          int hit = -1;
-#pragma unroll
-          for (int i = 3; i >= 0; --i)
-            if (e4[i] == h) hit = i;
-          if (hit >= 0) {
-            const uint64_t ckl = vkl[bk * 4 + hit];
-            wave_lds_sync();  // the bytes are read after their ready word
-            if (ckl != 0ull) {
-              const ulonglong2 cb = vb[bk * 4 + hit];
-              if (ckl != kl || ((tb[0] ^ cb.x) & mlo) | ((tb[1] ^ cb.y) & mhi)) atomicOr(&a.status[1], 1u);
-              continue;
-            }
-          }
-        }
-        // probe: the slot's fields are loaded together with its hash
+        wc_ident(lo, hi, tl, tw0, tw1);
         uint64_t sl = h & a.t_mask;
-        uint64_t th, tref;
-        uint32_t tk, tln;
-        for (;;) {  // (global loads: a generic WcSlot load would be a flat load)
-          const uint4 q0 = wc_gload16(reinterpret_cast<const uint8_t*>(a.t + sl));
-          const uint4 q1 = wc_gload16(reinterpret_cast<const uint8_t*>(a.t + sl) + 16);
-          th = (uint64_t)q0.y << 32 | q0.x;
-          tref = (uint64_t)q0.w << 32 | q0.z;
-          tk = q1.x;
-          tln = q1.y;
-          if (th == h || th == 0ull) break;
-          sl = (sl + 1) & a.t_mask;
-        }
-        const bool tar = !(tref & WC_REF_BATCH);  // persisted: an arena offset
-        if (th != h) {
+        while (a.t[sl].h != h && a.t[sl].h != 0ull) sl = (sl + 1) & a.t_mask;
+        if (a.t[sl].h != h) {
           atomicOr(&a.status[1], 2u);  // lost token (table overflow)
           continue;
         }
-        const uint8_t* rep = tar ? a.arena + tref : a.bytes + (tref & ~WC_REF_BATCH);
-        bool eq = tk == key && tln == tl;
-        if (a.dbg == 1) {
-          if (!eq) atomicOr(&a.status[1], 1u);
+        if (tl <= WC_SHORT) {
+          if (a.t[sl].w0 != tw0 || a.t[sl].w1 != tw1 || a.t[sl].w2 != (WC_MARK | key)) atomicOr(&a.status[1], 1u);
           continue;
         }
-        if (eq && fast && tar) {
-          // the representative in the arena (persisted before this pass; the
-          // arena keeps 32 bytes of slack past its top): three aligned 8-byte
-          // loads against the token's registers
-          const uintptr_t ra = (uintptr_t)rep & ~(uintptr_t)7;
-          const uint32_t sh = (uint32_t)((uintptr_t)rep & 7) * 8;
-          const __attribute__((address_space(1))) uint64_t* rp = (const __attribute__((address_space(1))) uint64_t*)ra;
-          const uint64_t r0 = rp[0], r1 = rp[1], r2 = rp[2];
-          const uint64_t rlo = sh ? (r0 >> sh) | (r1 << (64 - sh)) : r0;
-          const uint64_t rhi = sh ? (r1 >> sh) | (r2 << (64 - sh)) : r1;
-          if (((tb[0] ^ rlo) & mlo) | ((tb[1] ^ rhi) & mhi)) {
-            atomicOr(&a.status[1], 1u);
-            continue;
-          }
-          // checked: into the cache (claim an empty slot of the bucket; the
-          // bytes go in before the ready word)
-          const ulonglong2* q = reinterpret_cast<const ulonglong2*>(&vh[bk * 4]);
-          const ulonglong2 x0 = q[0], x1 = q[1];
-          const uint64_t e4[4] = {x0.x, x0.y, x1.x, x1.y};
-          bool done = false;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (done || e4[i] != 0ull) continue;
-            const unsigned long long prev = atomicCAS(&vh[bk * 4 + i], 0ull, (unsigned long long)h);
-            if (prev == 0ull) {
-              vb[bk * 4 + i] = make_ulonglong2(tb[0] & mlo, tb[1] & mhi);
-              wave_lds_sync();
-              vkl[bk * 4 + i] = kl;
-            }
-            done = prev == 0ull || prev == h;
-          }
-          continue;
-        }
-        // 8 independent byte loads per step (one latency per 8 bytes)
-        for (uint32_t j0 = 0; eq && j0 < tl; j0 += 8) {
-          uint8_t r[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = j0 + j < tl ? rep[j0 + j] : 0;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) eq = eq && (j0 + j >= tl || r[j] == v.at(s + j0 + j));
-        }
-        if (!eq) atomicOr(&a.status[1], 1u);  // hash collision between distinct words
+        const WcMeta m = a.tm[sl];
+        bool eq = m.key == key && m.len == tl;
+        const uint8_t* rep = (m.ref & WC_REF_BATCH) ? a.bytes + (m.ref & ~WC_REF_BATCH) : a.arena + m.ref;
+        for (uint32_t j = 0; eq && j < tl; ++j) eq = rep[j] == v.at(s + j);
+        if (!eq) atomicOr(&a.status[1], 1u);
       }
     }
   }
 }
 
-// New words of this batch: copy their bytes into the persistent arena.
-// arena_top[1] counts the table's words.
+// New words of this batch: their bytes into the persistent arena (a word of
+// up to WC_SHORT bytes from its identity, a longer one from its batch
+// occurrence).  arena_top[1] counts the table's words.
 // (words and new bytes are summed per workgroup in LDS; one device atomic per
 // workgroup reserves its arena range and adds its word count)
 __global__ __launch_bounds__(256) void wc_persist_kernel(WcArgs a, uint8_t* arena, unsigned long long* arena_top) {
@@ -2388,9 +2455,10 @@ __global__ __launch_bounds__(256) void wc_persist_kernel(WcArgs a, uint8_t* aren
   __syncthreads();
   const uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool v = sl <= a.t_mask && a.t[sl].h != 0ull;
-  const uint64_t ref = v ? a.t[sl].ref : 0ull;
-  const bool fresh = v && (ref & WC_REF_BATCH);
-  const uint32_t n = fresh ? a.t[sl].len : 0u;
+  WcMeta m{};
+  if (v) m = a.tm[sl];
+  const bool fresh = v && (m.ref & WC_REF_BATCH);
+  const uint32_t n = fresh ? m.len : 0u;
   unsigned long long loc = 0;
   if (v) atomicAdd(&bw, 1ull);
   if (fresh) {
@@ -2405,9 +2473,15 @@ __global__ __launch_bounds__(256) void wc_persist_kernel(WcArgs a, uint8_t* aren
   __syncthreads();
   if (!fresh) return;
   const uint64_t at = bbase + loc;
-  const uint8_t* src = a.bytes + (ref & ~WC_REF_BATCH);
-  for (uint32_t j = 0; j < n; ++j) arena[at + j] = src[j];
-  a.t[sl].ref = at;
+  if (n <= WC_SHORT) {
+    uint64_t lo, hi;
+    wc_ident_bytes(a.t[sl].w0, a.t[sl].w1, lo, hi);
+    for (uint32_t j = 0; j < n; ++j) arena[at + j] = (uint8_t)((j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8))) & 0xFF);
+  } else {
+    const uint8_t* src = a.bytes + (m.ref & ~WC_REF_BATCH);
+    for (uint32_t j = 0; j < n; ++j) arena[at + j] = src[j];
+  }
+  a.tm[sl].ref = at;
 }
 
 // token count of every document (sizes the worddocumentcount dedupe table)
@@ -2481,14 +2555,17 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   b.n_chunks = n_chunks;
   if (a.wdc) {
     if (!a.n_groups) return CCRDT_OK;
-    // (measured on the 8 GiB corpus: 1024 entries 48.6 ms, 512 51.2, 2048 58.4 --
-    // the dedupe path of the misses wants the occupancy of the smaller table)
-    // (one-document groups of 16 waves on 4096 / 2048 entries: 61.6 / 63.6 ms)
+    // (measured on the 8 GiB corpus, round 5's hash-keyed table: 1024 entries
+    // 48.6 ms, 512 51.2, 2048 58.4 -- the dedupe path of the misses wants the
+    // occupancy of the smaller table; one-document groups of 16 waves on 4096
+    // / 2048 entries: 61.6 / 63.6 ms)
     hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)a.n_groups), dim3(256), 0, st, b);
   } else {
-    // (one 16-wave workgroup per CU sharing 4096 entries: 26.2 ms; 4 waves
-    // sharing 2048: 29.0; 8 sharing 4096: 27.0; 16 sharing 2048: 29.4)
-    hipLaunchKernelGGL((wc_insert_kernel<4096, 16>), dim3((unsigned)((n_chunks + 15) / 16)), dim3(1024), 0, st, b);
+    // (identities take 20 B of LDS per entry and the pipelined identity
+    // reads ~145 VGPRs: 12 waves (3 per SIMD) share 4096 entries; measured on
+    // the 8 GiB corpus: 35.5 ms, 8 waves on 4096 entries 36.0, 16 waves on
+    // 3072 entries (128 VGPRs, spilling) 35.8)
+    hipLaunchKernelGGL((wc_insert_kernel<4096, 12>), dim3((unsigned)((n_chunks + 11) / 12)), dim3(768), 0, st, b);
   }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
@@ -2498,10 +2575,15 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   if (!n_chunks) return CCRDT_OK;
   WcArgs b = a;
   b.n_chunks = n_chunks;
-  // (measured: a 512-word cache at 16 waves per CU beats 1024 words at 8)
-  // (16 waves sharing 2048 / 1024 cached words: +1 ms)
-  constexpr int WC_VTAB = 512, WC_VW = 4;
-  hipLaunchKernelGGL((wc_verify_kernel<WC_VTAB, WC_VW>), dim3((unsigned)((n_chunks + WC_VW - 1) / WC_VW)), dim3(64 * WC_VW), 0, st, b);
+  constexpr int WC_VW = 4;
+  hipLaunchKernelGGL((wc_verify_kernel<WC_VW>), dim3((unsigned)((n_chunks + WC_VW - 1) / WC_VW)), dim3(64 * WC_VW), 0, st, b);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+int wc_launch_check(const WcArgs& a, uint32_t n, hipStream_t st) {
+  if (!n) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_check_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, n);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }
@@ -2529,8 +2611,14 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
       atomicOr(&a.status[1], 8u);
       return;
     }
-    const uint64_t g = wc_global_insert(a, h, key, len, s);
+    bool claimed;
+    const uint64_t g = wc_global_insert(a, h, claimed);
     if (g != ~0ull) {
+      if (claimed) {
+        uint64_t w0, w1;
+        wc_ident_mem(a.bytes + s, len, w0, w1);
+        wc_publish(a, g, w0, w1, key, len, WC_REF_BATCH | s);
+      }
       const unsigned long long c = (unsigned long long)cnt[i];
       const unsigned long long o = atomicAdd(&a.t_cnt[g], c);
       if (o + c > 0x7FFFFFFFFFFFFFFFull) atomicOr(&a.status[1], 4u);  // leaves int64
@@ -2544,9 +2632,9 @@ __global__ void wc_merge_kernel(WcArgs a, const uint64_t* wkey, const uint64_t* 
     atomicOr(&a.status[1], 2u);
     return;
   }
-  const uint64_t ref = a.t[sl].ref;
-  const uint8_t* rep = !(ref & WC_REF_BATCH) ? a.arena + ref : a.bytes + (ref & ~WC_REF_BATCH);
-  bool eq = a.t[sl].key == key && a.t[sl].len == len;
+  const WcMeta m = a.tm[sl];
+  const uint8_t* rep = !(m.ref & WC_REF_BATCH) ? a.arena + m.ref : a.bytes + (m.ref & ~WC_REF_BATCH);
+  bool eq = m.key == key && m.len == len;
   for (uint32_t j = 0; eq && j < len; ++j) eq = rep[j] == a.bytes[s + j];
   if (!eq) atomicOr(&a.status[1], 1u);
 }
@@ -2563,10 +2651,11 @@ __device__ __forceinline__ uint64_t wc_owner_mix(uint64_t z) {  // splitmix64
   return z ^ (z >> 31);
 }
 __device__ __forceinline__ uint32_t wc_slot_owner(const WcArgs& a, uint64_t sl, uint32_t world) {
-  const uint8_t* w = a.arena + a.t[sl].ref;
+  const WcMeta m = a.tm[sl];
+  const uint8_t* w = a.arena + m.ref;
   uint64_t f = 0xCBF29CE484222325ull;
-  for (uint32_t j = 0; j < a.t[sl].len; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
-  return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)a.t[sl].key * 0x9E3779B97F4A7C15ull)) % world);
+  for (uint32_t j = 0; j < m.len; ++j) f = (f ^ w[j]) * 0x100000001B3ull;
+  return (uint32_t)(wc_owner_mix(f ^ ((uint64_t)m.key * 0x9E3779B97F4A7C15ull)) % world);
 }
 // Both passes add per owner into LDS first and reserve with one device
 // atomic per (workgroup, owner): a device-scope cursor per owner taking one
@@ -2583,7 +2672,7 @@ __global__ __launch_bounds__(256) void wc_owner_count_kernel(WcArgs a, uint32_t 
   if (sl <= a.t_mask && a.t[sl].h != 0ull) {
     const uint32_t o = wc_slot_owner(a, sl, world);
     owner[sl] = o;
-    const unsigned long long v = (1ull << 40) + a.t[sl].len;
+    const unsigned long long v = (1ull << 40) + a.tm[sl].len;
     if (lds) atomicAdd(&lcur[o], v);
     else atomicAdd(&cur[o], v);
   }
@@ -2602,7 +2691,7 @@ __global__ __launch_bounds__(256) void wc_owner_scatter_kernel(WcArgs a, const u
   uint32_t len = 0, o = 0;
   unsigned long long c = 0;
   if (v) {
-    len = a.t[sl].len;
+    len = a.tm[sl].len;
     o = owner[sl];
     // rows and bytes advance together in one packed cursor, so a row's bytes
     // start at the sum of the lengths of the rows before it
@@ -2614,10 +2703,10 @@ __global__ __launch_bounds__(256) void wc_owner_scatter_kernel(WcArgs a, const u
   if (!v) return;
   if (lds) c += lbase[o];
   const uint64_t w = c >> 40, b = c & ((1ull << 40) - 1);
-  meta[w * 3] = a.t[sl].key;
+  meta[w * 3] = a.tm[sl].key;
   meta[w * 3 + 1] = len;
   meta[w * 3 + 2] = (int64_t)a.t_cnt[sl];
-  const uint8_t* src = a.arena + a.t[sl].ref;
+  const uint8_t* src = a.arena + a.tm[sl].ref;
   for (uint32_t j = 0; j < len; ++j) out[b + j] = src[j];
 }
 // rows (key, len, count) -> the merge kernel's per-word arrays
@@ -2663,23 +2752,27 @@ int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff,
 // Re-insert the words of an old table into a fresh (larger) table.  The hash
 // is recomputed from the word's persisted bytes under the table's seed, so a
 // re-seeded batch (a collision) starts from a consistent table.
-__global__ void wc_rehash_kernel(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, WcArgs a) {
+__global__ void wc_rehash_kernel(const WcSlot* old, const WcMeta* oldm, const unsigned long long* ocnt, uint64_t on,
+                                 WcArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= on) return;
   const WcSlot o = old[i];
   if (o.h == 0ull) return;
-  const uint64_t h = wc_hkey(a, wc_hash_bytes(a.arena + o.ref, o.len), o.key, o.len);
+  const WcMeta m = oldm[i];
+  const uint64_t h = wc_hkey(a, wc_hash_bytes(a.arena + m.ref, m.len), m.key, m.len);
   uint64_t sl = h & a.t_mask;
   while (atomicCAS(&a.t[sl].h, 0ull, h) != 0ull) sl = (sl + 1) & a.t_mask;
-  a.t[sl].key = o.key;
-  a.t[sl].len = o.len;
-  a.t[sl].ref = o.ref;
+  // (plain stores: the passes that read them run after this kernel)
+  a.t[sl].w0 = o.w0;
+  a.t[sl].w1 = o.w1;
+  a.t[sl].w2 = o.w2;
+  a.tm[sl] = m;
   a.t_cnt[sl] = ocnt[i];
 }
-int wc_launch_rehash(const WcSlot* old, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
-                     hipStream_t st) {
+int wc_launch_rehash(const WcSlot* old, const WcMeta* oldm, const unsigned long long* ocnt, uint64_t on,
+                     const WcArgs& a, hipStream_t st) {
   if (!on) return CCRDT_OK;
-  hipLaunchKernelGGL(wc_rehash_kernel, dim3((unsigned)((on + 255) / 256)), dim3(256), 0, st, old, ocnt, on, a);
+  hipLaunchKernelGGL(wc_rehash_kernel, dim3((unsigned)((on + 255) / 256)), dim3(256), 0, st, old, oldm, ocnt, on, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

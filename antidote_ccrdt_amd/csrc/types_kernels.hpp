@@ -130,21 +130,44 @@ struct LbDownArgs {
 constexpr uint64_t WC_TILE = 4096;  // bytes of a document per wave step (64 per lane)
 constexpr uint64_t WC_TPW = 8;  // tiles per wave (a chunk; measured 8 / 16 / 32: 8 best)
 
-// A word-table slot: everything one probe or one compare needs lies in one
-// 32-byte record (one cache sector), not in five arrays.  The counts live in
-// their own array: the Zipf head's atomics would otherwise keep the lines
-// every probe reads busy.
-//   ref: the word's bytes, an arena offset once persisted, or
-//        WC_REF_BATCH | the batch byte position of its first occurrence
+// A word-table slot: everything one probe or one identity compare needs lies
+// in one 32-byte record (one cache sector): the hash and the word's identity
+// (wc_ident: its length and up to WC_SHORT bytes, then its key), each word
+// nonzero once written, so a reader that sees all three nonzero holds the
+// final identity.  The counts live in their own array (the Zipf head's
+// atomics would otherwise keep the lines every probe reads busy), the
+// representative's bytes and the key / length as plain integers in WcMeta
+// (read only by the passes after the insert kernel).
 struct alignas(32) WcSlot {
-  unsigned long long h;  // 0 = empty
+  unsigned long long h;   // 0 = empty
+  unsigned long long w0;  // WC_MARK | length << 56 | bytes 0..6 (a long word: WC_MARK | 0x7F << 56)
+  unsigned long long w1;  // WC_MARK | bytes 7..13 (a long word: WC_MARK)
+  unsigned long long w2;  // WC_MARK | key
+};
+static_assert(sizeof(WcSlot) == 32, "WcSlot is 32 bytes");
+//   ref: the word's bytes, an arena offset once persisted, or
+//        WC_REF_BATCH | the batch byte position of an occurrence (a word of
+//        up to WC_SHORT bytes is persisted from its identity instead)
+struct alignas(16) WcMeta {
   uint64_t ref;
   uint32_t key;
   uint32_t len;
-  uint64_t spare;
 };
-static_assert(sizeof(WcSlot) == 32, "WcSlot is 32 bytes");
 constexpr uint64_t WC_REF_BATCH = 1ull << 63;
+constexpr uint64_t WC_MARK = 1ull << 63;
+constexpr uint32_t WC_SHORT = 14;  // words of up to 14 bytes are identified by their slot's words
+
+// A token whose identity the insert kernel could not settle (a word of more
+// than WC_SHORT bytes, or a slot whose identity words were not visible yet),
+// checked after the kernel by wc_check_kernel: a = its identity w0 (short)
+// or WC_CHK_LONG | its batch position, b = w1 or its length.
+struct WcChk {
+  uint32_t slot;
+  uint32_t key;
+  uint64_t a;
+  uint64_t b;
+};
+constexpr uint64_t WC_CHK_LONG = 1ull << 63;
 
 struct WcArgs {
   int64_t n_keys;
@@ -165,6 +188,7 @@ struct WcArgs {
   int32_t wdc;               // 1 = worddocumentcount (per-doc distinct)
   // word table (persistent across batches): one 32-byte slot per word
   WcSlot* t;
+  WcMeta* tm;
   unsigned long long* t_cnt;
   uint64_t t_mask;
   uint64_t seed;             // word-hash seed of the table (every h of the table is under it)
@@ -173,8 +197,10 @@ struct WcArgs {
   // per-document dedupe table (worddocumentcount)
   uint64_t* d_hash;
   uint64_t d_mask;
-  uint32_t* status;          // [0] table overflow, [1] hash collision
-  int32_t dbg;               // diagnostic (CCRDT_WC_DBG): 1 verify without the byte compare, 2 without the probe
+  uint32_t* status;          // [0] table overflow, [1] hash collision | token lost | check list full (16), [2] check records
+  WcChk* chk;                // the check list (wc_check_kernel), chk_cap records
+  uint32_t chk_cap;
+  int32_t dbg;               // diagnostic (CCRDT_WC_IDBG): 5 = the insert kernel without its count adds
   uint64_t n_chunks;         // chunks of this insert launch
 };
 

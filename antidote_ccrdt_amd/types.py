@@ -262,6 +262,13 @@ class WordcountEngine(_Engine):
         check(lib.ccrdt_wc_sizes(self.h, C.byref(a), C.byref(b)), "wc_sizes")
         return int(a.value), int(b.value)
 
+    def last_checks(self) -> int:
+        """Check-list records of the last batch (tokens the insert kernel left
+        open), or -1 when it was verified token by token."""
+        n = C.c_int64()
+        check(lib.ccrdt_wc_last_checks(self.h, C.byref(n)), "wc_last_checks")
+        return int(n.value)
+
     def export(self):
         """(key_ptr, word_off, word_bytes, count): words sorted by bytes per key."""
         nw, nb = self.sizes()

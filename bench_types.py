@@ -210,14 +210,16 @@ def bench_wordcount(args, rng, wdc):
         o = orc.WcOracle(1, wdc)
         cpu = cpu_leg(lambda: o.apply(np.array([0, nd_s], np.uint64), off[:nd_s + 1], b[:nbytes]),
                       nbytes, "bytes/s", f"first {nd_s} documents = {nbytes} bytes")
-    # The roofline is the whole step (insert + persist + the byte-exact verify
-    # pass, all required for an exact result), not the insert kernel alone.
+    # The roofline is the whole step (insert + persist + the check of the
+    # tokens the insert kernel left open, all required for an exact result),
+    # not the insert kernel alone.
     line("wdc" if wdc else "wordcount",
          f"antidote_ccrdt_{name} update/2: {b.shape[0] / 2**30:.0f} GiB Zipf(1) corpus, {n_docs} docs "
          "of 1 MiB, 1M-word vocabulary (1/8 of the 64 GB 8-GPU config), one object, corpus in HBM",
          b.shape[0], "bytes/s", ms, ms, alg,
          {"distinct_words": nw, "word_bytes": nb, "gen_s": round(CORPUS.get("gen_s", 0), 1),
-          "insert_kernel_ms": kms, "roofline_time": "whole step (insert + persist + verify)",
+          "insert_kernel_ms": kms, "check_records": eng.last_checks() if hasattr(_lib.lib, "ccrdt_wc_last_checks") else None,
+          "roofline_time": "whole step (insert + persist + check list)",
           "insert_kernel_frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS}, cpu)
     d.close()
     del eng

@@ -464,6 +464,11 @@ typedef struct {
 int ccrdt_wc_apply(ccrdt_engine* e, const ccrdt_wc_docs* docs);
 int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* dev_docs);
 int ccrdt_wc_sizes(ccrdt_engine* e, int64_t* n_words, int64_t* n_bytes);
+/* Diagnostics of the last ccrdt_wc_apply(_device): the tokens the insert
+ * kernel left to its check list (words of more than 14 bytes, slots whose
+ * identity was not yet visible), or -1 when the batch was verified token by
+ * token (the list filled up). */
+int ccrdt_wc_last_checks(ccrdt_engine* e, int64_t* n_checked);
 /* value/1 (:47-48) = the map word -> count; per key, words sorted by bytes
  * (Erlang binary order): key_ptr[n_keys+1] over words, word_off[n_words+1]
  * over word_bytes. */

@@ -273,6 +273,59 @@ def test_wordcount_lds_overflow_path(gpu):
         assert e.value() == o.value()
 
 
+def _identity_docs(rng):
+    """Words around the identity boundary (14 / 15 / 16 bytes), words that
+    differ only past byte 7 or only in length, zero bytes inside and at the
+    end of words, over three keys (workgroups span keys)."""
+    base = [b"abcdefghijklmn", b"abcdefghijklmno", b"abcdefghijklmnop", b"abcdefgh", b"abcdefgX",
+            b"abcdefghijklmX", b"a\x00", b"a", b"a\x00\x00", b"\x00", b"\x00" * 14, b"\x00" * 15,
+            b"\xff" * 14, b"xy" * 40]
+    out = []
+    for _ in range(3):
+        idx = rng.integers(0, len(base), 20000)
+        out.append([b" ".join(base[i] for i in idx[j::4]) for j in range(4)])
+    return out
+
+
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_identity_boundaries(gpu, wdc, monkeypatch):
+    """Exactness rests on the identity compares in the insert kernel and the
+    check list (the long words go there); equal to the oracle either way, and
+    equal again when the list is forced full (token-by-token verify pass)."""
+    docs = _identity_docs(np.random.default_rng(5 + wdc))
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    o = orc.WcOracle(3, wdc)
+    o.apply_docs(docs)
+    want = o.export()
+    e = E(3)
+    e.apply_docs(docs)
+    assert e.last_checks() > 0  # the 15- and 16-byte words and "xy" * 40
+    for x, y in zip(e.export(), want):
+        assert np.array_equal(x, y)
+    monkeypatch.setenv("CCRDT_WC_CHK_CAP", "0")
+    f = E(3)
+    f.apply_docs(docs)
+    assert f.last_checks() == -1
+    for x, y in zip(f.export(), want):
+        assert np.array_equal(x, y)
+
+
+def test_wordcount_short_words_need_no_checks(gpu):
+    """A corpus of words of at most 14 bytes, one key: every token is settled
+    by identity compares inside the insert kernel (LDS or global table); only
+    slots whose identity was not yet visible reach the check list."""
+    n_docs, db = 8, 1 << 20
+    b, off = np.empty(n_docs * db, np.uint8), np.empty(n_docs + 1, np.uint64)
+    _lib.check(_lib.lib.ccrdt_gen_corpus(n_docs, db, 200_000, 7, 4, _lib.ptr(b), _lib.ptr(off)), "gen_corpus")
+    e, o = WordcountEngine(1), orc.WcOracle(1, False)
+    kp = np.array([0, n_docs], np.uint64)
+    e.apply(kp, off, b)
+    o.apply(kp, off, b)
+    assert 0 <= e.last_checks() < 0.01 * n_docs * db / 7
+    for x, y in zip(e.export(), o.export()):
+        assert np.array_equal(x, y)
+
+
 def test_wdc_all_distinct_words(gpu):
     """worddocumentcount on documents of all-distinct words: every (document,
     word) pair reaches the global dedupe table (same counts as the oracle)."""
