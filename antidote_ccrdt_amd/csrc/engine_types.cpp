@@ -42,6 +42,8 @@ int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
                     int verify, hipStream_t st);
 int wc_launch_check(const WcArgs& a, uint32_t n, hipStream_t st);
+int wc_launch_cl_count(const WcClArgs& c, hipStream_t st);
+int wc_launch_cl_sum(const WcClArgs& c, hipStream_t st);
 int wc_launch_rehash(const WcSlot* old, const WcMeta* oldm, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
                      hipStream_t st);
 }  // namespace ccrdt
@@ -115,7 +117,7 @@ void ccrdt_engine::release_types() {
   }
   for (DevBuf* d : {&tb.hb_off, &tb.hb_cap, &tb.hb_a, &tb.hb_b, &tb.hb_c, &tb.hb_d})
     d->release();
-  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.chk, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
+  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.chk, &tb.cl, &tb.cl_bcnt, &tb.fl, &tb.bkt, &tb.cl_small, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
                     &tb.status, &tb.ex_cnt, &tb.ex, &tb.kp})
     d->release();
   for (auto& d : tb.stage) d.release();
@@ -1187,6 +1189,19 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   uint64_t chk_cap = std::min<uint64_t>(docs->n_bytes / 128 + 65536, 1ull << 27);
   if (getenv("CCRDT_WC_CHK_CAP")) chk_cap = strtoull(getenv("CCRDT_WC_CHK_CAP"), nullptr, 0);
   CCRDT_TRY(T.chk.ensure(std::max<uint64_t>(chk_cap, 1) * sizeof(WcChk)));
+  // the count list (WcArgs::cl): token blocks for the LDS misses' counts
+  // (room for a sixteenth of the bytes plus a block per chunk), one flush
+  // region per insert workgroup; CCRDT_WC_NOLIST=1 keeps the device adds
+  const uint64_t n_chunks = tptr[nd];
+  const bool wdc = e->type == CCRDT_WORDDOCUMENTCOUNT;
+  bool use_cl = !(getenv("CCRDT_WC_NOLIST") && atoi(getenv("CCRDT_WC_NOLIST")));
+  const uint64_t cl_entries = docs->n_bytes / 16 + n_chunks * WC_BLK;
+  uint32_t shard_blocks = (uint32_t)std::min<uint64_t>((cl_entries / WC_BLK + WC_NSHARD - 1) / WC_NSHARD + 1,
+                                                       0xFFFFFFFFull / WC_BLK / WC_NSHARD);
+  if (getenv("CCRDT_WC_CL_BLOCKS")) shard_blocks = (uint32_t)strtoul(getenv("CCRDT_WC_CL_BLOCKS"), nullptr, 0);  // test hook
+  const uint64_t n_tb = (uint64_t)WC_NSHARD * shard_blocks;
+  const uint32_t fl_tab = wdc ? WC_TAB_WDC : WC_TAB_WC;
+  const uint64_t n_fl = wdc ? gptr[nd] : (n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC;
   for (int attempt = 0;; ++attempt) {
     // new table (rehash of the current words), then the batch
     CCRDT_TRY(wc_alloc_table(e, out, slots));
@@ -1197,6 +1212,24 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     CCRDT_HIP(hipMemsetAsync(T.status.p, 0, 16, e->stream));
     a.chk = T.chk.as<WcChk>();
     a.chk_cap = (uint32_t)std::min<uint64_t>(chk_cap, 0xFFFFFFFFull);
+    // (bucket sums: buckets of 2^WC_CL_MAXSH slots -- few buckets, so the
+    // scatter pass writes long runs -- at most WC_CL_NB of them)
+    uint32_t lg = 0;
+    while ((1ull << lg) < slots) ++lg;
+    const uint32_t bsh = std::min<uint32_t>(lg, WC_CL_MAXSH);
+    const bool cl_on = use_cl && (slots >> bsh) <= WC_CL_NB && n_tb * WC_BLK + n_fl * fl_tab < (1ull << 32);
+    if (cl_on) {
+      CCRDT_TRY(T.cl.ensure(n_tb * WC_BLK * 4));
+      CCRDT_TRY(T.cl_bcnt.ensure(n_tb * 4));
+      CCRDT_TRY(T.fl.ensure(std::max<uint64_t>(n_fl * fl_tab, 1) * 8));
+      CCRDT_TRY(T.cl_small.ensure((WC_NSHARD + 2 * WC_CL_NB) * 4 + (WC_CL_NB + 1) * 8));
+      CCRDT_HIP(hipMemsetAsync(T.cl_small.p, 0, (WC_NSHARD + 2 * WC_CL_NB) * 4, e->stream));
+      a.cl = T.cl.as<uint32_t>();
+      a.cl_bcnt = T.cl_bcnt.as<uint32_t>();
+      a.cl_cur = T.cl_small.as<uint32_t>();
+      a.cl_shard_blocks = shard_blocks;
+      a.fl = T.fl.as<uint64_t>();
+    }
     a.doc_off = docs->doc_off;
     a.bytes = docs->bytes;
     a.n_bytes = docs->n_bytes;
@@ -1234,6 +1267,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.d_hash = T.d_hash.as<uint64_t>();
         a.d_mask = ds - 1;
       }
+      a.fl_base = a.wdc ? a.group0 : 0;  // (wordcount: one launch)
       a.dbg = getenv("CCRDT_WC_IDBG") ? atoi(getenv("CCRDT_WC_IDBG")) : 0;
       CCRDT_TRY(wc_launch_insert(a, tptr[d1] - tptr[d0], e->stream));
       a.dbg = 0;
@@ -1243,14 +1277,40 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     uint32_t st[3];
     CCRDT_TRY(read_status3(e, st));
     CCRDT_HIP(hipEventElapsedTime(&e->last_kernel_ms, e->evk0, e->evk1));
-    if (st[0] && attempt < 4) {  // table (or dedupe table) too small
+    if (st[0] && attempt < 4) {  // table (or dedupe table) too small, count list full
       if (st[0] & 1u) slots *= 4;
       if (st[0] & 2u) dmul *= 4;
+      if (st[0] & 4u) use_cl = false;
       continue;
     }
     if (st[0]) {
       set_error("wc_apply: word table overflow");
       return CCRDT_ENOMEM;
+    }
+    // the count list summed into the counts, per bucket of slots
+    if (cl_on) {
+      WcClArgs c{};
+      c.cl = T.cl.as<uint32_t>();
+      c.bcnt = T.cl_bcnt.as<uint32_t>();
+      c.cur = T.cl_small.as<uint32_t>();
+      c.shard_blocks = shard_blocks;
+      c.fl = T.fl.as<uint64_t>();
+      c.tab = fl_tab;
+      c.n_tb = n_tb;
+      c.n_fl = n_fl;
+      c.bsh = bsh;
+      c.nb = (uint32_t)(slots >> bsh);
+      c.bkt_cnt = T.cl_small.as<uint32_t>() + WC_NSHARD;
+      c.bkt_cur = c.bkt_cnt + WC_CL_NB;
+      c.bkt_off = reinterpret_cast<uint64_t*>(c.bkt_cur + WC_CL_NB);
+      c.t_cnt = a.t_cnt;
+      c.status = a.status;
+      CCRDT_TRY(wc_launch_cl_count(c, e->stream));
+      std::vector<uint64_t> tot;
+      CCRDT_TRY(d2h_at(tot, T.cl_small, (WC_NSHARD + 2 * WC_CL_NB) / 2 + c.nb, 1, e->stream));
+      CCRDT_TRY(T.bkt.ensure(std::max<uint64_t>(tot[0], 1) * 4));
+      c.bkt = T.bkt.as<uint32_t>();
+      CCRDT_TRY(wc_launch_cl_sum(c, e->stream));
     }
     // the batch's new words into the arena first (the check list's long
     // words are compared against a compact, cache-resident copy)

@@ -2154,15 +2154,15 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // A token that missed the LDS table, resolved one round after its first-slot
 // read (pk: that slot's hash and identity words as read then): find or claim
 // its word, settle its identity, count it.
-__device__ __forceinline__ void wc_resolve(const WcArgs& a, const WcPeek& pk, uint64_t h, uint32_t key, uint32_t tl,
-                                           uint64_t pos, uint64_t tw0, uint64_t tw1, uint64_t doc) {
+__device__ __forceinline__ bool wc_resolve(const WcArgs& a, const WcPeek& pk, uint64_t h, uint32_t key, uint32_t tl,
+                                           uint64_t pos, uint64_t tw0, uint64_t tw1, uint64_t doc, uint64_t& gs_out) {
   bool claimed = false;
   uint64_t gs, sw0 = pk.w0, sw1 = pk.w1, sw2 = pk.w2;
   if (pk.h == h) {
     gs = h & a.t_mask;  // (the common case stays out of the probe loop)
   } else {
     gs = wc_global_insert_at(a, h, h & a.t_mask, pk.h, claimed);
-    if (gs == ~0ull) return;
+    if (gs == ~0ull) return false;
     if (!claimed) {
       const WcPeek q = wc_peek(a, gs);
       sw0 = q.w0;
@@ -2172,7 +2172,34 @@ __device__ __forceinline__ void wc_resolve(const WcArgs& a, const WcPeek& pk, ui
   }
   if (claimed) wc_publish(a, gs, tw0, tw1, key, tl, WC_REF_BATCH | pos);
   else if (wc_settle(a, tw0, tw1, key, sw0, sw1, sw2)) wc_chk_push(a, gs, key, tl, tw0, tw1, pos);
-  if (a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, doc))) atomicAdd(&a.t_cnt[gs], 1ull);
+  gs_out = gs;
+  return a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, doc));
+}
+
+// The count list.  A wave appends the slots of the tokens it counts to a
+// block of WC_BLK entries it owns, taken from one of WC_NSHARD shards (one
+// device atomic per block, spread over 64 words); wc_cl_count / wc_cl_scatter
+// / wc_cl_hist then sum them per bucket of slots in LDS and add each slot's
+// total to t_cnt once -- instead of one device atomic per token (the Zipf
+// tail's ~40 % of the tokens: 13 ms of the 8 GiB corpus's insert kernel).
+__device__ __forceinline__ void wc_cl_push(const WcArgs& a, bool need, uint32_t gs, uint32_t& blk, uint32_t& fill,
+                                           uint32_t shard) {
+  const uint64_t m = ballot(need);
+  if (!m) return;
+  const uint32_t n = (uint32_t)__builtin_popcountll(m);
+  if (fill + n > WC_BLK) {  // close the wave's block, take the next one of its shard
+    uint32_t idx = 0;
+    if (lane_id() == 0) {
+      if (blk != ~0u) a.cl_bcnt[blk] = fill;
+      idx = atomicAdd(&a.cl_cur[shard], 1u);
+      if (idx >= a.cl_shard_blocks) atomicOr(&a.status[0], 4u);  // list full: the batch is re-run with adds
+    }
+    idx = __builtin_amdgcn_readfirstlane(idx);
+    blk = idx < a.cl_shard_blocks ? shard * a.cl_shard_blocks + idx : ~0u;
+    fill = 0;
+  }
+  if (need && blk != ~0u) a.cl[(uint64_t)blk * WC_BLK + fill + mbcnt(m)] = gs;
+  fill += n;
 }
 
 // The tokens that START in a chunk (WC_TPW tiles of WC_TILE bytes of one
@@ -2245,6 +2272,9 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   uint32_t ptl = 0;
   bool pend = false;
   WcPeek pk0 = {0, 0, 0, 0}, pk1 = {0, 0, 0, 0};
+  // this wave's count-list block (wave-uniform)
+  uint32_t cblk = ~0u, cfill = WC_BLK;
+  const uint32_t shard = (blockIdx.x * WAVES + (uint32_t)wv) % WC_NSHARD;
 
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();  // the previous tile's staged bytes are no longer read
@@ -2314,7 +2344,11 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
         // without a miss reads slot 0), then the previous round's misses are
         // resolved
         pk_new = wc_peek(a, counted ? 0ull : (h & a.t_mask));
-        if (pend) wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d);
+        bool cnt = false;
+        uint64_t cgs = 0;
+        if (pend) cnt = wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
+        if (a.cl) wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
+        else if (cnt) atomicAdd(&a.t_cnt[cgs], 1ull);
         pend = !counted;
         ph = h;
         ptl = tl;
@@ -2328,14 +2362,26 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
       }
     }
   }
-  if (pend) wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d);
+  {
+    bool cnt = false;
+    uint64_t cgs = 0;
+    if (pend) cnt = wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
+    if (a.cl) {
+      wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
+      if (cblk != ~0u && lane == 0) a.cl_bcnt[cblk] = cfill;  // the wave's last block
+    } else if (cnt) {
+      atomicAdd(&a.t_cnt[cgs], 1ull);
+    }
+  }
   __syncthreads();
   // flush: every entry into the global table (its identity settled there or
   // left to the check list), with its count (worddocumentcount: once per
   // document, through the dedupe table: other workgroups of the document may
   // hold the word too)
+  uint64_t* const fl = a.cl ? a.fl + (a.fl_base + blockIdx.x) * (uint64_t)TAB : nullptr;
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
     const ulonglong2 e = make_ulonglong2(lw0[i], lw1[i]);
+    if (fl) fl[i] = ~0ull;  // (a counted entry rewrites it below)
     if (e.x == 0ull) continue;
     const uint32_t tl = wc_ident_len(e.x);
     uint64_t lo, hi;
@@ -2350,8 +2396,162 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
       const WcPeek q = wc_peek(a, gs);
       if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
     }
-    if (!a.wdc || wc_doc_first(a, gs, gdoc)) atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
+    if (!a.wdc || wc_doc_first(a, gs, gdoc)) {
+      if (fl) fl[i] = gs | (uint64_t)lc[i] << 32;
+      else atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
+    }
   }
+}
+
+// ---- the count list, summed per bucket of 2^bsh slots (wc_cl_*): units are
+// the token blocks (n_tb = WC_NSHARD * cl_shard_blocks) and then the flush
+// regions (n_fl of tab entries); a workgroup of the count and scatter passes
+// takes WC_CL_UG consecutive units, so its entries of one bucket go out as
+// one run.
+constexpr uint32_t WC_CL_UG = 64;
+// A tile of units (8 token blocks, or 8192 / tab flush regions): each unit's
+// entry count and base in LDS first, then every entry of the tile loaded at
+// once (one unit after the other left a workgroup waiting out one latency
+// per unit).  Entry k of thread t is tile position t + k * TB.
+constexpr uint32_t WC_CL_T = 8192, WC_CL_TB = 512, WC_CL_PER = WC_CL_T / WC_CL_TB;
+struct WcClTile {
+  uint32_t n[8];
+  uint64_t base[8];
+};
+__device__ __forceinline__ uint64_t wc_cl_tile(const WcClArgs& c, WcClTile& ut, uint64_t u, uint64_t u1,
+                                               uint32_t (&slot)[WC_CL_PER], uint32_t (&cnt)[WC_CL_PER]) {
+  const bool tok = u < c.n_tb;
+  const uint32_t lg = tok ? 10u : (c.tab == 4096 ? 12u : 10u);  // log2 of the unit's capacity
+  uint64_t ue = u + (WC_CL_T >> lg);
+  if (tok && ue > c.n_tb) ue = c.n_tb;
+  if (ue > u1) ue = u1;
+  const uint32_t t = threadIdx.x;
+  __syncthreads();  // (the previous tile's metadata is no longer read)
+  if (t < ue - u) {
+    const uint64_t un = u + t;
+    if (tok) {
+      const uint32_t sh = (uint32_t)(un / c.shard_blocks), bi = (uint32_t)(un - (uint64_t)sh * c.shard_blocks);
+      ut.n[t] = bi < c.cur[sh] ? c.bcnt[un] : 0u;
+      ut.base[t] = un * WC_BLK;
+    } else {
+      ut.n[t] = c.tab;
+      ut.base[t] = (un - c.n_tb) * c.tab;
+    }
+  }
+  __syncthreads();
+  const uint32_t nu = (uint32_t)(ue - u);
+#pragma unroll
+  for (uint32_t k = 0; k < WC_CL_PER; ++k) {
+    const uint32_t idx = t + k * WC_CL_TB, ui = idx >> lg, j = idx & ((1u << lg) - 1);
+    slot[k] = 0;
+    cnt[k] = 0;
+    if (ui >= nu || j >= ut.n[ui]) continue;
+    if (tok) {
+      slot[k] = c.cl[ut.base[ui] + j];
+      cnt[k] = 1;
+    } else {
+      const uint64_t x = c.fl[ut.base[ui] + j];
+      slot[k] = (uint32_t)x;
+      cnt[k] = x == ~0ull ? 0u : (uint32_t)(x >> 32);
+    }
+  }
+  return ue;
+}
+
+__global__ __launch_bounds__(WC_CL_TB) void wc_cl_count_kernel(WcClArgs c) {
+  __shared__ uint32_t hist[WC_CL_NB];
+  __shared__ WcClTile ut;
+  for (uint32_t b = threadIdx.x; b < c.nb; b += WC_CL_TB) hist[b] = 0;
+  const uint32_t lim = (1u << (32 - c.bsh)) - 1;  // larger counts are added directly
+  const uint64_t u0 = (uint64_t)blockIdx.x * WC_CL_UG, u1 = u0 + WC_CL_UG < c.n_tb + c.n_fl ? u0 + WC_CL_UG : c.n_tb + c.n_fl;
+  for (uint64_t u = u0; u < u1;) {
+    uint32_t slot[WC_CL_PER], cnt[WC_CL_PER];
+    u = wc_cl_tile(c, ut, u, u1, slot, cnt);
+#pragma unroll
+    for (uint32_t k = 0; k < WC_CL_PER; ++k)
+      if (cnt[k] && cnt[k] <= lim) atomicAdd(&hist[slot[k] >> c.bsh], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < c.nb; b += WC_CL_TB)
+    if (hist[b]) atomicAdd(&c.bkt_cnt[b], hist[b]);
+}
+
+// one workgroup: offsets and cursors of the buckets (nb <= WC_CL_NB)
+__global__ __launch_bounds__(WC_CL_NB) void wc_cl_scan_kernel(WcClArgs c) {
+  __shared__ uint64_t v[WC_CL_NB];
+  const uint32_t t = threadIdx.x;
+  v[t] = t < c.nb ? c.bkt_cnt[t] : 0;
+  __syncthreads();
+  for (uint32_t d = 1; d < WC_CL_NB; d <<= 1) {  // inclusive Hillis-Steele
+    const uint64_t x = t >= d ? v[t - d] : 0;
+    __syncthreads();
+    v[t] += x;
+    __syncthreads();
+  }
+  if (t < c.nb) {
+    const uint64_t ex = v[t] - c.bkt_cnt[t];
+    c.bkt_off[t] = ex;
+    c.bkt_cur[t] = (uint32_t)ex;
+  }
+  if (t == 0) c.bkt_off[c.nb] = v[WC_CL_NB - 1];
+}
+
+// Each tile: entries ranked within their bucket by LDS atomics, one device
+// atomic per (tile, bucket) reserves the bucket's run, entries written at
+// run base + rank.
+__global__ __launch_bounds__(WC_CL_TB) void wc_cl_scatter_kernel(WcClArgs c) {
+  __shared__ uint32_t hist[WC_CL_NB], base[WC_CL_NB];
+  __shared__ WcClTile ut;
+  for (uint32_t b = threadIdx.x; b < c.nb; b += WC_CL_TB) hist[b] = 0;
+  const uint32_t lim = (1u << (32 - c.bsh)) - 1, mask = (1u << c.bsh) - 1;
+  const uint64_t u0 = (uint64_t)blockIdx.x * WC_CL_UG, u1 = u0 + WC_CL_UG < c.n_tb + c.n_fl ? u0 + WC_CL_UG : c.n_tb + c.n_fl;
+  for (uint64_t u = u0; u < u1;) {
+    uint32_t slot[WC_CL_PER], cnt[WC_CL_PER], rank[WC_CL_PER];
+    u = wc_cl_tile(c, ut, u, u1, slot, cnt);
+#pragma unroll
+    for (uint32_t k = 0; k < WC_CL_PER; ++k) {
+      rank[k] = 0;
+      if (cnt[k] > lim) {  // (a count past the entry's field)
+        atomicAdd(&c.t_cnt[slot[k]], (unsigned long long)cnt[k]);
+        cnt[k] = 0;
+      }
+      if (cnt[k]) rank[k] = atomicAdd(&hist[slot[k] >> c.bsh], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < c.nb; b += WC_CL_TB) {
+      base[b] = hist[b] ? atomicAdd(&c.bkt_cur[b], hist[b]) : 0u;
+      hist[b] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < WC_CL_PER; ++k)
+      if (cnt[k]) c.bkt[base[slot[k] >> c.bsh] + rank[k]] = (slot[k] & mask) | cnt[k] << c.bsh;
+  }
+}
+
+// one workgroup per bucket: its entries summed per slot in LDS, each slot's
+// total added to t_cnt by its owner alone (no atomic)
+__global__ __launch_bounds__(1024) void wc_cl_hist_kernel(WcClArgs c) {
+  __shared__ unsigned long long sum[1u << WC_CL_MAXSH];
+  const uint32_t ns = 1u << c.bsh, b = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < ns; i += 1024) sum[i] = 0;
+  __syncthreads();
+  const uint64_t o0 = c.bkt_off[b], o1 = c.bkt_off[b + 1];
+  const uint32_t mask = ns - 1;
+  for (uint64_t j0 = o0; j0 < o1; j0 += 8 * 1024) {  // (eight loads in flight per thread)
+    uint32_t e[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint64_t j = j0 + threadIdx.x + k * 1024;
+      e[k] = j < o1 ? c.bkt[j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+      if (e[k] >> c.bsh) atomicAdd(&sum[e[k] & mask], (unsigned long long)(e[k] >> c.bsh));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < ns; i += 1024)
+    if (sum[i]) c.t_cnt[((uint64_t)b << c.bsh) | i] += sum[i];
 }
 
 // The check list: tokens whose identity the insert kernel left open, compared
@@ -2559,13 +2759,14 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     // 48.6 ms, 512 51.2, 2048 58.4 -- the dedupe path of the misses wants the
     // occupancy of the smaller table; one-document groups of 16 waves on 4096
     // / 2048 entries: 61.6 / 63.6 ms)
-    hipLaunchKernelGGL((wc_insert_kernel<1024, 4>), dim3((unsigned)a.n_groups), dim3(256), 0, st, b);
+    hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
   } else {
     // (identities take 20 B of LDS per entry and the pipelined identity
     // reads ~145 VGPRs: 12 waves (3 per SIMD) share 4096 entries; measured on
     // the 8 GiB corpus: 35.5 ms, 8 waves on 4096 entries 36.0, 16 waves on
     // 3072 entries (128 VGPRs, spilling) 35.8)
-    hipLaunchKernelGGL((wc_insert_kernel<4096, 12>), dim3((unsigned)((n_chunks + 11) / 12)), dim3(768), 0, st, b);
+    hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
+                       dim3(64 * WC_WAVES_WC), 0, st, b);
   }
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
@@ -2577,6 +2778,28 @@ int wc_launch_verify(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
   b.n_chunks = n_chunks;
   constexpr int WC_VW = 4;
   hipLaunchKernelGGL((wc_verify_kernel<WC_VW>), dim3((unsigned)((n_chunks + WC_VW - 1) / WC_VW)), dim3(64 * WC_VW), 0, st, b);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// the count list summed into t_cnt: count, scan, scatter, per-bucket sums.
+// bkt_cnt must be zeroed; total = entries (read back by the caller between
+// the count and scatter passes to size bkt).
+int wc_launch_cl_count(const WcClArgs& c, hipStream_t st) {
+  const uint64_t units = c.n_tb + c.n_fl;
+  if (!units) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_cl_count_kernel, dim3((unsigned)((units + WC_CL_UG - 1) / WC_CL_UG)), dim3(WC_CL_TB), 0, st, c);
+  CCRDT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(wc_cl_scan_kernel, dim3(1), dim3(WC_CL_NB), 0, st, c);
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+int wc_launch_cl_sum(const WcClArgs& c, hipStream_t st) {
+  const uint64_t units = c.n_tb + c.n_fl;
+  if (!units) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_cl_scatter_kernel, dim3((unsigned)((units + WC_CL_UG - 1) / WC_CL_UG)), dim3(WC_CL_TB), 0, st, c);
+  CCRDT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(wc_cl_hist_kernel, dim3(c.nb), dim3(1024), 0, st, c);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

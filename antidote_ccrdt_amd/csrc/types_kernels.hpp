@@ -159,15 +159,14 @@ constexpr uint32_t WC_SHORT = 14;  // words of up to 14 bytes are identified by 
 
 // A token whose identity the insert kernel could not settle (a word of more
 // than WC_SHORT bytes, or a slot whose identity words were not visible yet),
-// checked after the kernel by wc_check_kernel: a = its identity w0 (short)
-// or WC_CHK_LONG | its batch position, b = w1 or its length.
+// checked after the kernel by wc_check_kernel: a = its identity w0 (WC_MARK
+// set) or, for a long word, its batch position; b = w1 or its length.
 struct WcChk {
   uint32_t slot;
   uint32_t key;
   uint64_t a;
   uint64_t b;
 };
-constexpr uint64_t WC_CHK_LONG = 1ull << 63;
 
 struct WcArgs {
   int64_t n_keys;
@@ -200,8 +199,41 @@ struct WcArgs {
   uint32_t* status;          // [0] table overflow, [1] hash collision | token lost | check list full (16), [2] check records
   WcChk* chk;                // the check list (wc_check_kernel), chk_cap records
   uint32_t chk_cap;
+  // The count list (wc_cl_*): the insert kernel's count adds, summed after
+  // it by slot bucket instead of one device atomic per token.  nullptr: the
+  // adds go to t_cnt directly (tables above 2^23 slots; a full list re-runs
+  // the batch that way).
+  uint32_t* cl;              // token entries (global slot), blocks of WC_BLK
+  uint32_t* cl_bcnt;         // [blocks] entries of each block (written when the block is closed)
+  uint32_t* cl_cur;          // [WC_NSHARD] blocks taken from each shard
+  uint32_t cl_shard_blocks;  // blocks per shard
+  uint64_t* fl;              // flush entries: per insert workgroup one per LDS entry (slot | count << 32; ~0 = none)
+  uint64_t fl_base;          // flush region of this launch's first workgroup
   int32_t dbg;               // diagnostic (CCRDT_WC_IDBG): 5 = the insert kernel without its count adds
   uint64_t n_chunks;         // chunks of this insert launch
+};
+
+// The count list (types_kernels.hip wc_cl_*): blocks of WC_BLK token
+// entries taken from WC_NSHARD shards; summed per bucket of 2^bsh slots
+// (at most WC_CL_NB buckets, 2^WC_CL_MAXSH slots each).
+constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH = 13;
+// insert workgroups: LDS entries x waves (wordcount, worddocumentcount)
+constexpr uint32_t WC_TAB_WC = 4096, WC_WAVES_WC = 12, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
+struct WcClArgs {
+  const uint32_t* cl;
+  const uint32_t* bcnt;
+  const uint32_t* cur;
+  uint32_t shard_blocks;
+  const uint64_t* fl;
+  uint32_t tab;
+  uint64_t n_tb, n_fl;
+  uint32_t bsh, nb;
+  uint32_t* bkt_cnt;   // [nb] entries per bucket
+  uint32_t* bkt_cur;   // [nb] scatter cursors (from the scan)
+  uint64_t* bkt_off;   // [nb + 1] bucket offsets
+  uint32_t* bkt;       // entries by bucket: slot within the bucket | count << bsh
+  unsigned long long* t_cnt;
+  uint32_t* status;
 };
 
 }  // namespace ccrdt

@@ -310,6 +310,30 @@ def test_wordcount_identity_boundaries(gpu, wdc, monkeypatch):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("wdc", [False, True])
+@pytest.mark.parametrize("mode", ["list", "list_full", "adds"])
+def test_wordcount_count_list(gpu, wdc, mode, monkeypatch):
+    """The LDS misses' counts are summed through the count list (per bucket of
+    slots, no device atomic per token); a list that fills up re-runs the batch
+    with device adds (CCRDT_WC_CL_BLOCKS=1: one block per shard), and
+    CCRDT_WC_NOLIST=1 takes the adds from the start.  Two batches: the second
+    adds to counts the first left (rehashed table)."""
+    if mode == "list_full":
+        monkeypatch.setenv("CCRDT_WC_CL_BLOCKS", "1")
+    if mode == "adds":
+        monkeypatch.setenv("CCRDT_WC_NOLIST", "1")
+    n_docs, db = 16, 1 << 19
+    b, off = np.empty(n_docs * db, np.uint8), np.empty(n_docs + 1, np.uint64)
+    _lib.check(_lib.lib.ccrdt_gen_corpus(n_docs, db, 300_000, 21, 4, _lib.ptr(b), _lib.ptr(off)), "gen_corpus")
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    e, o = E(3), orc.WcOracle(3, wdc)
+    for kp in (np.array([0, 4, 10, n_docs], np.uint64), np.array([0, 8, 9, n_docs], np.uint64)):
+        e.apply(kp, off, b)
+        o.apply(kp, off, b)
+        for x, y in zip(e.export(), o.export()):
+            assert np.array_equal(x, y)
+
+
 def test_wordcount_short_words_need_no_checks(gpu):
     """A corpus of words of at most 14 bytes, one key: every token is settled
     by identity compares inside the insert kernel (LDS or global table); only
