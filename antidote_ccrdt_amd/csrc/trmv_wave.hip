@@ -1149,8 +1149,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
+#ifndef TRMV_W_OCC
+#define TRMV_W_OCC 4
+#endif
 template <bool FRESH>
-__global__ __launch_bounds__(64 * W_WAVES, 4) void trmv_wave_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(64 * W_WAVES, TRMV_W_OCC) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];

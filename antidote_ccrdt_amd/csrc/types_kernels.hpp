@@ -218,7 +218,11 @@ struct WcArgs {
 // (at most WC_CL_NB buckets, 2^WC_CL_MAXSH slots each).
 constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH = 13;
 // insert workgroups: LDS entries x waves (wordcount, worddocumentcount)
-constexpr uint32_t WC_TAB_WC = 4096, WC_WAVES_WC = 12, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
+#ifndef WC_AB_TAB  // (A/B builds only)
+#define WC_AB_TAB 4096
+#define WC_AB_WAVES 12
+#endif
+constexpr uint32_t WC_TAB_WC = WC_AB_TAB, WC_WAVES_WC = WC_AB_WAVES, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
 struct WcClArgs {
   const uint32_t* cl;
   const uint32_t* bcnt;
