@@ -10,7 +10,7 @@
 // The mapping onto gfx950:
 //  * occupancy: elements are addressed by index, Masked slabs are u8 index
 //    lists, removal clocks are one shared table of 24 rows, so a key's LDS
-//    stays small and four waves fit per SIMD (__launch_bounds__);
+//    stays small and five waves fit per SIMD (__launch_bounds__);
 //  * latency: every global load a key needs is issued before its first use:
 //    a key's ops, and then its removal clocks (8 lanes per clock row,
 //    coalesced), are loaded while the wave still works on the previous key;
@@ -1149,11 +1149,11 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
-#ifndef TRMV_W_OCC
-#define TRMV_W_OCC 4
-#endif
+// 5 waves per SIMD (96 VGPRs, 3 spilled on the FRESH path; 20 one-wave
+// workgroups of 8 KB fill the CU's LDS): tier 0 2.206 -> 2.163 ms against 4
+// (105 VGPRs), A/B round 6
 template <bool FRESH>
-__global__ __launch_bounds__(64 * W_WAVES, TRMV_W_OCC) void trmv_wave_kernel(TrmvApplyArgs a) {
+__global__ __launch_bounds__(64 * W_WAVES, 5) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];

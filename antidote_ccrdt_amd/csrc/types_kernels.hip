@@ -2213,7 +2213,7 @@ __device__ __forceinline__ void wc_cl_push(const WcArgs& a, bool need, uint32_t 
 // wait for each other inside the chunk loop (each has its own staging buffer
 // and token list); only the table's set-up and its final flush are
 // workgroup-wide.
-// TAB x WAVES: 4096 x 12 (wordcount: one workgroup per CU), 1024 x 4
+// TAB x WAVES: 3072 x 16 (wordcount: one workgroup per CU), 1024 x 4
 // (worddocumentcount).  worddocumentcount: its LDS entries are per (document,
 // word), so a workgroup's chunks are chunks of one document (group_doc /
 // group_ptr; the last group of a document may leave waves idle).
@@ -2761,10 +2761,10 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     // / 2048 entries: 61.6 / 63.6 ms)
     hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
   } else {
-    // (identities take 20 B of LDS per entry and the pipelined identity
-    // reads ~145 VGPRs: 12 waves (3 per SIMD) share 4096 entries; measured on
-    // the 8 GiB corpus: 35.5 ms, 8 waves on 4096 entries 36.0, 16 waves on
-    // 3072 entries (128 VGPRs, spilling) 35.8)
+    // (identities take 20 B of LDS per entry: 16 waves (4 per SIMD, 128
+    // VGPRs with a few spills) share 3072 entries; measured on the 8 GiB
+    // corpus with the count list: 27.1 ms per step, 12 waves on 4096
+    // entries (~150 VGPRs, 3 per SIMD) 28.9)
     hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
                        dim3(64 * WC_WAVES_WC), 0, st, b);
   }
