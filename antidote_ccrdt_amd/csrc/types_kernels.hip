@@ -2213,7 +2213,7 @@ __device__ __forceinline__ void wc_cl_push(const WcArgs& a, bool need, uint32_t 
 // wait for each other inside the chunk loop (each has its own staging buffer
 // and token list); only the table's set-up and its final flush are
 // workgroup-wide.
-// TAB x WAVES: 3072 x 16 (wordcount: one workgroup per CU), 1024 x 4
+// TAB x WAVES: 3584 x 16 (wordcount: one workgroup per CU), 1024 x 4
 // (worddocumentcount).  worddocumentcount: its LDS entries are per (document,
 // word), so a workgroup's chunks are chunks of one document (group_doc /
 // group_ptr; the last group of a document may leave waves idle).
@@ -2421,7 +2421,9 @@ struct WcClTile {
 __device__ __forceinline__ uint64_t wc_cl_tile(const WcClArgs& c, WcClTile& ut, uint64_t u, uint64_t u1,
                                                uint32_t (&slot)[WC_CL_PER], uint32_t (&cnt)[WC_CL_PER]) {
   const bool tok = u < c.n_tb;
-  const uint32_t lg = tok ? 10u : (c.tab == 4096 ? 12u : 10u);  // log2 of the unit's capacity
+  // log2 of the unit's stride in the tile (a flush region's tab entries need
+  // not be a power of two: its last positions are skipped by j < n)
+  const uint32_t lg = tok ? 10u : 32u - (uint32_t)__builtin_clz(c.tab - 1u);
   uint64_t ue = u + (WC_CL_T >> lg);
   if (tok && ue > c.n_tb) ue = c.n_tb;
   if (ue > u1) ue = u1;
@@ -2762,9 +2764,9 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
   } else {
     // (identities take 20 B of LDS per entry: 16 waves (4 per SIMD, 128
-    // VGPRs with a few spills) share 3072 entries; measured on the 8 GiB
-    // corpus with the count list: 27.1 ms per step, 12 waves on 4096
-    // entries (~150 VGPRs, 3 per SIMD) 28.9)
+    // VGPRs with a few spills) share 3584 entries; measured on the 8 GiB
+    // corpus with the count list: 26.4 ms per step, 3072 entries 27.5, 12
+    // waves on 4096 entries (~150 VGPRs, 3 per SIMD) 28.9)
     hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
                        dim3(64 * WC_WAVES_WC), 0, st, b);
   }

@@ -219,7 +219,7 @@ struct WcArgs {
 constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH = 13;
 // insert workgroups: LDS entries x waves (wordcount, worddocumentcount)
 #ifndef WC_AB_TAB  // (A/B builds only)
-#define WC_AB_TAB 3072
+#define WC_AB_TAB 3584
 #define WC_AB_WAVES 16
 #endif
 constexpr uint32_t WC_TAB_WC = WC_AB_TAB, WC_WAVES_WC = WC_AB_WAVES, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
