@@ -1146,11 +1146,11 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   for (uint64_t d = 0; d < nd; ++d)
     for (uint64_t c = tptr[d]; c < tptr[d + 1]; ++c) cdoc[c] = (uint32_t)d;
   CCRDT_TRY(h2d(*e, T.stage[5], cdoc.data(), cdoc.size() * 4));
-  // worddocumentcount: groups of 4 chunks of one document (one workgroup each)
+  // worddocumentcount: groups of WC_WAVES_WDC chunks of one document (one workgroup each)
   std::vector<uint64_t> gptr(nd + 1, 0);
   std::vector<uint32_t> gdoc;
   if (e->type == CCRDT_WORDDOCUMENTCOUNT) {
-    for (uint64_t d = 0; d < nd; ++d) gptr[d + 1] = gptr[d] + (tptr[d + 1] - tptr[d] + 3) / 4;
+    for (uint64_t d = 0; d < nd; ++d) gptr[d + 1] = gptr[d] + (tptr[d + 1] - tptr[d] + WC_WAVES_WDC - 1) / WC_WAVES_WDC;
     gdoc.resize(gptr[nd] + 1, 0u);
     for (uint64_t d = 0; d < nd; ++d)
       for (uint64_t g = gptr[d]; g < gptr[d + 1]; ++g) gdoc[g] = (uint32_t)d;

@@ -1149,11 +1149,13 @@ __device__ __forceinline__ int trmv_wave_key(const TrmvApplyArgs& a, uint32_t ke
 }
 }  // namespace
 
-// 5 waves per SIMD (96 VGPRs, 3 spilled on the FRESH path; 20 one-wave
+// OCC waves per SIMD.  5 (96 VGPRs, 3 spilled on the FRESH path; 20 one-wave
 // workgroups of 8 KB fill the CU's LDS): tier 0 2.206 -> 2.163 ms against 4
-// (105 VGPRs), A/B round 6
-template <bool FRESH>
-__global__ __launch_bounds__(64 * W_WAVES, 5) void trmv_wave_kernel(TrmvApplyArgs a) {
+// (105 VGPRs), A/B round 6.  The overlapped hand-on launches the 4-wave
+// build: at 5 waves tier 0 holds all of the LDS and the consumers beside it
+// waited (one-eighth size: tail 0.013 -> 0.037 ms).
+template <bool FRESH, int OCC>
+__global__ __launch_bounds__(64 * W_WAVES, OCC) void trmv_wave_kernel(TrmvApplyArgs a) {
   __shared__ WaveLds<FRESH> lds[W_WAVES];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveLds<FRESH>& L = lds[wv];
@@ -1201,7 +1203,9 @@ __global__ __launch_bounds__(64 * W_WAVES, 5) void trmv_wave_kernel(TrmvApplyArg
 }
 
 // grid_keys = keys the grid covers (all keys for the first tier)
-void trmv_wave_preload() { preload_kernels(trmv_wave_kernel<true>, trmv_wave_kernel<false>); }
+void trmv_wave_preload() {
+  preload_kernels(trmv_wave_kernel<true, 5>, trmv_wave_kernel<false, 5>, trmv_wave_kernel<true, 4>);
+}
 
 // waves of the launch trmv_launch_wave makes for grid_keys keys
 uint32_t trmv_wave_waves(uint64_t grid_keys) {
@@ -1214,9 +1218,12 @@ int trmv_launch_wave(const TrmvApplyArgs& a, uint64_t grid_keys, hipStream_t st)
   const uint64_t per_block = (uint64_t)W_WAVES * W_KPW;
   const uint64_t blocks = (grid_keys + per_block - 1) / per_block;
   if (a.fresh)
-    hipLaunchKernelGGL(trmv_wave_kernel<true>, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+    if (a.pub)  // overlapped hand-on: room for the consumers
+      hipLaunchKernelGGL((trmv_wave_kernel<true, 4>), dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+    else
+      hipLaunchKernelGGL((trmv_wave_kernel<true, 5>), dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
   else
-    hipLaunchKernelGGL(trmv_wave_kernel<false>, dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
+    hipLaunchKernelGGL((trmv_wave_kernel<false, 5>), dim3((unsigned)blocks), dim3(64 * W_WAVES), 0, st, a);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -222,7 +222,12 @@ constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH =
 #define WC_AB_TAB 3584
 #define WC_AB_WAVES 16
 #endif
-constexpr uint32_t WC_TAB_WC = WC_AB_TAB, WC_WAVES_WC = WC_AB_WAVES, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
+#ifndef WC_AB_TAB_WDC  // (A/B builds only)
+#define WC_AB_TAB_WDC 1024
+#define WC_AB_WAVES_WDC 4
+#endif
+constexpr uint32_t WC_TAB_WC = WC_AB_TAB, WC_WAVES_WC = WC_AB_WAVES, WC_TAB_WDC = WC_AB_TAB_WDC,
+                   WC_WAVES_WDC = WC_AB_WAVES_WDC;
 struct WcClArgs {
   const uint32_t* cl;
   const uint32_t* bcnt;
