@@ -535,7 +535,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "trmv_wave_kernel<true> (tier 0)",
+                "kernel": "trmv_wave_kernel<true, 5> (tier 0)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

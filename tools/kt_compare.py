@@ -24,7 +24,7 @@ def main():
         raise SystemExit("missing kernel trace or bench line")
     rows = list(csv.DictReader(open(tr[0])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    t0 = [r for r in rows if "trmv_wave_kernel<true>" in r["Kernel_Name"]]
+    t0 = [r for r in rows if "trmv_wave_kernel<true, 5>" in r["Kernel_Name"]]
     W, K = line["warmup"], line["steps"]
     timed = t0[W:W + K]
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]

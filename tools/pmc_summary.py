@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--kernel", default="")
     ap.add_argument("--bench-json", help="write bench.py's roofline.traffic source here")
-    ap.add_argument("--dominant", default="trmv_wave_kernel<true>")
+    ap.add_argument("--dominant", default="trmv_wave_kernel<true, 5>")
     ap.add_argument("--steady", default="trmv_resident_kernel",
                     help="the steady-state leg's kernel (bench.py detail.steady_state.roofline)")
     ap.add_argument("--per-dispatch", default="",
