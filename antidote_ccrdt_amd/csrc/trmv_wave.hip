@@ -77,7 +77,7 @@ constexpr int W_RCAP = 24;   // clock rows: old Removals rows + this batch's rmv
 constexpr int W_WAVES = 1;  // waves (keys in flight) per workgroup (4 before A/B r04 run 31)
 #define ST_OUT(p, v) (*(p) = (v))
 #define LD_IN(p) (*(p))
-constexpr int W_KPW = 8;  // consecutive keys per wave chunk (1..64; A/B r03: 2/3/4/16 slower)
+constexpr int W_KPW = 8;  // consecutive keys per wave chunk (1..64; A/B r03: 2/3/4/16 slower; r06 at 5 waves: 4/16 slower)
 constexpr int W_MD = (W_KPW + 7) / 8;  // metadata registers of a chunk header
 static_assert(W_KPW >= 1 && W_KPW <= 64, "1..64 keys per wave chunk");
 constexpr unsigned long long W_EMPTY = 0x8000000000000000ull;  // an Id of INT64_MIN takes tier 1
