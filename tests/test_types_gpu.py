@@ -334,6 +334,36 @@ def test_wordcount_count_list(gpu, wdc, mode, monkeypatch):
             assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("wdc", [False, True])
+def test_wordcount_random_lengths_multi_batch(gpu, wdc):
+    """Random words of 0..40 bytes over every byte value but the separators
+    (zero bytes included), a Zipf-like reuse so both the LDS tables and the
+    global table see repeats, documents of 0..300 KiB over 4 keys, three
+    batches onto the same engine (the rehash carries identities and counts),
+    vs the oracle after each batch."""
+    rng = np.random.default_rng(77 + wdc)
+    alphabet = np.array([c for c in range(256) if c not in (0x0A, 0x20)], np.uint8)
+    vocab = [bytes(rng.choice(alphabet, int(rng.integers(0, 41)))) for _ in range(6000)]
+    p = 1.0 / np.arange(1, len(vocab) + 1) ** 0.9
+    p /= p.sum()
+    E = WordDocumentCountEngine if wdc else WordcountEngine
+    e, o = E(4), orc.WcOracle(4, wdc)
+    for _ in range(3):
+        docs = []
+        for k in range(4):
+            dk = []
+            for _ in range(int(rng.integers(0, 4))):
+                n = int(rng.integers(0, 40000))
+                idx = rng.choice(len(vocab), n, p=p)
+                seps = rng.choice([b" ", b"\n", b"  "], n, p=[0.8, 0.15, 0.05])
+                dk.append(b"".join(vocab[i] + sp for i, sp in zip(idx, seps)))
+            docs.append(dk)
+        e.apply_docs(docs)
+        o.apply_docs(docs)
+        for x, y in zip(e.export(), o.export()):
+            assert np.array_equal(x, y)
+
+
 def test_wordcount_short_words_need_no_checks(gpu):
     """A corpus of words of at most 14 bytes, one key: every token is settled
     by identity compares inside the insert kernel (LDS or global table); only
