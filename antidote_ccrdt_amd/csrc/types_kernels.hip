@@ -2132,6 +2132,13 @@ __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64
   const uint64_t dh = ((doc + 1) << 40) | g;
   uint64_t sl = wc_mix(dh, 0x5151, 0) & a.d_mask;
   for (uint64_t probe = 0; probe <= a.d_mask && probe < WC_MAXPROBE; ++probe) {
+    // An entry goes 0 -> its pair once per launch (the table is cleared
+    // before each), so a read that sees it nonzero holds the final pair (a
+    // stale read only ever sees 0): repeats and occupied probes settle
+    // without an atomic.
+    const unsigned long long seen = __hip_atomic_load((unsigned long long*)&a.d_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == dh) return false;
+    if (seen != 0ull) { sl = (sl + 1) & a.d_mask; continue; }
     const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], 0ull, (unsigned long long)dh);
     if (prev == 0ull) return true;
     if (prev == dh) return false;
