@@ -30,10 +30,13 @@ struct TypeBufs {
   DevBuf t_tab[2], t_meta[2], t_cnt[2];  // word table: WcSlot[t_slots], WcMeta[t_slots], counts[t_slots]
   uint64_t t_slots[2] = {0, 0};
   DevBuf arena, arena_top, d_hash, chk;  // chk: the insert kernel's check list (WcChk)
+  // the dedupe table (d_hash): slots cleared since its last reset, the last
+  // launch's document tags end there (WcArgs::d_base)
+  uint64_t d_clean = 0, d_base = 0;
   DevBuf cl, cl_bcnt, fl, bkt, cl_small;  // the count list (WcArgs::cl) and its bucket sums
   uint64_t arena_cap = 0;
-  uint64_t wc_seed = 0;
-  int64_t wc_checks = 0;  // the last batch's check-list records (-1: verified token by token)  // word-hash seed; a batch that meets a collision is re-run once with a new one
+  uint64_t wc_seed = 0;   // word-hash seed; a batch that meets a collision is re-run once with a new one
+  int64_t wc_checks = 0;  // the last batch's check-list records (-1: verified token by token)
   // scratch shared by the types
   DevBuf caps, part, ovf_a, ovf_b, status, ex_cnt, ex, kp, stage[8];
   // HBM class of topk / leaderboard (keys beyond the LDS classes)

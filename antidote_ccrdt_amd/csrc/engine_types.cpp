@@ -1237,12 +1237,16 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     // worddocumentcount: the (document, word) dedupe table is sized by the
     // chunk's tokens; documents are processed in chunks of <= 2^28 tokens
     // (wordcount: one launch)
+    // (test hooks: CCRDT_WC_LAUNCH_TOKENS, the tokens per launch;
+    // CCRDT_WC_DTAGS, the document tags before the dedupe table is cleared)
+    const uint64_t launch_tok = getenv("CCRDT_WC_LAUNCH_TOKENS") ? strtoull(getenv("CCRDT_WC_LAUNCH_TOKENS"), nullptr, 0) : (1ull << 28);
+    const uint64_t dtags = getenv("CCRDT_WC_DTAGS") ? strtoull(getenv("CCRDT_WC_DTAGS"), nullptr, 0) : (1ull << 24);
     uint64_t d0 = 0;
     while (d0 < nd) {
       uint64_t d1 = d0, tk = 0;
-      // (worddocumentcount dedupe entries hold the launch-local document
-      // index in 24 bits: at most 2^23 documents per launch)
-      while (d1 < nd && (d1 == d0 || !a.wdc || (tk + ntok[d1] <= (1ull << 28) && d1 - d0 < (1ull << 23))))
+      // (worddocumentcount dedupe entries hold a document tag in 24 bits: at
+      // most 2^23 documents per launch)
+      while (d1 < nd && (d1 == d0 || !a.wdc || (tk + ntok[d1] <= launch_tok && d1 - d0 < (1ull << 23))))
         tk += ntok[d1++];
       a.n_docs = (int64_t)(d1 - d0);
       a.doc_key = T.stage[0].as<uint64_t>() + d0;
@@ -1262,10 +1266,24 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         // the Zipf corpus and the re-run cost 13 ms); an overflow re-runs the
         // batch with four times the slots
         const uint64_t ds = pow2_at_least(std::max<uint64_t>(2 * tk, 1024) * dmul);
+        // not cleared per launch: the launch's document tags lie above every
+        // earlier launch's (WcArgs::d_base), so the old pairs read as free;
+        // only a new buffer, slots never cleared, or spent tags (2^24) clear
+        const uint64_t b0 = T.d_hash.bytes;
         CCRDT_TRY(T.d_hash.ensure(ds * 8));
-        CCRDT_HIP(hipMemsetAsync(T.d_hash.p, 0, ds * 8, e->stream));
+        if (T.d_hash.bytes != b0) T.d_clean = T.d_base = 0;
+        if (T.d_base + (d1 - d0) >= dtags || getenv("CCRDT_WC_DCLEAR")) {  // (diagnostic: every launch)
+          T.d_clean = std::max(T.d_clean, ds);
+          CCRDT_HIP(hipMemsetAsync(T.d_hash.p, 0, T.d_clean * 8, e->stream));
+          T.d_base = 0;
+        } else if (ds > T.d_clean) {
+          CCRDT_HIP(hipMemsetAsync(T.d_hash.as<uint64_t>() + T.d_clean, 0, (ds - T.d_clean) * 8, e->stream));
+          T.d_clean = ds;
+        }
         a.d_hash = T.d_hash.as<uint64_t>();
         a.d_mask = ds - 1;
+        a.d_base = T.d_base;
+        T.d_base += d1 - d0;
       }
       a.fl_base = a.wdc ? a.group0 : 0;  // (wordcount: one launch)
       a.dbg = getenv("CCRDT_WC_IDBG") ? atoi(getenv("CCRDT_WC_IDBG")) : 0;

@@ -2126,23 +2126,29 @@ __device__ __forceinline__ void wc_chk_push(const WcArgs& a, uint64_t sl, uint32
 
 __device__ __forceinline__ bool wc_doc_first(const WcArgs& a, uint64_t g, uint64_t doc) {
   // worddocumentcount: first occurrence of (doc, word) in the global dedupe
-  // table.  The entry is the exact pair -- (launch-local document + 1) << 40 |
-  // the word's table slot g (one slot per distinct word) -- so no two pairs
-  // share an entry; the hash only picks where to probe.
-  const uint64_t dh = ((doc + 1) << 40) | g;
+  // table.  The entry is the exact pair -- the document's tag (d_base + its
+  // launch-local index + 1) << 40 | the word's table slot g (one slot per
+  // distinct word) -- so no two pairs share an entry; the hash only picks
+  // where to probe.  Tags grow launch after launch, so an entry whose tag is
+  // at most d_base is a pair of an earlier launch, free to take: the table
+  // is not cleared between launches.  A slot goes from free to a pair of
+  // this launch once, so a read that sees such a pair holds it for good (a
+  // stale read sees a free slot, and the CAS finds out): repeats and
+  // occupied probes settle without an atomic.
+  const uint64_t dh = ((a.d_base + doc + 1) << 40) | g;
   uint64_t sl = wc_mix(dh, 0x5151, 0) & a.d_mask;
-  for (uint64_t probe = 0; probe <= a.d_mask && probe < WC_MAXPROBE; ++probe) {
-    // An entry goes 0 -> its pair once per launch (the table is cleared
-    // before each), so a read that sees it nonzero holds the final pair (a
-    // stale read only ever sees 0): repeats and occupied probes settle
-    // without an atomic.
-    const unsigned long long seen = __hip_atomic_load((unsigned long long*)&a.d_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long seen = __hip_atomic_load((unsigned long long*)&a.d_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint64_t probe = 0; probe <= a.d_mask && probe < WC_MAXPROBE;) {
     if (seen == dh) return false;
-    if (seen != 0ull) { sl = (sl + 1) & a.d_mask; continue; }
-    const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], 0ull, (unsigned long long)dh);
-    if (prev == 0ull) return true;
-    if (prev == dh) return false;
-    sl = (sl + 1) & a.d_mask;
+    if ((seen >> 40) > a.d_base) {  // another pair of this launch
+      sl = (sl + 1) & a.d_mask;
+      ++probe;
+      seen = __hip_atomic_load((unsigned long long*)&a.d_hash[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    const unsigned long long prev = atomicCAS((unsigned long long*)&a.d_hash[sl], seen, (unsigned long long)dh);
+    if (prev == seen) return true;
+    seen = prev;  // (this slot again, with what it holds)
   }
   atomicOr(&a.status[0], 2u);
   return false;

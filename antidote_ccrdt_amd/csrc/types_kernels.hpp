@@ -196,6 +196,7 @@ struct WcArgs {
   // per-document dedupe table (worddocumentcount)
   uint64_t* d_hash;
   uint64_t d_mask;
+  uint64_t d_base;           // document tags of this launch: d_base + 1 .. d_base + n_docs (< 2^24)
   uint32_t* status;          // [0] table overflow, [1] hash collision | token lost | check list full (16), [2] check records
   WcChk* chk;                // the check list (wc_check_kernel), chk_cap records
   uint32_t chk_cap;

@@ -364,6 +364,30 @@ def test_wordcount_random_lengths_multi_batch(gpu, wdc):
             assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("dtags", [None, "7", "2"])
+def test_wdc_dedupe_tags_across_launches(gpu, monkeypatch, dtags):
+    """worddocumentcount's dedupe table is not cleared between launches: each
+    launch's documents get tags above every earlier launch's, so old pairs
+    read as free slots.  Small launches (a few documents each, many per
+    batch) over several batches, with the default tag space (no clear) and
+    with tag spaces so small that the table is cleared every few launches
+    or every launch; the same words recur in every document so stale pairs
+    of the same word sit in the table.  vs the oracle after each batch."""
+    monkeypatch.setenv("CCRDT_WC_LAUNCH_TOKENS", "3000")
+    if dtags:
+        monkeypatch.setenv("CCRDT_WC_DTAGS", dtags)
+    rng = np.random.default_rng(5)
+    vocab = [b"w%d" % i for i in range(400)]
+    e, o = WordDocumentCountEngine(3), orc.WcOracle(3, True)
+    for _ in range(4):
+        docs = [[b" ".join(vocab[i] for i in rng.integers(0, len(vocab), int(rng.integers(0, 2500))))
+                 for _ in range(int(rng.integers(0, 6)))] for _ in range(3)]
+        e.apply_docs(docs)
+        o.apply_docs(docs)
+        for x, y in zip(e.export(), o.export()):
+            assert np.array_equal(x, y)
+
+
 def test_wordcount_short_words_need_no_checks(gpu):
     """A corpus of words of at most 14 bytes, one key: every token is settled
     by identity compares inside the insert kernel (LDS or global table); only
