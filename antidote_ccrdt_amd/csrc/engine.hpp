@@ -33,6 +33,7 @@ struct TypeBufs {
   // the dedupe table (d_hash): slots cleared since its last reset, the last
   // launch's document tags end there (WcArgs::d_base)
   uint64_t d_clean = 0, d_base = 0;
+  DevBuf dl, dl_pre, dl_cur;  // worddocumentcount's document lists (WcArgs::dl)
   DevBuf cl, cl_bcnt, fl, bkt, cl_small;  // the count list (WcArgs::cl) and its bucket sums
   uint64_t arena_cap = 0;
   uint64_t wc_seed = 0;   // word-hash seed; a batch that meets a collision is re-run once with a new one

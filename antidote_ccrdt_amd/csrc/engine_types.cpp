@@ -42,6 +42,7 @@ int wc_launch_meta_split(const int64_t* meta, uint64_t n, uint64_t* wkey, int64_
 int wc_launch_merge(const WcArgs& a, const uint64_t* wkey, const uint64_t* woff, const int64_t* cnt, uint64_t n,
                     int verify, hipStream_t st);
 int wc_launch_check(const WcArgs& a, uint32_t n, hipStream_t st);
+int wc_launch_dl(const WcArgs& a, uint64_t n_docs, uint32_t passes, hipStream_t st);
 int wc_launch_cl_count(const WcClArgs& c, hipStream_t st);
 int wc_launch_cl_sum(const WcClArgs& c, hipStream_t st);
 int wc_launch_rehash(const WcSlot* old, const WcMeta* oldm, const unsigned long long* ocnt, uint64_t on, const WcArgs& a,
@@ -117,7 +118,7 @@ void ccrdt_engine::release_types() {
   }
   for (DevBuf* d : {&tb.hb_off, &tb.hb_cap, &tb.hb_a, &tb.hb_b, &tb.hb_c, &tb.hb_d})
     d->release();
-  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.chk, &tb.cl, &tb.cl_bcnt, &tb.fl, &tb.bkt, &tb.cl_small, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
+  for (DevBuf* d : {&tb.arena, &tb.arena_top, &tb.d_hash, &tb.dl, &tb.dl_pre, &tb.dl_cur, &tb.chk, &tb.cl, &tb.cl_bcnt, &tb.fl, &tb.bkt, &tb.cl_small, &tb.caps, &tb.part, &tb.ovf_a, &tb.ovf_b,
                     &tb.status, &tb.ex_cnt, &tb.ex, &tb.kp})
     d->release();
   for (auto& d : tb.stage) d.release();
@@ -1195,6 +1196,15 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   const uint64_t n_chunks = tptr[nd];
   const bool wdc = e->type == CCRDT_WORDDOCUMENTCOUNT;
   bool use_cl = !(getenv("CCRDT_WC_NOLIST") && atoi(getenv("CCRDT_WC_NOLIST")));
+  // worddocumentcount: document lists instead of the dedupe table
+  // (CCRDT_WC_DLIST=0: the dedupe table; also when the word table needs more
+  // than WC_DL_MAXPASS bitmap passes, or a document's list overflows)
+  bool use_dl = wdc && !(getenv("CCRDT_WC_DLIST") && !atoi(getenv("CCRDT_WC_DLIST")));
+  if (use_dl && nd) {
+    std::vector<uint64_t> pre(nd + 1, 0);
+    for (uint64_t d = 0; d < nd; ++d) pre[d + 1] = pre[d] + ntok[d];
+    CCRDT_TRY(h2d(*e, T.dl_pre, pre.data(), (nd + 1) * 8));
+  }
   const uint64_t cl_entries = docs->n_bytes / 16 + n_chunks * WC_BLK;
   uint32_t shard_blocks = (uint32_t)std::min<uint64_t>((cl_entries / WC_BLK + WC_NSHARD - 1) / WC_NSHARD + 1,
                                                        0xFFFFFFFFull / WC_BLK / WC_NSHARD);
@@ -1218,6 +1228,8 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     while ((1ull << lg) < slots) ++lg;
     const uint32_t bsh = std::min<uint32_t>(lg, WC_CL_MAXSH);
     const bool cl_on = use_cl && (slots >> bsh) <= WC_CL_NB && n_tb * WC_BLK + n_fl * fl_tab < (1ull << 32);
+    const uint32_t dl_passes = (uint32_t)((slots + WC_DL_BITS - 1) / WC_DL_BITS);
+    const bool dl_on = use_dl && dl_passes <= WC_DL_MAXPASS;
     if (cl_on) {
       CCRDT_TRY(T.cl.ensure(n_tb * WC_BLK * 4));
       CCRDT_TRY(T.cl_bcnt.ensure(n_tb * 4));
@@ -1228,7 +1240,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       a.cl_bcnt = T.cl_bcnt.as<uint32_t>();
       a.cl_cur = T.cl_small.as<uint32_t>();
       a.cl_shard_blocks = shard_blocks;
-      a.fl = T.fl.as<uint64_t>();
+      a.fl = dl_on ? nullptr : T.fl.as<uint64_t>();  // (document lists: the flush appends pairs instead)
     }
     a.doc_off = docs->doc_off;
     a.bytes = docs->bytes;
@@ -1241,13 +1253,26 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
     // CCRDT_WC_DTAGS, the document tags before the dedupe table is cleared)
     const uint64_t launch_tok = getenv("CCRDT_WC_LAUNCH_TOKENS") ? strtoull(getenv("CCRDT_WC_LAUNCH_TOKENS"), nullptr, 0) : (1ull << 28);
     const uint64_t dtags = getenv("CCRDT_WC_DTAGS") ? strtoull(getenv("CCRDT_WC_DTAGS"), nullptr, 0) : (1ull << 24);
+    // (worddocumentcount dedupe entries hold a document tag in 24 bits: at
+    // most 2^23 documents per launch)
+    auto launch_end = [&](uint64_t x0, uint64_t& tk) {
+      uint64_t x1 = x0;
+      tk = 0;
+      while (x1 < nd && (x1 == x0 || !a.wdc || (tk + ntok[x1] <= launch_tok && x1 - x0 < (1ull << 23))))
+        tk += ntok[x1++];
+      return x1;
+    };
+    uint64_t max_tk = 0, max_docs = 0;  // (the document lists are sized once for every launch)
+    for (uint64_t x0 = 0, tk = 0; x0 < nd;) {
+      const uint64_t x1 = launch_end(x0, tk);
+      max_tk = std::max(max_tk, tk);
+      max_docs = std::max(max_docs, x1 - x0);
+      x0 = x1;
+    }
     uint64_t d0 = 0;
     while (d0 < nd) {
-      uint64_t d1 = d0, tk = 0;
-      // (worddocumentcount dedupe entries hold a document tag in 24 bits: at
-      // most 2^23 documents per launch)
-      while (d1 < nd && (d1 == d0 || !a.wdc || (tk + ntok[d1] <= launch_tok && d1 - d0 < (1ull << 23))))
-        tk += ntok[d1++];
+      uint64_t tk = 0;
+      const uint64_t d1 = launch_end(d0, tk);
       a.n_docs = (int64_t)(d1 - d0);
       a.doc_key = T.stage[0].as<uint64_t>() + d0;
       a.doc_off = docs->doc_off + d0;
@@ -1261,7 +1286,16 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.group0 = gptr[d0];
         a.n_groups = gptr[d1] - gptr[d0];
       }
-      if (a.wdc) {
+      if (a.wdc && dl_on) {
+        CCRDT_TRY(T.dl.ensure(std::max<uint64_t>(max_tk, 1) * 4));
+        CCRDT_TRY(T.dl_cur.ensure(std::max<uint64_t>(max_docs, 1) * 4));
+        CCRDT_HIP(hipMemsetAsync(T.dl_cur.p, 0, (d1 - d0) * 4, e->stream));
+        a.dl = T.dl.as<uint32_t>();
+        a.dl_pre = T.dl_pre.as<uint64_t>() + d0;
+        a.dl_cur = T.dl_cur.as<uint32_t>();
+        a.d_hash = nullptr;
+      } else if (a.wdc) {
+        a.dl = nullptr;
         // two slots per token (measured: half a slot per token overflowed on
         // the Zipf corpus and the re-run cost 13 ms); an overflow re-runs the
         // batch with four times the slots
@@ -1289,6 +1323,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       a.dbg = getenv("CCRDT_WC_IDBG") ? atoi(getenv("CCRDT_WC_IDBG")) : 0;
       CCRDT_TRY(wc_launch_insert(a, tptr[d1] - tptr[d0], e->stream));
       a.dbg = 0;
+      if (a.wdc && dl_on) CCRDT_TRY(wc_launch_dl(a, d1 - d0, dl_passes, e->stream));
       d0 = d1;
     }
     CCRDT_HIP(hipEventRecord(e->evk1, e->stream));
@@ -1299,6 +1334,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       if (st[0] & 1u) slots *= 4;
       if (st[0] & 2u) dmul *= 4;
       if (st[0] & 4u) use_cl = false;
+      if (st[0] & 8u) use_dl = false;
       continue;
     }
     if (st[0]) {
@@ -1315,7 +1351,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
       c.fl = T.fl.as<uint64_t>();
       c.tab = fl_tab;
       c.n_tb = n_tb;
-      c.n_fl = n_fl;
+      c.n_fl = dl_on ? 0 : n_fl;
       c.bsh = bsh;
       c.nb = (uint32_t)(slots >> bsh);
       c.bkt_cnt = T.cl_small.as<uint32_t>() + WC_NSHARD;

@@ -2186,7 +2186,7 @@ __device__ __forceinline__ bool wc_resolve(const WcArgs& a, const WcPeek& pk, ui
   if (claimed) wc_publish(a, gs, tw0, tw1, key, tl, WC_REF_BATCH | pos);
   else if (wc_settle(a, tw0, tw1, key, sw0, sw1, sw2)) wc_chk_push(a, gs, key, tl, tw0, tw1, pos);
   gs_out = gs;
-  return a.dbg != 5 && (!a.wdc || wc_doc_first(a, gs, doc));
+  return a.dbg != 5 && (!a.wdc || a.dl || wc_doc_first(a, gs, doc));
 }
 
 // The count list.  A wave appends the slots of the tokens it counts to a
@@ -2213,6 +2213,27 @@ __device__ __forceinline__ void wc_cl_push(const WcArgs& a, bool need, uint32_t 
   }
   if (need && blk != ~0u) a.cl[(uint64_t)blk * WC_BLK + fill + mbcnt(m)] = gs;
   fill += n;
+}
+
+// worddocumentcount's document lists: the wave's pairs (all of one document,
+// launch-local doc) appended to the document's region, one device atomic per
+// wave round.  The region holds the document's token count of entries, and a
+// document never has more pairs to append than tokens (an LDS entry stands for
+// at least one token, a miss for one); past it the batch is re-run with the
+// dedupe table (status 8).
+__device__ __forceinline__ void wc_dl_push(const WcArgs& a, bool need, uint32_t gs, uint64_t doc) {
+  const uint64_t m = ballot(need);
+  if (!m) return;
+  const uint32_t n = (uint32_t)__builtin_popcountll(m);
+  uint32_t base = 0;
+  if (lane_id() == 0) base = atomicAdd(&a.dl_cur[doc], n);
+  base = __builtin_amdgcn_readfirstlane(base);
+  const uint64_t r0 = a.dl_pre[doc] - a.dl_pre[0], rn = a.dl_pre[doc + 1] - a.dl_pre[doc];
+  if ((uint64_t)base + n > rn) {
+    if (lane_id() == 0) atomicOr(&a.status[0], 8u);
+    return;
+  }
+  if (need) a.dl[r0 + base + mbcnt(m)] = gs;
 }
 
 // The tokens that START in a chunk (WC_TPW tiles of WC_TILE bytes of one
@@ -2360,7 +2381,8 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
         bool cnt = false;
         uint64_t cgs = 0;
         if (pend) cnt = wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
-        if (a.cl) wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
+        if (a.dl) wc_dl_push(a, cnt, (uint32_t)cgs, d);
+        else if (a.cl) wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
         else if (cnt) atomicAdd(&a.t_cnt[cgs], 1ull);
         pend = !counted;
         ph = h;
@@ -2379,7 +2401,9 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
     bool cnt = false;
     uint64_t cgs = 0;
     if (pend) cnt = wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
-    if (a.cl) {
+    if (a.dl) {
+      wc_dl_push(a, cnt, (uint32_t)cgs, d);
+    } else if (a.cl) {
       wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
       if (cblk != ~0u && lane == 0) a.cl_bcnt[cblk] = cfill;  // the wave's last block
     } else if (cnt) {
@@ -2391,28 +2415,37 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   // left to the check list), with its count (worddocumentcount: once per
   // document, through the dedupe table: other workgroups of the document may
   // hold the word too)
-  uint64_t* const fl = a.cl ? a.fl + (a.fl_base + blockIdx.x) * (uint64_t)TAB : nullptr;
+  // (document lists: the entries' pairs go to the group's document's region;
+  // TAB is a multiple of the workgroup, so every wave appends with all lanes)
+  uint64_t* const fl = a.cl && a.fl ? a.fl + (a.fl_base + blockIdx.x) * (uint64_t)TAB : nullptr;
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
     const ulonglong2 e = make_ulonglong2(lw0[i], lw1[i]);
     if (fl) fl[i] = ~0ull;  // (a counted entry rewrites it below)
-    if (e.x == 0ull) continue;
-    const uint32_t tl = wc_ident_len(e.x);
-    uint64_t lo, hi;
-    wc_ident_bytes(e.x, e.y, lo, hi);
-    const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
-    bool claimed;
-    const uint64_t gs = wc_global_insert(a, h, claimed);
-    if (gs == ~0ull) continue;
-    if (claimed) {
-      wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
-    } else {
-      const WcPeek q = wc_peek(a, gs);
-      if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
+    bool pair = false;
+    uint64_t gs = ~0ull;
+    if (e.x != 0ull) {
+      const uint32_t tl = wc_ident_len(e.x);
+      uint64_t lo, hi;
+      wc_ident_bytes(e.x, e.y, lo, hi);
+      const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
+      bool claimed;
+      gs = wc_global_insert(a, h, claimed);
+      if (gs != ~0ull) {
+        if (claimed) {
+          wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
+        } else {
+          const WcPeek q = wc_peek(a, gs);
+          if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
+        }
+        if (a.dl) {
+          pair = true;
+        } else if (!a.wdc || wc_doc_first(a, gs, gdoc)) {
+          if (fl) fl[i] = gs | (uint64_t)lc[i] << 32;
+          else atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
+        }
+      }
     }
-    if (!a.wdc || wc_doc_first(a, gs, gdoc)) {
-      if (fl) fl[i] = gs | (uint64_t)lc[i] << 32;
-      else atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
-    }
+    if (a.dl) wc_dl_push(a, pair, (uint32_t)gs, gdoc);
   }
 }
 
@@ -2783,6 +2816,55 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
                        dim3(64 * WC_WAVES_WC), 0, st, b);
   }
+  CCRDT_HIP(hipGetLastError());
+  return CCRDT_OK;
+}
+
+// worddocumentcount's document lists: one workgroup per document of the
+// launch keeps the distinct slots of its region and counts each once (count
+// list, or t_cnt when there is none).  An LDS bitmap covers WC_DL_BITS slots;
+// pass p reads the region and takes the slots of [p, p + 1) * WC_DL_BITS.
+// Four entries per thread are loaded before any is used (one workgroup per CU:
+// the bitmap is 128 KiB).
+constexpr uint32_t WC_DL_TB = 1024, WC_DL_UNR = 4;
+__global__ __launch_bounds__(WC_DL_TB) void wc_dl_kernel(WcArgs a, uint32_t passes) {
+  __shared__ uint32_t bm[WC_DL_BITS / 32];
+  const uint64_t d = blockIdx.x;
+  const uint64_t rn = a.dl_pre[d + 1] - a.dl_pre[d];
+  const uint32_t n = (uint32_t)min((uint64_t)a.dl_cur[d], rn);
+  const uint32_t* r = a.dl + (a.dl_pre[d] - a.dl_pre[0]);
+  const uint32_t wv = threadIdx.x >> 6;
+  uint32_t cblk = ~0u, cfill = WC_BLK;
+  const uint32_t shard = (uint32_t)((blockIdx.x * (WC_DL_TB / 64) + wv) % WC_NSHARD);
+  for (uint32_t p = 0; p < passes; ++p) {
+    for (uint32_t i = threadIdx.x; i < WC_DL_BITS / 32; i += WC_DL_TB) bm[i] = 0u;
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < n; i0 += WC_DL_TB * WC_DL_UNR) {
+      uint32_t sv[WC_DL_UNR];
+#pragma unroll
+      for (uint32_t u = 0; u < WC_DL_UNR; ++u) {
+        const uint32_t i = i0 + u * WC_DL_TB + threadIdx.x;
+        sv[u] = i < n ? r[i] : ~0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < WC_DL_UNR; ++u) {
+        bool fresh = false;
+        if (sv[u] != ~0u && sv[u] / WC_DL_BITS == p) {
+          const uint32_t b = sv[u] % WC_DL_BITS, bit = 1u << (b & 31);
+          fresh = !(atomicOr(&bm[b >> 5], bit) & bit);
+        }
+        if (a.cl) wc_cl_push(a, fresh, sv[u], cblk, cfill, shard);
+        else if (fresh) atomicAdd(&a.t_cnt[sv[u]], 1ull);
+      }
+    }
+    __syncthreads();
+  }
+  if (a.cl && cblk != ~0u && lane_id() == 0) a.cl_bcnt[cblk] = cfill;  // the wave's last block
+}
+
+int wc_launch_dl(const WcArgs& a, uint64_t n_docs, uint32_t passes, hipStream_t st) {
+  if (!n_docs || !passes) return CCRDT_OK;
+  hipLaunchKernelGGL(wc_dl_kernel, dim3((unsigned)n_docs), dim3(WC_DL_TB), 0, st, a, passes);
   CCRDT_HIP(hipGetLastError());
   return CCRDT_OK;
 }

@@ -197,7 +197,15 @@ struct WcArgs {
   uint64_t* d_hash;
   uint64_t d_mask;
   uint64_t d_base;           // document tags of this launch: d_base + 1 .. d_base + n_docs (< 2^24)
-  uint32_t* status;          // [0] table overflow, [1] hash collision | token lost | check list full (16), [2] check records
+  // worddocumentcount's document lists (nullptr: the dedupe table above):
+  // every (document, word) pair the insert kernel does not settle in LDS goes
+  // to its document's region as the word's slot; wc_dl_kernel then counts each
+  // document's distinct slots once (an LDS bitmap per document, no device
+  // atomic per pair)
+  uint32_t* dl;              // regions, one per document of the launch: its tokens' worth of entries
+  const uint64_t* dl_pre;    // [launch docs + 1] token prefix: region of d = [dl_pre[d], dl_pre[d + 1]) - dl_pre[0]
+  uint32_t* dl_cur;          // [launch docs] entries appended
+  uint32_t* status;          // [0] table overflow (1) | dedupe table (2) | count list full (4) | document list full (8), [1] hash collision | token lost | check list full (16), [2] check records
   WcChk* chk;                // the check list (wc_check_kernel), chk_cap records
   uint32_t chk_cap;
   // The count list (wc_cl_*): the insert kernel's count adds, summed after
@@ -222,6 +230,9 @@ constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH =
 // (A/B round 6: wordcount 3584 x 16 26.4 ms per step, 3072 x 16 27.5, 4096 x 12 28.9;
 // worddocumentcount 1024 x 4 51.7, 3584 x 16 51.6, 1536 x 8 62.9)
 constexpr uint32_t WC_TAB_WC = 3584, WC_WAVES_WC = 16, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
+static_assert(WC_TAB_WDC % (64 * WC_WAVES_WDC) == 0, "the flush's document-list appends are wave-wide");
+// wc_dl_kernel: slots per pass of its LDS bitmap (128 KiB), passes at most
+constexpr uint32_t WC_DL_BITS = 1u << 20, WC_DL_MAXPASS = 8;
 struct WcClArgs {
   const uint32_t* cl;
   const uint32_t* bcnt;

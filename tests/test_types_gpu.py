@@ -373,6 +373,7 @@ def test_wdc_dedupe_tags_across_launches(gpu, monkeypatch, dtags):
     with tag spaces so small that the table is cleared every few launches
     or every launch; the same words recur in every document so stale pairs
     of the same word sit in the table.  vs the oracle after each batch."""
+    monkeypatch.setenv("CCRDT_WC_DLIST", "0")  # (the dedupe table, not the document lists)
     monkeypatch.setenv("CCRDT_WC_LAUNCH_TOKENS", "3000")
     if dtags:
         monkeypatch.setenv("CCRDT_WC_DTAGS", dtags)
@@ -382,6 +383,32 @@ def test_wdc_dedupe_tags_across_launches(gpu, monkeypatch, dtags):
     for _ in range(4):
         docs = [[b" ".join(vocab[i] for i in rng.integers(0, len(vocab), int(rng.integers(0, 2500))))
                  for _ in range(int(rng.integers(0, 6)))] for _ in range(3)]
+        e.apply_docs(docs)
+        o.apply_docs(docs)
+        for x, y in zip(e.export(), o.export()):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("slots", [None, str(1 << 22)])
+@pytest.mark.parametrize("launch_tokens", [None, "3000"])
+def test_wdc_document_lists(gpu, monkeypatch, slots, launch_tokens):
+    """worddocumentcount's document lists (the default): every pair the insert
+    kernel does not settle in LDS goes to its document's region, and one
+    workgroup per document counts its distinct slots through an LDS bitmap
+    of 2^20 slots per pass.  A word table of 2^22 slots (four passes), one
+    launch or many per batch, words recurring within and across documents,
+    long words (past the 14-byte identities) and empty tokens, several
+    batches: vs the oracle after each."""
+    if slots:
+        monkeypatch.setenv("CCRDT_WC_SLOTS", slots)
+    if launch_tokens:
+        monkeypatch.setenv("CCRDT_WC_LAUNCH_TOKENS", launch_tokens)
+    rng = np.random.default_rng(11)
+    vocab = [b"w%d" % i for i in range(3000)] + [b"long_word_%020d" % i for i in range(300)] + [b""]
+    e, o = WordDocumentCountEngine(4), orc.WcOracle(4, True)
+    for _ in range(3):
+        docs = [[b" ".join(vocab[i] for i in rng.integers(0, len(vocab), int(rng.integers(0, 6000))))
+                 for _ in range(int(rng.integers(0, 5)))] for _ in range(4)]
         e.apply_docs(docs)
         o.apply_docs(docs)
         for x, y in zip(e.export(), o.export()):
