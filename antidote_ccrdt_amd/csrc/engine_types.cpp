@@ -1200,9 +1200,14 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
   // (CCRDT_WC_DLIST=0: the dedupe table; also when the word table needs more
   // than WC_DL_MAXPASS bitmap passes, or a document's list overflows)
   bool use_dl = wdc && !(getenv("CCRDT_WC_DLIST") && !atoi(getenv("CCRDT_WC_DLIST")));
+  // region of a document: twice its tokens + a block per wave (wc_dl_push)
+  std::vector<uint64_t> dl_rn(use_dl ? nd : 0);
   if (use_dl && nd) {
     std::vector<uint64_t> pre(nd + 1, 0);
-    for (uint64_t d = 0; d < nd; ++d) pre[d + 1] = pre[d] + ntok[d];
+    for (uint64_t d = 0; d < nd; ++d) {
+      dl_rn[d] = 2 * ntok[d] + (gptr[d + 1] - gptr[d]) * WC_WAVES_WDC * WC_DL_BLK;
+      pre[d + 1] = pre[d] + dl_rn[d];
+    }
     CCRDT_TRY(h2d(*e, T.dl_pre, pre.data(), (nd + 1) * 8));
   }
   const uint64_t cl_entries = docs->n_bytes / 16 + n_chunks * WC_BLK;
@@ -1262,10 +1267,12 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         tk += ntok[x1++];
       return x1;
     };
-    uint64_t max_tk = 0, max_docs = 0;  // (the document lists are sized once for every launch)
+    uint64_t max_rn = 0, max_docs = 0;  // (the document lists are sized once for every launch)
     for (uint64_t x0 = 0, tk = 0; x0 < nd;) {
       const uint64_t x1 = launch_end(x0, tk);
-      max_tk = std::max(max_tk, tk);
+      uint64_t rn = 0;
+      for (uint64_t x = x0; x < x1 && use_dl; ++x) rn += dl_rn[x];
+      max_rn = std::max(max_rn, rn);
       max_docs = std::max(max_docs, x1 - x0);
       x0 = x1;
     }
@@ -1287,7 +1294,7 @@ int ccrdt_wc_apply_device(ccrdt_engine* e, const ccrdt_wc_docs* docs) {
         a.n_groups = gptr[d1] - gptr[d0];
       }
       if (a.wdc && dl_on) {
-        CCRDT_TRY(T.dl.ensure(std::max<uint64_t>(max_tk, 1) * 4));
+        CCRDT_TRY(T.dl.ensure(std::max<uint64_t>(max_rn, 1) * 4));
         CCRDT_TRY(T.dl_cur.ensure(std::max<uint64_t>(max_docs, 1) * 4));
         CCRDT_HIP(hipMemsetAsync(T.dl_cur.p, 0, (d1 - d0) * 4, e->stream));
         a.dl = T.dl.as<uint32_t>();

@@ -2216,24 +2216,40 @@ __device__ __forceinline__ void wc_cl_push(const WcArgs& a, bool need, uint32_t 
 }
 
 // worddocumentcount's document lists: the wave's pairs (all of one document,
-// launch-local doc) appended to the document's region, one device atomic per
-// wave round.  The region holds the document's token count of entries, and a
-// document never has more pairs to append than tokens (an LDS entry stands for
-// at least one token, a miss for one); past it the batch is re-run with the
+// launch-local doc) appended to the document's region, in blocks of WC_DL_BLK
+// entries the wave reserves with one device atomic (dpos / dend: the wave's
+// current block).  A block the wave leaves (a push that does not fit, or the
+// wave's end, wc_dl_close) has its rest filled with ~0u, which the count pass
+// skips.  The region holds twice the document's tokens plus a block per wave
+// of the document (a document never has more pairs than tokens: an LDS entry
+// stands for at least one token, a miss for one; a block left early loses less
+// than 64 of its WC_DL_BLK entries); past it the batch is re-run with the
 // dedupe table (status 8).
-__device__ __forceinline__ void wc_dl_push(const WcArgs& a, bool need, uint32_t gs, uint64_t doc) {
+__device__ __forceinline__ void wc_dl_push(const WcArgs& a, bool need, uint32_t gs, uint64_t doc, uint32_t& dpos,
+                                           uint32_t& dend) {
   const uint64_t m = ballot(need);
   if (!m) return;
   const uint32_t n = (uint32_t)__builtin_popcountll(m);
-  uint32_t base = 0;
-  if (lane_id() == 0) base = atomicAdd(&a.dl_cur[doc], n);
-  base = __builtin_amdgcn_readfirstlane(base);
-  const uint64_t r0 = a.dl_pre[doc] - a.dl_pre[0], rn = a.dl_pre[doc + 1] - a.dl_pre[doc];
-  if ((uint64_t)base + n > rn) {
-    if (lane_id() == 0) atomicOr(&a.status[0], 8u);
-    return;
+  const uint64_t r0 = a.dl_pre[doc] - a.dl_pre[0];
+  if (dpos + n > dend) {
+    if (lane_id() < dend - dpos) a.dl[r0 + dpos + lane_id()] = ~0u;  // (fewer than 64 left)
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&a.dl_cur[doc], WC_DL_BLK);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if ((uint64_t)base + WC_DL_BLK > a.dl_pre[doc + 1] - a.dl_pre[doc]) {
+      if (lane_id() == 0) atomicOr(&a.status[0], 8u);
+      dpos = dend = 0;
+      return;
+    }
+    dpos = base;
+    dend = base + WC_DL_BLK;
   }
-  if (need) a.dl[r0 + base + mbcnt(m)] = gs;
+  if (need) a.dl[r0 + dpos + mbcnt(m)] = gs;
+  dpos += n;
+}
+__device__ __forceinline__ void wc_dl_close(const WcArgs& a, uint64_t doc, uint32_t dpos, uint32_t dend) {
+  const uint64_t r0 = a.dl_pre[doc] - a.dl_pre[0];
+  for (uint32_t i = dpos + lane_id(); i < dend; i += 64) a.dl[r0 + i] = ~0u;
 }
 
 // The tokens that START in a chunk (WC_TPW tiles of WC_TILE bytes of one
@@ -2309,6 +2325,7 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   // this wave's count-list block (wave-uniform)
   uint32_t cblk = ~0u, cfill = WC_BLK;
   const uint32_t shard = (blockIdx.x * WAVES + (uint32_t)wv) % WC_NSHARD;
+  uint32_t dpos = 0, dend = 0;  // this wave's document-list block (wave-uniform)
 
   for (int ti = 0; act && ti < (int)WC_TPW && tile <= len; ++ti, tile += WC_TILE) {
     wave_lds_sync();  // the previous tile's staged bytes are no longer read
@@ -2381,7 +2398,7 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
         bool cnt = false;
         uint64_t cgs = 0;
         if (pend) cnt = wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
-        if (a.dl) wc_dl_push(a, cnt, (uint32_t)cgs, d);
+        if (a.dl) wc_dl_push(a, cnt, (uint32_t)cgs, d, dpos, dend);
         else if (a.cl) wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
         else if (cnt) atomicAdd(&a.t_cnt[cgs], 1ull);
         pend = !counted;
@@ -2402,7 +2419,7 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
     uint64_t cgs = 0;
     if (pend) cnt = wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
     if (a.dl) {
-      wc_dl_push(a, cnt, (uint32_t)cgs, d);
+      wc_dl_push(a, cnt, (uint32_t)cgs, d, dpos, dend);
     } else if (a.cl) {
       wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
       if (cblk != ~0u && lane == 0) a.cl_bcnt[cblk] = cfill;  // the wave's last block
@@ -2445,8 +2462,9 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
         }
       }
     }
-    if (a.dl) wc_dl_push(a, pair, (uint32_t)gs, gdoc);
+    if (a.dl) wc_dl_push(a, pair, (uint32_t)gs, gdoc, dpos, dend);
   }
+  if (a.dl) wc_dl_close(a, gdoc, dpos, dend);
 }
 
 // ---- the count list, summed per bucket of 2^bsh slots (wc_cl_*): units are
