@@ -230,7 +230,7 @@ constexpr uint32_t WC_BLK = 1024, WC_NSHARD = 64, WC_CL_NB = 1024, WC_CL_MAXSH =
 // (A/B round 6: wordcount 3584 x 16 26.4 ms per step, 3072 x 16 27.5, 4096 x 12 28.9;
 // worddocumentcount 1024 x 4 51.7, 3584 x 16 51.6, 1536 x 8 62.9)
 constexpr uint32_t WC_TAB_WC = 3584, WC_WAVES_WC = 16, WC_TAB_WDC = 1024, WC_WAVES_WDC = 4;
-static_assert(WC_TAB_WDC % (64 * WC_WAVES_WDC) == 0, "the flush's document-list appends are wave-wide");
+static_assert(WC_TAB_WDC % 64 == 0, "the flush's document-list appends are wave-wide");
 // wc_dl_kernel: slots per pass of its LDS bitmap (128 KiB), passes at most;
 // the entries a wave reserves at once in its document's list
 constexpr uint32_t WC_DL_BITS = 1u << 20, WC_DL_MAXPASS = 8, WC_DL_BLK = 256;
