@@ -2167,6 +2167,7 @@ __device__ __forceinline__ void wc_tile(const WcArgs& a, uint64_t t, uint64_t& d
 // A token that missed the LDS table, resolved one round after its first-slot
 // read (pk: that slot's hash and identity words as read then): find or claim
 // its word, settle its identity, count it.
+template <bool WDC, bool DL>
 __device__ __forceinline__ bool wc_resolve(const WcArgs& a, const WcPeek& pk, uint64_t h, uint32_t key, uint32_t tl,
                                            uint64_t pos, uint64_t tw0, uint64_t tw1, uint64_t doc, uint64_t& gs_out) {
   bool claimed = false;
@@ -2186,7 +2187,7 @@ __device__ __forceinline__ bool wc_resolve(const WcArgs& a, const WcPeek& pk, ui
   if (claimed) wc_publish(a, gs, tw0, tw1, key, tl, WC_REF_BATCH | pos);
   else if (wc_settle(a, tw0, tw1, key, sw0, sw1, sw2)) wc_chk_push(a, gs, key, tl, tw0, tw1, pos);
   gs_out = gs;
-  return a.dbg != 5 && (!a.wdc || a.dl || wc_doc_first(a, gs, doc));
+  return a.dbg != 5 && (!WDC || DL || wc_doc_first(a, gs, doc));
 }
 
 // The count list.  A wave appends the slots of the tokens it counts to a
@@ -2271,7 +2272,11 @@ __device__ __forceinline__ void wc_dl_close(const WcArgs& a, uint64_t doc, uint3
 // reader that finds w0 but not yet w1 takes another entry: two entries of one
 // word only cost two flushes (wordcount adds both counts; worddocumentcount's
 // dedupe table admits one of them).
-template <int TAB, int WAVES>
+// WDC: worddocumentcount; DL: its document lists (a.dl), else its dedupe
+// table -- template flags, so the wordcount build carries none of their code
+// (the document lists' registers spilled into wordcount's loop: 61 -> 103
+// spilled VGPRs, insert kernel 21.6 -> 22.4 ms).
+template <int TAB, int WAVES, bool WDC, bool DL>
 __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   static_assert(TAB % 4 == 0, "buckets of 4 entries");
   constexpr uint64_t NB = TAB / 4;
@@ -2369,7 +2374,7 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
             for (int i = 3; i >= 0; --i)
               if (ex[i] == tw0) m = i;
             if (m >= 0 && lw1[bk * 4 + m] == tw1) {
-              if (!a.wdc) atomicAdd(&lc[bk * 4 + m], 1u);
+              if (!WDC) atomicAdd(&lc[bk * 4 + m], 1u);
               counted = true;
             } else {
 #pragma unroll
@@ -2379,11 +2384,11 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
                 const unsigned long long prev = atomicCAS(&lw0[sl], 0ull, (unsigned long long)tw0);
                 if (prev == 0ull) {  // new word of the group
                   lw1[sl] = tw1;
-                  if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                  if (!WDC) atomicAdd(&lc[sl], 1u);
                   else lc[sl] = 1u;
                   counted = true;
                 } else if (prev == tw0 && lw1[sl] == tw1) {
-                  if (!a.wdc) atomicAdd(&lc[sl], 1u);
+                  if (!WDC) atomicAdd(&lc[sl], 1u);
                   counted = true;
                 }
               }
@@ -2397,8 +2402,8 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
         pk_new = wc_peek(a, counted ? 0ull : (h & a.t_mask));
         bool cnt = false;
         uint64_t cgs = 0;
-        if (pend) cnt = wc_resolve(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
-        if (a.dl) wc_dl_push(a, cnt, (uint32_t)cgs, d, dpos, dend);
+        if (pend) cnt = wc_resolve<WDC, DL>(a, pk_prev, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
+        if (DL) wc_dl_push(a, cnt, (uint32_t)cgs, d, dpos, dend);
         else if (a.cl) wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
         else if (cnt) atomicAdd(&a.t_cnt[cgs], 1ull);
         pend = !counted;
@@ -2417,8 +2422,8 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   {
     bool cnt = false;
     uint64_t cgs = 0;
-    if (pend) cnt = wc_resolve(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
-    if (a.dl) {
+    if (pend) cnt = wc_resolve<WDC, DL>(a, pk0, ph, key, ptl, ppos, ptw0, ptw1, d, cgs);
+    if (DL) {
       wc_dl_push(a, cnt, (uint32_t)cgs, d, dpos, dend);
     } else if (a.cl) {
       wc_cl_push(a, cnt, (uint32_t)cgs, cblk, cfill, shard);
@@ -2432,39 +2437,56 @@ __global__ __launch_bounds__(64 * WAVES) void wc_insert_kernel(WcArgs a) {
   // left to the check list), with its count (worddocumentcount: once per
   // document, through the dedupe table: other workgroups of the document may
   // hold the word too)
-  // (document lists: the entries' pairs go to the group's document's region;
-  // TAB is a multiple of the workgroup, so every wave appends with all lanes)
-  uint64_t* const fl = a.cl && a.fl ? a.fl + (a.fl_base + blockIdx.x) * (uint64_t)TAB : nullptr;
+  if constexpr (DL) {
+    // document lists: the entries' pairs go to the group's document's region
+    // (TAB is a multiple of 64, so every wave appends with all its lanes)
+    for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
+      const ulonglong2 e = make_ulonglong2(lw0[i], lw1[i]);
+      uint64_t gs = ~0ull;
+      if (e.x != 0ull) {
+        const uint32_t tl = wc_ident_len(e.x);
+        uint64_t lo, hi;
+        wc_ident_bytes(e.x, e.y, lo, hi);
+        const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
+        bool claimed;
+        gs = wc_global_insert(a, h, claimed);
+        if (gs != ~0ull) {
+          if (claimed) {
+            wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
+          } else {
+            const WcPeek q = wc_peek(a, gs);
+            if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
+          }
+        }
+      }
+      wc_dl_push(a, gs != ~0ull, (uint32_t)gs, gdoc, dpos, dend);
+    }
+    wc_dl_close(a, gdoc, dpos, dend);
+    return;
+  }
+  uint64_t* const fl = a.cl ? a.fl + (a.fl_base + blockIdx.x) * (uint64_t)TAB : nullptr;
   for (int i = (int)threadIdx.x; i < TAB; i += 64 * WAVES) {
     const ulonglong2 e = make_ulonglong2(lw0[i], lw1[i]);
     if (fl) fl[i] = ~0ull;  // (a counted entry rewrites it below)
-    bool pair = false;
-    uint64_t gs = ~0ull;
-    if (e.x != 0ull) {
-      const uint32_t tl = wc_ident_len(e.x);
-      uint64_t lo, hi;
-      wc_ident_bytes(e.x, e.y, lo, hi);
-      const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
-      bool claimed;
-      gs = wc_global_insert(a, h, claimed);
-      if (gs != ~0ull) {
-        if (claimed) {
-          wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
-        } else {
-          const WcPeek q = wc_peek(a, gs);
-          if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
-        }
-        if (a.dl) {
-          pair = true;
-        } else if (!a.wdc || wc_doc_first(a, gs, gdoc)) {
-          if (fl) fl[i] = gs | (uint64_t)lc[i] << 32;
-          else atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
-        }
-      }
+    if (e.x == 0ull) continue;
+    const uint32_t tl = wc_ident_len(e.x);
+    uint64_t lo, hi;
+    wc_ident_bytes(e.x, e.y, lo, hi);
+    const uint64_t h = wc_hkey(a, wc_hash_regs(lo, hi, tl), group_key, tl);
+    bool claimed;
+    const uint64_t gs = wc_global_insert(a, h, claimed);
+    if (gs == ~0ull) continue;
+    if (claimed) {
+      wc_publish(a, gs, e.x, e.y, group_key, tl, WC_REF_BATCH);  // (persisted from its identity)
+    } else {
+      const WcPeek q = wc_peek(a, gs);
+      if (wc_settle(a, e.x, e.y, group_key, q.w0, q.w1, q.w2)) wc_chk_push(a, gs, group_key, tl, e.x, e.y, 0);
     }
-    if (a.dl) wc_dl_push(a, pair, (uint32_t)gs, gdoc, dpos, dend);
+    if (!WDC || wc_doc_first(a, gs, gdoc)) {
+      if (fl) fl[i] = gs | (uint64_t)lc[i] << 32;
+      else atomicAdd(&a.t_cnt[gs], (unsigned long long)lc[i]);
+    }
   }
-  if (a.dl) wc_dl_close(a, gdoc, dpos, dend);
 }
 
 // ---- the count list, summed per bucket of 2^bsh slots (wc_cl_*): units are
@@ -2825,13 +2847,16 @@ int wc_launch_insert(const WcArgs& a, uint64_t n_chunks, hipStream_t st) {
     // 48.6 ms, 512 51.2, 2048 58.4 -- the dedupe path of the misses wants the
     // occupancy of the smaller table; one-document groups of 16 waves on 4096
     // / 2048 entries: 61.6 / 63.6 ms)
-    hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
+    if (a.dl)
+      hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC, true, true>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
+    else
+      hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WDC, WC_WAVES_WDC, true, false>), dim3((unsigned)a.n_groups), dim3(64 * WC_WAVES_WDC), 0, st, b);
   } else {
     // (identities take 20 B of LDS per entry: 16 waves (4 per SIMD, 128
     // VGPRs with a few spills) share 3584 entries; measured on the 8 GiB
     // corpus with the count list: 26.4 ms per step, 3072 entries 27.5, 12
     // waves on 4096 entries (~150 VGPRs, 3 per SIMD) 28.9)
-    hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
+    hipLaunchKernelGGL((wc_insert_kernel<WC_TAB_WC, WC_WAVES_WC, false, false>), dim3((unsigned)((n_chunks + WC_WAVES_WC - 1) / WC_WAVES_WC)),
                        dim3(64 * WC_WAVES_WC), 0, st, b);
   }
   CCRDT_HIP(hipGetLastError());
